@@ -1,0 +1,186 @@
+"""Training-step throughput of the ALIGNN hot path on MI355X (BASELINE.json metric).
+
+One step = the per-batch body of ``train_epoch_hetero`` (scripts/train.py:639-699) on a batch of
+B synthetic MP-like graphs (60 atoms / 720 bonds / 7,920 triplets each), D=256, H=4,
+L=4, dropout 0.15, feature jitter 0.1: forward, hetero NLL, backward, clip_grad_norm_(5), AdamW.
+Inputs are collated and resident in HBM before the timed region (CSR built once per batch).
+
+Multi-GPU: one process per GPU (torch.distributed.run); each rank trains on its own batch of B
+graphs (weak scaling) and the gradients are averaged with ONE all_reduce over the flat gradient
+buffer (13.2 MB fp32) per step — the data-parallel exchange of SURVEY §8e.
+
+Prints one JSON line (rank 0).  Also reports the dominant kernel's roofline (HIP events around
+its launches inside the timed region) and the oracle's CPU throughput on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gnn-elasticity-predictor_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "graphs/sec fwd+bwd (ALIGNN, ~60-atom MP crystals) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=32, help="graphs per GPU (BASELINE config 2: 32)")
+    p.add_argument("--hidden", type=int, default=256)
+    p.add_argument("--layers", type=int, default=4)
+    p.add_argument("--heads", type=int, default=4)
+    p.add_argument("--dropout", type=float, default=0.15)
+    p.add_argument("--lg-offset", default="num_nodes", choices=["num_nodes", "num_edges"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--no-roofline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args, B):
+    """The oracle (PyTorch-CPU restatement, fp32) on a bounded sample of the same workload:
+    full fwd + NLL + bwd + clip + AdamW steps on the same synthetic graphs."""
+    from oracle import model_ref
+    from oracle.pyg_ref import RefData, collate
+
+    from alignn_mi355x.synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS, mp_like_graph
+    import alignn_mi355x as A
+
+    torch.manual_seed(0)
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads, 0.0), 2)
+    st = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    gs = [mp_like_graph(g) for g in range(B)]
+    b = collate([RefData(**{k: getattr(d, k) for k in d.keys()}) for d in gs], lg_offset=args.lg_offset)
+    threads = torch.get_num_threads()
+    model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)  # warm-up
+    t0 = time.perf_counter()
+    model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=args.cpu_steps)
+    dt = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(B * args.cpu_steps / dt, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} steps x {B} graphs (fp32 fwd+bwd+clip+AdamW, dropout 0) after 1 warm-up; "
+                      f"{cpu_model}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import alignn_mi355x as A
+    from alignn_mi355x import profiling
+    from alignn_mi355x.synthetic import mp_like_batch
+
+    B = args.batch
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
+                                                      args.dropout), 2).to(dev)
+    trainer = A.FusedTrainer(model)
+    batch = mp_like_batch(B, first=rank * B, lg_offset=args.lg_offset).to(dev)
+    grad = trainer.st.grad
+
+    def step(i):
+        seed = 1000003 * rank + i
+        trainer.forward_backward(batch, seed)
+        if world > 1:
+            dist.all_reduce(grad)
+            grad.mul_(1.0 / world)
+        torch.nn.utils.clip_grad_norm_([trainer.p_base, trainer.p_sigma], max_norm=5.0)
+        trainer.opt.step()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    # pick the dominant kernel (untimed probe step with events around every launch)
+    dominant = None
+    if not args.no_roofline:
+        profiling.enable(None)
+        step(args.warmup)
+        torch.cuda.synchronize()
+        summ = profiling.summary()
+        profiling.disable()
+        dominant = max(summ, key=lambda k: summ[k]["total_ms"])
+        profiling.enable(dominant)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + 1 + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    profiling.disable()
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    result = None
+    if rank == 0:
+        value = B * world * args.steps / dt
+        roof = None
+        if dominant is not None:
+            s = profiling.summary()[dominant]
+            avg_s = s["avg_ms"] / 1e3
+            if s["flops_per_launch"] > 0:
+                ach = s["flops_per_launch"] / avg_s / 1e12
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / FP32_MFMA_TFLOPS, 4), "traffic": None, "kernel": dominant,
+                        "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
+                        "flops_per_launch": s["flops_per_launch"]}
+            else:
+                ach = s["bytes_per_launch"] / avg_s / 1e9
+                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dominant,
+                        "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
+                        "bytes_per_launch": s["bytes_per_launch"]}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, B)
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"B={B} synthetic MP-like graphs per GPU (60 atoms/720 bonds/7920 triplets), "
+                                   f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
+                       "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
+                       "dropout": args.dropout},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

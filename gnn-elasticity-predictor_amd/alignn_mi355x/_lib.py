@@ -1,0 +1,107 @@
+"""ctypes binding of ``libalignn_hip.so`` (the C ABI declared in ``include/alignn_hip.h``).
+
+The library is built in-tree (``csrc/Makefile`` -> ``alignn_mi355x/libalignn_hip.so``).  There is no
+CPU or PyTorch fallback: if the library is missing or cannot be loaded, :func:`lib` raises.
+``torch`` is imported first so that the HIP runtime torch ships (SONAME ``libamdhip64.so.7``) is
+the one the library binds to — one runtime, one device context, shared streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must load torch's HIP runtime before the library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libalignn_hip.so")
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_u64 = ctypes.c_uint64
+c_f32 = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64), ("batch", c_i64),
+        ("A", c_vp), ("sam", c_i64), ("sak", c_i64), ("sab", c_i64),
+        ("B", c_vp), ("sbk", c_i64), ("sbn", c_i64), ("sbb", c_i64),
+        ("C", c_vp), ("scm", c_i64), ("scn", c_i64), ("scb", c_i64),
+        ("bias", c_vp), ("sbias_b", c_i64),
+        ("rowscale", c_vp), ("srs_m", c_i64), ("srs_b", c_i64),
+        ("bias2", c_vp), ("sb2_b", c_i64),
+        ("mask", c_vp), ("smk_m", c_i64), ("smk_n", c_i64),
+        ("alpha", c_f32), ("beta", c_f32),
+        ("relu", c_i32), ("split_k", c_i32),
+        ("workspace", c_vp), ("workspace_elems", c_i64),
+    ]
+
+
+_SIGNATURES = {
+    "alignn_version": ([], c_i32),
+    "alignn_last_error": ([], ctypes.c_char_p),
+    "alignn_gemm_f32": ([ctypes.POINTER(GemmArgs), c_vp], c_i32),
+    "alignn_colsum_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
+    "alignn_graph_prep": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "alignn_gather_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
+    "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_tconv_bwd_dst": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                              c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                              c_i32, c_f32, c_u64, c_vp], c_i32),
+    "alignn_tconv_bwd_src": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                              c_i64, c_vp], c_i32),
+    "alignn_gate_ln_fwd": ([c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
+                            c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_gate_ln_bwd": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_readout_feats_fwd": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_f32, c_u64, c_vp],
+                                 c_i32),
+    "alignn_readout_pool_bwd": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp],
+                                c_i32),
+    "alignn_dropout_f32": ([c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_u64, c_vp], c_i32),
+    "alignn_hetero_nll": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp],
+                          c_i32),
+    "alignn_add_noise_f32": ([c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
+}
+
+EXPORTED = tuple(_SIGNATURES.keys())
+
+_lib = None
+_lock = threading.Lock()
+
+
+class AlignnHipError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the library and declare every signature (no GPU work happens here)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise AlignnHipError(
+                f"libalignn_hip.so not found at {path}: build it with `make -C "
+                f"gnn-elasticity-predictor_amd/csrc` or __graft_entry__.build() (there is no CPU fallback)")
+        lib_ = ctypes.CDLL(path)
+        for name, (argtypes, restype) in _SIGNATURES.items():
+            fn = getattr(lib_, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = lib_
+        return _lib
+
+
+def lib() -> ctypes.CDLL:
+    return _lib if _lib is not None else load()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().alignn_last_error()
+        msg = msg.decode() if msg else ""
+        raise AlignnHipError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,402 @@
+"""ALIGNN forward/backward engine over libalignn_hip (MI355X, fp32).
+
+One call of :meth:`AlignnEngine.forward` runs the whole ``HeteroAlignnRegressor.forward``
+(``scripts/train.py:537-586``); :meth:`AlignnEngine.backward` produces every parameter gradient
+into a flat buffer (layout: :mod:`layout`).  All arithmetic is in HIP kernels: MFMA GEMMs for the
+dense projections, fused CSR attention kernels for TransformerConv message passing, fused row
+kernels for gate/LayerNorm/ReLU/dropout/residual and readout.  Torch supplies memory and the stream.
+
+Data layout in HBM (D = hidden, H = heads, C = D/H):
+  * node/edge state    [N, D] / [E, D] row-major fp32
+  * QKVR               [n, 4D]   (Q | K | V | R=skip) of each TransformerConv
+  * U, S, Vd, Sz       [n, H, D] per-target-node per-head vectors of the edge-feature algebra
+  * angle embedding    [T, D]    in line-graph target-sorted order (coalesced per segment)
+  * CSR                int32 offsets/permutations per graph (ops.GraphCSR)
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+from .layout import AlignnConfig, offsets
+
+MIN_LOGVAR_FLOOR = -2.9  # train.py:39
+
+
+# ------------------------------------------------------------------------------------------------
+# Parameter / gradient views over a flat buffer
+# ------------------------------------------------------------------------------------------------
+class _Conv:
+    __slots__ = ("Wqkvr", "bqkvr", "We", "wbeta", "lnw", "lnb", "Wp", "bp")
+
+
+class FlatViews:
+    """Named views (state-dict names) + fused operand views of one flat fp32 buffer."""
+
+    def __init__(self, flat: torch.Tensor, cfg: AlignnConfig, hetero: bool = True):
+        self.flat = flat
+        self.cfg = cfg
+        self.hetero = hetero
+        self.prefix = pre = "base." if hetero else ""
+        offs, total, self.sigma_start = offsets(cfg, hetero)
+        if flat.numel() != total:
+            raise ValueError(f"flat buffer has {flat.numel()} elements, layout needs {total}")
+        self.named: Dict[str, torch.Tensor] = {}
+        for name, (o, shape) in offs.items():
+            n = 1
+            for s in shape:
+                n *= s
+            self.named[name] = flat[o:o + n].view(shape)
+        D = cfg.hidden
+        self.edge: List[_Conv] = [self._conv(f"{pre}edge_blocks.{l}.", offs, D, False) for l in range(cfg.layers)]
+        self.node: List[_Conv] = [self._conv(f"{pre}node_blocks.{l}.", offs, D, True) for l in range(cfg.layers)]
+        T = cfg.target_dim
+
+        def rows(name, k):
+            o = offs[name][0]
+            return flat[o:o + k * D].view(k, D) if k * D else None
+
+        def vec(name, k):
+            o = offs[name][0]
+            return flat[o:o + k]
+
+        if hetero:
+            self.Wmean, self.bmean = rows("mean_heads.0.weight", T), vec("mean_heads.0.bias", T)
+            self.Wlogvar, self.blogvar = rows("logvar_heads.0.weight", T), vec("logvar_heads.0.bias", T)
+        else:
+            self.Wout, self.bout = rows("output_heads.0.weight", T), vec("output_heads.0.bias", T)
+
+    def enc(self, which: str, idx: int, kind: str) -> torch.Tensor:
+        return self.named[f"{self.prefix}{which}_encoder.{idx}.{kind}"]
+
+    def _conv(self, p: str, offs, D: int, node: bool) -> _Conv:
+        c = _Conv()
+        o = offs[p + "conv.lin_query.weight"][0]
+        c.Wqkvr = self.flat[o:o + 4 * D * D].view(4 * D, D)
+        o = offs[p + "conv.lin_query.bias"][0]
+        c.bqkvr = self.flat[o:o + 4 * D]
+        c.We = self.named[p + "conv.lin_edge.weight"]
+        c.wbeta = self.named[p + "conv.lin_beta.weight"].view(-1)
+        c.lnw = self.named[p + "norm.weight"]
+        c.lnb = self.named[p + "norm.bias"]
+        c.Wp = self.named[p + "edge_proj.weight"] if node else None
+        c.bp = self.named[p + "edge_proj.bias"] if node else None
+        return c
+
+    def __getitem__(self, name: str) -> torch.Tensor:
+        return self.named[name]
+
+
+# ------------------------------------------------------------------------------------------------
+# Per-batch device preparation (cached on the batch)
+# ------------------------------------------------------------------------------------------------
+class BatchCache:
+    """CSR lists of the atom graph and the line graph, target-sorted angle inputs, ptr."""
+
+    def __init__(self, batch, validate: bool = True):
+        x = batch.x
+        if not x.is_cuda:
+            raise ValueError("batch must be on the HIP device (batch.to('cuda')); the engine has no CPU path")
+        self.N = int(x.size(0))
+        self.E = int(batch.edge_index.size(1))
+        self.T = int(batch.lg_edge_index.size(1))
+        self.ag = ops.GraphCSR(batch.edge_index, self.N)
+        self.lg = ops.GraphCSR(batch.lg_edge_index, self.E)
+        la = batch.lg_edge_attr
+        self.angle_dim = int(la.size(-1)) if la.dim() == 2 else 0
+        if self.T > 0 and la.numel() > 0:
+            self.xa = ops.gather_rows(la.contiguous().float(), self.lg.perm_dst[: self.T])
+        else:
+            self.xa = None
+        if hasattr(batch, "batch") and batch.batch is not None:
+            self.batch_vec = batch.batch.to(torch.int64).contiguous()
+        else:
+            self.batch_vec = torch.zeros(self.N, dtype=torch.int64, device=x.device)
+        if hasattr(batch, "ptr") and batch.ptr is not None:
+            self.ptr = batch.ptr.to(torch.int64).contiguous()
+        else:  # host logic (plumbing): counts per graph
+            B = int(self.batch_vec.max().item()) + 1 if self.N else 0
+            cnt = torch.bincount(self.batch_vec, minlength=B)
+            self.ptr = torch.cat([cnt.new_zeros(1), cnt.cumsum(0)])
+        self.B = int(self.ptr.numel() - 1)
+        if validate:
+            self.ag.check_indices("edge_index")
+            self.lg.check_indices("lg_edge_index")
+
+
+def batch_cache(batch, validate: bool = True) -> BatchCache:
+    bc = getattr(batch, "_alignn_cache", None)
+    if bc is None:
+        bc = BatchCache(batch, validate)
+        try:
+            batch._alignn_cache = bc
+        except AttributeError:
+            pass
+    return bc
+
+
+def site_seed(seed: int, site: int) -> int:
+    return (seed * 0x9E3779B1 + site * 0x85EBCA77 + 0x165667B1) & (2**63 - 1)
+
+
+class _Ctx:
+    pass
+
+
+# ------------------------------------------------------------------------------------------------
+# One conv block (EdgeUpdateBlock / NodeUpdateBlock) — shared by the full engine and the
+# standalone drop-in modules.
+#   x_new = x + dropout(relu(LN(TransformerConv(x, graph, f))))
+# with the edge features f (rows F[feat_row[t]] or F[t]) projected by M_h = W_e,h P (+ w̄ = W_e p).
+# ------------------------------------------------------------------------------------------------
+def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, feat_row, with_proj: bool,
+                  H: int, p_drop: float, seed_att: int, seed_blk: int):
+    n, D = X.shape
+    C = D // H
+    dev = X.device
+    c = _Ctx()
+    c.X, c.F, c.feat_row = X, F, feat_row
+    if with_proj:
+        c.M = torch.empty(D, D, device=dev)
+        ops.gemm(cv.We, cv.Wp, c.M)  # M = W_edge @ W_proj
+        c.wbar = torch.empty(D, device=dev)
+        ops.gemm(cv.We, cv.bp.view(D, 1), c.wbar.view(D, 1))  # w̄ = W_edge @ b_proj
+    else:
+        c.M, c.wbar = cv.We, None
+    c.QKVR = torch.empty(n, 4 * D, device=dev)
+    ops.gemm(X, cv.Wqkvr.t(), c.QKVR, bias=cv.bqkvr)
+    c.U = torch.empty(n, H, D, device=dev)
+    ops.gemm(c.QKVR[:, :D].view(n, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
+    c.outp = torch.empty(n, D, device=dev)
+    c.S = torch.empty(n, H, D, device=dev)
+    c.sumA = torch.empty(n, H, device=dev)
+    c.mstat = torch.empty(n, H, device=dev)
+    c.den = torch.empty(n, H, device=dev)
+    ops.tconv_fwd(g, D, H, c.QKVR, c.U, c.wbar, F, feat_row, c.outp, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att)
+    if with_proj:
+        ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp.view(n, H, C).transpose(0, 1),
+                 beta=1.0, rowscale=c.sumA.t(), bias2=c.wbar.view(H, C))
+    else:
+        ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp.view(n, H, C).transpose(0, 1),
+                 beta=1.0)
+    X_new = torch.empty(n, D, device=dev)
+    c.beta = torch.empty(n, device=dev)
+    c.mu = torch.empty(n, device=dev)
+    c.rstd = torch.empty(n, device=dev)
+    ops.gate_ln_fwd(c.outp, c.QKVR[:, 3 * D:], cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop,
+                    seed_blk)
+    c.p, c.seed_att, c.seed_blk, c.H, c.with_proj = p_drop, seed_att, seed_blk, H, with_proj
+    return X_new, c
+
+
+def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
+                   dF_accumulate: bool) -> None:
+    """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
+    dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
+    Parameter gradients are accumulated into gv (its gate/LN grads with +=, the rest overwritten)."""
+    n, D = c.X.shape
+    H = c.H
+    C = D // H
+    dev = dX.device
+    m = g.m
+    dout = torch.empty(n, D, device=dev)
+    dQKVR = torch.empty(n, 4 * D, device=dev)
+    ops.gate_ln_bwd(dX, c.outp, c.QKVR[:, 3 * D:], cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout,
+                    dQKVR[:, 3 * D:], gv.wbeta, gv.lnw, gv.lnb, c.p, c.seed_blk)
+    Vd = torch.empty(n, H, D, device=dev)
+    ops.gemm(dout.view(n, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
+    Sz = torch.empty(n, H, D, device=dev)
+    sigz = torch.empty(n, H, device=dev)
+    dz_e = torch.empty(max(m, 1), H, device=dev)
+    al_e = torch.empty(max(m, 1), H, device=dev)
+    ops.tconv_bwd_dst(g, D, H, c.QKVR, c.U, Vd, c.wbar, c.F, c.feat_row, dout, c.outp, c.mstat, c.den,
+                      dQKVR[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att)
+    ops.tconv_bwd_src(g, D, H, c.QKVR, dout, dz_e, al_e, dQKVR[:, D:3 * D])
+    Qh = c.QKVR[:, :D].view(n, H, C).permute(1, 2, 0)
+    Oh = dout.view(n, H, C).permute(1, 2, 0)
+    dQv = dQKVR[:, :D].view(n, H, C).transpose(0, 1)
+    if c.with_proj:
+        ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0, rowscale=sigz.t(),
+                 bias2=c.wbar.view(H, C))
+        dM = torch.empty(D, D, device=dev)
+        ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
+        ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
+        dwbar = torch.empty(D, device=dev)
+        ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
+        ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
+        ops.gemm(dM, cv.Wp.t(), gv.We)                                  # dW_edge = dM W_p^T + dw̄ b_p^T
+        ops.gemm(dwbar.view(D, 1), cv.bp.view(1, D), gv.We, beta=1.0)
+        ops.gemm(cv.We.t(), dM, gv.Wp)                                  # dW_p = W_edge^T dM
+        ops.gemm(cv.We.t(), dwbar.view(D, 1), gv.bp.view(D, 1))        # db_p = W_edge^T dw̄
+    else:
+        ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0)
+        ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
+        ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
+    ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                             # residual + projections
+    ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
+    ops.colsum(dQKVR, gv.bqkvr)
+
+
+# ------------------------------------------------------------------------------------------------
+# Engine
+# ------------------------------------------------------------------------------------------------
+class AlignnEngine:
+    """``mode``: 'hetero' -> [B, 2T] = [mean | logvar] (HeteroAlignnRegressor.forward),
+    'base' -> [B, T] (AlignnRegressor.forward), 'embed' -> shared [B, D] (embed)."""
+
+    def __init__(self, cfg: AlignnConfig):
+        cfg.validate()
+        self.cfg = cfg
+
+    def _mlp_fwd(self, x, W1, b1, W2, b2):
+        D = self.cfg.hidden
+        h1 = torch.empty(x.size(0), D, device=x.device)
+        ops.gemm(x, W1.t(), h1, bias=b1, relu=True)
+        out = torch.empty(x.size(0), D, device=x.device)
+        ops.gemm(h1, W2.t(), out, bias=b2)
+        return h1, out
+
+    def _mlp_bwd(self, dout, x, h1, W2, gW1, gb1, gW2, gb2):
+        ops.gemm(dout.t(), h1, gW2)
+        ops.colsum(dout, gb2)
+        dh1 = torch.empty_like(h1)
+        ops.gemm(dout, W2, dh1, mask=h1)
+        ops.gemm(dh1.t(), x, gW1)
+        ops.colsum(dh1, gb1)
+
+    def forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
+                x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
+        cfg = self.cfg
+        D, H, L = cfg.hidden, cfg.heads, cfg.layers
+        p_drop = cfg.dropout if training else 0.0
+        dev = batch.x.device
+        N, E, T, B = bc.N, bc.E, bc.T, bc.B
+        ctx = _Ctx()
+        ctx.seed, ctx.p, ctx.mode = seed, p_drop, mode
+        x = (batch.x if x is None else x).contiguous()
+        global_x = (batch.global_x if global_x is None else global_x).contiguous()
+        ctx.x = x
+        edge_attr = batch.edge_attr.contiguous()
+        ctx.edge_attr = edge_attr
+        # encoders (train.py:547-556)
+        ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
+                                   P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
+        if edge_attr.numel() > 0:
+            ctx.h1e, e = self._mlp_fwd(edge_attr, P.enc("edge", 0, "weight"), P.enc("edge", 0, "bias"),
+                                       P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
+        else:
+            ctx.h1e, e = None, torch.zeros(E, D, device=dev)
+        ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
+        if ctx.has_angle:
+            ctx.h1a, a = self._mlp_fwd(bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
+                                       P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"))
+        else:
+            ctx.h1a, a = None, torch.zeros(T, D, device=dev)
+        ctx.a = a
+        ctx.edge, ctx.node = [], []
+        for l in range(L):
+            # EdgeUpdateBlock (train.py:312-317): line graph, angle embedding in target-sorted order
+            if T > 0 and E > 0:
+                e, c = block_forward(P.edge[l], e, bc.lg, a, None, False, H, p_drop, site_seed(seed, 4 * l),
+                                     site_seed(seed, 4 * l + 1))
+            else:
+                c = None
+            ctx.edge.append(c)
+            # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
+            if E > 0:
+                h, c = block_forward(P.node[l], h, bc.ag, e, bc.ag.perm_dst, True, H, p_drop,
+                                     site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
+            else:
+                c = None
+            ctx.node.append(c)
+        ctx.h = h
+        # readout (train.py:562-574)
+        gdim = global_x.numel() // max(B, 1)
+        sg = batch.sg_one_hot.contiguous()
+        sgdim = sg.numel() // max(B, 1)
+        if gdim + sgdim != cfg.global_dim:
+            raise ValueError(f"global features: got {gdim}+{sgdim}, model expects {cfg.global_dim}")
+        W = D + gdim + sgdim
+        ctx.feats = torch.empty(B, W, device=dev)
+        ops.readout_feats_fwd(h, bc.ptr, global_x, gdim, sg, sgdim, ctx.feats, p_drop, site_seed(seed, 4 * L))
+        ctx.pre = torch.empty(B, D, device=dev)
+        ops.gemm(ctx.feats, P.named[P.prefix + "feat_proj.0.weight"].t(), ctx.pre,
+                 bias=P.named[P.prefix + "feat_proj.0.bias"], relu=True)
+        ctx.shared = torch.empty(B, D, device=dev)
+        ops.dropout(ctx.pre, ctx.shared, None, p_drop, site_seed(seed, 4 * L + 1))
+        ctx.bc = bc
+        Tt = cfg.target_dim
+        if mode == "embed":
+            return ctx.shared, ctx
+        if mode == "hetero":
+            out = torch.empty(B, 2 * Tt, device=dev)
+            ops.gemm(ctx.shared, P.Wmean.t(), out[:, :Tt], bias=P.bmean)
+            ops.gemm(ctx.shared, P.Wlogvar.t(), out[:, Tt:], bias=P.blogvar)
+            return out, ctx
+        out = torch.empty(B, Tt, device=dev)
+        ops.gemm(ctx.shared, P.Wout.t(), out, bias=P.bout)
+        return out, ctx
+
+    def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
+        """Writes d(loss)/d(param) for every parameter into G (overwrites; head grads are zero in
+        'embed' mode).  ``dout`` is the gradient of the forward's output."""
+        cfg = self.cfg
+        D, L = cfg.hidden, cfg.layers
+        Tt = cfg.target_dim
+        bc = ctx.bc
+        N, E, T, B = bc.N, bc.E, bc.T, bc.B
+        dev = dout.device
+        p_drop, seed = ctx.p, ctx.seed
+        pre = P.prefix
+        g = G.named
+        G.flat.zero_()
+        dout = dout.contiguous()
+        # heads (train.py:582-585)
+        if ctx.mode == "embed":
+            dshared = dout
+        else:
+            dshared = torch.empty(B, D, device=dev)
+            if ctx.mode == "hetero":
+                ops.gemm(dout[:, :Tt].t(), ctx.shared, G.Wmean)
+                ops.colsum(dout[:, :Tt], G.bmean)
+                ops.gemm(dout[:, Tt:].t(), ctx.shared, G.Wlogvar)
+                ops.colsum(dout[:, Tt:], G.blogvar)
+                ops.gemm(dout[:, :Tt], P.Wmean, dshared)
+                ops.gemm(dout[:, Tt:], P.Wlogvar, dshared, beta=1.0)
+            else:
+                ops.gemm(dout.t(), ctx.shared, G.Wout)
+                ops.colsum(dout, G.bout)
+                ops.gemm(dout, P.Wout, dshared)
+        # feat_proj + readout (train.py:562-573)
+        dpre = torch.empty(B, D, device=dev)
+        ops.dropout(dshared, dpre, ctx.pre, p_drop, site_seed(seed, 4 * L + 1))
+        Wf = P.named[pre + "feat_proj.0.weight"]
+        ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"])
+        ops.colsum(dpre, g[pre + "feat_proj.0.bias"])
+        Wfeat = ctx.feats.size(1)
+        dfeats = torch.zeros(B, Wfeat, device=dev)
+        ops.gemm(dpre, Wf[:, :D], dfeats[:, :D])
+        dh = torch.empty(N, D, device=dev)
+        ops.readout_pool_bwd(dfeats, bc.ptr, bc.batch_vec, dh, False, p_drop, site_seed(seed, 4 * L))
+        de = torch.zeros(E, D, device=dev)
+        da = torch.empty(T, D, device=dev) if T > 0 else None
+        da_written = False
+        for l in reversed(range(L)):
+            c = ctx.node[l]
+            if c is not None:
+                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True)
+            c = ctx.edge[l]
+            if c is not None:
+                block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, da_written)
+                da_written = True
+        # encoders
+        if ctx.has_angle and da_written:
+            self._mlp_bwd(da, bc.xa, ctx.h1a, P.enc("angle", 2, "weight"), G.enc("angle", 0, "weight"),
+                          G.enc("angle", 0, "bias"), G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
+        if ctx.h1e is not None:
+            self._mlp_bwd(de, ctx.edge_attr, ctx.h1e, P.enc("edge", 2, "weight"), G.enc("edge", 0, "weight"),
+                          G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))
+        self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
+                      G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))

@@ -1,0 +1,278 @@
+"""Tensor-level wrappers over the C ABI (``_lib``).  Torch tensors provide device memory, strides
+and the current HIP stream; all arithmetic runs in ``libalignn_hip.so``.  No fallbacks."""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib, profiling
+from ._lib import GemmArgs, check
+
+_NUM_CUS = 256
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _require(t: torch.Tensor, name: str, dtype=torch.float32):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device (HIP) tensor; the engine has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+
+
+# ------------------------------------------------------------------------------------------------
+# Workspace (grown on demand, reused; allocate before any graph capture)
+# ------------------------------------------------------------------------------------------------
+class _Workspace:
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
+        cur = self.buf.get((key, device, dtype))
+        if cur is None or cur.numel() < n:
+            cur = torch.empty(max(n, 1), device=device, dtype=dtype)
+            self.buf[(key, device, dtype)] = cur
+        return cur
+
+
+WS = _Workspace()
+
+
+# ------------------------------------------------------------------------------------------------
+# GEMM
+# ------------------------------------------------------------------------------------------------
+def _as3(t: torch.Tensor):
+    if t.dim() == 2:
+        return 1, 0, t.stride(0), t.stride(1), t.size(0), t.size(1)
+    if t.dim() == 3:
+        return t.size(0), t.stride(0), t.stride(1), t.stride(2), t.size(1), t.size(2)
+    raise ValueError("gemm operands must be 2-D or 3-D (batched) views")
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
+         bias: Optional[torch.Tensor] = None, rowscale: Optional[torch.Tensor] = None,
+         bias2: Optional[torch.Tensor] = None, relu: bool = False, mask: Optional[torch.Tensor] = None,
+         split_k: Optional[int] = None) -> torch.Tensor:
+    """C = act(alpha * A @ B + beta * C + bias + rowscale[:,None] * bias2) [* (mask > 0)].
+
+    A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D);
+    bias/bias2 [.., N], rowscale [.., M] (strided views too)."""
+    ba, sab, sam, sak, M, K = _as3(A)
+    bb, sbb, sbk, sbn, K2, N = _as3(B)
+    bc, scb, scm, scn, M2, N2 = _as3(C)
+    batch = max(ba, bb, bc)
+    if K2 != K or M2 != M or N2 != N or bc != batch or ba not in (1, batch) or bb not in (1, batch):
+        raise ValueError(f"gemm shape mismatch: A{tuple(A.shape)} B{tuple(B.shape)} C{tuple(C.shape)}")
+    a = GemmArgs()
+    a.M, a.N, a.K, a.batch = M, N, K, batch
+    a.A, a.sam, a.sak, a.sab = A.data_ptr(), sam, sak, (sab if ba > 1 else 0)
+    a.B, a.sbk, a.sbn, a.sbb = B.data_ptr(), sbk, sbn, (sbb if bb > 1 else 0)
+    a.C, a.scm, a.scn, a.scb = C.data_ptr(), scm, scn, (scb if bc > 1 else 0)
+    if bias is not None:
+        a.bias = bias.data_ptr()
+        a.sbias_b = bias.stride(0) if bias.dim() == 2 else 0
+    if rowscale is not None:
+        if bias2 is None:
+            raise ValueError("rowscale needs bias2")
+        a.rowscale = rowscale.data_ptr()
+        a.srs_m = rowscale.stride(-1)
+        a.srs_b = rowscale.stride(0) if rowscale.dim() == 2 else 0
+        a.bias2 = bias2.data_ptr()
+        a.sb2_b = bias2.stride(0) if bias2.dim() == 2 else 0
+    if mask is not None:
+        a.mask, a.smk_m, a.smk_n = mask.data_ptr(), mask.stride(0), mask.stride(1)
+    a.alpha, a.beta, a.relu = float(alpha), float(beta), int(bool(relu))
+    if split_k is None:
+        split_k = choose_split_k(M, N, K, batch)
+    a.split_k = int(split_k)
+    if split_k > 1:
+        need = split_k * batch * M * N
+        ws = WS.get("gemm", need, C.device)
+        a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
+    key = f"gemm_f32 M{M} N{N} K{K} b{batch}"
+    if profiling.active(key) or profiling.active("*gemm"):
+        nbytes = 4.0 * batch * (M * K + K * N + M * N * (2 if beta else 1))
+        profiling.launch(key, 2.0 * M * N * K * batch, nbytes,
+                         lambda: check(_lib.lib().alignn_gemm_f32(ctypes.byref(a), stream_ptr()), "alignn_gemm_f32"))
+    else:
+        check(_lib.lib().alignn_gemm_f32(ctypes.byref(a), stream_ptr()), "alignn_gemm_f32")
+    return C
+
+
+def choose_split_k(M: int, N: int, K: int, batch: int) -> int:
+    bm = 128 if M >= 128 else 64
+    bn = 128 if N >= 128 else 64
+    tiles = math.ceil(M / bm) * math.ceil(N / bn) * batch
+    if tiles >= _NUM_CUS or K < 1024:
+        return 1
+    split = min(math.ceil(2 * _NUM_CUS / tiles), max(1, K // 512))
+    return max(1, split)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
+           relu: bool = False) -> torch.Tensor:
+    """out = x @ w.T + b (nn.Linear)."""
+    if out is None:
+        out = torch.empty(x.size(0), w.size(0), device=x.device, dtype=x.dtype)
+    return gemm(x, w.t(), out, bias=b, relu=relu)
+
+
+def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    M, N = X.shape
+    ws = WS.get("colsum", 256 * N, X.device)
+    check(_lib.lib().alignn_colsum_f32(X.data_ptr(), M, N, X.stride(0), out.data_ptr(), int(accumulate),
+                                       ws.data_ptr(), stream_ptr()), "alignn_colsum_f32")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Graph preparation
+# ------------------------------------------------------------------------------------------------
+class GraphCSR:
+    """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
+
+    __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err")
+
+    def __init__(self, edge_index: torch.Tensor, n: int):
+        if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
+            raise ValueError("edge_index must be int64 [2, m]")
+        ei = edge_index.contiguous()
+        dev = ei.device
+        m = ei.size(1)
+        self.n, self.m = n, m
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.off_dst = torch.empty(n + 1, **i32)
+        self.perm_dst = torch.empty(max(m, 1), **i32)
+        self.src_at = torch.empty(max(m, 1), **i32)
+        self.dst_at = torch.empty(max(m, 1), **i32)
+        self.off_src = torch.empty(n + 1, **i32)
+        self.pos_src = torch.empty(max(m, 1), **i32)
+        self.err = torch.zeros(1, **i32)
+        ws = WS.get("graph", 2 * n + 64, dev, torch.int32)
+        check(_lib.lib().alignn_graph_prep(ei.data_ptr(), m, n, self.off_dst.data_ptr(), self.perm_dst.data_ptr(),
+                                           self.src_at.data_ptr(), self.dst_at.data_ptr(), self.off_src.data_ptr(),
+                                           self.pos_src.data_ptr(), ws.data_ptr(), self.err.data_ptr(),
+                                           stream_ptr()), "alignn_graph_prep")
+
+    def check_indices(self, what: str) -> None:
+        """Host check of the device error flag (one sync).  PyG raises IndexError here."""
+        if int(self.err.item()) != 0:
+            raise IndexError(f"{what}: edge index out of range [0, {self.n})")
+
+
+def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    rows = idx.numel()
+    cols = src.size(1)
+    if out is None:
+        out = torch.empty(rows, cols, device=src.device, dtype=src.dtype)
+    check(_lib.lib().alignn_gather_rows_f32(src.data_ptr(), src.stride(0), idx.data_ptr(), rows, cols,
+                                            out.data_ptr(), out.stride(0), stream_ptr()), "alignn_gather_rows_f32")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# TransformerConv attention
+# ------------------------------------------------------------------------------------------------
+def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str) -> float:
+    """Compulsory HBM bytes of one launch (every operand touched once, ideal caching)."""
+    f = 4.0
+    if kind == "fwd":   # Q,K,V + U + F rows + CSR in; aggV + S + 3 stats out
+        return f * (3 * n * D + n * H * D + m * D + 2 * m + n + n * D + n * H * D + 3 * n * H)
+    if kind == "bwd_dst":  # Q,K,V,U,Vd,dout,outp,F,stats in; dQ,Sz,sigz,dz,alpha,dF out
+        return f * (3 * n * D + 2 * n * H * D + 2 * n * D + m * D + 2 * n * H + 2 * m + n
+                    + n * D + n * H * D + n * H + 2 * m * H + m * D)
+    return f * (2 * n * D + 2 * m * H + 2 * m + n + 2 * n * D)  # bwd_src
+
+
+def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, wbar: Optional[torch.Tensor],
+              F: torch.Tensor, feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float, seed: int):
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd"), lambda: check(_lib.lib().alignn_tconv_fwd(g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
+                                      QKVR.data_ptr(), QKVR.stride(0), U.data_ptr(), _p(wbar), F.data_ptr(),
+                                      F.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(),
+                                      den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+          "alignn_tconv_fwd"))
+
+
+def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, dout, outp, mstat, den,
+                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: bool, drop_p: float, seed: int):
+    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_dst"), lambda: check(_lib.lib().alignn_tconv_bwd_dst(
+        g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row), QKVR.data_ptr(), QKVR.stride(0),
+        U.data_ptr(), Vd.data_ptr(), _p(wbar), F.data_ptr(), F.stride(0), dout.data_ptr(), outp.data_ptr(),
+        mstat.data_ptr(), den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
+        dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF), 0 if dF is None else dF.stride(0), int(accumulate_dF),
+        float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_bwd_dst"))
+
+
+def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):
+    profiling.launch(f"tconv_bwd_src n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_src"), lambda: check(_lib.lib().alignn_tconv_bwd_src(g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(),
+                                          g.dst_at.data_ptr(), QKVR.data_ptr(), QKVR.stride(0), dout.data_ptr(),
+                                          dz_e.data_ptr(), alpha_e.data_ptr(), dKV.data_ptr(), dKV.stride(0),
+                                          stream_ptr()), "alignn_tconv_bwd_src"))
+
+
+# ------------------------------------------------------------------------------------------------
+# Row ops
+# ------------------------------------------------------------------------------------------------
+def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed):
+    n, D = outp.shape
+    check(_lib.lib().alignn_gate_ln_fwd(n, D, outp.data_ptr(), R.data_ptr(), R.stride(0), wbeta.data_ptr(),
+                                        X.data_ptr(), X.stride(0), ln_w.data_ptr(), ln_b.data_ptr(), Xnew.data_ptr(),
+                                        Xnew.stride(0), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),
+                                        float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_gate_ln_fwd")
+
+
+def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_wbeta, d_ln_w, d_ln_b, drop_p, seed):
+    n, D = outp.shape
+    ws = WS.get("gate_ln", 1024 * 5 * D, outp.device)
+    check(_lib.lib().alignn_gate_ln_bwd(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), R.data_ptr(),
+                                        R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+                                        beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(), dout.data_ptr(),
+                                        dR.data_ptr(), dR.stride(0), d_wbeta.data_ptr(), d_ln_w.data_ptr(),
+                                        d_ln_b.data_ptr(), ws.data_ptr(), float(drop_p), int(seed) & (2**64 - 1),
+                                        stream_ptr()), "alignn_gate_ln_bwd")
+
+
+def readout_feats_fwd(h, ptr, global_x, gdim, sg, sgdim, feats, drop_p, seed):
+    B = ptr.numel() - 1
+    D = h.size(1)
+    check(_lib.lib().alignn_readout_feats_fwd(B, D, h.data_ptr(), ptr.data_ptr(), global_x.data_ptr(), gdim,
+                                              sg.data_ptr(), sgdim, feats.data_ptr(), float(drop_p),
+                                              int(seed) & (2**64 - 1), stream_ptr()), "alignn_readout_feats_fwd")
+
+
+def readout_pool_bwd(dfeats, ptr, batch, dh, accumulate, drop_p, seed):
+    B = ptr.numel() - 1
+    N, D = dh.shape
+    check(_lib.lib().alignn_readout_pool_bwd(B, N, D, dfeats.data_ptr(), dfeats.stride(0), ptr.data_ptr(),
+                                             batch.data_ptr(), dh.data_ptr(), int(accumulate), float(drop_p),
+                                             int(seed) & (2**64 - 1), stream_ptr()), "alignn_readout_pool_bwd")
+
+
+def dropout(x, y, relu_ref=None, drop_p=0.0, seed=0):
+    rows, cols = x.shape
+    check(_lib.lib().alignn_dropout_f32(rows, cols, x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0),
+                                        _p(relu_ref), 0 if relu_ref is None else relu_ref.stride(0), float(drop_p),
+                                        int(seed) & (2**64 - 1), stream_ptr()), "alignn_dropout_f32")
+    return y
+
+
+def hetero_nll(heads, y, log_means, log_stds, floor, l2, loss, dheads):
+    B = heads.size(0)
+    T = heads.size(1) // 2
+    check(_lib.lib().alignn_hetero_nll(B, T, heads.data_ptr(), heads.stride(0), y.data_ptr(), log_means.data_ptr(),
+                                       log_stds.data_ptr(), float(floor), float(l2), loss.data_ptr(),
+                                       dheads.data_ptr(), dheads.stride(0), stream_ptr()), "alignn_hetero_nll")
+
+
+def add_noise(x: torch.Tensor, std: float, seed: int):
+    check(_lib.lib().alignn_add_noise_f32(x.numel(), x.data_ptr(), float(std), int(seed) & (2**64 - 1),
+                                          stream_ptr()), "alignn_add_noise_f32")

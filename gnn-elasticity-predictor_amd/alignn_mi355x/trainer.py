@@ -1,0 +1,79 @@
+"""Fused training step — the per-batch body of ``train_epoch_hetero`` (``scripts/train.py:639-699``).
+
+Per step: feature jitter (train.py:641-646) -> forward (train.py:655) -> hetero NLL + log-sigma L2
+(train.py:656-681) -> backward -> ``clip_grad_norm_(5.0)`` -> AdamW with the reference's two
+parameter groups (train.py:1516-1542).  Forward, loss and backward run in libalignn_hip without
+autograd; parameters and gradients live in one flat buffer each, so clip + AdamW touch two
+contiguous segments (base + mean heads | logvar heads).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+from torch import nn
+
+from . import ops
+from .engine import MIN_LOGVAR_FLOOR, batch_cache, site_seed
+from .model import HeteroAlignnRegressor
+from .synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS
+
+
+class FusedTrainer:
+    def __init__(self, model: HeteroAlignnRegressor, lr: float = 3e-4, weight_decay: float = 1e-4,
+                 sigma_lr: Optional[float] = 3e-4, max_norm: float = 5.0, log_sigma_l2: float = 0.1,
+                 feature_jitter_std: float = 0.1, min_logvar_floor: float = MIN_LOGVAR_FLOOR,
+                 target_log_means: Sequence[float] = TARGET_LOG_MEANS,
+                 target_log_stds: Sequence[float] = TARGET_LOG_STDS, fused_adamw: bool = True):
+        self.model = model
+        st = model._ensure_flat()
+        self.st = st
+        s0 = st.P.sigma_start
+        # two contiguous segments == the reference's two param groups
+        self.p_base = nn.Parameter(st.flat[:s0])
+        self.p_sigma = nn.Parameter(st.flat[s0:])
+        self.p_base.grad = st.grad[:s0]
+        self.p_sigma.grad = st.grad[s0:]
+        sigma_lr = lr if not sigma_lr else sigma_lr  # train.py:1521-1522 (0 disables the cap)
+        kw = {"fused": True} if (fused_adamw and st.flat.is_cuda) else {}
+        self.opt = torch.optim.AdamW([{"params": [self.p_base], "lr": lr}, {"params": [self.p_sigma], "lr": sigma_lr}],
+                                     lr=lr, weight_decay=weight_decay, **kw)
+        self.max_norm = max_norm
+        self.l2 = log_sigma_l2
+        self.jitter = feature_jitter_std
+        self.floor = min_logvar_floor
+        dev = st.flat.device
+        self.log_means = torch.tensor(list(target_log_means), dtype=torch.float32, device=dev)
+        self.log_stds = torch.tensor(list(target_log_stds), dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, device=dev)
+        self.step_count = 0
+
+    def set_lr(self, lr: float, sigma_lr: Optional[float] = None) -> None:
+        self.opt.param_groups[0]["lr"] = lr
+        self.opt.param_groups[1]["lr"] = lr if sigma_lr is None else sigma_lr
+
+    def forward_backward(self, batch, seed: int, training: bool = True) -> torch.Tensor:
+        """Forward + loss + backward into the flat gradient buffer; returns the loss (device)."""
+        model, st = self.model, self.st
+        bc = batch_cache(batch)
+        x, gx = batch.x, batch.global_x
+        if training and self.jitter > 0.0:
+            x = x.clone()
+            gx = gx.clone()
+            ops.add_noise(x, self.jitter, site_seed(seed, 1 << 20))
+            ops.add_noise(gx, self.jitter, site_seed(seed, (1 << 20) + 1))
+        out, ctx = model._engine.forward(st.P, batch, bc, training, seed, x, gx, "hetero")
+        dout = torch.empty_like(out)
+        ops.hetero_nll(out, batch.y.contiguous().float(), self.log_means, self.log_stds, self.floor, self.l2,
+                       self.loss, dout)
+        model._engine.backward(st.P, st.G, ctx, dout)
+        return self.loss
+
+    def step(self, batch, seed: Optional[int] = None) -> torch.Tensor:
+        if seed is None:
+            seed = int(torch.randint(0, 2**62, (1,)).item())
+        loss = self.forward_backward(batch, seed)
+        torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
+        self.opt.step()
+        self.step_count += 1
+        return loss

@@ -1,0 +1,78 @@
+// common.h — shared device helpers for libalignn_hip (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/alignn_hip.h"
+
+#define ALIGNN_WAVE 64
+
+namespace alignn {
+
+// ---------------------------------------------------------------------------------------------
+// Error handling (no exceptions cross the ABI)
+// ---------------------------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+int hip_status(hipError_t e, const char* what);
+
+#define ALIGNN_LAUNCH_CHECK(what)                                 \
+  do {                                                            \
+    hipError_t _e = hipGetLastError();                            \
+    if (_e != hipSuccess) return ::alignn::hip_status(_e, what);  \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// Wave-level reductions (64 lanes).  __shfl_xor lowers to DPP/ds_swizzle/bpermute as the
+// compiler sees fit; the 32-lane stage crosses the two halves.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// Sum within aligned groups of `width` lanes (width power of two <= 64).
+__device__ __forceinline__ float group_sum(float v, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Counter-based random numbers (dropout masks / jitter).  Each call site gets its own 64-bit
+// seed from the host; the element counter makes the mask reproducible in the backward pass.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t x = seed ^ (idx * 0x9E3779B97F4A7C15ULL);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)(x >> 32);
+}
+// keep-probability (1-p) Bernoulli, returns the dropout multiplier (0 or 1/(1-p)).
+__device__ __forceinline__ float dropout_mul(uint64_t seed, uint64_t idx, uint32_t thresh, float inv_keep) {
+  return hash_u32(seed, idx) >= thresh ? inv_keep : 0.0f;
+}
+
+struct DropParams {
+  uint64_t seed;
+  uint32_t thresh;   // p * 2^32
+  float inv_keep;    // 1/(1-p)
+  int active;
+};
+inline DropParams make_drop(float p, uint64_t seed) {
+  DropParams d;
+  d.seed = seed;
+  d.active = p > 0.0f ? 1 : 0;
+  double t = (double)p * 4294967296.0;
+  d.thresh = p > 0.0f ? (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t) : 0u;
+  d.inv_keep = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
+  return d;
+}
+
+}  // namespace alignn

@@ -1,0 +1,354 @@
+// gemm.hip — fp32 GEMM on gfx950 MFMA (v_mfma_f32_32x32x2_f32: exact f32 fma chain, 64 cyc/SIMD).
+//
+// Replaces the cuBLAS addmm/mm behind every nn.Linear / PyG Linear of the reference's hot path
+// (SURVEY §2 implicit-kernel table) and their autograd backward products.
+//
+// Tiling: BM x BN block (64 or 128 each), BK = 16, 256 threads = 4 waves in a 2x2 grid, each wave
+// owns (BM/2)x(BN/2) = MI x NI subtiles of 32x32.  One K-tile per iteration, double-buffered LDS
+// with register prefetch of the next tile (issue global loads before the MFMAs, write LDS after).
+//
+// k-slot assignment: an MFMA 32x32x2 sums over two k-slots, lane half h = lane>>5 supplying slot h.
+// Over the 8 MFMAs of a 16-deep K-tile, step s uses k = 8h + s for lane half h, so a lane's eight
+// k-values are contiguous: one pair of ds_read_b128 per subtile when the LDS image is [row][k],
+// eight ds_read_b32 when it is [k][row].  Both operands use the same assignment, so the sum over
+// k is complete (in a permuted order — still an exact per-product-rounded fp32 chain).
+//
+// LDS images follow global contiguity (no transposes while staging):
+//   operand contiguous along k   -> [row][BK+4]   (80-B rows: ds_read_b128 conflict-free)
+//   operand contiguous along row -> [BK][ROWS+4]
+#include "common.h"
+
+namespace alignn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 16;
+constexpr int KPAD = BK + 4;
+
+struct GemmParams {
+  int64_t M, N, K, batch;
+  const float* A; int64_t sam, sak, sab;
+  const float* B; int64_t sbk, sbn, sbb;
+  float* C; int64_t scm, scn, scb;
+  const float* bias; int64_t sbias_b;
+  const float* rowscale; int64_t srs_m, srs_b;
+  const float* bias2; int64_t sb2_b;
+  const float* mask; int64_t smk_m, smk_n;
+  float alpha, beta;
+  int relu;
+  int split_k;
+  int64_t kchunk;
+  float* ws;
+  int vecA, vecB;
+};
+
+// Loads one operand tile (ROWS x BK) into registers.  KC: load along k (general strides,
+// float4 when stride_k==1 and aligned); !KC: load along rows (stride_row == 1).
+template <int ROWS, bool KC>
+struct TileLoader {
+  static constexpr int F4 = ROWS * BK / 4 / 256;  // float4 per thread (1 or 2)
+  float4 r[F4];
+
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t srow, int64_t sk, int64_t row0,
+                                       int64_t rows, int64_t k0, int64_t kend, int vec) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      int idx = threadIdx.x + 256 * i;
+      int64_t gr, gk;
+      if (KC) {
+        gr = row0 + (idx >> 2);
+        gk = k0 + (idx & 3) * 4;
+      } else {
+        gk = k0 + (idx / (ROWS / 4));
+        gr = row0 + (idx % (ROWS / 4)) * 4;
+      }
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (KC) {
+        if (gr < rows) {
+          if (vec && gk + 3 < kend) {
+            float4 t = *reinterpret_cast<const float4*>(P + gr * srow + gk);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (gk + j < kend) v[j] = P[gr * srow + (gk + j) * sk];
+          }
+        }
+      } else {
+        if (gk < kend) {
+          if (vec && gr + 3 < rows) {
+            float4 t = *reinterpret_cast<const float4*>(P + gk * sk + gr);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (gr + j < rows) v[j] = P[gk * sk + gr + j];
+          }
+        }
+      }
+      r[i] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+
+  __device__ __forceinline__ void store(float* __restrict__ lds) const {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      int idx = threadIdx.x + 256 * i;
+      if (KC) {
+        int rr = idx >> 2, kk = (idx & 3) * 4;
+        *reinterpret_cast<float4*>(lds + rr * KPAD + kk) = r[i];
+      } else {
+        int kk = idx / (ROWS / 4), rr = (idx % (ROWS / 4)) * 4;
+        *reinterpret_cast<float4*>(lds + kk * (ROWS + 4) + rr) = r[i];
+      }
+    }
+  }
+};
+
+template <int ROWS, bool KC>
+constexpr int lds_floats() {
+  return KC ? ROWS * KPAD : BK * (ROWS + 4);
+}
+
+// Reads the 8 k-values of lane half h for subtile row `row` (0..ROWS-1).
+template <int ROWS, bool KC>
+__device__ __forceinline__ void read_frag(const float* __restrict__ lds, int row, int h, float (&f)[8]) {
+  if (KC) {
+    float4 a = *reinterpret_cast<const float4*>(lds + row * KPAD + 8 * h);
+    float4 b = *reinterpret_cast<const float4*>(lds + row * KPAD + 8 * h + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) f[s] = lds[(8 * h + s) * (ROWS + 4) + row];
+  }
+}
+
+__device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, int64_t row, int64_t col, float acc) {
+  float v = p.alpha * acc;
+  float* Cb = p.C + b * p.scb;
+  if (p.beta != 0.f) v += p.beta * Cb[row * p.scm + col * p.scn];
+  if (p.bias) v += p.bias[b * p.sbias_b + col];
+  if (p.rowscale) v += p.rowscale[b * p.srs_b + row * p.srs_m] * p.bias2[b * p.sb2_b + col];
+  if (p.relu) v = fmaxf(v, 0.f);
+  if (p.mask) v = p.mask[row * p.smk_m + col * p.smk_n] > 0.f ? v : 0.f;
+  return v;
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
+  constexpr int MI = BM / 64, NI = BN / 64;
+  constexpr int LA = lds_floats<BM, A_KC>(), LB = lds_floats<BN, B_KC>();
+  __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
+
+  const int64_t tiles_n = (p.N + BN - 1) / BN;
+  const int64_t tile = blockIdx.x;
+  const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int64_t b = blockIdx.z / p.split_k;
+  const int sidx = blockIdx.z % p.split_k;
+  const int64_t kb = (int64_t)sidx * p.kchunk;
+  const int64_t ke = min(p.K, kb + p.kchunk);
+
+  const float* A = p.A + b * p.sab;
+  const float* B = p.B + b * p.sbb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  TileLoader<BM, A_KC> la;
+  TileLoader<BN, B_KC> lb;
+  // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
+  la.load(A, p.sam, p.sak, m0, p.M, kb, ke, p.vecA);
+  lb.load(B, p.sbn, p.sbk, n0, p.N, kb, ke, p.vecB);
+  la.store(smem);
+  lb.store(smem + LA);
+  __syncthreads();
+
+  int cur = 0;
+  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) {
+      la.load(A, p.sam, p.sak, m0, p.M, k0 + BK, ke, p.vecA);
+      lb.load(B, p.sbn, p.sbk, n0, p.N, k0 + BK, ke, p.vecB);
+    }
+    const float* As = smem + cur * (LA + LB);
+    const float* Bs = As + LA;
+    float fa[MI][8], fb[NI][8];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) read_frag<BM, A_KC>(As, wm * (BM / 2) + i * 32 + l32, h, fa[i]);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) read_frag<BN, B_KC>(Bs, wn * (BN / 2) + j * 32 + l32, h, fb[j]);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+    if (more) {
+      float* nxt = smem + (cur ^ 1) * (LA + LB);
+      la.store(nxt);
+      lb.store(nxt + LA);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // Epilogue. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int64_t col = n0 + wn * (BN / 2) + j * 32 + l32;
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        if (p.split_k > 1) {
+          p.ws[(((int64_t)sidx * p.batch + b) * p.M + row) * p.N + col] = acc[i][j][r];
+        } else {
+          p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
+        }
+      }
+    }
+}
+
+__global__ void splitk_reduce_kernel(GemmParams p) {
+  const int64_t total = p.batch * p.M * p.N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t col = i % p.N;
+    const int64_t row = (i / p.N) % p.M;
+    const int64_t b = i / (p.N * p.M);
+    float s = 0.f;
+    for (int k = 0; k < p.split_k; ++k) s += p.ws[(((int64_t)k * p.batch + b) * p.M + row) * p.N + col];
+    p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, s);
+  }
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC>
+static void launch(const GemmParams& p, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC>), grid, dim3(256), 0, s, p);
+}
+
+template <int BM, int BN>
+static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, hipStream_t s) {
+  if (akc && bkc) launch<BM, BN, true, true>(p, grid, s);
+  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, s);
+  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, s);
+  else launch<BM, BN, false, false>(p, grid, s);
+}
+
+static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+}  // namespace alignn
+
+using namespace alignn;
+
+extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
+  if (!a || a->M < 0 || a->N < 0 || a->K < 0 || a->batch < 1) {
+    set_error("gemm: bad shape");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (a->M == 0 || a->N == 0) return ALIGNN_OK;
+  if (a->rowscale && !a->bias2) {
+    set_error("gemm: rowscale without bias2");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GemmParams p;
+  p.M = a->M; p.N = a->N; p.K = a->K; p.batch = a->batch;
+  p.A = a->A; p.sam = a->sam; p.sak = a->sak; p.sab = a->sab;
+  p.B = a->B; p.sbk = a->sbk; p.sbn = a->sbn; p.sbb = a->sbb;
+  p.C = a->C; p.scm = a->scm; p.scn = a->scn; p.scb = a->scb;
+  p.bias = a->bias; p.sbias_b = a->sbias_b;
+  p.rowscale = a->rowscale; p.srs_m = a->srs_m; p.srs_b = a->srs_b;
+  p.bias2 = a->bias2; p.sb2_b = a->sb2_b;
+  p.mask = a->mask; p.smk_m = a->smk_m; p.smk_n = a->smk_n;
+  p.alpha = a->alpha; p.beta = a->beta; p.relu = a->relu;
+  int split = a->split_k < 1 ? 1 : a->split_k;
+  if (a->K == 0) split = 1;
+  // A is "k-contiguous" unless it is contiguous along m only.
+  const bool akc = !(a->sam == 1 && a->sak != 1);
+  const bool bkc = !(a->sbn == 1 && a->sbk != 1);
+  p.vecA = akc ? (a->sak == 1 && a->sam % 4 == 0 && a->sab % 4 == 0 && aligned16(a->A))
+               : (a->sak % 4 == 0 && a->sab % 4 == 0 && aligned16(a->A));
+  p.vecB = bkc ? (a->sbk == 1 && a->sbn % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B))
+               : (a->sbk % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B));
+  int64_t kchunk = (a->K + split - 1) / split;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  if (kchunk == 0) kchunk = BK;
+  split = (int)((a->K + kchunk - 1) / kchunk);
+  if (split < 1) split = 1;
+  p.kchunk = kchunk;
+  p.split_k = split;
+  p.ws = a->workspace;
+  if (split > 1 && (!a->workspace || a->workspace_elems < (int64_t)split * a->batch * a->M * a->N)) {
+    set_error("gemm: split_k=%d needs %lld workspace floats", split, (long long)split * a->batch * a->M * a->N);
+    return ALIGNN_E_WORKSPACE;
+  }
+  // Tile choice: 128x128 for large problems, 64-wide on a small dimension.
+  const int bm = a->M >= 128 ? 128 : 64;
+  const int bn = a->N >= 128 ? 128 : 64;
+  const int64_t tiles = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
+  dim3 grid((unsigned)tiles, 1, (unsigned)(a->batch * split));
+  if (bm == 128 && bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, s);
+  else if (bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, s);
+  else if (bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, s);
+  else dispatch_layout<64, 64>(p, akc, bkc, grid, s);
+  ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
+  if (split > 1) {
+    int64_t total = a->batch * a->M * a->N;
+    int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
+    ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");
+  }
+  return ALIGNN_OK;
+}
+
+// -------------------------------------------------------------------------------------------
+// Column sums (bias gradients): stage 1 — each of up to 256 blocks sums a contiguous row range
+// for a 256-column strip; stage 2 — fixed-order sum over the row-range partials.
+// -------------------------------------------------------------------------------------------
+namespace alignn {
+__global__ void colsum_stage1(const float* __restrict__ X, int64_t M, int64_t N, int64_t ldx, int64_t rows_per,
+                              float* __restrict__ part) {
+  const int64_t col = blockIdx.y * 256 + threadIdx.x;
+  const int64_t r0 = blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  if (col >= N) return;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += X[r * ldx + col];
+  part[blockIdx.x * N + col] = s;
+}
+__global__ void colsum_stage2(const float* __restrict__ part, int nparts, int64_t N, float* __restrict__ out, int acc) {
+  const int64_t col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
+  float s = 0.f;
+  for (int i = 0; i < nparts; ++i) s += part[i * N + col];
+  out[col] = acc ? out[col] + s : s;
+}
+}  // namespace alignn
+
+extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
+                                 float* workspace, void* stream) {
+  if (M < 0 || N < 0) return ALIGNN_E_BAD_SHAPE;
+  if (N == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int nparts = (int)std::min<int64_t>(256, std::max<int64_t>(1, (M + 63) / 64));
+  int64_t rows_per = (M + nparts - 1) / nparts;
+  if (rows_per == 0) rows_per = 1;
+  dim3 g1(nparts, (unsigned)((N + 255) / 256));
+  hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
+  ALIGNN_LAUNCH_CHECK("colsum_stage1");
+  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, workspace, nparts, N, out,
+                     accumulate);
+  ALIGNN_LAUNCH_CHECK("colsum_stage2");
+  return ALIGNN_OK;
+}

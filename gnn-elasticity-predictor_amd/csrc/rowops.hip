@@ -1,0 +1,420 @@
+// rowops.hip — row-wise fused kernels: TransformerConv beta gate + LayerNorm + ReLU + dropout +
+// residual (forward/backward), readout pooling/concat, dropout, hetero-Gaussian NLL, jitter.
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+#include "vec.h"
+
+namespace alignn {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int hip_status(hipError_t e, const char* what) {
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return ALIGNN_E_HIP;
+}
+
+static int grid_for(int64_t work, int block = 256, int64_t cap = 8192) {
+  int64_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Gate + LayerNorm + ReLU + dropout + residual.  One wave per row, VPL features per lane.
+//   PyG TransformerConv (beta=True):  beta = sigmoid(lin_beta([o, r, o - r])); y = beta r + (1-beta) o
+//   train.py:316-317 / :335-336:      x_new = x + dropout(relu(LayerNorm(y)))   (eps 1e-5)
+// ---------------------------------------------------------------------------------------------
+struct GateFwdParams {
+  int64_t n;
+  int D;
+  const float* outp; const float* R; int64_t ldr;
+  const float* wbeta;
+  const float* X; int64_t ldx;
+  const float* lnw; const float* lnb;
+  float* Xn; int64_t ldxn;
+  float* beta; float* mu; float* rstd;
+  DropParams drop;
+};
+
+template <int VPL>
+__global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.n) return;
+  const int D = p.D, j0 = lane * VPL;
+  const bool act = j0 < D;
+  float o[VPL], r[VPL], w1[VPL], w2[VPL], w3[VPL];
+  vzero(o); vzero(r); vzero(w1); vzero(w2); vzero(w3);
+  if (act) {
+    vload(p.outp + row * D + j0, o);
+    vload(p.R + row * p.ldr + j0, r);
+    vload(p.wbeta + j0, w1);
+    vload(p.wbeta + D + j0, w2);
+    vload(p.wbeta + 2 * D + j0, w3);
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) part += o[i] * w1[i] + r[i] * w2[i] + (o[i] - r[i]) * w3[i];
+  const float logit = wave_sum(part);
+  const float b = 1.0f / (1.0f + __expf(-logit));
+  float y[VPL];
+  float sy = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    y[i] = b * r[i] + (1.0f - b) * o[i];
+    sy += y[i];
+  }
+  const float mean = wave_sum(sy) / (float)D;
+  float sv = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const float c = act ? (y[i] - mean) : 0.f;
+    sv += c * c;
+  }
+  const float var = wave_sum(sv) / (float)D;
+  const float rs = 1.0f / sqrtf(var + 1e-5f);
+  if (act) {
+    float g[VPL], bb[VPL], x[VPL], out[VPL];
+    vload(p.lnw + j0, g);
+    vload(p.lnb + j0, bb);
+    vload(p.X + row * p.ldx + j0, x);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float a = fmaxf((y[i] - mean) * rs * g[i] + bb[i], 0.f);
+      if (p.drop.active) a *= dropout_mul(p.drop.seed, (uint64_t)row * D + j0 + i, p.drop.thresh, p.drop.inv_keep);
+      out[i] = x[i] + a;
+    }
+    vstore(p.Xn + row * p.ldxn + j0, out);
+  }
+  if (lane == 0) {
+    p.beta[row] = b;
+    p.mu[row] = mean;
+    p.rstd[row] = rs;
+  }
+}
+
+struct GateBwdParams {
+  int64_t n;
+  int D;
+  const float* dXn; int64_t lddx;
+  const float* outp; const float* R; int64_t ldr;
+  const float* wbeta; const float* lnw; const float* lnb;
+  const float* beta; const float* mu; const float* rstd;
+  float* dout; float* dR; int64_t lddr;
+  float* part;  // [nwaves][5*D]
+  int nwaves;
+  DropParams drop;
+};
+
+template <int VPL>
+__global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int D = p.D, j0 = lane * VPL;
+  const bool act = j0 < D;
+  float w1[VPL], w2[VPL], w3[VPL], g[VPL], bb[VPL];
+  vzero(w1); vzero(w2); vzero(w3); vzero(g); vzero(bb);
+  if (act) {
+    vload(p.wbeta + j0, w1);
+    vload(p.wbeta + D + j0, w2);
+    vload(p.wbeta + 2 * D + j0, w3);
+    vload(p.lnw + j0, g);
+    vload(p.lnb + j0, bb);
+  }
+  float a_g[VPL], a_b[VPL], a_w1[VPL], a_w2[VPL], a_w3[VPL];
+  vzero(a_g); vzero(a_b); vzero(a_w1); vzero(a_w2); vzero(a_w3);
+  for (int64_t row = wid; row < p.n; row += p.nwaves) {
+    float o[VPL], r[VPL], gx[VPL];
+    vzero(o); vzero(r); vzero(gx);
+    if (act) {
+      vload(p.outp + row * D + j0, o);
+      vload(p.R + row * p.ldr + j0, r);
+      vload(p.dXn + row * p.lddx + j0, gx);
+    }
+    const float b = p.beta[row], mean = p.mu[row], rs = p.rstd[row];
+    float yh[VPL], gyh[VPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const float y = b * r[i] + (1.0f - b) * o[i];
+      yh[i] = act ? (y - mean) * rs : 0.f;
+      const float ln = yh[i] * g[i] + bb[i];
+      float ga = gx[i];
+      if (p.drop.active && act)
+        ga *= dropout_mul(p.drop.seed, (uint64_t)row * D + j0 + i, p.drop.thresh, p.drop.inv_keep);
+      const float gl = (act && ln > 0.f) ? ga : 0.f;
+      a_g[i] = fmaf(gl, yh[i], a_g[i]);
+      a_b[i] += gl;
+      gyh[i] = gl * g[i];
+      s1 += gyh[i];
+      s2 += gyh[i] * yh[i];
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+    float dy[VPL];
+    float sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      dy[i] = act ? rs * (gyh[i] - m1 - yh[i] * m2) : 0.f;
+      sb += dy[i] * (r[i] - o[i]);
+    }
+    const float dbeta = wave_sum(sb);
+    const float dl = dbeta * b * (1.0f - b);
+    if (act) {
+      float dov[VPL], drv[VPL];
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        dov[i] = (1.0f - b) * dy[i] + dl * (w1[i] + w3[i]);
+        drv[i] = b * dy[i] + dl * (w2[i] - w3[i]);
+        a_w1[i] = fmaf(dl, o[i], a_w1[i]);
+        a_w2[i] = fmaf(dl, r[i], a_w2[i]);
+        a_w3[i] = fmaf(dl, o[i] - r[i], a_w3[i]);
+      }
+      vstore(p.dout + row * D + j0, dov);
+      vstore(p.dR + row * p.lddr + j0, drv);
+    }
+  }
+  if (act && wid < p.nwaves) {
+    float* base = p.part + (int64_t)wid * 5 * D;
+    vstore(base + j0, a_w1);
+    vstore(base + D + j0, a_w2);
+    vstore(base + 2 * D + j0, a_w3);
+    vstore(base + 3 * D + j0, a_g);
+    vstore(base + 4 * D + j0, a_b);
+  }
+}
+
+// out[c] += sum_w part[w][c] for c < 5D, mapped to (d_wbeta[0..3D), d_lnw, d_lnb).
+__global__ void gate_ln_reduce_kernel(const float* __restrict__ part, int nwaves, int D, float* __restrict__ dwb,
+                                      float* __restrict__ dlnw, float* __restrict__ dlnb) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 5 * D) return;
+  float s = 0.f;
+  for (int w = 0; w < nwaves; ++w) s += part[(int64_t)w * 5 * D + c];
+  if (c < 3 * D) dwb[c] += s;
+  else if (c < 4 * D) dlnw[c - 3 * D] += s;
+  else dlnb[c - 4 * D] += s;
+}
+
+static int vpl_for(int D) {
+  if (D <= 64) return 1;
+  if (D == 128) return 2;
+  if (D == 256) return 4;
+  if (D == 512) return 8;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Readout (train.py:562-573): feats[b] = dropout([mean_{i in graph b} h_i, global_x_b, sg_b])
+// ---------------------------------------------------------------------------------------------
+__global__ void readout_fwd_kernel(int64_t B, int D, const float* __restrict__ h, const int64_t* __restrict__ ptr,
+                                   const float* __restrict__ gx, int gdim, const float* __restrict__ sg, int sgdim,
+                                   float* __restrict__ feats, DropParams drop) {
+  const int64_t b = blockIdx.x;
+  const int W = D + gdim + sgdim;
+  const int64_t s = ptr[b], e = ptr[b + 1];
+  const float inv = 1.0f / (float)max((int64_t)1, e - s);
+  for (int c = threadIdx.x; c < W; c += blockDim.x) {
+    float v;
+    if (c < D) {
+      float acc = 0.f;
+      for (int64_t i = s; i < e; ++i) acc += h[i * D + c];
+      v = acc * inv;
+    } else if (c < D + gdim) {
+      v = gx[b * gdim + (c - D)];
+    } else {
+      v = sg[b * sgdim + (c - D - gdim)];
+    }
+    if (drop.active) v *= dropout_mul(drop.seed, (uint64_t)b * W + c, drop.thresh, drop.inv_keep);
+    feats[b * W + c] = v;
+  }
+}
+
+__global__ void pool_bwd_kernel(int64_t N, int D, const float* __restrict__ dfeats, int64_t ldf,
+                                const int64_t* __restrict__ ptr, const int64_t* __restrict__ batch,
+                                float* __restrict__ dh, int acc, DropParams drop) {
+  const int64_t total = N * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t node = i / D;
+    const int c = (int)(i % D);
+    const int64_t b = batch[node];
+    const float cnt = (float)max((int64_t)1, ptr[b + 1] - ptr[b]);
+    float v = dfeats[b * ldf + c] / cnt;
+    if (drop.active) v *= dropout_mul(drop.seed, (uint64_t)b * ldf + c, drop.thresh, drop.inv_keep);
+    dh[i] = acc ? dh[i] + v : v;
+  }
+}
+
+__global__ void dropout_kernel(int64_t rows, int64_t cols, const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
+                               int64_t ldy, const float* __restrict__ ref, int64_t ldr, DropParams drop) {
+  const int64_t total = rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols, c = i % cols;
+    float v = x[r * ldx + c];
+    if (drop.active) v *= dropout_mul(drop.seed, (uint64_t)i, drop.thresh, drop.inv_keep);
+    if (ref) v = ref[r * ldr + c] > 0.f ? v : 0.f;
+    y[r * ldy + c] = v;
+  }
+}
+
+// Hetero NLL forward+gradient, single block (B*T is small).
+__global__ __launch_bounds__(256) void hetero_nll_kernel(int64_t B, int T, const float* __restrict__ heads, int64_t ldh,
+                                                         const float* __restrict__ y, const float* __restrict__ lm,
+                                                         const float* __restrict__ ls, float floor, float l2,
+                                                         float* __restrict__ loss, float* __restrict__ dh, int64_t lddh) {
+  __shared__ float red[256];
+  const int64_t total = B * T;
+  const float inv = 1.0f / (float)total;
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
+    const int64_t b = i / T;
+    const int t = (int)(i % T);
+    const float mu = heads[b * ldh + t];
+    const float lvr = heads[b * ldh + T + t];
+    const float lv = fmaxf(lvr, floor);
+    const float yz = (logf(y[b * T + t]) - lm[t]) / ls[t];
+    const float var = expf(lv);
+    const float diff = mu - yz;
+    acc += 0.5f * (lv + diff * diff / var) + l2 * (0.5f * lv) * (0.5f * lv);
+    dh[b * lddh + t] = inv * diff / var;
+    const float dlv = inv * (0.5f * (1.0f - diff * diff / var) + l2 * 0.5f * lv);
+    dh[b * lddh + T + t] = lvr >= floor ? dlv : 0.f;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0] * inv;
+}
+
+__global__ void add_noise_kernel(int64_t n, float* __restrict__ x, float stdv, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = hash_u32(seed, 2 * (uint64_t)i), b = hash_u32(seed, 2 * (uint64_t)i + 1);
+    const float u1 = ((float)a + 1.0f) * 2.3283064e-10f;  // (0, 1]
+    const float u2 = (float)b * 2.3283064e-10f;
+    const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
+    x[i] += stdv * z;
+  }
+}
+
+}  // namespace alignn
+
+using namespace alignn;
+
+extern "C" int alignn_version(void) { return 1; }
+extern "C" const char* alignn_last_error(void) { return g_err; }
+
+extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const float* R, int64_t ldr,
+                                  const float* wbeta, const float* X, int64_t ldx, const float* ln_w,
+                                  const float* ln_b, float* Xnew, int64_t ldxn, float* beta, float* mu, float* rstd,
+                                  float drop_p, uint64_t seed, void* stream) {
+  const int vpl = vpl_for(D);
+  if (!vpl) {
+    set_error("gate_ln_fwd: unsupported hidden %d", D);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  if (n == 0) return ALIGNN_OK;
+  GateFwdParams p{n, D, outp, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd, make_drop(drop_p, seed)};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 g((unsigned)((n + 3) / 4));
+  switch (vpl) {
+    case 1: hipLaunchKernelGGL(gate_ln_fwd_kernel<1>, g, dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(gate_ln_fwd_kernel<2>, g, dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(gate_ln_fwd_kernel<4>, g, dim3(256), 0, s, p); break;
+    default: hipLaunchKernelGGL(gate_ln_fwd_kernel<8>, g, dim3(256), 0, s, p); break;
+  }
+  ALIGNN_LAUNCH_CHECK("gate_ln_fwd_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                  const float* R, int64_t ldr, const float* wbeta, const float* ln_w, const float* ln_b,
+                                  const float* beta, const float* mu, const float* rstd, float* dout, float* dR,
+                                  int64_t lddr, float* d_wbeta, float* d_ln_w, float* d_ln_b, float* workspace,
+                                  float drop_p, uint64_t seed, void* stream) {
+  const int vpl = vpl_for(D);
+  if (!vpl) {
+    set_error("gate_ln_bwd: unsupported hidden %d", D);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  if (n == 0) return ALIGNN_OK;
+  const int nwaves = (int)std::min<int64_t>(1024, n);
+  GateBwdParams p{n, D, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
+                  nwaves, make_drop(drop_p, seed)};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 g((unsigned)((nwaves + 3) / 4));
+  switch (vpl) {
+    case 1: hipLaunchKernelGGL(gate_ln_bwd_kernel<1>, g, dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(gate_ln_bwd_kernel<2>, g, dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(gate_ln_bwd_kernel<4>, g, dim3(256), 0, s, p); break;
+    default: hipLaunchKernelGGL(gate_ln_bwd_kernel<8>, g, dim3(256), 0, s, p); break;
+  }
+  ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
+  hipLaunchKernelGGL(gate_ln_reduce_kernel, dim3((unsigned)((5 * D + 255) / 256)), dim3(256), 0, s, workspace, nwaves,
+                     D, d_wbeta, d_ln_w, d_ln_b);
+  ALIGNN_LAUNCH_CHECK("gate_ln_reduce_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_readout_feats_fwd(int64_t B, int32_t D, const float* h, const int64_t* ptr, const float* global_x,
+                                        int32_t gdim, const float* sg, int32_t sgdim, float* feats, float drop_p,
+                                        uint64_t seed, void* stream) {
+  if (B == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(readout_fwd_kernel, dim3((unsigned)B), dim3(256), 0, s, B, D, h, ptr, global_x, gdim, sg, sgdim,
+                     feats, make_drop(drop_p, seed));
+  ALIGNN_LAUNCH_CHECK("readout_fwd_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_readout_pool_bwd(int64_t B, int64_t N, int32_t D, const float* dfeats, int64_t ldf,
+                                       const int64_t* ptr, const int64_t* batch, float* dh, int32_t accumulate,
+                                       float drop_p, uint64_t seed, void* stream) {
+  (void)B;
+  if (N == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid_for(N * D)), dim3(256), 0, s, N, D, dfeats, ldf, ptr, batch, dh,
+                     accumulate, make_drop(drop_p, seed));
+  ALIGNN_LAUNCH_CHECK("pool_bwd_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_dropout_f32(int64_t rows, int64_t cols, const float* x, int64_t ldx, float* y, int64_t ldy,
+                                  const float* relu_ref, int64_t ldr, float drop_p, uint64_t seed, void* stream) {
+  if (rows * cols == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, rows, cols, x, ldx, y, ldy, relu_ref,
+                     ldr, make_drop(drop_p, seed));
+  ALIGNN_LAUNCH_CHECK("dropout_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
+                                 const float* log_means, const float* log_stds, float floor, float l2, float* loss,
+                                 float* dheads, int64_t lddh, void* stream) {
+  if (B <= 0 || T <= 0) return ALIGNN_E_BAD_SHAPE;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(hetero_nll_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, log_means, log_stds, floor, l2,
+                     loss, dheads, lddh);
+  ALIGNN_LAUNCH_CHECK("hetero_nll_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_add_noise_f32(int64_t n, float* x, float stdv, uint64_t seed, void* stream) {
+  if (n == 0 || stdv == 0.f) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, x, stdv, seed);
+  ALIGNN_LAUNCH_CHECK("add_noise_kernel");
+  return ALIGNN_OK;
+}

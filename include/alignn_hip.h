@@ -1,0 +1,183 @@
+/*
+ * alignn_hip.h — C ABI of libalignn_hip.so, the MI355X (gfx950) ALIGNN message-passing engine.
+ *
+ * Drop-in boundary: these entry points replace the PyTorch/PyG ops that the
+ * reference's hot path launches implicitly.  Each declaration cites the reference call site it
+ * replaces.  All tensors are raw device pointers + explicit sizes/strides (elements, not bytes);
+ * fp32 data, int32 graph indices (int64 accepted where the reference hands over PyG edge_index).
+ * Every function enqueues on `stream` (a hipStream_t passed as void*), allocates nothing,
+ * never synchronises, and returns 0 on success or a negative ALIGNN_E* code.  Results are
+ * deterministic (no float atomics; CSR segmented reductions).
+ */
+#ifndef ALIGNN_HIP_H
+#define ALIGNN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALIGNN_OK 0
+#define ALIGNN_E_BAD_SHAPE -1
+#define ALIGNN_E_UNSUPPORTED -2
+#define ALIGNN_E_HIP -3
+#define ALIGNN_E_WORKSPACE -4
+
+/* Library/version and error introspection. */
+int alignn_version(void);
+const char* alignn_last_error(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Dense projections (MFMA f32 32x32x2, exact fp32).  Replaces every nn.Linear / PyG Linear
+ * addmm+mm on the path: encoders train.py:350-364, TransformerConv lin_query/key/value/skip/
+ * edge (PyG 2.7.0, built at train.py:308/:326), edge_proj train.py:325/:333, feat_proj
+ * train.py:368-372, heads train.py:534-535, and their autograd backward (dX, dW).
+ *
+ *   C[b](m,n) = act( alpha * sum_k A[b](m,k) * B[b](k,n)  + beta * C[b](m,n)
+ *                    + bias[b](n) + rowscale[b](m) * bias2[b](n) ) * (mask ? (mask(m,n) > 0) : 1)
+ * with A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn], C(m,n) = C[m*scm + n*scn].
+ * Fast path: (sak == 1 or sam == 1) and (sbk == 1 or sbn == 1); others fall back to scalar loads.
+ * split_k > 1 accumulates fp32 partial slabs in `workspace` (>= split_k*batch*M*N floats) and
+ * reduces them in a second kernel in fixed order.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct AlignnGemmArgs {
+  int64_t M, N, K, batch;
+  const float* A; int64_t sam, sak, sab;
+  const float* B; int64_t sbk, sbn, sbb;
+  float* C; int64_t scm, scn, scb;
+  const float* bias; int64_t sbias_b;              /* may be NULL */
+  const float* rowscale; int64_t srs_m, srs_b;     /* may be NULL (with bias2) */
+  const float* bias2; int64_t sb2_b;
+  const float* mask; int64_t smk_m, smk_n;         /* relu-backward mask source, may be NULL */
+  float alpha, beta;
+  int32_t relu;
+  int32_t split_k;
+  float* workspace; int64_t workspace_elems;
+} AlignnGemmArgs;
+
+int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
+
+/* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
+ * Two-stage, fixed order.  workspace >= 256*N floats. */
+int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
+                      float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Graph preparation: CSR neighbour lists in HBM.  Replaces PyG MessagePassing.collect's
+ * index_select by edge_index[0]/[1] and the scatter/ index_add by edge_index[1]
+ * (TransformerConv propagate, train.py:315/:334).
+ *
+ * From PyG edge_index (int64 [2, m], row 0 = source j, row 1 = target i) over n nodes:
+ *   off_dst[n+1], perm_dst[m]  : edges grouped by target, original edge order kept in a group
+ *   src_at[m], dst_at[m]       : endpoints of the edge at each target-sorted position
+ *   off_src[n+1], pos_src[m]   : target-sorted positions grouped by source (ascending)
+ * workspace >= 2*n + 64 int32.  *err_flag (device int32) is OR-ed with 1 when an index is out of
+ * [0, n) (PyG raises IndexError there; the caller checks the flag).
+ * ---------------------------------------------------------------------------------------- */
+int alignn_graph_prep(const int64_t* edge_index, int64_t m, int64_t n,
+                      int32_t* off_dst, int32_t* perm_dst, int32_t* src_at, int32_t* dst_at,
+                      int32_t* off_src, int32_t* pos_src,
+                      int32_t* workspace, int32_t* err_flag, void* stream);
+
+/* rows_out[i, :] = rows_in[idx[i], :] (float, ld in elements).  Used to lay per-edge inputs out
+ * in target-sorted order (lg_edge_attr, train.py:553-554) once per batch. */
+int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows,
+                           int64_t cols, float* out, int64_t ld_out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused TransformerConv attention (PyG 2.7.0 TransformerConv.message/aggregate + utils.softmax,
+ * SURVEY §8a A5), heads H, hidden D = H*C, edge features of dim D projected per head by
+ * M_h = W_edge[h] @ P (P = identity for lin_edge on raw features, P = edge_proj.weight for the
+ * atom graph) with w̄ = W_edge @ p (p = edge_proj.bias).  The edge-feature GEMM over the m edges
+ * is never formed: per target node d the kernel consumes u[d,h] = M_h^T Q[d,h] (an n-row GEMM)
+ * and produces S[d,h] = sum_t alpha'_t f_t, which the caller maps back through M_h (exact algebra,
+ * DESIGN.md §3).  One wavefront per target segment, online segment softmax.
+ *
+ * Layouts: QKVR [n, ldq] with Q at col 0, K at D, V at 2D (R at 3D is for the gate kernel);
+ * U, S, Vd, Sz: [n, H, D]; F rows of length D at stride ldf, row of edge position t is
+ * feat_row[t] (or t when feat_row == NULL).  Stats mstat/den/sumA: [n, H].
+ * Dropout on alpha (p = drop_p, training): keep mask from a counter hash of (seed, t, h).
+ * ---------------------------------------------------------------------------------------- */
+int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
+                     const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
+                     const float* QKVR, int64_t ldq, const float* U, const float* wbar,
+                     const float* F, int64_t ldf,
+                     float* aggV, float* S, float* sumA, float* mstat, float* den,
+                     float drop_p, uint64_t seed, void* stream);
+
+/* Backward, target side: per target node d, recomputes z/alpha and, with dzs = dL/dz / sqrt(C)
+ * (z = the scaled score), writes
+ *   dQpart[d]  (cols of dQKVR given by dq, ld lddq) = sum_t dzs_t K_src
+ *   Sz[d,h] = sum_t dzs f_t,  sigz[d,h] = sum_t dzs
+ *   dz_e[t,h] = dzs, alpha_e[t,h] = alpha' (for the source-side pass)
+ *   dF[row(t)] (+)= sum_h dzs u[d,h] + alpha' Vd[d,h]   (row(t) = feat_row[t] or t)
+ * given dout (gradient of the aggregated message, [n, D]), outp (the aggregated message),
+ * Vd[d,h] = M_h^T dout[d,h]. */
+int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H,
+                         const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
+                         const float* QKVR, int64_t ldq, const float* U, const float* Vd,
+                         const float* wbar, const float* F, int64_t ldf,
+                         const float* dout, const float* outp, const float* mstat, const float* den,
+                         float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
+                         float* dF, int64_t lddf, int32_t accumulate_dF,
+                         float drop_p, uint64_t seed, void* stream);
+
+/* Backward, source side (replaces the atomic index_add of the gather backward): per source node
+ *   dK[s] = sum_{t: src(t)=s} dzs_t Q[dst(t)],  dV[s] = sum alpha'_t dout[dst(t)]
+ * written into dQKVR columns D..3D (ld lddq). */
+int alignn_tconv_bwd_src(int64_t n, int64_t m, int32_t D, int32_t H,
+                         const int32_t* off_src, const int32_t* pos_src, const int32_t* dst_at,
+                         const float* QKVR, int64_t ldq, const float* dout,
+                         const float* dz_e, const float* alpha_e, float* dKV, int64_t lddkv, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Gate + LayerNorm + ReLU + dropout + residual, fused row kernel.  Replaces TransformerConv's
+ * beta gate (lin_beta/sigmoid/blend, PyG forward) and train.py:316-317 / :335-336
+ * (LayerNorm eps 1e-5, ReLU, Dropout, residual add).
+ *   beta = sigmoid(<[o, r, o-r], wbeta>), y = beta r + (1-beta) o, x_new = x + drop(relu(LN(y)))
+ * o = outp [n,D], r = R (ldr), x = X (ldx); saves beta/mu/rstd [n].
+ * ---------------------------------------------------------------------------------------- */
+int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const float* R, int64_t ldr,
+                       const float* wbeta, const float* X, int64_t ldx, const float* ln_w, const float* ln_b,
+                       float* Xnew, int64_t ldxn, float* beta, float* mu, float* rstd,
+                       float drop_p, uint64_t seed, void* stream);
+
+/* Backward: given dXnew, writes dout [n,D], dR (ldr), and accumulates (+=) the parameter grads
+ * d_wbeta[3D], d_ln_w[D], d_ln_b[D] (fixed-order two-stage reduction; workspace >= 1024*5*D). */
+int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                       const float* R, int64_t ldr, const float* wbeta, const float* ln_w, const float* ln_b,
+                       const float* beta, const float* mu, const float* rstd,
+                       float* dout, float* dR, int64_t lddr, float* d_wbeta, float* d_ln_w, float* d_ln_b,
+                       float* workspace, float drop_p, uint64_t seed, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Readout (train.py:562-586): global_mean_pool over ptr (PyG, train.py:562), concat with
+ * global_x / sg_one_hot (train.py:563-572), dropout (train.py:573).
+ * feats [B, D + G]  (G = gdim + sgdim).  Backward scatters dpooled/count to the atoms.
+ * ---------------------------------------------------------------------------------------- */
+int alignn_readout_feats_fwd(int64_t B, int32_t D, const float* h, const int64_t* ptr,
+                             const float* global_x, int32_t gdim, const float* sg, int32_t sgdim,
+                             float* feats, float drop_p, uint64_t seed, void* stream);
+int alignn_readout_pool_bwd(int64_t B, int64_t N, int32_t D, const float* dfeats, int64_t ldf,
+                            const int64_t* ptr, const int64_t* batch, float* dh, int32_t accumulate,
+                            float drop_p, uint64_t seed, void* stream);
+
+/* Elementwise dropout (+ optional ReLU-mask backward): y = x * keep/(1-p) [* (ref > 0)] */
+int alignn_dropout_f32(int64_t rows, int64_t cols, const float* x, int64_t ldx, float* y, int64_t ldy,
+                       const float* relu_ref, int64_t ldr, float drop_p, uint64_t seed, void* stream);
+
+/* Hetero Gaussian NLL (train.py:656-681, no KNN weights), forward + gradient in one launch:
+ * loss = mean_b mean_t 0.5(lv + (mu-y)^2/e^lv) + l2 * mean((lv/2)^2), lv = clamp(logvar, floor).
+ * heads [B, ldh] hold mean at col 0..T-1 and logvar at T..2T-1; y_z = (log y - m)/s. */
+int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
+                      const float* log_means, const float* log_stds, float floor, float l2,
+                      float* loss, float* dheads, int64_t lddh, void* stream);
+
+/* Feature jitter (train.py:641-646): x += std * N(0,1) from a counter-based generator. */
+int alignn_add_noise_f32(int64_t n, float* x, float std, uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALIGNN_HIP_H */

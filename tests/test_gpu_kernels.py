@@ -1,0 +1,157 @@
+"""GPU unit parity of the individual HIP kernels (through the C ABI) against plain PyTorch fp32 /
+integer references.  Run with -m gpu on an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from alignn_mi355x import ops
+    return ops
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 53, 11), (128, 128, 16), (300, 257, 129), (2049, 1024, 256),
+                                   (64, 256, 23040)])
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+def test_gemm_layouts(M, N, K, layout):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 13 + K)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    B = torch.randn(K, N, generator=g).to(DEV)
+    Av = A if layout[0] == "n" else A.t().contiguous().t()
+    Bv = B if layout[1] == "n" else B.t().contiguous().t()
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(Av, Bv, C)
+    ref = A.double() @ B.double()
+    assert _rel(C, ref) < 2e-6
+
+
+def test_gemm_epilogues_and_batch():
+    ops = _ops()
+    torch.manual_seed(0)
+    H, M, K, N = 4, 300, 64, 256
+    A = torch.randn(H, M, K, device=DEV)
+    B = torch.randn(H, K, N, device=DEV)
+    C0 = torch.randn(H, M, N, device=DEV)
+    bias = torch.randn(H, N, device=DEV)
+    rs = torch.randn(H, M, device=DEV)
+    b2 = torch.randn(H, N, device=DEV)
+    C = C0.clone()
+    ops.gemm(A, B, C, alpha=0.5, beta=1.0, bias=bias, rowscale=rs, bias2=b2)
+    ref = 0.5 * (A.double() @ B.double()) + C0.double() + bias.double()[:, None, :] + rs.double()[:, :, None] * b2.double()[:, None, :]
+    assert _rel(C, ref) < 2e-6
+    # relu + mask
+    X = torch.randn(M, K, device=DEV)
+    W = torch.randn(N, K, device=DEV)
+    mask = torch.randn(M, N, device=DEV)
+    out = torch.empty(M, N, device=DEV)
+    ops.gemm(X, W.t(), out, relu=True, mask=mask)
+    ref = torch.relu(X.double() @ W.double().t()) * (mask > 0)
+    assert _rel(out, ref) < 2e-6
+
+
+def test_gemm_split_k_deterministic():
+    ops = _ops()
+    torch.manual_seed(1)
+    A = torch.randn(23040, 1024, device=DEV)
+    X = torch.randn(23040, 256, device=DEV)
+    out1 = torch.empty(1024, 256, device=DEV)
+    out2 = torch.empty(1024, 256, device=DEV)
+    ops.gemm(A.t(), X, out1, split_k=16)
+    ops.gemm(A.t(), X, out2, split_k=16)
+    assert torch.equal(out1, out2)
+    ref = A.double().t() @ X.double()
+    assert _rel(out1, ref) < 5e-6
+
+
+def test_colsum():
+    ops = _ops()
+    X = torch.randn(100003, 300, device=DEV)
+    out = torch.empty(300, device=DEV)
+    ops.colsum(X, out)
+    assert _rel(out, X.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("n,m", [(7, 19), (1000, 20000), (50, 0), (5, 1)])
+def test_graph_prep_bit_exact(n, m):
+    ops = _ops()
+    g = torch.Generator().manual_seed(n + m)
+    ei = torch.randint(0, n, (2, m), generator=g)
+    csr = ops.GraphCSR(ei.to(DEV), n)
+    torch.cuda.synchronize()
+    csr.check_indices("test")
+    dst = ei[1].numpy()
+    perm = np.argsort(dst, kind="stable")
+    off = np.concatenate([[0], np.cumsum(np.bincount(dst, minlength=n))])
+    assert np.array_equal(csr.off_dst.cpu().numpy(), off)
+    if m:
+        assert np.array_equal(csr.perm_dst[:m].cpu().numpy(), perm)
+        assert np.array_equal(csr.src_at[:m].cpu().numpy(), ei[0].numpy()[perm])
+        assert np.array_equal(csr.dst_at[:m].cpu().numpy(), dst[perm])
+        src_sorted = ei[0].numpy()[perm]
+        perm2 = np.argsort(src_sorted, kind="stable")
+        assert np.array_equal(csr.pos_src[:m].cpu().numpy(), perm2)
+
+
+def test_graph_prep_flags_out_of_range():
+    ops = _ops()
+    ei = torch.tensor([[0, 1, 5], [1, 2, 0]], device=DEV)
+    csr = ops.GraphCSR(ei, 3)
+    with pytest.raises(IndexError):
+        csr.check_indices("edge_index")
+
+
+def test_hetero_nll_matches_torch():
+    ops = _ops()
+    torch.manual_seed(3)
+    B, T = 32, 2
+    heads = torch.randn(B, 2 * T, device=DEV)
+    heads[0, T] = -5.0  # below the logvar floor: clamped, zero gradient
+    y = torch.rand(B * T, device=DEV) * 299 + 1
+    lm = torch.tensor([4.3228, 3.5567], device=DEV)
+    ls = torch.tensor([0.9051, 0.9405], device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    dh = torch.empty_like(heads)
+    ops.hetero_nll(heads, y, lm, ls, -2.9, 0.1, loss, dh)
+    h = heads.double().clone().requires_grad_(True)
+    mean, logvar = h[:, :T], h[:, T:]
+    tz = (torch.log(y.double().view(B, T)) - lm.double()) / ls.double()
+    lv = torch.clamp(logvar, min=-2.9)
+    ref = (0.5 * (lv + (mean - tz) ** 2 / torch.exp(lv))).mean(1).mean() + 0.1 * (0.5 * lv).pow(2).mean()
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-5 * abs(float(ref))
+    assert _rel(dh, h.grad) < 1e-5
+    assert float(dh[0, T]) == 0.0
+
+
+def test_dropout_statistics_and_replay():
+    ops = _ops()
+    x = torch.ones(1000, 1000, device=DEV)
+    y1 = torch.empty_like(x)
+    y2 = torch.empty_like(x)
+    ops.dropout(x, y1, None, 0.15, 1234)
+    ops.dropout(x, y2, None, 0.15, 1234)
+    assert torch.equal(y1, y2)
+    keep = (y1 > 0).float().mean().item()
+    assert abs(keep - 0.85) < 0.003
+    assert torch.allclose(y1[y1 > 0], torch.full_like(y1[y1 > 0], 1 / 0.85))
+    y3 = torch.empty_like(x)
+    ops.dropout(x, y3, None, 0.15, 1235)
+    assert not torch.equal(y1, y3)
+
+
+def test_add_noise_moments():
+    ops = _ops()
+    x = torch.zeros(4_000_000, device=DEV)
+    ops.add_noise(x, 0.1, 99)
+    assert abs(x.mean().item()) < 5e-4
+    assert abs(x.std().item() - 0.1) < 5e-4

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Runs GPU steps in order; stops at the first step whose exit code signals a crash/timeout
+# (anything other than 0 = ok and 1 = ordinary test failure).  Usage: tools/gpu_run.sh STEP...
+# STEP is one of: tests smoke bench prof
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+for step in "$@"; do
+  case "$step" in
+    tests) cmd=(timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider) ;;
+    tests-all) cmd=(timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider) ;;
+    smoke) cmd=(timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()") ;;
+    bench) cmd=(timeout -k 10 600 python bench.py --steps 20 --warmup 5) ;;
+    bench-quick) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline) ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "=== $step: ${cmd[*]}" | tee -a gpurun_out/run.log
+  "${cmd[@]}" > "gpurun_out/$step.log" 2>&1
+  rc=$?
+  echo "=== $step rc=$rc" | tee -a gpurun_out/run.log
+  tail -5 "gpurun_out/$step.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $step (rc=$rc)"; exit $rc; fi
+done
