@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--dump-probes", default="", help="write the per-op probe summary (JSON) to this path")
     return p.parse_args()
 
 
@@ -126,6 +127,9 @@ def main():
         summ = profiling.summary()
         profiling.disable()
         dominant = max(summ, key=lambda k: summ[k]["total_ms"])
+        if args.dump_probes and rank == 0:
+            with open(args.dump_probes, "w") as f:
+                json.dump(dict(sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"])), f, indent=1)
         profiling.enable(dominant)
 
     if world > 1:

@@ -52,6 +52,9 @@ class FlatViews:
         D = cfg.hidden
         self.edge: List[_Conv] = [self._conv(f"{pre}edge_blocks.{l}.", offs, D, False) for l in range(cfg.layers)]
         self.node: List[_Conv] = [self._conv(f"{pre}node_blocks.{l}.", offs, D, True) for l in range(cfg.layers)]
+        self.node_We = self._stack(offs, "node_blocks.{}.conv.lin_edge.weight", (D, D))
+        self.node_Wp = self._stack(offs, "node_blocks.{}.edge_proj.weight", (D, D))
+        self.node_bp = self._stack(offs, "node_blocks.{}.edge_proj.bias", (D,))
         T = cfg.target_dim
 
         def rows(name, k):
@@ -67,6 +70,20 @@ class FlatViews:
             self.Wlogvar, self.blogvar = rows("logvar_heads.0.weight", T), vec("logvar_heads.0.bias", T)
         else:
             self.Wout, self.bout = rows("output_heads.0.weight", T), vec("output_heads.0.bias", T)
+
+    def _stack(self, offs, pattern: str, shape):
+        """[L, *shape] strided view of one per-layer tensor (layers sit at a constant stride)."""
+        L = self.cfg.layers
+        if L == 0:
+            return None
+        o = [offs[self.prefix + pattern.format(l)][0] for l in range(L)]
+        stride = o[1] - o[0] if L > 1 else 0
+        if any(o[l] - o[0] != l * stride for l in range(L)):
+            raise AssertionError("per-layer parameters are not equally spaced in the flat layout")
+        inner = [1] * len(shape)
+        for i in range(len(shape) - 2, -1, -1):
+            inner[i] = inner[i + 1] * shape[i + 1]
+        return self.flat.as_strided((L, *shape), (stride, *inner), self.flat.storage_offset() + o[0])
 
     def enc(self, which: str, idx: int, kind: str) -> torch.Tensor:
         return self.named[f"{self.prefix}{which}_encoder.{idx}.{kind}"]
@@ -151,20 +168,38 @@ class _Ctx:
 #   x_new = x + dropout(relu(LN(TransformerConv(x, graph, f))))
 # with the edge features f (rows F[feat_row[t]] or F[t]) projected by M_h = W_e,h P (+ w̄ = W_e p).
 # ------------------------------------------------------------------------------------------------
-def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, feat_row, with_proj: bool,
-                  H: int, p_drop: float, seed_att: int, seed_blk: int):
+def proj_weights(We: torch.Tensor, Wp: torch.Tensor, bp: torch.Tensor):
+    """M = W_edge @ W_proj and w̄ = W_edge @ b_proj, for one conv ([D,D]) or stacked layers
+    ([L,D,D] strided views) in one batched GEMM each."""
+    lead = We.shape[:-2]
+    D = We.size(-1)
+    M = torch.empty(*lead, D, D, device=We.device)
+    wbar = torch.empty(*lead, D, device=We.device)
+    ops.gemm(We, Wp, M)
+    ops.gemm(We, bp.unsqueeze(-1), wbar.unsqueeze(-1))
+    return M, wbar
+
+
+def proj_grads(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
+    """Chain rule through M = W_edge W_proj, w̄ = W_edge b_proj (batched over stacked layers):
+    dW_edge = dM W_proj^T + dw̄ b_proj^T, dW_proj = W_edge^T dM, db_proj = W_edge^T dw̄."""
+    ops.gemm(dM, Wp.transpose(-1, -2), gWe)
+    ops.gemm(dwbar.unsqueeze(-1), bp.unsqueeze(-2), gWe, beta=1.0)
+    ops.gemm(We.transpose(-1, -2), dM, gWp)
+    ops.gemm(We.transpose(-1, -2), dwbar.unsqueeze(-1), gbp.unsqueeze(-1))
+
+
+def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, feat_row,
+                  M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
+                  seed_blk: int):
+    """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None."""
     n, D = X.shape
     C = D // H
     dev = X.device
     c = _Ctx()
     c.X, c.F, c.feat_row = X, F, feat_row
-    if with_proj:
-        c.M = torch.empty(D, D, device=dev)
-        ops.gemm(cv.We, cv.Wp, c.M)  # M = W_edge @ W_proj
-        c.wbar = torch.empty(D, device=dev)
-        ops.gemm(cv.We, cv.bp.view(D, 1), c.wbar.view(D, 1))  # w̄ = W_edge @ b_proj
-    else:
-        c.M, c.wbar = cv.We, None
+    c.M, c.wbar = M, wbar
+    with_proj = wbar is not None
     c.QKVR = torch.empty(n, 4 * D, device=dev)
     ops.gemm(X, cv.Wqkvr.t(), c.QKVR, bias=cv.bqkvr)
     c.U = torch.empty(n, H, D, device=dev)
@@ -192,10 +227,12 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, 
 
 
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
-                   dF_accumulate: bool) -> None:
+                   dF_accumulate: bool, dM: Optional[torch.Tensor] = None,
+                   dwbar: Optional[torch.Tensor] = None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
-    Parameter gradients are accumulated into gv (its gate/LN grads with +=, the rest overwritten)."""
+    Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
+    (c.wbar set) the gradients of M and w̄ are written to dM / dwbar for :func:`proj_grads`."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -220,16 +257,10 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     if c.with_proj:
         ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0, rowscale=sigz.t(),
                  bias2=c.wbar.view(H, C))
-        dM = torch.empty(D, D, device=dev)
         ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
         ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
-        dwbar = torch.empty(D, device=dev)
         ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
         ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
-        ops.gemm(dM, cv.Wp.t(), gv.We)                                  # dW_edge = dM W_p^T + dw̄ b_p^T
-        ops.gemm(dwbar.view(D, 1), cv.bp.view(1, D), gv.We, beta=1.0)
-        ops.gemm(cv.We.t(), dM, gv.Wp)                                  # dW_p = W_edge^T dM
-        ops.gemm(cv.We.t(), dwbar.view(D, 1), gv.bp.view(D, 1))        # db_p = W_edge^T dw̄
     else:
         ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0)
         ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
@@ -296,18 +327,20 @@ class AlignnEngine:
             ctx.h1a, a = None, torch.zeros(T, D, device=dev)
         ctx.a = a
         ctx.edge, ctx.node = [], []
+        if E > 0 and L > 0:
+            ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
         for l in range(L):
             # EdgeUpdateBlock (train.py:312-317): line graph, angle embedding in target-sorted order
             if T > 0 and E > 0:
-                e, c = block_forward(P.edge[l], e, bc.lg, a, None, False, H, p_drop, site_seed(seed, 4 * l),
-                                     site_seed(seed, 4 * l + 1))
+                e, c = block_forward(P.edge[l], e, bc.lg, a, None, P.edge[l].We, None, H, p_drop,
+                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1))
             else:
                 c = None
             ctx.edge.append(c)
             # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
             if E > 0:
-                h, c = block_forward(P.node[l], h, bc.ag, e, bc.ag.perm_dst, True, H, p_drop,
-                                     site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
+                h, c = block_forward(P.node[l], h, bc.ag, e, bc.ag.perm_dst, ctx.M_all[l], ctx.wbar_all[l], H,
+                                     p_drop, site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
             else:
                 c = None
             ctx.node.append(c)
@@ -383,14 +416,19 @@ class AlignnEngine:
         de = torch.zeros(E, D, device=dev)
         da = torch.empty(T, D, device=dev) if T > 0 else None
         da_written = False
+        if E > 0 and L > 0:
+            dM_all = torch.empty(L, D, D, device=dev)
+            dwbar_all = torch.empty(L, D, device=dev)
         for l in reversed(range(L)):
             c = ctx.node[l]
             if c is not None:
-                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True)
+                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l])
             c = ctx.edge[l]
             if c is not None:
                 block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, da_written)
                 da_written = True
+        if E > 0 and L > 0:
+            proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
         # encoders
         if ctx.has_angle and da_written:
             self._mlp_bwd(da, bc.xa, ctx.h1a, P.enc("angle", 2, "weight"), G.enc("angle", 0, "weight"),

@@ -22,7 +22,8 @@ import torch.nn.functional as F  # noqa: F401
 from torch import nn
 
 from . import ops
-from .engine import AlignnEngine, BatchCache, FlatViews, _Conv, batch_cache, block_backward, block_forward, site_seed
+from .engine import (AlignnEngine, BatchCache, FlatViews, _Conv, batch_cache, block_backward, block_forward,
+                     proj_grads, proj_weights, site_seed)
 from .layout import AlignnConfig, offsets
 
 
@@ -110,8 +111,11 @@ class _BlockFn(torch.autograd.Function):
         n = X.size(0)
         g = _csr_for(edge_index, n)
         cv = _conv_struct([p.detach() for p in ps])
-        with_proj = len(ps) > 12
-        Xn, c = block_forward(cv, X, g, Fe, g.perm_dst, with_proj, heads, p_drop, site_seed(seed, 0),
+        if len(ps) > 12:
+            M, wbar = proj_weights(cv.We, cv.Wp, cv.bp)
+        else:
+            M, wbar = cv.We, None
+        Xn, c = block_forward(cv, X, g, Fe, g.perm_dst, M, wbar, heads, p_drop, site_seed(seed, 0),
                               site_seed(seed, 1))
         ctx.meta, ctx.g, ctx.cv, ctx.c, ctx.nps = meta, g, cv, c, len(ps)
         ctx.F_shape = Fe.shape
@@ -132,7 +136,11 @@ class _BlockFn(torch.autograd.Function):
         gv.lnw, gv.lnb = torch.zeros_like(cv.lnw), torch.zeros_like(cv.lnb)
         if ctx.nps > 12:
             gv.Wp, gv.bp = torch.zeros_like(cv.Wp), torch.zeros_like(cv.bp)
-        block_backward(cv, gv, c, g, dX, dF, False)
+            dM, dwbar = torch.empty(D, D, device=dev), torch.empty(D, device=dev)
+            block_backward(cv, gv, c, g, dX, dF, False, dM, dwbar)
+            proj_grads(cv.We, cv.Wp, cv.bp, dM, dwbar, gv.We, gv.Wp, gv.bp)
+        else:
+            block_backward(cv, gv, c, g, dX, dF, False)
         grads = list(gv.Wqkvr.view(4, D, D).unbind(0)) + list(gv.bqkvr.view(4, D).unbind(0))
         grads += [gv.We, gv.wbeta.view(1, -1), gv.lnw, gv.lnb]
         if ctx.nps > 12:

@@ -109,12 +109,16 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
 
 
 def choose_split_k(M: int, N: int, K: int, batch: int) -> int:
+    """Split the K loop over workgroups when the output has too few tiles to fill 256 CUs:
+    aim at ~2 workgroups per CU, keep >= 128 of K per split (8 K-tiles) for large K and
+    >= 32 for small K (latency-bound tiny GEMMs)."""
     bm = 128 if M >= 128 else 64
     bn = 128 if N >= 128 else 64
     tiles = math.ceil(M / bm) * math.ceil(N / bn) * batch
-    if tiles >= _NUM_CUS or K < 1024:
+    if tiles >= _NUM_CUS or K < 64:
         return 1
-    split = min(math.ceil(2 * _NUM_CUS / tiles), max(1, K // 512))
+    min_chunk = 128 if K >= 4096 else 32
+    split = min(math.ceil(2 * _NUM_CUS / tiles), max(1, K // min_chunk))
     return max(1, split)
 
 

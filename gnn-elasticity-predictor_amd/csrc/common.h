@@ -75,4 +75,29 @@ inline DropParams make_drop(float p, uint64_t seed) {
   return d;
 }
 
+// Fixed-order column reduction of a [rows, N] partial buffer: out[c] (+)= sum_r part[r*N + c].
+// Grid: ceil(N/64) blocks of 256 threads (4 row-lanes x 64 columns).
+template <int kUnused = 0>
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int rows, int64_t N,
+                                                           float* __restrict__ out, int acc) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (col < N) {
+    int r = ty;
+    for (; r + 4 < rows; r += 8) {
+      s0 += part[(int64_t)r * N + col];
+      s1 += part[(int64_t)(r + 4) * N + col];
+    }
+    for (; r < rows; r += 4) s0 += part[(int64_t)r * N + col];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && col < N) {
+    const float t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    out[col] = acc ? out[col] + t : t;
+  }
+}
+
 }  // namespace alignn

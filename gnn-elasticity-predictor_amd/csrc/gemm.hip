@@ -314,25 +314,33 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
 }
 
 // -------------------------------------------------------------------------------------------
-// Column sums (bias gradients): stage 1 — each of up to 256 blocks sums a contiguous row range
-// for a 256-column strip; stage 2 — fixed-order sum over the row-range partials.
+// Column sums (bias gradients), two fixed-order stages.
+//   stage 1: block (R, strip) = 4 row-lanes x 64 columns; each thread sums rows r0+ty, r0+ty+4, ...
+//            of its row chunk (4 independent loads in flight), LDS-reduces the 4 row-lanes and
+//            writes one partial per (chunk, column).
+//   stage 2: one block per 64-column strip sums the R partials the same way.
 // -------------------------------------------------------------------------------------------
 namespace alignn {
-__global__ void colsum_stage1(const float* __restrict__ X, int64_t M, int64_t N, int64_t ldx, int64_t rows_per,
-                              float* __restrict__ part) {
-  const int64_t col = blockIdx.y * 256 + threadIdx.x;
-  const int64_t r0 = blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
-  if (col >= N) return;
-  float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += X[r * ldx + col];
-  part[blockIdx.x * N + col] = s;
-}
-__global__ void colsum_stage2(const float* __restrict__ part, int nparts, int64_t N, float* __restrict__ out, int acc) {
-  const int64_t col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= N) return;
-  float s = 0.f;
-  for (int i = 0; i < nparts; ++i) s += part[i * N + col];
-  out[col] = acc ? out[col] + s : s;
+__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ X, int64_t M, int64_t N, int64_t ldx,
+                                                     int64_t rows_per, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.y * 64 + tx;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < N) {
+    int64_t r = r0 + ty;
+    for (; r + 12 < r1; r += 16) {
+      s0 += X[r * ldx + col];
+      s1 += X[(r + 4) * ldx + col];
+      s2 += X[(r + 8) * ldx + col];
+      s3 += X[(r + 12) * ldx + col];
+    }
+    for (; r < r1; r += 4) s0 += X[r * ldx + col];
+  }
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ty == 0 && col < N) part[(int64_t)blockIdx.x * N + col] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 }  // namespace alignn
 
@@ -341,14 +349,22 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
   if (M < 0 || N < 0) return ALIGNN_E_BAD_SHAPE;
   if (N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int nparts = (int)std::min<int64_t>(256, std::max<int64_t>(1, (M + 63) / 64));
+  const unsigned strips = (unsigned)((N + 63) / 64);
+  // ~2 blocks per CU in stage 1, at least 64 rows per chunk, at most 256 chunks
+  int64_t want = std::max<int64_t>(1, 512 / (int64_t)strips);
+  int nparts = (int)std::min<int64_t>({256, want, std::max<int64_t>(1, (M + 63) / 64)});
   int64_t rows_per = (M + nparts - 1) / nparts;
   if (rows_per == 0) rows_per = 1;
-  dim3 g1(nparts, (unsigned)((N + 255) / 256));
-  hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
+  nparts = (int)((M + rows_per - 1) / rows_per);
+  if (nparts < 1) nparts = 1;
+  if (M == 0) {
+    hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(256), 0, s, workspace, 0, N, out, accumulate);
+    ALIGNN_LAUNCH_CHECK("colsum_stage2");
+    return ALIGNN_OK;
+  }
+  hipLaunchKernelGGL(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
   ALIGNN_LAUNCH_CHECK("colsum_stage1");
-  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, workspace, nparts, N, out,
-                     accumulate);
+  hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(256), 0, s, workspace, nparts, N, out, accumulate);
   ALIGNN_LAUNCH_CHECK("colsum_stage2");
   return ALIGNN_OK;
 }

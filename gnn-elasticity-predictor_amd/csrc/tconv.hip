@@ -30,6 +30,23 @@ struct FwdParams {
   DropParams drop;
 };
 
+// Edge operand ring: PF edges' K, V and feature rows in flight per wave (static slots; the loop is
+// unrolled by PF so every slot index is a compile-time constant).
+constexpr int PF = 4;
+
+template <int VPL>
+struct EdgeSlot {
+  float k[VPL], v[VPL], f[VPL];
+};
+
+template <int VPL>
+__device__ __forceinline__ void load_edge(EdgeSlot<VPL>& e, const float* __restrict__ QKVR, int64_t ldq, int D,
+                                          const float* __restrict__ F, int64_t ldf, int64_t src, int64_t row, int j0) {
+  vload(QKVR + src * ldq + D + j0, e.k);
+  vload(QKVR + src * ldq + 2 * D + j0, e.v);
+  vload(F + row * ldf + j0, e.f);
+}
+
 template <int VPL, int H>
 __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p) {
   const int lane = threadIdx.x & 63;
@@ -40,30 +57,10 @@ __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p) {
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
+  const int32_t beg = p.off[d], end = p.off[d + 1];
 
-  float q[VPL], u[H][VPL];
-  vzero(q);
-#pragma unroll
-  for (int h = 0; h < H; ++h) vzero(u[h]);
-  if (act) {
-    vload(p.QKVR + d * p.ldq + j0, q);
-#pragma unroll
-    for (int h = 0; h < H; ++h) vload(p.U + (d * H + h) * D + j0, u[h]);
-  }
-  float c[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) c[h] = 0.f;
-  if (p.wbar) {
-    float wb[VPL];
-    vzero(wb);
-    if (act) vload(p.wbar + j0, wb);
-    const float part = vdot(wb, q);
-#pragma unroll
-    for (int h = 0; h < H; ++h) c[h] = (h == hl) ? part : 0.f;
-    reduce_heads<H>(c, lane);
-  }
-
-  float m[H], s[H], sa[H], accS[H][VPL], accV[VPL];
+  float accS[H][VPL], accV[VPL];
+  float m[H], s[H], sa[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     m[h] = -INFINITY;
@@ -73,55 +70,78 @@ __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p) {
   }
   vzero(accV);
 
-  const int32_t beg = p.off[d], end = p.off[d + 1];
-  float k_c[VPL], v_c[VPL], f_c[VPL];
-  vzero(k_c); vzero(v_c); vzero(f_c);
-  if (beg < end && act) {
-    const int64_t s0 = p.src_at[beg];
-    const int64_t r0 = p.feat_row ? p.feat_row[beg] : beg;
-    vload(p.QKVR + s0 * p.ldq + D + j0, k_c);
-    vload(p.QKVR + s0 * p.ldq + 2 * D + j0, v_c);
-    vload(p.F + r0 * p.ldf + j0, f_c);
-  }
-  for (int32_t t = beg; t < end; ++t) {
-    float k_n[VPL], v_n[VPL], f_n[VPL];
-    vzero(k_n); vzero(v_n); vzero(f_n);
-    if (t + 1 < end && act) {
-      const int64_t s1 = p.src_at[t + 1];
-      const int64_t r1 = p.feat_row ? p.feat_row[t + 1] : (t + 1);
-      vload(p.QKVR + s1 * p.ldq + D + j0, k_n);
-      vload(p.QKVR + s1 * p.ldq + 2 * D + j0, v_n);
-      vload(p.F + r1 * p.ldf + j0, f_n);
+  if (beg < end) {
+    float q[VPL], u[H][VPL];
+    vzero(q);
+#pragma unroll
+    for (int h = 0; h < H; ++h) vzero(u[h]);
+    if (act) {
+      vload(p.QKVR + d * p.ldq + j0, q);
+#pragma unroll
+      for (int h = 0; h < H; ++h) vload(p.U + (d * H + h) * D + j0, u[h]);
     }
-    float pr[H];
+    float c[H];
 #pragma unroll
-    for (int h = 0; h < H; ++h) pr[h] = vdot(u[h], f_c);
-    const float qk = vdot(q, k_c);
+    for (int h = 0; h < H; ++h) c[h] = 0.f;
+    if (p.wbar) {
+      float wb[VPL];
+      vzero(wb);
+      if (act) vload(p.wbar + j0, wb);
+      const float part = vdot(wb, q);
 #pragma unroll
-    for (int h = 0; h < H; ++h) pr[h] += (h == hl) ? qk : 0.f;
-    reduce_heads<H>(pr, lane);
-    float corr[H], ed[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const float z = (pr[h] + c[h]) * scale;
-      const float mn = fmaxf(m[h], z);
-      corr[h] = __expf(m[h] - mn);
-      const float e = __expf(z - mn);
-      s[h] = fmaf(s[h], corr[h], e);
-      m[h] = mn;
-      ed[h] = p.drop.active ? e * dropout_mul(p.drop.seed, (uint64_t)t * H + h, p.drop.thresh, p.drop.inv_keep) : e;
-      sa[h] = fmaf(sa[h], corr[h], ed[h]);
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(accS[h][i], corr[h], ed[h] * f_c[i]);
+      for (int h = 0; h < H; ++h) c[h] = (h == hl) ? part : 0.f;
+      reduce_heads<H>(c, lane);
     }
-    const float cl = pick<H>(corr, hl), el = pick<H>(ed, hl);
+    EdgeSlot<VPL> ring[PF];
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) accV[i] = fmaf(accV[i], cl, el * v_c[i]);
+    for (int j = 0; j < PF; ++j) {
+      vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
+      const int32_t t = beg + j;
+      if (t < end && act) {
+        const int64_t src = p.src_at[t];
+        const int64_t row = p.feat_row ? p.feat_row[t] : t;
+        load_edge(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, src, row, j0);
+      }
+    }
+    for (int32_t tb = beg; tb < end; tb += PF) {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      k_c[i] = k_n[i];
-      v_c[i] = v_n[i];
-      f_c[i] = f_n[i];
+      for (int j = 0; j < PF; ++j) {
+        const int32_t t = tb + j;
+        if (t < end) {
+          EdgeSlot<VPL>& e = ring[j];
+          float pr[H];
+#pragma unroll
+          for (int h = 0; h < H; ++h) pr[h] = vdot(u[h], e.f);
+          const float qk = vdot(q, e.k);
+#pragma unroll
+          for (int h = 0; h < H; ++h) pr[h] += (h == hl) ? qk : 0.f;
+          reduce_heads<H>(pr, lane);
+          float corr[H], ed[H];
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            const float z = (pr[h] + c[h]) * scale;
+            const float mn = fmaxf(m[h], z);
+            corr[h] = __expf(m[h] - mn);
+            const float ex = __expf(z - mn);
+            s[h] = fmaf(s[h], corr[h], ex);
+            m[h] = mn;
+            ed[h] = p.drop.active ? ex * dropout_mul(p.drop.seed, (uint64_t)t * H + h, p.drop.thresh, p.drop.inv_keep)
+                                  : ex;
+            sa[h] = fmaf(sa[h], corr[h], ed[h]);
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(accS[h][i], corr[h], ed[h] * e.f[i]);
+          }
+          const float cl = pick<H>(corr, hl), el = pick<H>(ed, hl);
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) accV[i] = fmaf(accV[i], cl, el * e.v[i]);
+          const int32_t tn = t + PF;
+          if (tn < end && act) {
+            const int64_t src = p.src_at[tn];
+            const int64_t row = p.feat_row ? p.feat_row[tn] : tn;
+            load_edge(e, p.QKVR, p.ldq, D, p.F, p.ldf, src, row, j0);
+          }
+        }
+      }
     }
   }
 
@@ -184,47 +204,7 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p) {
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-
-  float q[VPL], go[VPL], op[VPL], u[H][VPL], vd[H][VPL];
-  vzero(q); vzero(go); vzero(op);
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    vzero(u[h]);
-    vzero(vd[h]);
-  }
-  if (act) {
-    vload(p.QKVR + d * p.ldq + j0, q);
-    vload(p.dout + d * D + j0, go);
-    vload(p.outp + d * D + j0, op);
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      vload(p.U + (d * H + h) * D + j0, u[h]);
-      vload(p.Vd + (d * H + h) * D + j0, vd[h]);
-    }
-  }
-  // per-head constants: c = <w̄_h, Q_h>, c2 = <w̄_h, dout_h>, delta = <dout_h, outp_h>
-  float c[H], c2[H], delta[H];
-  {
-    float wb[VPL];
-    vzero(wb);
-    if (p.wbar && act) vload(p.wbar + j0, wb);
-    const float pc = vdot(wb, q), pc2 = vdot(wb, go), pdl = vdot(go, op);
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      c[h] = (h == hl) ? pc : 0.f;
-      c2[h] = (h == hl) ? pc2 : 0.f;
-      delta[h] = (h == hl) ? pdl : 0.f;
-    }
-    reduce_heads<H>(c, lane);
-    reduce_heads<H>(c2, lane);
-    reduce_heads<H>(delta, lane);
-  }
-  float mst[H], inv_den[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    mst[h] = p.mstat[d * H + h];
-    inv_den[h] = 1.0f / p.den[d * H + h];
-  }
+  const int32_t beg = p.off[d], end = p.off[d + 1];
 
   float sz[H][VPL], sgz[H], dqa[VPL];
 #pragma unroll
@@ -234,91 +214,127 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p) {
   }
   vzero(dqa);
 
-  const int32_t beg = p.off[d], end = p.off[d + 1];
-  float k_c[VPL], v_c[VPL], f_c[VPL];
-  vzero(k_c); vzero(v_c); vzero(f_c);
-  int64_t row_c = 0;
   if (beg < end) {
-    row_c = p.feat_row ? p.feat_row[beg] : beg;
+    float q[VPL], go[VPL], op[VPL], u[H][VPL], vd[H][VPL];
+    vzero(q); vzero(go); vzero(op);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      vzero(u[h]);
+      vzero(vd[h]);
+    }
     if (act) {
-      const int64_t s0 = p.src_at[beg];
-      vload(p.QKVR + s0 * p.ldq + D + j0, k_c);
-      vload(p.QKVR + s0 * p.ldq + 2 * D + j0, v_c);
-      vload(p.F + row_c * p.ldf + j0, f_c);
-    }
-  }
-  for (int32_t t = beg; t < end; ++t) {
-    float k_n[VPL], v_n[VPL], f_n[VPL];
-    vzero(k_n); vzero(v_n); vzero(f_n);
-    int64_t row_n = 0;
-    if (t + 1 < end) {
-      row_n = p.feat_row ? p.feat_row[t + 1] : (t + 1);
-      if (act) {
-        const int64_t s1 = p.src_at[t + 1];
-        vload(p.QKVR + s1 * p.ldq + D + j0, k_n);
-        vload(p.QKVR + s1 * p.ldq + 2 * D + j0, v_n);
-        vload(p.F + row_n * p.ldf + j0, f_n);
+      vload(p.QKVR + d * p.ldq + j0, q);
+      vload(p.dout + d * D + j0, go);
+      vload(p.outp + d * D + j0, op);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        vload(p.U + (d * H + h) * D + j0, u[h]);
+        vload(p.Vd + (d * H + h) * D + j0, vd[h]);
       }
     }
-    float pz[H], pg[H];
+    // per-head constants: c = <w̄_h, Q_h>, c2 = <w̄_h, dout_h>, delta = <dout_h, outp_h>
+    float c[H], c2[H], delta[H];
+    {
+      float wb[VPL];
+      vzero(wb);
+      if (p.wbar && act) vload(p.wbar + j0, wb);
+      const float pc = vdot(wb, q), pc2 = vdot(wb, go), pdl = vdot(go, op);
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      pz[h] = vdot(u[h], f_c);
-      pg[h] = vdot(vd[h], f_c);
-    }
-    const float qk = vdot(q, k_c), gv = vdot(go, v_c);
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      pz[h] += (h == hl) ? qk : 0.f;
-      pg[h] += (h == hl) ? gv : 0.f;
-    }
-    reduce_heads<H>(pz, lane);
-    reduce_heads<H>(pg, lane);
-    float dz[H], al[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const float z = (pz[h] + c[h]) * scale;
-      const float alpha = __expf(z - mst[h]) * inv_den[h];
-      const float mul = p.drop.active ? dropout_mul(p.drop.seed, (uint64_t)t * H + h, p.drop.thresh, p.drop.inv_keep) : 1.f;
-      al[h] = alpha * mul;                      // alpha' (dropped, used in the aggregation)
-      const float dal = (pg[h] + c2[h]) * mul;  // d alpha (pre-dropout)
-      dz[h] = alpha * (dal - delta[h]) * scale;  // dz * (1/sqrt(C)): every consumer wants it scaled
-      sgz[h] += dz[h];
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(dz[h], f_c[i], sz[h][i]);
-    }
-    const float dzl = pick<H>(dz, hl);
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, k_c[i], dqa[i]);
-    if (p.dF && act) {
-      float df[VPL];
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int h = 0; h < H; ++h) a = fmaf(dz[h], u[h][i], fmaf(al[h], vd[h][i], a));
-        df[i] = a;
+      for (int h = 0; h < H; ++h) {
+        c[h] = (h == hl) ? pc : 0.f;
+        c2[h] = (h == hl) ? pc2 : 0.f;
+        delta[h] = (h == hl) ? pdl : 0.f;
       }
-      float* dst = p.dF + row_c * p.lddf + j0;
-      if (p.acc_dF) {
-        float old[VPL];
-        vload(dst, old);
+      reduce_heads<H>(c, lane);
+      reduce_heads<H>(c2, lane);
+      reduce_heads<H>(delta, lane);
+    }
+    float mst[H], inv_den[H];
 #pragma unroll
-        for (int i = 0; i < VPL; ++i) df[i] += old[i];
+    for (int h = 0; h < H; ++h) {
+      mst[h] = p.mstat[d * H + h];
+      inv_den[h] = 1.0f / p.den[d * H + h];
+    }
+
+    EdgeSlot<VPL> ring[PF];
+    int64_t rows[PF];
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
+      const int32_t t = beg + j;
+      rows[j] = 0;
+      if (t < end) {
+        rows[j] = p.feat_row ? p.feat_row[t] : t;
+        if (act) load_edge(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)p.src_at[t], rows[j], j0);
       }
-      vstore(dst, df);
     }
-    if (lane < H) {
-      p.dz_e[(int64_t)t * H + lane] = pick<H>(dz, lane);
-      p.alpha_e[(int64_t)t * H + lane] = pick<H>(al, lane);
-    }
+    for (int32_t tb = beg; tb < end; tb += PF) {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      k_c[i] = k_n[i];
-      v_c[i] = v_n[i];
-      f_c[i] = f_n[i];
+      for (int j = 0; j < PF; ++j) {
+        const int32_t t = tb + j;
+        if (t < end) {
+          EdgeSlot<VPL>& e = ring[j];
+          float pz[H], pg[H];
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            pz[h] = vdot(u[h], e.f);
+            pg[h] = vdot(vd[h], e.f);
+          }
+          const float qk = vdot(q, e.k), gv = vdot(go, e.v);
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            pz[h] += (h == hl) ? qk : 0.f;
+            pg[h] += (h == hl) ? gv : 0.f;
+          }
+          reduce_heads<H>(pz, lane);
+          reduce_heads<H>(pg, lane);
+          float dz[H], al[H];
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            const float z = (pz[h] + c[h]) * scale;
+            const float alpha = __expf(z - mst[h]) * inv_den[h];
+            const float mul =
+                p.drop.active ? dropout_mul(p.drop.seed, (uint64_t)t * H + h, p.drop.thresh, p.drop.inv_keep) : 1.f;
+            al[h] = alpha * mul;                      // alpha' (dropped, used in the aggregation)
+            const float dal = (pg[h] + c2[h]) * mul;  // d alpha (pre-dropout)
+            dz[h] = alpha * (dal - delta[h]) * scale;  // dz * (1/sqrt(C)): every consumer wants it scaled
+            sgz[h] += dz[h];
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(dz[h], e.f[i], sz[h][i]);
+          }
+          const float dzl = pick<H>(dz, hl);
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, e.k[i], dqa[i]);
+          if (p.dF && act) {
+            float df[VPL];
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) {
+              float a = 0.f;
+#pragma unroll
+              for (int h = 0; h < H; ++h) a = fmaf(dz[h], u[h][i], fmaf(al[h], vd[h][i], a));
+              df[i] = a;
+            }
+            float* dst = p.dF + rows[j] * p.lddf + j0;
+            if (p.acc_dF) {
+              float old[VPL];
+              vload(dst, old);
+#pragma unroll
+              for (int i = 0; i < VPL; ++i) df[i] += old[i];
+            }
+            vstore(dst, df);
+          }
+          if (lane < H) {
+            p.dz_e[(int64_t)t * H + lane] = pick<H>(dz, lane);
+            p.alpha_e[(int64_t)t * H + lane] = pick<H>(al, lane);
+          }
+          const int32_t tn = t + PF;
+          if (tn < end) {
+            rows[j] = p.feat_row ? p.feat_row[tn] : tn;
+            if (act) load_edge(e, p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)p.src_at[tn], rows[j], j0);
+          }
+        }
+      }
     }
-    row_c = row_n;
   }
   if (act) {
     vstore(p.dq + d * p.lddq + j0, dqa);
@@ -355,19 +371,30 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
   vzero(dv);
   const int32_t beg = p.off_src[s], end = p.off_src[s + 1];
   if (act) {
-    for (int32_t i = beg; i < end; ++i) {
-      const int64_t pos = p.pos_src[i];
-      const int64_t dd = p.dst_at[pos];
-      const float dz = p.dz_e[pos * H + hl];
-      const float al = p.alpha_e[pos * H + hl];
-      float qv[VPL], gv[VPL];
-      vload(p.QKVR + dd * p.ldq + j0, qv);
-      vload(p.dout + dd * D + j0, gv);
+    for (int32_t ib = beg; ib < end; ib += PF) {
+      float qv[PF][VPL], gv[PF][VPL], dz[PF], al[PF];
 #pragma unroll
-      for (int k = 0; k < VPL; ++k) {
-        dk[k] = fmaf(dz, qv[k], dk[k]);
-        dv[k] = fmaf(al, gv[k], dv[k]);
+      for (int j = 0; j < PF; ++j) {  // issue all loads of the group first
+        vzero(qv[j]);
+        vzero(gv[j]);
+        dz[j] = 0.f;
+        al[j] = 0.f;
+        if (ib + j < end) {
+          const int64_t pos = p.pos_src[ib + j];
+          const int64_t dd = p.dst_at[pos];
+          dz[j] = p.dz_e[pos * H + hl];
+          al[j] = p.alpha_e[pos * H + hl];
+          vload(p.QKVR + dd * p.ldq + j0, qv[j]);
+          vload(p.dout + dd * D + j0, gv[j]);
+        }
       }
+#pragma unroll
+      for (int j = 0; j < PF; ++j)
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          dk[k] = fmaf(dz[j], qv[j][k], dk[k]);
+          dv[k] = fmaf(al[j], gv[j][k], dv[k]);
+        }
     }
     vstore(p.dKV + s * p.lddkv + j0, dk);
     vstore(p.dKV + s * p.lddkv + D + j0, dv);

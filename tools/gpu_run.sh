@@ -11,6 +11,8 @@ for step in "$@"; do
     smoke) cmd=(timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()") ;;
     bench) cmd=(timeout -k 10 600 python bench.py --steps 20 --warmup 5) ;;
     bench-quick) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline) ;;
+    probes) cmd=(timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --dump-probes gpurun_out/probes.json) ;;
+    rocprof) cmd=(timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "=== $step: ${cmd[*]}" | tee -a gpurun_out/run.log
