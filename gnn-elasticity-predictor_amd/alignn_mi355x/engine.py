@@ -52,6 +52,7 @@ class FlatViews:
         D = cfg.hidden
         self.edge: List[_Conv] = [self._conv(f"{pre}edge_blocks.{l}.", offs, D, False) for l in range(cfg.layers)]
         self.node: List[_Conv] = [self._conv(f"{pre}node_blocks.{l}.", offs, D, True) for l in range(cfg.layers)]
+        self.edge_We = self._stack(offs, "edge_blocks.{}.conv.lin_edge.weight", (D, D))
         self.node_We = self._stack(offs, "node_blocks.{}.conv.lin_edge.weight", (D, D))
         self.node_Wp = self._stack(offs, "node_blocks.{}.edge_proj.weight", (D, D))
         self.node_bp = self._stack(offs, "node_blocks.{}.edge_proj.bias", (D,))
@@ -189,6 +190,17 @@ def proj_grads(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
     ops.gemm(We.transpose(-1, -2), dwbar.unsqueeze(-1), gbp.unsqueeze(-1))
 
 
+def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
+    """proj_grads for L stacked edge projections W_edge[l] that share ONE (W_proj, b_proj) — the
+    angle encoder's second Linear folded into every line-graph conv: the shared gradients are the
+    sums over layers (batch-reduced GEMMs)."""
+    L = We.size(0)
+    ops.gemm(dM, Wp.expand(L, *Wp.shape).transpose(-1, -2), gWe)
+    ops.gemm(dwbar.unsqueeze(-1), bp.expand(L, bp.numel()).unsqueeze(-2), gWe, beta=1.0)
+    ops.gemm(We.transpose(-1, -2), dM, gWp, reduce_batch=True)
+    ops.gemm(We.transpose(-1, -2), dwbar.unsqueeze(-1), gbp.unsqueeze(-1), reduce_batch=True)
+
+
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int):
@@ -227,7 +239,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, 
 
 
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
-                   dF_accumulate: bool, dM: Optional[torch.Tensor] = None,
+                   dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
@@ -280,6 +292,7 @@ class AlignnEngine:
     def __init__(self, cfg: AlignnConfig):
         cfg.validate()
         self.cfg = cfg
+        self.debug = None  # dict -> backward stores intermediate gradients (diagnostics only)
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -319,20 +332,29 @@ class AlignnEngine:
                                        P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
         else:
             ctx.h1e, e = None, torch.zeros(E, D, device=dev)
+        # Angle encoder (train.py:553-554): only its hidden layer is materialised.  Its second Linear
+        # (W2, b2) is folded into every line-graph conv's edge projection, M_l = W_edge,l W2 and
+        # w̄_l = W_edge,l b2 — exact algebra, so the [T, D] x [D, D] GEMM and its two
+        # backward GEMMs never run.
         ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
         if ctx.has_angle:
-            ctx.h1a, a = self._mlp_fwd(bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
-                                       P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"))
+            a = torch.empty(T, D, device=dev)
+            ops.gemm(bc.xa, P.enc("angle", 0, "weight").t(), a, bias=P.enc("angle", 0, "bias"), relu=True)
+            ctx.h1a = a
         else:
             ctx.h1a, a = None, torch.zeros(T, D, device=dev)
         ctx.a = a
         ctx.edge, ctx.node = [], []
+        if T > 0 and E > 0 and L > 0 and ctx.has_angle:
+            W2, b2 = P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias")
+            ctx.Ml_all, ctx.wl_all = proj_weights(P.edge_We, W2.expand(L, D, D), b2.expand(L, D))
         if E > 0 and L > 0:
             ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
         for l in range(L):
             # EdgeUpdateBlock (train.py:312-317): line graph, angle embedding in target-sorted order
             if T > 0 and E > 0:
-                e, c = block_forward(P.edge[l], e, bc.lg, a, None, P.edge[l].We, None, H, p_drop,
+                Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
+                e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1))
             else:
                 c = None
@@ -419,20 +441,39 @@ class AlignnEngine:
         if E > 0 and L > 0:
             dM_all = torch.empty(L, D, D, device=dev)
             dwbar_all = torch.empty(L, D, device=dev)
+        line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
+        if line_proj:
+            dMl_all = torch.empty(L, D, D, device=dev)
+            dwl_all = torch.empty(L, D, device=dev)
         for l in reversed(range(L)):
             c = ctx.node[l]
+            if self.debug is not None:
+                self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l])
+            if self.debug is not None:
+                self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
             if c is not None:
-                block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, da_written)
+                # dF of the line convs is the gradient of the angle hidden layer, summed over layers;
+                # the last (l = 0) applies the ReLU mask in place
+                flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
+                if line_proj:
+                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l])
+                else:
+                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags)
                 da_written = True
+        if self.debug is not None:
+            self.debug["de0"] = de.clone()
         if E > 0 and L > 0:
             proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
+        if line_proj:
+            proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all, dwl_all,
+                              G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
         # encoders
         if ctx.has_angle and da_written:
-            self._mlp_bwd(da, bc.xa, ctx.h1a, P.enc("angle", 2, "weight"), G.enc("angle", 0, "weight"),
-                          G.enc("angle", 0, "bias"), G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
+            ops.gemm(da.t(), bc.xa, G.enc("angle", 0, "weight"))  # da is the masked hidden-layer gradient
+            ops.colsum(da, G.enc("angle", 0, "bias"))
         if ctx.h1e is not None:
             self._mlp_bwd(de, ctx.edge_attr, ctx.h1e, P.enc("edge", 2, "weight"), G.enc("edge", 0, "weight"),
                           G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))

@@ -61,16 +61,20 @@ def _as3(t: torch.Tensor):
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, rowscale: Optional[torch.Tensor] = None,
          bias2: Optional[torch.Tensor] = None, relu: bool = False, mask: Optional[torch.Tensor] = None,
-         split_k: Optional[int] = None) -> torch.Tensor:
+         split_k: Optional[int] = None, reduce_batch: bool = False) -> torch.Tensor:
     """C = act(alpha * A @ B + beta * C + bias + rowscale[:,None] * bias2) [* (mask > 0)].
 
     A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D);
-    bias/bias2 [.., N], rowscale [.., M] (strided views too)."""
+    bias/bias2 [.., N], rowscale [.., M] (strided views too).  ``reduce_batch``: A/B batched, C is
+    2-D and receives the sum over the batch (K must be a multiple of 16)."""
     ba, sab, sam, sak, M, K = _as3(A)
     bb, sbb, sbk, sbn, K2, N = _as3(B)
     bc, scb, scm, scn, M2, N2 = _as3(C)
     batch = max(ba, bb, bc)
-    if K2 != K or M2 != M or N2 != N or bc != batch or ba not in (1, batch) or bb not in (1, batch):
+    if reduce_batch:
+        if bc != 1 or K2 != K or M2 != M or N2 != N or ba not in (1, batch) or bb not in (1, batch):
+            raise ValueError(f"gemm(reduce_batch) shape mismatch: A{tuple(A.shape)} B{tuple(B.shape)} C{tuple(C.shape)}")
+    elif K2 != K or M2 != M or N2 != N or bc != batch or ba not in (1, batch) or bb not in (1, batch):
         raise ValueError(f"gemm shape mismatch: A{tuple(A.shape)} B{tuple(B.shape)} C{tuple(C.shape)}")
     a = GemmArgs()
     a.M, a.N, a.K, a.batch = M, N, K, batch
@@ -91,11 +95,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if mask is not None:
         a.mask, a.smk_m, a.smk_n = mask.data_ptr(), mask.stride(0), mask.stride(1)
     a.alpha, a.beta, a.relu = float(alpha), float(beta), int(bool(relu))
+    a.reduce_batch = int(bool(reduce_batch) and batch > 1)
     if split_k is None:
-        split_k = choose_split_k(M, N, K, batch)
+        split_k = choose_split_k(M, N, K * batch, 1) if a.reduce_batch else choose_split_k(M, N, K, batch)
     a.split_k = int(split_k)
     if split_k > 1:
-        need = split_k * batch * M * N
+        need = split_k * (1 if a.reduce_batch else batch) * M * N
         ws = WS.get("gemm", need, C.device)
         a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
     key = f"gemm_f32 M{M} N{N} K{K} b{batch}"
@@ -144,7 +149,9 @@ def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torc
 class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
-    __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err")
+    __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched")
+
+    HEAVY_THRESHOLD = 32  # in-degree above which a target node gets a 4-wave workgroup
 
     def __init__(self, edge_index: torch.Tensor, n: int):
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
@@ -161,11 +168,28 @@ class GraphCSR:
         self.off_src = torch.empty(n + 1, **i32)
         self.pos_src = torch.empty(max(m, 1), **i32)
         self.err = torch.zeros(1, **i32)
+        self._sched = None
         ws = WS.get("graph", 2 * n + 64, dev, torch.int32)
         check(_lib.lib().alignn_graph_prep(ei.data_ptr(), m, n, self.off_dst.data_ptr(), self.perm_dst.data_ptr(),
                                            self.src_at.data_ptr(), self.dst_at.data_ptr(), self.off_src.data_ptr(),
                                            self.pos_src.data_ptr(), ws.data_ptr(), self.err.data_ptr(),
                                            stream_ptr()), "alignn_graph_prep")
+
+    def schedule(self):
+        """Light/heavy target-node lists for the attention kernels (host-built once per graph:
+        one small device->host copy of the offsets)."""
+        if self._sched is None:
+            off = self.off_dst.cpu()
+            deg = off[1:] - off[:-1]
+            heavy_mask = deg > self.HEAVY_THRESHOLD
+            idx = torch.arange(self.n, dtype=torch.int32)
+            light = idx[~heavy_mask].to(self.off_dst.device)
+            heavy = idx[heavy_mask].to(self.off_dst.device)
+            sc = _lib.Schedule()
+            sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
+            sc.heavy, sc.n_heavy = (heavy.data_ptr() if heavy.numel() else None), heavy.numel()
+            self._sched = (sc, light, heavy)
+        return self._sched[0]
 
     def check_indices(self, what: str) -> None:
         """Host check of the device error flag (one sync).  PyG raises IndexError here."""
@@ -199,7 +223,8 @@ def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str) -> float:
 
 def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, wbar: Optional[torch.Tensor],
               F: torch.Tensor, feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float, seed: int):
-    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd"), lambda: check(_lib.lib().alignn_tconv_fwd(g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd"), lambda: check(_lib.lib().alignn_tconv_fwd(
+        g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row), ctypes.byref(g.schedule()),
                                       QKVR.data_ptr(), QKVR.stride(0), U.data_ptr(), _p(wbar), F.data_ptr(),
                                       F.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(),
                                       den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
@@ -207,9 +232,11 @@ def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, 
 
 
 def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, dout, outp, mstat, den,
-                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: bool, drop_p: float, seed: int):
+                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: int, drop_p: float, seed: int):
+    """accumulate_dF: bit 0 add into dF, bit 1 apply the ReLU mask (F > 0) to the result."""
     profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_dst"), lambda: check(_lib.lib().alignn_tconv_bwd_dst(
-        g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row), QKVR.data_ptr(), QKVR.stride(0),
+        g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row), ctypes.byref(g.schedule()),
+        QKVR.data_ptr(), QKVR.stride(0),
         U.data_ptr(), Vd.data_ptr(), _p(wbar), F.data_ptr(), F.stride(0), dout.data_ptr(), outp.data_ptr(),
         mstat.data_ptr(), den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
         dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF), 0 if dF is None else dF.stride(0), int(accumulate_dF),

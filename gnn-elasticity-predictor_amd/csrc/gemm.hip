@@ -40,6 +40,7 @@ struct GemmParams {
   int64_t kchunk;
   float* ws;
   int vecA, vecB;
+  int reduce_batch;  // sum the batch into one output: K loop runs over (batch, k), K % BK == 0
 };
 
 // Loads one operand tile (ROWS x BK) into registers.  KC: load along k (general strides,
@@ -144,13 +145,19 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int64_t tiles_n = (p.N + BN - 1) / BN;
   const int64_t tile = blockIdx.x;
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-  const int64_t b = blockIdx.z / p.split_k;
+  const int64_t b = p.reduce_batch ? 0 : blockIdx.z / p.split_k;
   const int sidx = blockIdx.z % p.split_k;
+  const int64_t Ktot = p.reduce_batch ? p.K * p.batch : p.K;
   const int64_t kb = (int64_t)sidx * p.kchunk;
-  const int64_t ke = min(p.K, kb + p.kchunk);
+  const int64_t ke = min(Ktot, kb + p.kchunk);
 
   const float* A = p.A + b * p.sab;
   const float* B = p.B + b * p.sbb;
+  // (batch, local k) of a global k index; identity unless the batch is reduced
+  auto tileA = [&](int64_t k0) { return p.reduce_batch ? p.A + (k0 / p.K) * p.sab : A; };
+  auto tileB = [&](int64_t k0) { return p.reduce_batch ? p.B + (k0 / p.K) * p.sbb : B; };
+  auto kloc = [&](int64_t k0) { return p.reduce_batch ? k0 % p.K : k0; };
+  auto kend = [&](int64_t k0) { return p.reduce_batch ? p.K : ke; };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
 
@@ -165,8 +172,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   TileLoader<BM, A_KC> la;
   TileLoader<BN, B_KC> lb;
   // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
-  la.load(A, p.sam, p.sak, m0, p.M, kb, ke, p.vecA);
-  lb.load(B, p.sbn, p.sbk, n0, p.N, kb, ke, p.vecB);
+  la.load(tileA(kb), p.sam, p.sak, m0, p.M, kloc(kb), kend(kb), p.vecA);
+  lb.load(tileB(kb), p.sbn, p.sbk, n0, p.N, kloc(kb), kend(kb), p.vecB);
   la.store(smem);
   lb.store(smem + LA);
   __syncthreads();
@@ -175,8 +182,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   for (int64_t k0 = kb; k0 < ke; k0 += BK) {
     const bool more = k0 + BK < ke;
     if (more) {
-      la.load(A, p.sam, p.sak, m0, p.M, k0 + BK, ke, p.vecA);
-      lb.load(B, p.sbn, p.sbk, n0, p.N, k0 + BK, ke, p.vecB);
+      la.load(tileA(k0 + BK), p.sam, p.sak, m0, p.M, kloc(k0 + BK), kend(k0 + BK), p.vecA);
+      lb.load(tileB(k0 + BK), p.sbn, p.sbk, n0, p.N, kloc(k0 + BK), kend(k0 + BK), p.vecB);
     }
     const float* As = smem + cur * (LA + LB);
     const float* Bs = As + LA;
@@ -213,7 +220,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         const int64_t row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= p.M) continue;
         if (p.split_k > 1) {
-          p.ws[(((int64_t)sidx * p.batch + b) * p.M + row) * p.N + col] = acc[i][j][r];
+          p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
         } else {
           p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
         }
@@ -222,13 +229,24 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 }
 
 __global__ void splitk_reduce_kernel(GemmParams p) {
-  const int64_t total = p.batch * p.M * p.N;
+  const int64_t total = (p.reduce_batch ? 1 : p.batch) * p.M * p.N;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t col = i % p.N;
     const int64_t row = (i / p.N) % p.M;
     const int64_t b = i / (p.N * p.M);
-    float s = 0.f;
-    for (int k = 0; k < p.split_k; ++k) s += p.ws[(((int64_t)k * p.batch + b) * p.M + row) * p.N + col];
+    const int64_t nb = p.reduce_batch ? 1 : p.batch;
+    const int64_t stride = nb * p.M * p.N;
+    const float* w = p.ws + (b * p.M + row) * p.N + col;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 3 < p.split_k; k += 4) {
+      s0 += w[(int64_t)k * stride];
+      s1 += w[(int64_t)(k + 1) * stride];
+      s2 += w[(int64_t)(k + 2) * stride];
+      s3 += w[(int64_t)(k + 3) * stride];
+    }
+    for (; k < p.split_k; ++k) s0 += w[(int64_t)k * stride];
+    const float s = (s0 + s1) + (s2 + s3);
     p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, s);
   }
 }
@@ -273,6 +291,13 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   p.bias2 = a->bias2; p.sb2_b = a->sb2_b;
   p.mask = a->mask; p.smk_m = a->smk_m; p.smk_n = a->smk_n;
   p.alpha = a->alpha; p.beta = a->beta; p.relu = a->relu;
+  p.reduce_batch = a->reduce_batch && a->batch > 1;
+  if (p.reduce_batch && a->K % BK != 0) {
+    set_error("gemm: reduce_batch needs K %% %d == 0 (K=%lld)", BK, (long long)a->K);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  const int64_t Ktot = p.reduce_batch ? a->K * a->batch : a->K;
+  const int64_t nbatch_out = p.reduce_batch ? 1 : a->batch;
   int split = a->split_k < 1 ? 1 : a->split_k;
   if (a->K == 0) split = 1;
   // A is "k-contiguous" unless it is contiguous along m only.
@@ -282,30 +307,30 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
                : (a->sak % 4 == 0 && a->sab % 4 == 0 && aligned16(a->A));
   p.vecB = bkc ? (a->sbk == 1 && a->sbn % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B))
                : (a->sbk % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B));
-  int64_t kchunk = (a->K + split - 1) / split;
+  int64_t kchunk = (Ktot + split - 1) / split;
   kchunk = (kchunk + BK - 1) / BK * BK;
   if (kchunk == 0) kchunk = BK;
-  split = (int)((a->K + kchunk - 1) / kchunk);
+  split = (int)((Ktot + kchunk - 1) / kchunk);
   if (split < 1) split = 1;
   p.kchunk = kchunk;
   p.split_k = split;
   p.ws = a->workspace;
-  if (split > 1 && (!a->workspace || a->workspace_elems < (int64_t)split * a->batch * a->M * a->N)) {
-    set_error("gemm: split_k=%d needs %lld workspace floats", split, (long long)split * a->batch * a->M * a->N);
+  if (split > 1 && (!a->workspace || a->workspace_elems < (int64_t)split * nbatch_out * a->M * a->N)) {
+    set_error("gemm: split_k=%d needs %lld workspace floats", split, (long long)split * nbatch_out * a->M * a->N);
     return ALIGNN_E_WORKSPACE;
   }
   // Tile choice: 128x128 for large problems, 64-wide on a small dimension.
   const int bm = a->M >= 128 ? 128 : 64;
   const int bn = a->N >= 128 ? 128 : 64;
   const int64_t tiles = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
-  dim3 grid((unsigned)tiles, 1, (unsigned)(a->batch * split));
+  dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * split));
   if (bm == 128 && bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, s);
   else if (bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, s);
   else if (bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, s);
   else dispatch_layout<64, 64>(p, akc, bkc, grid, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (split > 1) {
-    int64_t total = a->batch * a->M * a->N;
+    int64_t total = nbatch_out * a->M * a->N;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");

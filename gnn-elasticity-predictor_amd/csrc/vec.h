@@ -55,55 +55,53 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
-// All-reduce H per-lane partials over the 64 lanes; every lane receives all H sums.
-// H == 4: transpose-reduce (2 + 1 exchanges halve the live values, then 4 plain butterfly steps)
-// and 4 readlanes — 7 shuffles instead of 24.
+__device__ __forceinline__ float f_bits(unsigned u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ unsigned u_bits(float f) { return __builtin_bit_cast(unsigned, f); }
+
+// x summed over its 16-lane row (every lane of the row gets the sum): DPP quad_perm xor1, xor2,
+// row_half_mirror, row_mirror — each fused into a v_add_f32_dpp.
+__device__ __forceinline__ float row_sum16(float x) {
+  x += f_bits((unsigned)__builtin_amdgcn_update_dpp(0, (int)u_bits(x), 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+  x += f_bits((unsigned)__builtin_amdgcn_update_dpp(0, (int)u_bits(x), 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+  x += f_bits((unsigned)__builtin_amdgcn_update_dpp(0, (int)u_bits(x), 0x141, 0xF, 0xF, true));  // row_half_mirror
+  x += f_bits((unsigned)__builtin_amdgcn_update_dpp(0, (int)u_bits(x), 0x140, 0xF, 0xF, true));  // row_mirror
+  return x;
+}
+
+// All-reduce N per-lane partials over the 64 lanes and broadcast: afterwards every lane holds all
+// N sums (wave-uniform).  Select-free transpose-reduction: v_permlane32_swap pairs value i with
+// value i+P/2 across the two wave halves (lanes < 32 keep the first half of the values, lanes >= 32
+// the second), v_permlane16_swap does the same across rows of 16, then each remaining value is
+// summed within its row by DPP and row r's values are read out with v_readlane.
+// N = 16: 12 swaps + 12 adds + 16 DPP adds + 16 readlanes (vs 96 shuffles for 16 butterflies).
+template <int N>
+__device__ __forceinline__ void reduce_bcast(float (&v)[N], int lane) {
+  (void)lane;
+  constexpr int P = (N + 3) / 4 * 4;
+  float a[P / 2];
+#pragma unroll
+  for (int i = 0; i < P / 2; ++i) {
+    const float x = i < N ? v[i] : 0.f;
+    const float y = (i + P / 2) < N ? v[i + P / 2] : 0.f;
+    const auto r = __builtin_amdgcn_permlane32_swap(u_bits(x), u_bits(y), false, false);
+    a[i] = f_bits(r[0]) + f_bits(r[1]);
+  }
+  float b[P / 4];
+#pragma unroll
+  for (int i = 0; i < P / 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u_bits(a[i]), u_bits(a[i + P / 4]), false, false);
+    b[i] = row_sum16(f_bits(r[0]) + f_bits(r[1]));
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < P / 4; ++i)
+      if (r * (P / 4) + i < N) v[r * (P / 4) + i] = readlane_f(b[i], 16 * r);
+}
+
 template <int H>
 __device__ __forceinline__ void reduce_heads(float (&p)[H], int lane) {
-  if constexpr (H == 4) {
-    const bool hi = lane >= 32;
-    // step xor 32: keep heads {0,1} (lo) or {2,3} (hi)
-    float send0 = hi ? p[0] : p[2];
-    float send1 = hi ? p[1] : p[3];
-    float keep0 = hi ? p[2] : p[0];
-    float keep1 = hi ? p[3] : p[1];
-    keep0 += __shfl_xor(send0, 32, 64);
-    keep1 += __shfl_xor(send1, 32, 64);
-    // step xor 16: keep one head
-    const bool b4 = (lane >> 4) & 1;
-    float send = b4 ? keep0 : keep1;
-    float v = b4 ? keep1 : keep0;
-    v += __shfl_xor(send, 16, 64);
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    // lane groups: 0-15 head 0, 16-31 head 1, 32-47 head 2, 48-63 head 3
-    p[0] = readlane_f(v, 0);
-    p[1] = readlane_f(v, 16);
-    p[2] = readlane_f(v, 32);
-    p[3] = readlane_f(v, 48);
-  } else if constexpr (H == 2) {
-    const bool hi = lane >= 32;
-    float send = hi ? p[0] : p[1];
-    float v = hi ? p[1] : p[0];
-    v += __shfl_xor(send, 32, 64);
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    p[0] = readlane_f(v, 0);
-    p[1] = readlane_f(v, 32);
-  } else if constexpr (H == 1) {
-    float v = p[0];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    p[0] = readlane_f(v, 0);
-  } else {
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float v = p[h];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      p[h] = readlane_f(v, 0);
-    }
-  }
+  reduce_bcast<H>(p, lane);
 }
 
 // Branch-free select of element `idx` (runtime, per lane) of a small register array.

@@ -39,7 +39,8 @@ const char* alignn_last_error(void);
  * with A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn], C(m,n) = C[m*scm + n*scn].
  * Fast path: (sak == 1 or sam == 1) and (sbk == 1 or sbn == 1); others fall back to scalar loads.
  * split_k > 1 accumulates fp32 partial slabs in `workspace` (>= split_k*batch*M*N floats) and
- * reduces them in a second kernel in fixed order.
+ * reduces them in a second kernel in fixed order.  reduce_batch = 1 sums the batch into C itself
+ * (used for weights shared by all layers, e.g. the folded angle-encoder projection).
  * ---------------------------------------------------------------------------------------- */
 typedef struct AlignnGemmArgs {
   int64_t M, N, K, batch;
@@ -54,6 +55,8 @@ typedef struct AlignnGemmArgs {
   int32_t relu;
   int32_t split_k;
   float* workspace; int64_t workspace_elems;
+  int32_t reduce_batch;   /* 1: C = sum over the batch (one output; K % 16 == 0) */
+  int32_t reserved;
 } AlignnGemmArgs;
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
@@ -98,9 +101,20 @@ int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, i
  * U, S, Vd, Sz: [n, H, D]; F rows of length D at stride ldf, row of edge position t is
  * feat_row[t] (or t when feat_row == NULL).  Stats mstat/den/sumA: [n, H].
  * Dropout on alpha (p = drop_p, training): keep mask from a counter hash of (seed, t, h).
+ *
+ * Schedule (may be NULL = every target node gets one wavefront): `light` nodes get one wave each,
+ * `heavy` nodes (long in-edge lists, e.g. the PyG lg_edge_index offset quirk) a
+ * workgroup of four waves that split the edges and merge in fixed order.  Every node must appear
+ * in exactly one of the two lists (nodes without in-edges too: their outputs are written as 0).
  * ---------------------------------------------------------------------------------------- */
+typedef struct AlignnSchedule {
+  const int32_t* light; int64_t n_light;
+  const int32_t* heavy; int64_t n_heavy;
+} AlignnSchedule;
+
 int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
                      const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
+                     const AlignnSchedule* sched,
                      const float* QKVR, int64_t ldq, const float* U, const float* wbar,
                      const float* F, int64_t ldf,
                      float* aggV, float* S, float* sumA, float* mstat, float* den,
@@ -112,11 +126,13 @@ int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
  *   Sz[d,h] = sum_t dzs f_t,  sigz[d,h] = sum_t dzs
  *   dz_e[t,h] = dzs, alpha_e[t,h] = alpha' (for the source-side pass)
  *   dF[row(t)] (+)= sum_h dzs u[d,h] + alpha' Vd[d,h]   (row(t) = feat_row[t] or t)
+ *   accumulate_dF: bit 0 = add to dF, bit 1 = multiply the result by (F[row(t)] > 0) (F is a
+ *   ReLU output, e.g. the angle-encoder hidden layer: its backward mask is applied in place)
  * given dout (gradient of the aggregated message, [n, D]), outp (the aggregated message),
  * Vd[d,h] = M_h^T dout[d,h]. */
 int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H,
                          const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
-                         const float* QKVR, int64_t ldq, const float* U, const float* Vd,
+                         const AlignnSchedule* sched, const float* QKVR, int64_t ldq, const float* U, const float* Vd,
                          const float* wbar, const float* F, int64_t ldf,
                          const float* dout, const float* outp, const float* mstat, const float* den,
                          float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,

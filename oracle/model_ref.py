@@ -64,7 +64,7 @@ def num_layers(st: Dict[str, torch.Tensor]) -> int:
     return l
 
 
-def hetero_forward(st, data, heads, dropout=0.0, training=False, return_shared=False):
+def hetero_forward(st, data, heads, dropout=0.0, training=False, return_shared=False, retain=None):
     """``HeteroAlignnRegressor.forward`` (train.py:537-586).  Returns (mean [B,T], logvar [B,T])."""
     hidden = st["base.node_encoder.2.weight"].size(0)
     node_state = _mlp2(data.x, st, "base.node_encoder.")
@@ -77,11 +77,20 @@ def hetero_forward(st, data, heads, dropout=0.0, training=False, return_shared=F
         angle_emb = _mlp2(data.lg_edge_attr, st, "base.angle_encoder.")
     else:
         angle_emb = torch.zeros(data.lg_edge_index.size(1), edge_state.size(-1), dtype=node_state.dtype)
+    if retain is not None:
+        edge_state.retain_grad()
+        retain["e0"] = edge_state
     for l in range(num_layers(st)):
         edge_state = edge_block(st, f"base.edge_blocks.{l}.", edge_state, data.lg_edge_index, angle_emb,
                                 heads, dropout, training)
+        if retain is not None:
+            edge_state.retain_grad()
+            retain[f"e{l + 1}"] = edge_state
         node_state = node_block(st, f"base.node_blocks.{l}.", node_state, data.edge_index, edge_state,
                                 heads, dropout, training)
+        if retain is not None:
+            node_state.retain_grad()
+            retain[f"h{l + 1}"] = node_state
     pooled = global_mean_pool(node_state, data.batch)
     global_x = data.global_x
     if global_x.dim() == 1:

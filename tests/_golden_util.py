@@ -40,3 +40,18 @@ def grad_scale(g, tag):
     """Largest |grad| over all parameters of a golden case (used as the floor for rel_err)."""
     import numpy as np
     return max(float(np.abs(v).max()) for k, v in g.items() if k.startswith(f"{tag}/grad/"))
+
+
+def norm_err(a, b, floor=0.0):
+    """||a-b||_F / max(||b||_F, floor): the gradient criterion.  A max-abs criterion is ill-posed for
+    gradients behind ReLUs: an activation within fp32 rounding of 0 can take the other side of the
+    kink than in the fp64 reference, which moves single gradient entries by O(1) relative."""
+    a = torch.as_tensor(a, dtype=torch.float64).detach().cpu()
+    b = torch.as_tensor(b, dtype=torch.float64).detach().cpu()
+    if a.numel() == 0:
+        return 0.0
+    return float((a - b).norm() / max(float(b.norm()), floor, 1e-30))
+
+
+def grad_norm_scale(grads):
+    return max(float(torch.as_tensor(v, dtype=torch.float64).norm()) for v in grads)
