@@ -14,7 +14,7 @@ import threading
 import torch  # noqa: F401  (must load torch's HIP runtime before the library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libalignn_hip.so")
+LIB_PATH = os.environ.get("ALIGNN_HIP_LIB") or os.path.join(_HERE, "libalignn_hip.so")  # override: kernel A/B runs
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
@@ -44,6 +44,12 @@ class Schedule(ctypes.Structure):
     _fields_ = [("light", c_vp), ("n_light", c_i64), ("heavy", c_vp), ("n_heavy", c_i64)]
 
 
+class EdgeEncoder(ctypes.Structure):
+    _fields_ = [("x", c_vp), ("ldx", c_i64), ("kin", c_i32), ("accumulate", c_i32),
+                ("w1", c_vp), ("b1", c_vp), ("dw1", c_vp), ("db1", c_vp),
+                ("workspace", c_vp), ("workspace_elems", c_i64)]
+
+
 _SIGNATURES = {
     "alignn_version": ([], c_i32),
     "alignn_last_error": ([], ctypes.c_char_p),
@@ -52,9 +58,10 @@ _SIGNATURES = {
     "alignn_graph_prep": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_gather_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
-                          c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_tconv_bwd_workspace": ([c_i32, c_i32, c_i32], c_i64),
     "alignn_tconv_bwd_dst": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
-                              c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                              c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                               c_i32, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_bwd_src": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                               c_i64, c_vp], c_i32),

@@ -201,15 +201,16 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
     ops.gemm(We.transpose(-1, -2), dwbar.unsqueeze(-1), gbp.unsqueeze(-1), reduce_batch=True)
 
 
-def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, feat_row,
+def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
-                  seed_blk: int):
-    """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None."""
+                  seed_blk: int, enc: Optional[ops.EdgeEncoder] = None):
+    """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
+    enc: edge features recomputed in-kernel from raw inputs (then F is None)."""
     n, D = X.shape
     C = D // H
     dev = X.device
     c = _Ctx()
-    c.X, c.F, c.feat_row = X, F, feat_row
+    c.X, c.F, c.feat_row, c.enc = X, F, feat_row, enc
     c.M, c.wbar = M, wbar
     with_proj = wbar is not None
     c.QKVR = torch.empty(n, 4 * D, device=dev)
@@ -221,7 +222,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, 
     c.sumA = torch.empty(n, H, device=dev)
     c.mstat = torch.empty(n, H, device=dev)
     c.den = torch.empty(n, H, device=dev)
-    ops.tconv_fwd(g, D, H, c.QKVR, c.U, c.wbar, F, feat_row, c.outp, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att)
+    ops.tconv_fwd(g, D, H, c.QKVR, c.U, c.wbar, F, feat_row, c.outp, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att,
+                  enc=enc)
     if with_proj:
         ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp.view(n, H, C).transpose(0, 1),
                  beta=1.0, rowscale=c.sumA.t(), bias2=c.wbar.view(H, C))
@@ -240,11 +242,12 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: torch.Tensor, 
 
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
-                   dwbar: Optional[torch.Tensor] = None) -> None:
+                   dwbar: Optional[torch.Tensor] = None, enc_grads=None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
-    (c.wbar set) the gradients of M and w̄ are written to dM / dwbar for :func:`proj_grads`."""
+    (c.wbar set) the gradients of M and w̄ are written to dM / dwbar for :func:`proj_grads`.
+    With an in-kernel edge encoder (c.enc), enc_grads = (dW1, db1) receive its gradients (+=)."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -260,8 +263,12 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     sigz = torch.empty(n, H, device=dev)
     dz_e = torch.empty(max(m, 1), H, device=dev)
     al_e = torch.empty(max(m, 1), H, device=dev)
+    enc = None
+    if c.enc is not None:
+        enc = ops.EdgeEncoder(c.enc.x, c.enc.w1, c.enc.b1, enc_grads[0], enc_grads[1], accumulate=True)
+        dF = None
     ops.tconv_bwd_dst(g, D, H, c.QKVR, c.U, Vd, c.wbar, c.F, c.feat_row, dout, c.outp, c.mstat, c.den,
-                      dQKVR[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att)
+                      dQKVR[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
     ops.tconv_bwd_src(g, D, H, c.QKVR, dout, dz_e, al_e, dQKVR[:, D:3 * D])
     Qh = c.QKVR[:, :D].view(n, H, C).permute(1, 2, 0)
     Oh = dout.view(n, H, C).permute(1, 2, 0)
@@ -293,6 +300,9 @@ class AlignnEngine:
         cfg.validate()
         self.cfg = cfg
         self.debug = None  # dict -> backward stores intermediate gradients (diagnostics only)
+        # recompute the angle hidden layer inside the line convs (kin <= 16) instead of materialising
+        # it: measured slower than streaming the materialised rows so far (occupancy-bound), so off
+        self.recompute_angle = False
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -337,13 +347,18 @@ class AlignnEngine:
         # w̄_l = W_edge,l b2 — exact algebra, so the [T, D] x [D, D] GEMM and its two
         # backward GEMMs never run.
         ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
-        if ctx.has_angle:
+        # With few raw angle inputs (kin <= 16) even the hidden layer is not materialised: the line
+        # convs recompute relu(W1 x_t + b1) per edge in-kernel (ops.EdgeEncoder).
+        ctx.angle_enc = None
+        a = None
+        if ctx.has_angle and self.recompute_angle and bc.xa.size(1) <= ops.ENC_MAX_KIN and T > 0:
+            ctx.angle_enc = ops.EdgeEncoder(bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"))
+        elif ctx.has_angle:
             a = torch.empty(T, D, device=dev)
             ops.gemm(bc.xa, P.enc("angle", 0, "weight").t(), a, bias=P.enc("angle", 0, "bias"), relu=True)
-            ctx.h1a = a
         else:
-            ctx.h1a, a = None, torch.zeros(T, D, device=dev)
-        ctx.a = a
+            a = torch.zeros(T, D, device=dev)
+        ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
         if T > 0 and E > 0 and L > 0 and ctx.has_angle:
             W2, b2 = P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias")
@@ -355,7 +370,7 @@ class AlignnEngine:
             if T > 0 and E > 0:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
-                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1))
+                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), enc=ctx.angle_enc)
             else:
                 c = None
             ctx.edge.append(c)
@@ -436,7 +451,8 @@ class AlignnEngine:
         dh = torch.empty(N, D, device=dev)
         ops.readout_pool_bwd(dfeats, bc.ptr, bc.batch_vec, dh, False, p_drop, site_seed(seed, 4 * L))
         de = torch.zeros(E, D, device=dev)
-        da = torch.empty(T, D, device=dev) if T > 0 else None
+        da = torch.empty(T, D, device=dev) if (T > 0 and ctx.angle_enc is None) else None
+        enc_grads = (G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias")) if ctx.angle_enc is not None else None
         da_written = False
         if E > 0 and L > 0:
             dM_all = torch.empty(L, D, D, device=dev)
@@ -459,7 +475,8 @@ class AlignnEngine:
                 # the last (l = 0) applies the ReLU mask in place
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
                 if line_proj:
-                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l])
+                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
+                                   enc_grads=enc_grads)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags)
                 da_written = True
@@ -471,7 +488,7 @@ class AlignnEngine:
             proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all, dwl_all,
                               G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
         # encoders
-        if ctx.has_angle and da_written:
+        if ctx.has_angle and da_written and ctx.angle_enc is None:
             ops.gemm(da.t(), bc.xa, G.enc("angle", 0, "weight"))  # da is the masked hidden-layer gradient
             ops.colsum(da, G.enc("angle", 0, "bias"))
         if ctx.h1e is not None:

@@ -183,7 +183,10 @@ class GraphCSR:
             deg = off[1:] - off[:-1]
             heavy_mask = deg > self.HEAVY_THRESHOLD
             idx = torch.arange(self.n, dtype=torch.int32)
-            light = idx[~heavy_mask].to(self.off_dst.device)
+            # light list: nodes with in-edges first, in-degree-0 nodes last (the kernels skip
+            # per-workgroup setup for items that start with an empty node)
+            light_mask = ~heavy_mask
+            light = torch.cat([idx[light_mask & (deg > 0)], idx[light_mask & (deg == 0)]]).to(self.off_dst.device)
             heavy = idx[heavy_mask].to(self.off_dst.device)
             sc = _lib.Schedule()
             sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
@@ -210,37 +213,91 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor
 # ------------------------------------------------------------------------------------------------
 # TransformerConv attention
 # ------------------------------------------------------------------------------------------------
-def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str) -> float:
-    """Compulsory HBM bytes of one launch (every operand touched once, ideal caching)."""
+def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, kin: int = 0) -> float:
+    """Compulsory HBM bytes of one launch (every operand touched once, ideal caching).  kin > 0:
+    edge features recomputed from kin raw inputs per edge (no [m, D] feature / gradient rows)."""
     f = 4.0
-    if kind == "fwd":   # Q,K,V + U + F rows + CSR in; aggV + S + 3 stats out
-        return f * (3 * n * D + n * H * D + m * D + 2 * m + n + n * D + n * H * D + 3 * n * H)
-    if kind == "bwd_dst":  # Q,K,V,U,Vd,dout,outp,F,stats in; dQ,Sz,sigz,dz,alpha,dF out
-        return f * (3 * n * D + 2 * n * H * D + 2 * n * D + m * D + 2 * n * H + 2 * m + n
-                    + n * D + n * H * D + n * H + 2 * m * H + m * D)
+    feat = m * kin if kin else m * D
+    if kind == "fwd":   # Q,K,V + U + edge features + CSR in; aggV + S + 3 stats out
+        return f * (3 * n * D + n * H * D + feat + 2 * m + n + n * D + n * H * D + 3 * n * H)
+    if kind == "bwd_dst":  # Q,K,V,U,Vd,dout,outp,features,stats in; dQ,Sz,sigz,dz,alpha(,dF) out
+        return f * (3 * n * D + 2 * n * H * D + 2 * n * D + feat + 2 * n * H + 2 * m + n
+                    + n * D + n * H * D + n * H + 2 * m * H + (0 if kin else m * D))
     return f * (2 * n * D + 2 * m * H + 2 * m + n + 2 * n * D)  # bwd_src
 
 
+ENC_MAX_KIN = 16
+
+
+class EdgeEncoder:
+    """Edge features recomputed in the attention kernels as relu(W1 x + b1) from kin <= 16 raw
+    inputs per edge (the angle encoder's hidden layer, train.py:353-356); see
+    ``AlignnEdgeEncoder`` in include/alignn_hip.h.  x is in edge-position (target-sorted) order.
+    For the backward, dw1/db1 receive the encoder gradients (accumulated)."""
+
+    def __init__(self, x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
+                 dw1: Optional[torch.Tensor] = None, db1: Optional[torch.Tensor] = None, accumulate: bool = True):
+        _require(x, "enc.x")
+        _require(w1, "enc.w1")
+        _require(b1, "enc.b1")
+        if x.dim() != 2 or x.stride(1) != 1 or not w1.is_contiguous() or not (1 <= x.size(1) <= ENC_MAX_KIN):
+            raise ValueError("EdgeEncoder: x must be [m, kin] row-major with 1 <= kin <= 16, w1 contiguous")
+        self.x, self.w1, self.b1, self.dw1, self.db1, self.accumulate = x, w1, b1, dw1, db1, accumulate
+        self.kin = x.size(1)
+
+    def struct(self, D: int = 0, H: int = 0, backward: bool = False) -> "_lib.EdgeEncoder":
+        ws, n_ws = None, 0
+        if backward:
+            n_ws = _enc_ws_elems(D, H, self.kin)
+            ws = WS.get("tconv_enc", n_ws, self.x.device)
+        return _lib.EdgeEncoder(self.x.data_ptr(), self.x.stride(0), self.kin, 1 if self.accumulate else 0,
+                                self.w1.data_ptr(), self.b1.data_ptr(), _p(self.dw1), _p(self.db1),
+                                None if ws is None else ws.data_ptr(), n_ws)
+
+
+_ENC_WS = {}
+
+
+def _enc_ws_elems(D: int, H: int, kin: int) -> int:
+    key = (D, H, kin)
+    if key not in _ENC_WS:
+        n = int(_lib.lib().alignn_tconv_bwd_workspace(D, H, kin))
+        if n < 0:
+            raise ValueError(f"tconv: unsupported encoder shape D={D} H={H} kin={kin}")
+        _ENC_WS[key] = max(n, 1)
+    return _ENC_WS[key]
+
+
 def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, wbar: Optional[torch.Tensor],
-              F: torch.Tensor, feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float, seed: int):
-    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd"), lambda: check(_lib.lib().alignn_tconv_fwd(
-        g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row), ctypes.byref(g.schedule()),
-                                      QKVR.data_ptr(), QKVR.stride(0), U.data_ptr(), _p(wbar), F.data_ptr(),
-                                      F.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(),
-                                      den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
-          "alignn_tconv_fwd"))
+              F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float,
+              seed: int, enc: Optional[EdgeEncoder] = None):
+    es = None if enc is None else enc.struct()
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd", enc.kin if enc else 0),
+                     lambda: check(_lib.lib().alignn_tconv_fwd(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
+                         ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0), U.data_ptr(), _p(wbar),
+                         _p(F), 0 if F is None else F.stride(0), None if es is None else ctypes.byref(es),
+                         aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(), den.data_ptr(),
+                         float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_fwd"))
 
 
 def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, dout, outp, mstat, den,
-                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: int, drop_p: float, seed: int):
-    """accumulate_dF: bit 0 add into dF, bit 1 apply the ReLU mask (F > 0) to the result."""
-    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_dst"), lambda: check(_lib.lib().alignn_tconv_bwd_dst(
-        g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row), ctypes.byref(g.schedule()),
-        QKVR.data_ptr(), QKVR.stride(0),
-        U.data_ptr(), Vd.data_ptr(), _p(wbar), F.data_ptr(), F.stride(0), dout.data_ptr(), outp.data_ptr(),
-        mstat.data_ptr(), den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
-        dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF), 0 if dF is None else dF.stride(0), int(accumulate_dF),
-        float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_bwd_dst"))
+                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: int, drop_p: float, seed: int,
+                  enc: Optional[EdgeEncoder] = None):
+    """accumulate_dF: bit 0 add into dF, bit 1 apply the ReLU mask (F > 0) to the result.  With an
+    edge encoder, F/dF are unused and the encoder gradients go to enc.dw1/enc.db1."""
+    es = None if enc is None else enc.struct(D, H, backward=True)
+    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0,
+                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", enc.kin if enc else 0),
+                     lambda: check(_lib.lib().alignn_tconv_bwd_dst(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
+                         ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0),
+                         U.data_ptr(), Vd.data_ptr(), _p(wbar), _p(F), 0 if F is None else F.stride(0),
+                         None if es is None else ctypes.byref(es), dout.data_ptr(), outp.data_ptr(),
+                         mstat.data_ptr(), den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(),
+                         sigz.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF),
+                         0 if dF is None else dF.stride(0), int(accumulate_dF), float(drop_p),
+                         int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_bwd_dst"))
 
 
 def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):

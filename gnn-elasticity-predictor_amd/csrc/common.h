@@ -76,26 +76,33 @@ inline DropParams make_drop(float p, uint64_t seed) {
 }
 
 // Fixed-order column reduction of a [rows, N] partial buffer: out[c] (+)= sum_r part[r*N + c].
-// Grid: ceil(N/64) blocks of 256 threads (4 row-lanes x 64 columns).
+// Grid: ceil(N/64) blocks of 1024 threads (16 row-lanes x 64 columns); each thread keeps four
+// independent partial sums (rows ty, ty+16, ty+32, ty+48 of every 64-row stride) so 16 x 4 loads
+// per column are in flight; the 16 row-lanes are combined in lane order.
+constexpr int kColsumThreads = 1024;
 template <int kUnused = 0>
-__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int rows, int64_t N,
-                                                           float* __restrict__ out, int acc) {
-  __shared__ float red[4][64];
+__global__ __launch_bounds__(1024) void colsum_stage2(const float* __restrict__ part, int rows, int64_t N,
+                                                      float* __restrict__ out, int acc) {
+  __shared__ float red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + tx;
-  float s0 = 0.f, s1 = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int r = ty;
-    for (; r + 4 < rows; r += 8) {
+    for (; r + 48 < rows; r += 64) {
       s0 += part[(int64_t)r * N + col];
-      s1 += part[(int64_t)(r + 4) * N + col];
+      s1 += part[(int64_t)(r + 16) * N + col];
+      s2 += part[(int64_t)(r + 32) * N + col];
+      s3 += part[(int64_t)(r + 48) * N + col];
     }
-    for (; r < rows; r += 4) s0 += part[(int64_t)r * N + col];
+    for (; r < rows; r += 16) s0 += part[(int64_t)r * N + col];
   }
-  red[ty][tx] = s0 + s1;
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (ty == 0 && col < N) {
-    const float t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][tx];
     out[col] = acc ? out[col] + t : t;
   }
 }

@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     }
 }
 
-__global__ void splitk_reduce_kernel(GemmParams p) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   const int64_t total = (p.reduce_batch ? 1 : p.batch) * p.M * p.N;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t col = i % p.N;
@@ -237,17 +237,16 @@ __global__ void splitk_reduce_kernel(GemmParams p) {
     const int64_t nb = p.reduce_batch ? 1 : p.batch;
     const int64_t stride = nb * p.M * p.N;
     const float* w = p.ws + (b * p.M + row) * p.N + col;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    // eight independent chains (partial k goes to chain k % 8), combined in a fixed tree
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int k = 0;
-    for (; k + 3 < p.split_k; k += 4) {
-      s0 += w[(int64_t)k * stride];
-      s1 += w[(int64_t)(k + 1) * stride];
-      s2 += w[(int64_t)(k + 2) * stride];
-      s3 += w[(int64_t)(k + 3) * stride];
+    for (; k + 7 < p.split_k; k += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += w[(int64_t)(k + j) * stride];
     }
-    for (; k < p.split_k; ++k) s0 += w[(int64_t)k * stride];
-    const float s = (s0 + s1) + (s2 + s3);
-    p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, s);
+    for (int j = 0; k < p.split_k; ++k, ++j) s[j] += w[(int64_t)k * stride];
+    const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, t);
   }
 }
 
@@ -383,13 +382,13 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
   nparts = (int)((M + rows_per - 1) / rows_per);
   if (nparts < 1) nparts = 1;
   if (M == 0) {
-    hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(256), 0, s, workspace, 0, N, out, accumulate);
+    hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, 0, N, out, accumulate);
     ALIGNN_LAUNCH_CHECK("colsum_stage2");
     return ALIGNN_OK;
   }
   hipLaunchKernelGGL(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
   ALIGNN_LAUNCH_CHECK("colsum_stage1");
-  hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(256), 0, s, workspace, nparts, N, out, accumulate);
+  hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
   ALIGNN_LAUNCH_CHECK("colsum_stage2");
   return ALIGNN_OK;
 }

@@ -367,7 +367,8 @@ extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int6
   // adjacent in memory (the flat gradient layout), else three.
   const unsigned strips3 = (unsigned)((3 * D + 63) / 64), strips1 = (unsigned)((D + 63) / 64);
   if (d_ln_w == d_wbeta + 3 * D && d_ln_b == d_ln_w + D) {
-    hipLaunchKernelGGL(colsum_stage2<0>, dim3((unsigned)((5 * D + 63) / 64)), dim3(256), 0, s, workspace, nwaves,
+    hipLaunchKernelGGL(colsum_stage2<0>, dim3((unsigned)((5 * D + 63) / 64)), dim3(kColsumThreads), 0, s, workspace,
+                       nwaves,
                        (int64_t)5 * D, d_wbeta, 1);
   } else {
     // partial rows are 5D wide: view them through column offsets with row stride 5D via a

@@ -11,47 +11,101 @@
 // u_dh = M_h^T Q_dh (one n-row GEMM outside), and the message term sum_t alpha W_e,h f_t as
 // M_h (sum_t alpha f_t) — so the per-edge work is D-wide dot products and axpys, and the m-row GEMM
 // disappears.  M_h = W_e,h P and w̄ = W_e p fold the atom graph's edge_proj (P, p) in as well.
+//
+// Edge encoder (line graph): the edge features are the angle encoder's hidden layer
+// f_t = relu(W1 x_t + b1) (train.py:353-356 first Linear+ReLU; its second Linear is folded into M).
+// With KM > 0 the kernels recompute f_t from the raw angle features x_t (kin <= KM <= 16 floats per
+// edge; W1/b1 staged in LDS) instead of reading a materialised [m, D] array, and the backward
+// accumulates dW1 = sum_t (relu'(.) * g_t) x_t^T and db1 = sum_t relu'(.) * g_t directly (g_t = the
+// gradient w.r.t. f_t), so the [m, D] hidden layer and its gradient never exist in HBM.
 #include "common.h"
 #include "vec.h"
 
 namespace alignn {
 
-struct FwdParams {
-  int64_t n, m;
-  int D;
-  const int32_t* off;
-  const int32_t* src_at;
-  const int32_t* feat_row;
-  const float* QKVR; int64_t ldq;
-  const float* U;
-  const float* wbar;
-  const float* F; int64_t ldf;
-  float* aggV; float* S; float* sumA; float* mstat; float* den;
-  DropParams drop;
-};
-
 // ---------------------------------------------------------------------------------------------
-// Work decomposition.  Light target nodes (in-degree <= heavy threshold) get one wave each, four
-// per workgroup; heavy nodes get a whole workgroup whose four waves take interleaved groups of PF
-// edges and merge their partial states through LDS in fixed wave order (deterministic).  The
-// node lists come from the caller (AlignnSchedule); without one every node is light.
-// Edges are processed in groups of PF: the operands of the next group are in flight while the
-// current one computes, and the PF*H (or 2*PF*H) per-head dot products of a group are reduced
-// across the wave together (reduce_bcast: one transpose-reduction, then scalar broadcasts).
+// Work decomposition.  Work items: heavy target nodes (in-degree > threshold, one workgroup of
+// four waves each; the waves take interleaved groups of PF edges and merge through LDS in fixed
+// wave order), then light nodes four per workgroup (one wave each).  Heavy items come first so
+// the long ones start early.  Workgroups walk the item list with a grid stride (a bounded grid
+// when per-workgroup gradient partials are produced).  Edges are processed in groups of PF: the
+// operands of the next group are in flight while the current one computes, and the PF*H (or
+// 2*PF*H) per-head dot products of a group are reduced across the wave together (reduce_bcast).
 // ---------------------------------------------------------------------------------------------
 constexpr int PF = 4;
+
+struct Sched {
+  const int32_t* light;
+  int64_t n_light;
+  const int32_t* heavy;
+  int64_t n_heavy;
+  __host__ __device__ int64_t items() const { return n_heavy + (n_light + 3) / 4; }
+};
+
+struct EncParams {
+  const float* x; int64_t ldx; int kin;
+  const float* w1;  // [D, kin] (nn.Linear weight)
+  const float* b1;  // [D]
+};
 
 template <int VPL>
 struct EdgeSlot {
   float k[VPL], v[VPL], f[VPL];
+  float xr;  // KM > 0: lane (l & 15) holds x_t[l & 15]
 };
 
-template <int VPL>
+template <int VPL, int KM>
 __device__ __forceinline__ void load_edge(EdgeSlot<VPL>& e, const float* __restrict__ QKVR, int64_t ldq, int D,
-                                          const float* __restrict__ F, int64_t ldf, int64_t src, int64_t row, int j0) {
-  vload(QKVR + src * ldq + D + j0, e.k);
-  vload(QKVR + src * ldq + 2 * D + j0, e.v);
-  vload(F + row * ldf + j0, e.f);
+                                          const float* __restrict__ F, int64_t ldf, const EncParams& en,
+                                          int64_t src, int64_t row, int j0, bool act, int lane) {
+  if (act) {
+    vload(QKVR + src * ldq + D + j0, e.k);
+    vload(QKVR + src * ldq + 2 * D + j0, e.v);
+    if constexpr (KM == 0) vload(F + row * ldf + j0, e.f);
+  }
+  if constexpr (KM > 0) {
+    const int c = lane & 15;
+    e.xr = c < en.kin ? en.x[row * en.ldx + c] : 0.f;
+  }
+}
+
+// Encoder weights in LDS: ew[k*D + j] = W1[j, k] (zero rows for kin <= k < KM), ew[KM*D + j] = b1[j].
+template <int VPL, int KM>
+__device__ __forceinline__ void stage_enc(float* ew, const EncParams& en, int D) {
+  for (int i = threadIdx.x; i < (KM + 1) * D; i += blockDim.x) {
+    const int k = i / D, j = i - k * D;
+    float v;
+    if (k < KM) v = k < en.kin ? en.w1[(int64_t)j * en.kin + k] : 0.f;
+    else v = en.b1[j];
+    ew[i] = v;
+  }
+  __syncthreads();
+}
+
+// f[j] = relu(b1 + W1 x_j) for the PF slots of a group (this lane's VPL features).
+template <int VPL, int KM>
+__device__ __forceinline__ void enc_group(const float* ew, int D, int j0, EdgeSlot<VPL> (&ring)[PF]) {
+  float b[VPL];
+  vload(ew + KM * D + j0, b);
+#pragma unroll
+  for (int j = 0; j < PF; ++j)
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) ring[j].f[i] = b[i];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    float w[VPL];
+    vload(ew + k * D + j0, w);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const float xk = readlane_f(ring[j].xr, k);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) ring[j].f[i] = fmaf(xk, w[i], ring[j].f[i]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PF; ++j)
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) ring[j].f[i] = fmaxf(ring[j].f[i], 0.f);
 }
 
 // Dropout multipliers of one edge group: lane l < PF*H evaluates the hash of (t0 + l/H, l%H);
@@ -67,46 +121,48 @@ __device__ __forceinline__ void group_dropout(const DropParams& dp, int32_t t0, 
     for (int h = 0; h < H; ++h) mul[j][h] = dp.active ? readlane_f(mine, j * H + h) : 1.0f;
 }
 
-// Wave offset inside a heavy node's workgroup (0 for light nodes): groups g = wsub, wsub+nw, ...
-struct NodeWork {
-  int64_t d;
-  int wsub, nw;
-  bool valid;
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+#ifdef ALIGNN_TCONV_WPE
+#define TCONV_ATTR __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALIGNN_TCONV_WPE, ALIGNN_TCONV_WPE)))
+#else
+#define TCONV_ATTR __launch_bounds__(256)
+#endif
+
+// =============================================================================================
+// Forward
+// =============================================================================================
+struct FwdParams {
+  int64_t n, m;
+  int D;
+  const int32_t* off;
+  const int32_t* src_at;
+  const int32_t* feat_row;
+  const float* QKVR; int64_t ldq;
+  const float* U;
+  const float* wbar;
+  const float* F; int64_t ldf;
+  float* aggV; float* S; float* sumA; float* mstat; float* den;
+  DropParams drop;
 };
 
-__device__ __forceinline__ NodeWork node_work(const int32_t* __restrict__ nodes, int64_t count, int heavy) {
-  NodeWork w;
-  const int wave = threadIdx.x >> 6;
-  if (heavy) {
-    w.valid = blockIdx.x < count;
-    w.d = w.valid ? (int64_t)(nodes ? nodes[blockIdx.x] : blockIdx.x) : 0;
-    w.wsub = wave;
-    w.nw = 4;
-  } else {
-    const int64_t i = (int64_t)blockIdx.x * 4 + wave;
-    w.valid = i < count;
-    w.d = w.valid ? (int64_t)(nodes ? nodes[i] : i) : 0;
-    w.wsub = 0;
-    w.nw = 1;
-  }
-  return w;
-}
+template <int VPL, int H>
+constexpr int fwd_merge_floats() { return 4 * 64 * (3 * H + H * VPL + VPL); }
 
-template <int VPL, int H, bool HEAVY>
-__global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p, const int32_t* __restrict__ nodes, int64_t count) {
+// One target node.  heavy: all four waves of the workgroup call this for the same d (wsub =
+// wave, nw = 4) and merge; light: one wave (wsub = 0, nw = 1).
+template <int VPL, int H, int KM>
+__device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en, const float* ew, float* merge,
+                                         int64_t d, int wsub, int nw, bool heavy) {
   constexpr int NS = 3 * H + H * VPL + VPL;  // per-lane merge state: m, s, sa, accS, accV
-  __shared__ float merge[HEAVY ? 4 * 64 * NS : 1];
-  constexpr bool heavy = HEAVY;
   const int lane = threadIdx.x & 63;
-  const NodeWork w = node_work(nodes, count, heavy);
-  if (!heavy && !w.valid) return;  // wave-uniform
-  const int64_t d = w.d;
+  const int wave = threadIdx.x >> 6;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = w.valid ? p.off[d] : 0, end = w.valid ? p.off[d + 1] : 0;
+  const int32_t beg = p.off[d], end = p.off[d + 1];
 
   float accS[H][VPL], accV[VPL];
   float m[H], s[H], sa[H];
@@ -119,7 +175,7 @@ __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p, const int32
   }
   vzero(accV);
 
-  const int32_t first = beg + w.wsub * PF, stride = w.nw * PF;
+  const int32_t first = beg + wsub * PF, stride = nw * PF;
   if (first < end) {
     float q[VPL], u[H][VPL];
     vzero(q);
@@ -146,11 +202,14 @@ __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p, const int32
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
+      ring[j].xr = 0.f;
       const int32_t t = first + j;
-      if (t < end && act)
-        load_edge(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)p.src_at[t], p.feat_row ? (int64_t)p.feat_row[t] : t, j0);
+      if (t < end)
+        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[t],
+                           p.feat_row ? (int64_t)p.feat_row[t] : t, j0, act, lane);
     }
     for (int32_t tb = first; tb < end; tb += stride) {
+      if constexpr (KM > 0) enc_group<VPL, KM>(ew, D, j0, ring);
       // all PF*H scores of the group in one reduction
       float pr[PF * H];
 #pragma unroll
@@ -200,16 +259,15 @@ __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p, const int32
 #pragma unroll
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
-        if (tn < end && act)
-          load_edge(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)p.src_at[tn],
-                    p.feat_row ? (int64_t)p.feat_row[tn] : tn, j0);
+        if (tn < end)
+          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[tn],
+                             p.feat_row ? (int64_t)p.feat_row[tn] : tn, j0, act, lane);
       }
     }
   }
 
   if (heavy) {
     // merge the four waves' states in wave order through LDS (wave 0 writes the node)
-    const int wave = threadIdx.x >> 6;
     float* my = merge + (wave * 64 + lane) * NS;
 #pragma unroll
     for (int h = 0; h < H; ++h) {
@@ -222,63 +280,105 @@ __global__ __launch_bounds__(256) void tconv_fwd_kernel(FwdParams p, const int32
 #pragma unroll
     for (int i = 0; i < VPL; ++i) my[3 * H + H * VPL + i] = accV[i];
     __syncthreads();
-    if (wave != 0 || !w.valid) return;
+    if (wave == 0) {
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float mt = -INFINITY;
-      for (int v = 0; v < 4; ++v) mt = fmaxf(mt, merge[(v * 64 + lane) * NS + h]);
-      s[h] = 0.f;
-      sa[h] = 0.f;
+      for (int h = 0; h < H; ++h) {
+        float mt = -INFINITY;
+        for (int v = 0; v < 4; ++v) mt = fmaxf(mt, merge[(v * 64 + lane) * NS + h]);
+        s[h] = 0.f;
+        sa[h] = 0.f;
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) accS[h][i] = 0.f;
+        for (int i = 0; i < VPL; ++i) accS[h][i] = 0.f;
+        for (int v = 0; v < 4; ++v) {
+          const float* o = merge + (v * 64 + lane) * NS;
+          const float f = (o[h] == -INFINITY) ? 0.f : __expf(o[h] - mt);
+          s[h] = fmaf(o[H + h], f, s[h]);
+          sa[h] = fmaf(o[2 * H + h], f, sa[h]);
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(o[3 * H + h * VPL + i], f, accS[h][i]);
+        }
+        m[h] = mt;
+      }
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) accV[i] = 0.f;
       for (int v = 0; v < 4; ++v) {
         const float* o = merge + (v * 64 + lane) * NS;
-        const float f = (o[h] == -INFINITY) ? 0.f : __expf(o[h] - mt);
-        s[h] = fmaf(o[H + h], f, s[h]);
-        sa[h] = fmaf(o[2 * H + h], f, sa[h]);
+        const float mh = o[hl];
+        const float f = (mh == -INFINITY) ? 0.f : __expf(mh - pick<H>(m, hl));
 #pragma unroll
-        for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(o[3 * H + h * VPL + i], f, accS[h][i]);
+        for (int i = 0; i < VPL; ++i) accV[i] = fmaf(o[3 * H + H * VPL + i], f, accV[i]);
       }
-      m[h] = mt;
-    }
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) accV[i] = 0.f;
-    for (int v = 0; v < 4; ++v) {
-      const float* o = merge + (v * 64 + lane) * NS;
-      const float mh = o[hl];
-      const float f = (mh == -INFINITY) ? 0.f : __expf(mh - pick<H>(m, hl));
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) accV[i] = fmaf(o[3 * H + H * VPL + i], f, accV[i]);
     }
   }
 
-  float inv[H], dn[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    dn[h] = s[h] + 1e-16f;
-    inv[h] = 1.0f / dn[h];
-  }
-  if (act) {
+  if (!heavy || wave == 0) {
+    float inv[H], dn[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
+      dn[h] = s[h] + 1e-16f;
+      inv[h] = 1.0f / dn[h];
+    }
+    if (act) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float o[VPL];
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) o[i] = accS[h][i] * inv[h];
+        vstore(p.S + (d * H + h) * D + j0, o);
+      }
+      const float il = pick<H>(inv, hl);
       float o[VPL];
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) o[i] = accS[h][i] * inv[h];
-      vstore(p.S + (d * H + h) * D + j0, o);
+      for (int i = 0; i < VPL; ++i) o[i] = accV[i] * il;
+      vstore(p.aggV + d * D + j0, o);
     }
-    const float il = pick<H>(inv, hl);
-    float o[VPL];
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) o[i] = accV[i] * il;
-    vstore(p.aggV + d * D + j0, o);
+    if (lane < H) {
+      p.sumA[d * H + lane] = pick<H>(sa, lane) * pick<H>(inv, lane);
+      p.mstat[d * H + lane] = pick<H>(m, lane);
+      p.den[d * H + lane] = pick<H>(dn, lane);
+    }
   }
-  if (lane < H) {
-    p.sumA[d * H + lane] = pick<H>(sa, lane) * pick<H>(inv, lane);
-    p.mstat[d * H + lane] = pick<H>(m, lane);
-    p.den[d * H + lane] = pick<H>(dn, lane);
+  if (heavy) __syncthreads();  // merge buffer free for the next item
+}
+
+template <int VPL, int H, int KM>
+__global__ TCONV_ATTR void tconv_fwd_kernel(FwdParams p, Sched sc, EncParams en) {
+  constexpr int MERGE = fwd_merge_floats<VPL, H>();
+  constexpr int ENCW = KM > 0 ? (KM + 1) * 64 * VPL : 0;
+  __shared__ float smem[MERGE + ENCW];
+  float* ew = smem + MERGE;
+  const int wave = threadIdx.x >> 6;
+  const int64_t items = sc.items();
+  bool staged = false;
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    if constexpr (KM > 0) {
+      // stage the encoder weights once, and only for items with edges (light lists end with the
+      // in-degree-0 nodes, so an item whose first node is empty is empty)
+      if (!staged) {
+        bool need = it < sc.n_heavy;
+        if (!need) {
+          const int64_t i0 = (it - sc.n_heavy) * 4;
+          const int64_t d0 = sc.light ? (int64_t)sc.light[i0] : i0;
+          need = p.off[d0 + 1] > p.off[d0];
+        }
+        if (need) {
+          stage_enc<VPL, KM>(ew, en, p.D);
+          staged = true;
+        }
+      }
+    }
+    if (it < sc.n_heavy) {
+      fwd_node<VPL, H, KM>(p, en, ew, smem, (int64_t)sc.heavy[it], wave, 4, true);
+    } else {
+      const int64_t i = (it - sc.n_heavy) * 4 + wave;
+      if (i < sc.n_light) fwd_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)sc.light[i] : i, 0, 1, false);
+    }
   }
 }
 
+// =============================================================================================
+// Backward, target side
+// =============================================================================================
 struct BwdDstParams {
   int64_t n, m;
   int D;
@@ -301,21 +401,31 @@ struct BwdDstParams {
   DropParams drop;
 };
 
-template <int VPL, int H, bool HEAVY>
-__global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p, const int32_t* __restrict__ nodes,
-                                                            int64_t count) {
+template <int VPL, int H, int KM>
+constexpr int bwd_merge_floats() {
+  return cmax(4 * 64 * (H + H * VPL + VPL), KM > 0 ? (KM + 1) * 64 * VPL : 0);
+}
+
+template <int VPL, int KM>
+struct EncAcc {
+  float w[KM > 0 ? KM : 1][VPL];
+  float b[VPL];
+};
+
+template <int VPL, int H, int KM>
+__device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncParams& en, const float* ew,
+                                             float* merge, int64_t d, int wsub, int nw, bool heavy,
+                                             EncAcc<VPL, KM>& ea) {
   constexpr int NS = H + H * VPL + VPL;  // per-lane merge state: sigz, Sz, dq
-  __shared__ float merge[HEAVY ? 4 * 64 * NS : 1];
   const int lane = threadIdx.x & 63;
-  const NodeWork w = node_work(nodes, count, HEAVY);
-  if (!HEAVY && !w.valid) return;
-  const int64_t d = w.d;
+  const int wave = threadIdx.x >> 6;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = w.valid ? p.off[d] : 0, end = w.valid ? p.off[d + 1] : 0;
+  const int32_t beg = p.off[d], end = p.off[d + 1];
+  const bool do_dF = KM == 0 && p.dF != nullptr;
 
   float sz[H][VPL], sgz[H], dqa[VPL];
 #pragma unroll
@@ -325,7 +435,7 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p, cons
   }
   vzero(dqa);
 
-  const int32_t first = beg + w.wsub * PF, stride = w.nw * PF;
+  const int32_t first = beg + wsub * PF, stride = nw * PF;
   if (first < end) {
     float q[VPL], go[VPL], u[H][VPL], vd[H][VPL];
     vzero(q); vzero(go);
@@ -367,23 +477,24 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p, cons
     }
 
     EdgeSlot<VPL> ring[PF];
-    float old[PF][VPL];  // dF rows being accumulated (prefetched with the operands)
+    float old[KM == 0 ? PF : 1][VPL];  // dF rows being accumulated (prefetched with the operands)
     int64_t rows[PF];
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
-      vzero(old[j]);
+      ring[j].xr = 0.f;
+      if constexpr (KM == 0) vzero(old[j]);
       const int32_t t = first + j;
       rows[j] = 0;
       if (t < end) {
         rows[j] = p.feat_row ? p.feat_row[t] : t;
-        if (act) {
-          load_edge(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)p.src_at[t], rows[j], j0);
-          if (p.dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
-        }
+        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[t], rows[j], j0, act, lane);
+        if constexpr (KM == 0)
+          if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
       }
     }
     for (int32_t tb = first; tb < end; tb += stride) {
+      if constexpr (KM > 0) enc_group<VPL, KM>(ew, D, j0, ring);
       float pr[2 * PF * H];  // [score | d alpha'] per (edge, head)
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
@@ -416,17 +527,36 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p, cons
           const float dzl = pick<H>(dz, hl);
 #pragma unroll
           for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, ring[j].k[i], dqa[i]);
-          if (p.dF && act) {
-            float df[VPL];
+          if constexpr (KM > 0) {
+            // g = relu'(.) * sum_h (dz u + alpha' Vd); dW1 += g x^T, db1 += g
+            float g[VPL];
 #pragma unroll
             for (int i = 0; i < VPL; ++i) {
-              float a = old[j][i];
+              float a = 0.f;
 #pragma unroll
               for (int h = 0; h < H; ++h) a = fmaf(dz[h], u[h][i], fmaf(al[h], vd[h][i], a));
-              // bit 1: F is a ReLU output (angle-encoder hidden) -> apply its backward mask now
-              df[i] = (p.acc_dF & 2) ? (ring[j].f[i] > 0.f ? a : 0.f) : a;
+              g[i] = ring[j].f[i] > 0.f ? a : 0.f;
+              ea.b[i] += g[i];
             }
-            vstore(p.dF + rows[j] * p.lddf + j0, df);
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+              const float xk = readlane_f(ring[j].xr, k);
+#pragma unroll
+              for (int i = 0; i < VPL; ++i) ea.w[k][i] = fmaf(xk, g[i], ea.w[k][i]);
+            }
+          } else {
+            if (do_dF && act) {
+              float df[VPL];
+#pragma unroll
+              for (int i = 0; i < VPL; ++i) {
+                float a = old[j][i];
+#pragma unroll
+                for (int h = 0; h < H; ++h) a = fmaf(dz[h], u[h][i], fmaf(al[h], vd[h][i], a));
+                // bit 1: F is a ReLU output (angle-encoder hidden) -> apply its backward mask now
+                df[i] = (p.acc_dF & 2) ? (ring[j].f[i] > 0.f ? a : 0.f) : a;
+              }
+              vstore(p.dF + rows[j] * p.lddf + j0, df);
+            }
           }
           if (lane < H) {
             p.dz_e[(int64_t)t * H + lane] = pick<H>(dz, lane);
@@ -436,16 +566,15 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p, cons
         const int32_t tn = tb + stride + j;
         if (tn < end) {
           rows[j] = p.feat_row ? p.feat_row[tn] : tn;
-          if (act) {
-            load_edge(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)p.src_at[tn], rows[j], j0);
-            if (p.dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
-          }
+          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[tn], rows[j], j0, act,
+                             lane);
+          if constexpr (KM == 0)
+            if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
         }
       }
     }
   }
-  if (HEAVY) {
-    const int wave = threadIdx.x >> 6;
+  if (heavy) {
     float* my = merge + (wave * 64 + lane) * NS;
 #pragma unroll
     for (int h = 0; h < H; ++h) {
@@ -456,27 +585,125 @@ __global__ __launch_bounds__(256) void tconv_bwd_dst_kernel(BwdDstParams p, cons
 #pragma unroll
     for (int i = 0; i < VPL; ++i) my[H + H * VPL + i] = dqa[i];
     __syncthreads();
-    if (wave != 0 || !w.valid) return;
-    for (int v = 1; v < 4; ++v) {
-      const float* o = merge + (v * 64 + lane) * NS;
+    if (wave == 0) {
+      for (int v = 1; v < 4; ++v) {
+        const float* o = merge + (v * 64 + lane) * NS;
 #pragma unroll
-      for (int h = 0; h < H; ++h) {
-        sgz[h] += o[h];
+        for (int h = 0; h < H; ++h) {
+          sgz[h] += o[h];
 #pragma unroll
-        for (int i = 0; i < VPL; ++i) sz[h][i] += o[H + h * VPL + i];
+          for (int i = 0; i < VPL; ++i) sz[h][i] += o[H + h * VPL + i];
+        }
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) dqa[i] += o[H + H * VPL + i];
       }
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) dqa[i] += o[H + H * VPL + i];
     }
   }
-  if (act) {
-    vstore(p.dq + d * p.lddq + j0, dqa);
+  if (!heavy || wave == 0) {
+    if (act) {
+      vstore(p.dq + d * p.lddq + j0, dqa);
 #pragma unroll
-    for (int h = 0; h < H; ++h) vstore(p.Sz + (d * H + h) * D + j0, sz[h]);
+      for (int h = 0; h < H; ++h) vstore(p.Sz + (d * H + h) * D + j0, sz[h]);
+    }
+    if (lane < H) p.sigz[d * H + lane] = pick<H>(sgz, lane);
   }
-  if (lane < H) p.sigz[d * H + lane] = pick<H>(sgz, lane);
+  if (heavy) __syncthreads();
 }
 
+// part (KM > 0): per-workgroup encoder-gradient partials, [gridDim.x][(KM+1)*D] (rows k < KM: dW1
+// column k, row KM: db1), summed in fixed order by enc_grad_reduce.
+template <int VPL, int H, int KM>
+__global__ TCONV_ATTR void tconv_bwd_dst_kernel(BwdDstParams p, Sched sc, EncParams en,
+                                                            float* __restrict__ part) {
+  constexpr int MERGE = bwd_merge_floats<VPL, H, KM>();
+  constexpr int ENCW = KM > 0 ? (KM + 1) * 64 * VPL : 0;
+  __shared__ float smem[MERGE + ENCW];
+  float* ew = smem + MERGE;
+  if constexpr (KM > 0) stage_enc<VPL, KM>(ew, en, p.D);
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  EncAcc<VPL, KM> ea;
+  if constexpr (KM > 0) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) vzero(ea.w[k]);
+    vzero(ea.b);
+  }
+  const int64_t items = sc.items();
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    if (it < sc.n_heavy) {
+      bwd_dst_node<VPL, H, KM>(p, en, ew, smem, (int64_t)sc.heavy[it], wave, 4, true, ea);
+    } else {
+      const int64_t i = (it - sc.n_heavy) * 4 + wave;
+      if (i < sc.n_light)
+        bwd_dst_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)sc.light[i] : i, 0, 1, false, ea);
+    }
+  }
+  if constexpr (KM > 0) {
+    // fixed-order merge of the four waves' accumulators, then one partial row block per workgroup
+    constexpr int RS = 64 * VPL;  // LDS row stride
+    const int j0 = lane * VPL;
+    __syncthreads();
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int k = 0; k <= KM; ++k) {
+          const float* a = k < KM ? ea.w[k < KM ? k : 0] : ea.b;
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) {
+            float* r = smem + k * RS + j0 + i;
+            *r = (w == 0 ? 0.f : *r) + a[i];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    const int D = p.D;
+    float* out = part + (int64_t)blockIdx.x * (KM + 1) * D;
+    for (int i = threadIdx.x; i < (KM + 1) * D; i += blockDim.x) {
+      const int k = i / D, j = i - k * D;
+      out[i] = smem[k * RS + j];
+    }
+  }
+}
+
+// dW1[j, k] (+)= sum_g part[g][k*D + j] (k < kin), db1[j] (+)= sum_g part[g][KM*D + j].
+// Grid: ceil((kin+1)*D / 64) blocks of 4 row-lanes x 64 outputs.
+__global__ __launch_bounds__(1024) void enc_grad_reduce(const float* __restrict__ part, int G, int KM, int D, int kin,
+                                                        float* __restrict__ dw1, float* __restrict__ db1, int acc) {
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
+  const bool ok = c < (int64_t)(kin + 1) * D;
+  const int k = ok ? (int)(c / D) : 0;
+  const int j = (int)(c - (int64_t)k * D);
+  const int kk = k < kin ? k : KM;
+  const int64_t stride = (int64_t)(KM + 1) * D;
+  const float* src = part + kk * D + j;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (ok) {
+    int g = ty;
+    for (; g + 48 < G; g += 64) {
+      s0 += src[g * stride];
+      s1 += src[(g + 16) * stride];
+      s2 += src[(g + 32) * stride];
+      s3 += src[(g + 48) * stride];
+    }
+    for (; g < G; g += 16) s0 += src[g * stride];
+  }
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ty == 0 && ok) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][tx];
+    float* dst = k < kin ? dw1 + (int64_t)j * kin + k : db1 + j;
+    *dst = acc ? *dst + t : t;
+  }
+}
+
+// =============================================================================================
+// Backward, source side: dK, dV per source node over the by-source CSR (no atomics)
+// =============================================================================================
 struct BwdSrcParams {
   int64_t n, m;
   int D;
@@ -535,7 +762,7 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Dispatch on (VPL, H)
+// Dispatch on (VPL, H, KM)
 // ---------------------------------------------------------------------------------------------
 
 static int vpl_for(int D) {
@@ -546,7 +773,15 @@ static int vpl_for(int D) {
   return 0;
 }
 
-#define ALIGNN_DISPATCH(VPL_, H_, FN, ...)                                           \
+static int km_for(int kin) {
+  if (kin <= 0) return 0;
+  if (kin <= 8) return 8;
+  if (kin <= 12) return 12;
+  if (kin <= 16) return 16;
+  return -1;
+}
+
+#define ALIGNN_DISPATCH_VH(VPL_, H_, FN, ...)                                        \
   do {                                                                               \
     if (VPL_ == 1 && H_ == 1) FN<1, 1>(__VA_ARGS__);                                 \
     else if (VPL_ == 1 && H_ == 2) FN<1, 2>(__VA_ARGS__);                            \
@@ -563,31 +798,96 @@ static int vpl_for(int D) {
     else { set_error("tconv: unsupported D/H combination"); return ALIGNN_E_UNSUPPORTED; } \
   } while (0)
 
-struct Sched {
-  const int32_t* light;
-  int64_t n_light;
-  const int32_t* heavy;
-  int64_t n_heavy;
-};
+static int g_num_cus = 0;
+static int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cus = n;
+  }
+  return g_num_cus;
+}
+
+// Resident workgroups of a kernel on the whole device (bounded grid for the partial-producing
+// backward: its partial count, hence the reduction order, is fixed per device and shape).
+template <typename K>
+static int64_t resident_wgs(K kernel) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  return (int64_t)per_cu * num_cus();
+}
+
+template <int VPL, int H, int KM>
+static int64_t bwd_grid_cap() {
+  static int64_t cap = 0;
+  if (cap == 0) cap = resident_wgs(tconv_bwd_dst_kernel<VPL, H, KM>);
+  return cap;
+}
 
 template <int VPL, int H>
-static void launch_fwd(const FwdParams& p, const Sched& sc, hipStream_t s) {
-  if (sc.n_light > 0)
-    hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, false>), dim3((unsigned)((sc.n_light + 3) / 4)), dim3(256), 0, s, p,
-                       sc.light, sc.n_light);
-  if (sc.n_heavy > 0)
-    hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, true>), dim3((unsigned)sc.n_heavy), dim3(256), 0, s, p, sc.heavy,
-                       sc.n_heavy);
+static void launch_fwd(const FwdParams& p, const Sched& sc, const EncParams& en, int km, hipStream_t s) {
+  const int64_t items = sc.items();
+  if (items == 0) return;
+  const dim3 grid((unsigned)items), block(256);
+  switch (km) {
+    case 0: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 0>), grid, block, 0, s, p, sc, en); break;
+    case 8: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 8>), grid, block, 0, s, p, sc, en); break;
+    case 12: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 12>), grid, block, 0, s, p, sc, en); break;
+    default: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 16>), grid, block, 0, s, p, sc, en); break;
+  }
 }
+
+template <int VPL, int H, int KM>
+static int launch_bwd_dst_km(const BwdDstParams& p, const Sched& sc, const EncParams& en,
+                             const AlignnEdgeEncoder* enc, hipStream_t s) {
+  const int64_t items = sc.items();
+  if (KM == 0) {
+    if (items > 0)
+      hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, 0>), dim3((unsigned)items), dim3(256), 0, s, p, sc, en,
+                         nullptr);
+    return ALIGNN_OK;
+  }
+  const int64_t per = (int64_t)(KM + 1) * p.D;
+  int64_t G = bwd_grid_cap<VPL, H, KM>();
+  if (items < G) G = items;
+  if (G < 1) G = 1;
+  if (enc->workspace_elems / per < G) G = enc->workspace_elems / per;
+  if (G < 1 || enc->workspace == nullptr) {
+    set_error("tconv_bwd_dst: encoder workspace too small (%lld floats, need >= %lld)",
+              (long long)enc->workspace_elems, (long long)per);
+    return ALIGNN_E_WORKSPACE;
+  }
+  hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, KM>), dim3((unsigned)G), dim3(256), 0, s, p, sc, en,
+                     enc->workspace);
+  const int64_t outs = (int64_t)(en.kin + 1) * p.D;
+  hipLaunchKernelGGL(enc_grad_reduce, dim3((unsigned)((outs + 63) / 64)), dim3(1024), 0, s, enc->workspace, (int)G,
+                     KM, p.D, en.kin, enc->dw1, enc->db1, enc->accumulate);
+  return ALIGNN_OK;
+}
+
 template <int VPL, int H>
-static void launch_bwd_dst(const BwdDstParams& p, const Sched& sc, hipStream_t s) {
-  if (sc.n_light > 0)
-    hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, false>), dim3((unsigned)((sc.n_light + 3) / 4)), dim3(256), 0, s,
-                       p, sc.light, sc.n_light);
-  if (sc.n_heavy > 0)
-    hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, true>), dim3((unsigned)sc.n_heavy), dim3(256), 0, s, p, sc.heavy,
-                       sc.n_heavy);
+static int launch_bwd_dst(const BwdDstParams& p, const Sched& sc, const EncParams& en, const AlignnEdgeEncoder* enc,
+                          int km, hipStream_t s) {
+  switch (km) {
+    case 0: return launch_bwd_dst_km<VPL, H, 0>(p, sc, en, enc, s);
+    case 8: return launch_bwd_dst_km<VPL, H, 8>(p, sc, en, enc, s);
+    case 12: return launch_bwd_dst_km<VPL, H, 12>(p, sc, en, enc, s);
+    default: return launch_bwd_dst_km<VPL, H, 16>(p, sc, en, enc, s);
+  }
 }
+
+template <int VPL, int H>
+static int64_t bwd_ws_elems(int km, int D) {
+  switch (km) {
+    case 0: return 0;
+    case 8: return bwd_grid_cap<VPL, H, 8>() * 9 * D;
+    case 12: return bwd_grid_cap<VPL, H, 12>() * 13 * D;
+    default: return bwd_grid_cap<VPL, H, 16>() * 17 * D;
+  }
+}
+
 template <int VPL, int H>
 static void launch_bwd_src(const BwdSrcParams& p, hipStream_t s) {
   hipLaunchKernelGGL((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
@@ -610,7 +910,7 @@ static Sched make_sched(const AlignnSchedule* sc, int64_t n) {
 }
 
 static int check_dims(int D, int H) {
-  if (D <= 0 || H <= 0 || D % H != 0 || vpl_for(D) == 0 || (D < 64 && D % 1 != 0)) {
+  if (D <= 0 || H <= 0 || D % H != 0 || vpl_for(D) == 0) {
     set_error("tconv: unsupported hidden=%d heads=%d (hidden in {<=64,128,256,512}, divisible by heads)", D, H);
     return ALIGNN_E_UNSUPPORTED;
   }
@@ -622,33 +922,78 @@ static int check_dims(int D, int H) {
   return ALIGNN_OK;
 }
 
+// Validates the edge-feature source: exactly one of F (materialised rows) or enc (recomputed).
+static int edge_source(const float* F, const AlignnEdgeEncoder* enc, EncParams& en, int& km) {
+  en = EncParams{nullptr, 0, 0, nullptr, nullptr};
+  km = 0;
+  if (enc) {
+    km = km_for(enc->kin);
+    if (km <= 0 || !enc->x || !enc->w1 || !enc->b1 || enc->ldx < enc->kin) {
+      set_error("tconv: edge encoder needs 1 <= kin <= 16, x (ldx >= kin), w1 and b1 (kin=%d)", (int)enc->kin);
+      return ALIGNN_E_BAD_SHAPE;
+    }
+    en = EncParams{enc->x, enc->ldx, enc->kin, enc->w1, enc->b1};
+    return ALIGNN_OK;
+  }
+  if (!F) {
+    set_error("tconv: edge features F are required when no edge encoder is given");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  return ALIGNN_OK;
+}
+
 }  // namespace alignn
 
 using namespace alignn;
 
 extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
                                 const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
-                                const float* QKVR, int64_t ldq,
-                                const float* U, const float* wbar, const float* F, int64_t ldf, float* aggV,
-                                float* S, float* sumA, float* mstat, float* den, float drop_p, uint64_t seed,
-                                void* stream) {
+                                const float* QKVR, int64_t ldq, const float* U, const float* wbar, const float* F,
+                                int64_t ldf, const AlignnEdgeEncoder* enc, float* aggV, float* S, float* sumA,
+                                float* mstat, float* den, float drop_p, uint64_t seed, void* stream) {
   int rc = check_dims(D, H);
   if (rc) return rc;
   if (n == 0) return ALIGNN_OK;
+  EncParams en;
+  int km;
+  if ((rc = edge_source(F, enc, en, km))) return rc;
   FwdParams p{n, m, D, off_dst, src_at, feat_row, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
               make_drop(drop_p, seed)};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
   const Sched sc = make_sched(sched, n);
-  ALIGNN_DISPATCH(vpl, H, launch_fwd, p, sc, s);
+  ALIGNN_DISPATCH_VH(vpl, H, launch_fwd, p, sc, en, km, s);
   ALIGNN_LAUNCH_CHECK("tconv_fwd_kernel");
   return ALIGNN_OK;
 }
 
+extern "C" int64_t alignn_tconv_bwd_workspace(int32_t D, int32_t H, int32_t kin) {
+  if (check_dims(D, H)) return -1;
+  const int km = km_for(kin);
+  if (km < 0) return -1;
+  const int vpl = vpl_for(D);
+  int64_t r = -1;
+#define ALIGNN_WS(V_, H_) r = bwd_ws_elems<V_, H_>(km, D)
+  if (vpl == 1 && H == 1) ALIGNN_WS(1, 1);
+  else if (vpl == 1 && H == 2) ALIGNN_WS(1, 2);
+  else if (vpl == 1 && H == 4) ALIGNN_WS(1, 4);
+  else if (vpl == 2 && H == 1) ALIGNN_WS(2, 1);
+  else if (vpl == 2 && H == 2) ALIGNN_WS(2, 2);
+  else if (vpl == 2 && H == 4) ALIGNN_WS(2, 4);
+  else if (vpl == 4 && H == 1) ALIGNN_WS(4, 1);
+  else if (vpl == 4 && H == 2) ALIGNN_WS(4, 2);
+  else if (vpl == 4 && H == 4) ALIGNN_WS(4, 4);
+  else if (vpl == 4 && H == 8) ALIGNN_WS(4, 8);
+  else if (vpl == 8 && H == 4) ALIGNN_WS(8, 4);
+  else if (vpl == 8 && H == 8) ALIGNN_WS(8, 8);
+#undef ALIGNN_WS
+  return r;
+}
+
 extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
                                     const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
-                                    const float* QKVR, int64_t ldq,
-                                    const float* U, const float* Vd, const float* wbar, const float* F, int64_t ldf,
+                                    const float* QKVR, int64_t ldq, const float* U, const float* Vd,
+                                    const float* wbar, const float* F, int64_t ldf, const AlignnEdgeEncoder* enc,
                                     const float* dout, const float* outp, const float* mstat, const float* den,
                                     float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
                                     float* dF, int64_t lddf, int32_t accumulate_dF, float drop_p, uint64_t seed,
@@ -656,12 +1001,39 @@ extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, 
   int rc = check_dims(D, H);
   if (rc) return rc;
   if (n == 0) return ALIGNN_OK;
+  EncParams en;
+  int km;
+  if ((rc = edge_source(F, enc, en, km))) return rc;
+  if (enc && (!enc->dw1 || !enc->db1)) {
+    set_error("tconv_bwd_dst: edge encoder gradients dw1/db1 are required");
+    return ALIGNN_E_BAD_SHAPE;
+  }
   BwdDstParams p{n, m, D, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den,
-                 dq, lddq, Sz, sigz, dz_e, alpha_e, dF, lddf, accumulate_dF, make_drop(drop_p, seed)};
+                 dq, lddq, Sz, sigz, dz_e, alpha_e, enc ? nullptr : dF, lddf, accumulate_dF,
+                 make_drop(drop_p, seed)};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
   const Sched sc = make_sched(sched, n);
-  ALIGNN_DISPATCH(vpl, H, launch_bwd_dst, p, sc, s);
+  int lrc = ALIGNN_OK;
+#define ALIGNN_BWD(V_, H_) lrc = launch_bwd_dst<V_, H_>(p, sc, en, enc, km, s)
+  if (vpl == 1 && H == 1) ALIGNN_BWD(1, 1);
+  else if (vpl == 1 && H == 2) ALIGNN_BWD(1, 2);
+  else if (vpl == 1 && H == 4) ALIGNN_BWD(1, 4);
+  else if (vpl == 2 && H == 1) ALIGNN_BWD(2, 1);
+  else if (vpl == 2 && H == 2) ALIGNN_BWD(2, 2);
+  else if (vpl == 2 && H == 4) ALIGNN_BWD(2, 4);
+  else if (vpl == 4 && H == 1) ALIGNN_BWD(4, 1);
+  else if (vpl == 4 && H == 2) ALIGNN_BWD(4, 2);
+  else if (vpl == 4 && H == 4) ALIGNN_BWD(4, 4);
+  else if (vpl == 4 && H == 8) ALIGNN_BWD(4, 8);
+  else if (vpl == 8 && H == 4) ALIGNN_BWD(8, 4);
+  else if (vpl == 8 && H == 8) ALIGNN_BWD(8, 8);
+  else {
+    set_error("tconv: unsupported D/H combination");
+    return ALIGNN_E_UNSUPPORTED;
+  }
+#undef ALIGNN_BWD
+  if (lrc) return lrc;
   ALIGNN_LAUNCH_CHECK("tconv_bwd_dst_kernel");
   return ALIGNN_OK;
 }
@@ -676,7 +1048,7 @@ extern "C" int alignn_tconv_bwd_src(int64_t n, int64_t m, int32_t D, int32_t H, 
   BwdSrcParams p{n, m, D, off_src, pos_src, dst_at, QKVR, ldq, dout, dz_e, alpha_e, dKV, lddkv};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
-  ALIGNN_DISPATCH(vpl, H, launch_bwd_src, p, s);
+  ALIGNN_DISPATCH_VH(vpl, H, launch_bwd_src, p, s);
   ALIGNN_LAUNCH_CHECK("tconv_bwd_src_kernel");
   return ALIGNN_OK;
 }

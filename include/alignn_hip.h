@@ -112,11 +112,27 @@ typedef struct AlignnSchedule {
   const int32_t* heavy; int64_t n_heavy;
 } AlignnSchedule;
 
+/* Edge encoder (optional, replaces F): the edge features are the hidden layer of a
+ * Linear->ReLU edge encoder, f_t = relu(W1 x[row(t)] + b1) — the angle encoder's first Linear
+ * (train.py:353-356, applied at train.py:553-554; its second Linear is folded into M).  The kernels
+ * recompute f_t from the kin raw features (1 <= kin <= 16) instead of reading an [m, D] array.
+ * x: [*, ldx]; w1: [D, kin] (nn.Linear weight); b1: [D].
+ * Backward only: dw1 [D, kin] and db1 [D] receive the encoder's weight gradients (+= when
+ * accumulate), computed in-kernel from the gradient w.r.t. f_t and the ReLU mask — the [m, D]
+ * gradient is never written.  workspace: >= alignn_tconv_bwd_workspace(D, H, kin) floats (fewer
+ * lowers the kernel's parallelism; at least (KM+1)*D with KM = kin rounded up to 8/12/16). */
+typedef struct AlignnEdgeEncoder {
+  const float* x; int64_t ldx; int32_t kin; int32_t accumulate;
+  const float* w1; const float* b1;
+  float* dw1; float* db1;
+  float* workspace; int64_t workspace_elems;
+} AlignnEdgeEncoder;
+
 int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
                      const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
                      const AlignnSchedule* sched,
                      const float* QKVR, int64_t ldq, const float* U, const float* wbar,
-                     const float* F, int64_t ldf,
+                     const float* F, int64_t ldf, const AlignnEdgeEncoder* enc,
                      float* aggV, float* S, float* sumA, float* mstat, float* den,
                      float drop_p, uint64_t seed, void* stream);
 
@@ -129,15 +145,20 @@ int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
  *   accumulate_dF: bit 0 = add to dF, bit 1 = multiply the result by (F[row(t)] > 0) (F is a
  *   ReLU output, e.g. the angle-encoder hidden layer: its backward mask is applied in place)
  * given dout (gradient of the aggregated message, [n, D]), outp (the aggregated message),
- * Vd[d,h] = M_h^T dout[d,h]. */
+ * Vd[d,h] = M_h^T dout[d,h].  With an edge encoder, dF is not touched (the encoder's gradients go
+ * to enc->dw1/db1 instead). */
 int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H,
                          const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
                          const AlignnSchedule* sched, const float* QKVR, int64_t ldq, const float* U, const float* Vd,
-                         const float* wbar, const float* F, int64_t ldf,
+                         const float* wbar, const float* F, int64_t ldf, const AlignnEdgeEncoder* enc,
                          const float* dout, const float* outp, const float* mstat, const float* den,
                          float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
                          float* dF, int64_t lddf, int32_t accumulate_dF,
                          float drop_p, uint64_t seed, void* stream);
+
+/* Workspace (floats) alignn_tconv_bwd_dst needs for an edge encoder with kin inputs at full
+ * parallelism on the current device; 0 without encoder, -1 for unsupported arguments. */
+int64_t alignn_tconv_bwd_workspace(int32_t D, int32_t H, int32_t kin);
 
 /* Backward, source side (replaces the atomic index_add of the gather backward): per source node
  *   dK[s] = sum_{t: src(t)=s} dzs_t Q[dst(t)],  dV[s] = sum alpha'_t dout[dst(t)]

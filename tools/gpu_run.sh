@@ -1,7 +1,7 @@
 #!/bin/bash
 # Runs GPU steps in order; stops at the first step whose exit code signals a crash/timeout
 # (anything other than 0 = ok and 1 = ordinary test failure).  Usage: tools/gpu_run.sh STEP...
-# STEP is one of: tests smoke bench prof
+# STEP is one of: tests tests-all smoke bench bench-quick probes rocprof pmc-fetch pmc-write
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 for step in "$@"; do
@@ -13,6 +13,8 @@ for step in "$@"; do
     bench-quick) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline) ;;
     probes) cmd=(timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --dump-probes gpurun_out/probes.json) ;;
     rocprof) cmd=(timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline) ;;
+    pmc-fetch) cmd=(timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline) ;;
+    pmc-write) cmd=(timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "=== $step: ${cmd[*]}" | tee -a gpurun_out/run.log
