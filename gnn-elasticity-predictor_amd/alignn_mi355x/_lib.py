@@ -36,7 +36,8 @@ class GemmArgs(ctypes.Structure):
         ("alpha", c_f32), ("beta", c_f32),
         ("relu", c_i32), ("split_k", c_i32),
         ("workspace", c_vp), ("workspace_elems", c_i64),
-        ("reduce_batch", c_i32), ("reserved", c_i32),
+        ("reduce_batch", c_i32), ("tile", c_i32),
+        ("c_rows", c_vp),
     ]
 
 
@@ -53,10 +54,13 @@ class EdgeEncoder(ctypes.Structure):
 _SIGNATURES = {
     "alignn_version": ([], c_i32),
     "alignn_last_error": ([], ctypes.c_char_p),
+    "alignn_set_step_seed": ([c_vp], None),
     "alignn_gemm_f32": ([ctypes.POINTER(GemmArgs), c_vp], c_i32),
+    "alignn_gemm_workspace": ([ctypes.POINTER(GemmArgs)], c_i64),
     "alignn_colsum_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
     "alignn_graph_prep": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_gather_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
+    "alignn_scatter_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp], c_i32),
     "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_bwd_workspace": ([c_i32, c_i32, c_i32], c_i64),

@@ -122,6 +122,10 @@ class BatchCache:
         self.T = int(batch.lg_edge_index.size(1))
         self.ag = ops.GraphCSR(batch.edge_index, self.N)
         self.lg = ops.GraphCSR(batch.lg_edge_index, self.E)
+        if validate:
+            self.ag.check_indices("edge_index")
+            self.lg.check_indices("lg_edge_index")
+        self.lg = self._compact(self.lg, batch.lg_edge_index, self.E)
         la = batch.lg_edge_attr
         self.angle_dim = int(la.size(-1)) if la.dim() == 2 else 0
         if self.T > 0 and la.numel() > 0:
@@ -139,9 +143,29 @@ class BatchCache:
             cnt = torch.bincount(self.batch_vec, minlength=B)
             self.ptr = torch.cat([cnt.new_zeros(1), cnt.cumsum(0)])
         self.B = int(self.ptr.numel() - 1)
-        if validate:
-            self.ag.check_indices("edge_index")
-            self.lg.check_indices("lg_edge_index")
+
+    # A line-graph node (bond) with neither in- nor out-edges contributes nothing to the attention
+    # (empty segment, never a source).  Under PyG's lg_edge_index offset rule most
+    # bonds of a batch are such nodes (B=32: 2,580 of 23,040 active), so the line graph is re-indexed
+    # over the active bonds and the per-node GEMMs of the line convs run on those rows only.
+    COMPACT_FRACTION = 0.75
+
+    @classmethod
+    def _compact(cls, g: ops.GraphCSR, edge_index: torch.Tensor, n: int) -> ops.GraphCSR:
+        if n == 0 or g.m == 0:
+            return g
+        deg = (g.off_dst[1:] - g.off_dst[:-1]) + (g.off_src[1:] - g.off_src[:-1])
+        active = deg > 0
+        na = int(active.sum().item())
+        if na > cls.COMPACT_FRACTION * n:
+            return g
+        rows = torch.nonzero(active).flatten()
+        cmap = torch.full((n,), -1, dtype=torch.int64, device=edge_index.device)
+        cmap[rows] = torch.arange(na, dtype=torch.int64, device=edge_index.device)
+        gc = ops.GraphCSR(cmap[edge_index], na)
+        gc.rows = rows.to(torch.int32)
+        gc.n_full = n
+        return gc
 
 
 def batch_cache(batch, validate: bool = True) -> BatchCache:
@@ -205,37 +229,57 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int, enc: Optional[ops.EdgeEncoder] = None):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
-    enc: edge features recomputed in-kernel from raw inputs (then F is None)."""
+    enc: edge features recomputed in-kernel from raw inputs (then F is None).
+
+    Compacted graphs (g.rows set: the graph's nodes are the active subset ``rows`` of X's rows, see
+    BatchCache): Q/K/V, the attention and its per-node GEMMs run over the active rows only; the
+    skip projection, gate, LayerNorm and residual over all rows (an inactive node's aggregated
+    message is exactly 0: it has no in-edges)."""
     n, D = X.shape
     C = D // H
     dev = X.device
     c = _Ctx()
     c.X, c.F, c.feat_row, c.enc = X, F, feat_row, enc
     c.M, c.wbar = M, wbar
+    c.rows = rows = g.rows
     with_proj = wbar is not None
-    c.QKVR = torch.empty(n, 4 * D, device=dev)
-    ops.gemm(X, cv.Wqkvr.t(), c.QKVR, bias=cv.bqkvr)
-    c.U = torch.empty(n, H, D, device=dev)
-    ops.gemm(c.QKVR[:, :D].view(n, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
-    c.outp = torch.empty(n, D, device=dev)
-    c.S = torch.empty(n, H, D, device=dev)
-    c.sumA = torch.empty(n, H, device=dev)
-    c.mstat = torch.empty(n, H, device=dev)
-    c.den = torch.empty(n, H, device=dev)
-    ops.tconv_fwd(g, D, H, c.QKVR, c.U, c.wbar, F, feat_row, c.outp, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att,
+    if rows is None:
+        na = n
+        QKVR = torch.empty(n, 4 * D, device=dev)
+        ops.gemm(X, cv.Wqkvr.t(), QKVR, bias=cv.bqkvr)
+        c.Xa, c.QKV, c.R = X, QKVR[:, :3 * D], QKVR[:, 3 * D:]
+    else:
+        na = g.n
+        c.Xa = ops.gather_rows(X, rows)
+        c.QKV = torch.empty(na, 3 * D, device=dev)
+        ops.gemm(c.Xa, cv.Wqkvr[:3 * D].t(), c.QKV, bias=cv.bqkvr[:3 * D])
+        c.R = torch.empty(n, D, device=dev)
+        ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+    c.U = torch.empty(na, H, D, device=dev)
+    ops.gemm(c.QKV[:, :D].view(na, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
+    c.outp_a = torch.empty(na, D, device=dev)
+    c.S = torch.empty(na, H, D, device=dev)
+    c.sumA = torch.empty(na, H, device=dev)
+    c.mstat = torch.empty(na, H, device=dev)
+    c.den = torch.empty(na, H, device=dev)
+    ops.tconv_fwd(g, D, H, c.QKV, c.U, c.wbar, F, feat_row, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att,
                   enc=enc)
     if with_proj:
-        ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp.view(n, H, C).transpose(0, 1),
+        ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp_a.view(na, H, C).transpose(0, 1),
                  beta=1.0, rowscale=c.sumA.t(), bias2=c.wbar.view(H, C))
     else:
-        ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp.view(n, H, C).transpose(0, 1),
+        ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp_a.view(na, H, C).transpose(0, 1),
                  beta=1.0)
+    if rows is None:
+        c.outp = c.outp_a
+    else:
+        c.outp = torch.zeros(n, D, device=dev)
+        ops.scatter_rows(c.outp_a, rows, c.outp)
     X_new = torch.empty(n, D, device=dev)
     c.beta = torch.empty(n, device=dev)
     c.mu = torch.empty(n, device=dev)
     c.rstd = torch.empty(n, device=dev)
-    ops.gate_ln_fwd(c.outp, c.QKVR[:, 3 * D:], cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop,
-                    seed_blk)
+    ops.gate_ln_fwd(c.outp, c.R, cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop, seed_blk)
     c.p, c.seed_att, c.seed_blk, c.H, c.with_proj = p_drop, seed_att, seed_blk, H, with_proj
     return X_new, c
 
@@ -253,26 +297,34 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     C = D // H
     dev = dX.device
     m = g.m
+    rows = c.rows
+    na = n if rows is None else g.n
     dout = torch.empty(n, D, device=dev)
-    dQKVR = torch.empty(n, 4 * D, device=dev)
-    ops.gate_ln_bwd(dX, c.outp, c.QKVR[:, 3 * D:], cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout,
-                    dQKVR[:, 3 * D:], gv.wbeta, gv.lnw, gv.lnb, c.p, c.seed_blk)
-    Vd = torch.empty(n, H, D, device=dev)
-    ops.gemm(dout.view(n, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
-    Sz = torch.empty(n, H, D, device=dev)
-    sigz = torch.empty(n, H, device=dev)
+    if rows is None:
+        dQKVR = torch.empty(n, 4 * D, device=dev)
+        dQKV, dR = dQKVR[:, :3 * D], dQKVR[:, 3 * D:]
+    else:
+        dQKV = torch.empty(na, 3 * D, device=dev)
+        dR = torch.empty(n, D, device=dev)
+    ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
+                    gv.lnb, c.p, c.seed_blk)
+    dout_a = dout if rows is None else ops.gather_rows(dout, rows)
+    Vd = torch.empty(na, H, D, device=dev)
+    ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
+    Sz = torch.empty(na, H, D, device=dev)
+    sigz = torch.empty(na, H, device=dev)
     dz_e = torch.empty(max(m, 1), H, device=dev)
     al_e = torch.empty(max(m, 1), H, device=dev)
     enc = None
     if c.enc is not None:
         enc = ops.EdgeEncoder(c.enc.x, c.enc.w1, c.enc.b1, enc_grads[0], enc_grads[1], accumulate=True)
         dF = None
-    ops.tconv_bwd_dst(g, D, H, c.QKVR, c.U, Vd, c.wbar, c.F, c.feat_row, dout, c.outp, c.mstat, c.den,
-                      dQKVR[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
-    ops.tconv_bwd_src(g, D, H, c.QKVR, dout, dz_e, al_e, dQKVR[:, D:3 * D])
-    Qh = c.QKVR[:, :D].view(n, H, C).permute(1, 2, 0)
-    Oh = dout.view(n, H, C).permute(1, 2, 0)
-    dQv = dQKVR[:, :D].view(n, H, C).transpose(0, 1)
+    ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
+                      dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
+    ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
+    Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
+    Oh = dout_a.view(na, H, C).permute(1, 2, 0)
+    dQv = dQKV[:, :D].view(na, H, C).transpose(0, 1)
     if c.with_proj:
         ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0, rowscale=sigz.t(),
                  bias2=c.wbar.view(H, C))
@@ -284,9 +336,17 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0)
         ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
         ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
-    ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                             # residual + projections
-    ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
-    ops.colsum(dQKVR, gv.bqkvr)
+    if rows is None:
+        ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
+        ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
+        ops.colsum(dQKVR, gv.bqkvr)
+    else:
+        ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                    # residual + skip projection
+        ops.gemm(dQKV, cv.Wqkvr[:3 * D], dX, beta=1.0, c_rows=rows)     # + Q/K/V projections (active rows)
+        ops.gemm(dR.t(), c.X, gv.Wqkvr[3 * D:])
+        ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D])
+        ops.colsum(dR, gv.bqkvr[3 * D:])
+        ops.colsum(dQKV, gv.bqkvr[:3 * D])
 
 
 # ------------------------------------------------------------------------------------------------

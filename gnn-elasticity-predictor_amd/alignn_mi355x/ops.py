@@ -11,7 +11,6 @@ import torch
 from . import _lib, profiling
 from ._lib import GemmArgs, check
 
-_NUM_CUS = 256
 
 
 def _p(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -58,18 +57,40 @@ def _as3(t: torch.Tensor):
     raise ValueError("gemm operands must be 2-D or 3-D (batched) views")
 
 
+GEMM_TRACE: Optional[list] = None
+
+_STEP_SEED: Optional[torch.Tensor] = None
+
+
+def set_step_seed(t: Optional[torch.Tensor]) -> None:
+    """Register a device int64[1] that every dropout / jitter kernel launched afterwards mixes into
+    its site seed at run time (alignn_set_step_seed): a captured HIP graph then draws fresh masks on
+    each replay once the caller updates ``t``.  None: host seeds only."""
+    global _STEP_SEED
+    if t is not None and (t.dtype != torch.int64 or t.numel() != 1 or not t.is_cuda):
+        raise ValueError("step seed must be a device int64 tensor with one element")
+    _STEP_SEED = t
+    _lib.lib().alignn_set_step_seed(None if t is None else t.data_ptr())
+
+
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, rowscale: Optional[torch.Tensor] = None,
          bias2: Optional[torch.Tensor] = None, relu: bool = False, mask: Optional[torch.Tensor] = None,
-         split_k: Optional[int] = None, reduce_batch: bool = False) -> torch.Tensor:
+         split_k: Optional[int] = None, reduce_batch: bool = False,
+         c_rows: Optional[torch.Tensor] = None, tile: int = 0) -> torch.Tensor:
     """C = act(alpha * A @ B + beta * C + bias + rowscale[:,None] * bias2) [* (mask > 0)].
 
     A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D);
     bias/bias2 [.., N], rowscale [.., M] (strided views too).  ``reduce_batch``: A/B batched, C is
-    2-D and receives the sum over the batch (K must be a multiple of 16)."""
+    2-D and receives the sum over the batch (K must be a multiple of 16).  ``c_rows`` (int32 [M]):
+    logical row r of C is stored at C[c_rows[r]] (C then has any number of rows >= max index)."""
     ba, sab, sam, sak, M, K = _as3(A)
     bb, sbb, sbk, sbn, K2, N = _as3(B)
     bc, scb, scm, scn, M2, N2 = _as3(C)
+    if c_rows is not None:
+        if c_rows.dtype != torch.int32 or c_rows.numel() != M:
+            raise ValueError("gemm: c_rows must be int32 with M entries")
+        M2 = M
     batch = max(ba, bb, bc)
     if reduce_batch:
         if bc != 1 or K2 != K or M2 != M or N2 != N or ba not in (1, batch) or bb not in (1, batch):
@@ -96,13 +117,19 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
         a.mask, a.smk_m, a.smk_n = mask.data_ptr(), mask.stride(0), mask.stride(1)
     a.alpha, a.beta, a.relu = float(alpha), float(beta), int(bool(relu))
     a.reduce_batch = int(bool(reduce_batch) and batch > 1)
-    if split_k is None:
-        split_k = choose_split_k(M, N, K * batch, 1) if a.reduce_batch else choose_split_k(M, N, K, batch)
-    a.split_k = int(split_k)
-    if split_k > 1:
-        need = split_k * (1 if a.reduce_batch else batch) * M * N
+    if c_rows is not None:
+        a.c_rows = c_rows.data_ptr()
+    a.split_k = 0 if split_k is None else int(split_k)   # 0: the library plans tile shape and split-K
+    a.tile = int(tile)
+    need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
+    if need < 0:
+        raise ValueError("gemm: invalid shape")
+    if need > 0:
         ws = WS.get("gemm", need, C.device)
         a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
+    if GEMM_TRACE is not None:   # tuning hook (tools/gemm_bench.py): record the call's operands
+        GEMM_TRACE.append(dict(A=A, B=B, C=C, alpha=alpha, beta=beta, bias=bias, rowscale=rowscale, bias2=bias2,
+                               relu=relu, mask=mask, reduce_batch=reduce_batch, c_rows=c_rows))
     key = f"gemm_f32 M{M} N{N} K{K} b{batch}"
     if profiling.active(key) or profiling.active("*gemm"):
         nbytes = 4.0 * batch * (M * K + K * N + M * N * (2 if beta else 1))
@@ -111,20 +138,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     else:
         check(_lib.lib().alignn_gemm_f32(ctypes.byref(a), stream_ptr()), "alignn_gemm_f32")
     return C
-
-
-def choose_split_k(M: int, N: int, K: int, batch: int) -> int:
-    """Split the K loop over workgroups when the output has too few tiles to fill 256 CUs:
-    aim at ~2 workgroups per CU, keep >= 128 of K per split (8 K-tiles) for large K and
-    >= 32 for small K (latency-bound tiny GEMMs)."""
-    bm = 128 if M >= 128 else 64
-    bn = 128 if N >= 128 else 64
-    tiles = math.ceil(M / bm) * math.ceil(N / bn) * batch
-    if tiles >= _NUM_CUS or K < 64:
-        return 1
-    min_chunk = 128 if K >= 4096 else 32
-    split = min(math.ceil(2 * _NUM_CUS / tiles), max(1, K // min_chunk))
-    return max(1, split)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
@@ -149,7 +162,8 @@ def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torc
 class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
-    __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched")
+    __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
+                 "n_full")
 
     HEAVY_THRESHOLD = 32  # in-degree above which a target node gets a 4-wave workgroup
 
@@ -169,6 +183,8 @@ class GraphCSR:
         self.pos_src = torch.empty(max(m, 1), **i32)
         self.err = torch.zeros(1, **i32)
         self._sched = None
+        self.rows = None     # compacted graph: int32 ids of its nodes in the full node set
+        self.n_full = n
         ws = WS.get("graph", 2 * n + 64, dev, torch.int32)
         check(_lib.lib().alignn_graph_prep(ei.data_ptr(), m, n, self.off_dst.data_ptr(), self.perm_dst.data_ptr(),
                                            self.src_at.data_ptr(), self.dst_at.data_ptr(), self.off_src.data_ptr(),
@@ -213,6 +229,16 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor
 # ------------------------------------------------------------------------------------------------
 # TransformerConv attention
 # ------------------------------------------------------------------------------------------------
+def scatter_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """out[idx[i]] (+)= src[i] (idx: distinct int32 row indices)."""
+    if idx.dtype != torch.int32 or src.size(0) != idx.numel() or src.size(1) != out.size(1):
+        raise ValueError("scatter_rows: idx must be int32 with one entry per source row, equal widths")
+    check(_lib.lib().alignn_scatter_rows_f32(src.data_ptr(), src.stride(0), idx.data_ptr(), idx.numel(), src.size(1),
+                                             out.data_ptr(), out.stride(0), int(bool(accumulate)), stream_ptr()),
+          "alignn_scatter_rows_f32")
+    return out
+
+
 def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, kin: int = 0) -> float:
     """Compulsory HBM bytes of one launch (every operand touched once, ideal caching).  kin > 0:
     edge features recomputed from kin raw inputs per edge (no [m, D] feature / gradient rows)."""

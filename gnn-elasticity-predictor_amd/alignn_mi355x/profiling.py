@@ -22,6 +22,11 @@ def enable(only: Optional[str] = None) -> None:
     _events.clear()
 
 
+def clear() -> None:
+    """Drop recorded events (keeps the enabled state)."""
+    _events.clear()
+
+
 def disable() -> None:
     global _enabled
     _enabled = False
@@ -36,8 +41,11 @@ def launch(key: str, flops: float, nbytes: float, fn: Callable[[], None]) -> Non
     if not active(key):
         fn()
         return
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
+    # inside HIP-graph capture the events become event-record nodes of the graph (external), so
+    # after a replay they hold that replay's device times of this launch
+    ext = torch.cuda.is_current_stream_capturing()
+    s = torch.cuda.Event(enable_timing=True, external=ext)
+    e = torch.cuda.Event(enable_timing=True, external=ext)
     s.record()
     fn()
     e.record()

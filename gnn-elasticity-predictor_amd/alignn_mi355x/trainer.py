@@ -13,7 +13,7 @@ from typing import Optional, Sequence
 import torch
 from torch import nn
 
-from . import ops
+from . import ops, profiling
 from .engine import MIN_LOGVAR_FLOOR, batch_cache, site_seed
 from .model import HeteroAlignnRegressor
 from .synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS
@@ -35,7 +35,7 @@ class FusedTrainer:
         self.p_base.grad = st.grad[:s0]
         self.p_sigma.grad = st.grad[s0:]
         sigma_lr = lr if not sigma_lr else sigma_lr  # train.py:1521-1522 (0 disables the cap)
-        kw = {"fused": True} if (fused_adamw and st.flat.is_cuda) else {}
+        kw = {"fused": True, "capturable": True} if (fused_adamw and st.flat.is_cuda) else {}
         self.opt = torch.optim.AdamW([{"params": [self.p_base], "lr": lr}, {"params": [self.p_sigma], "lr": sigma_lr}],
                                      lr=lr, weight_decay=weight_decay, **kw)
         self.max_norm = max_norm
@@ -47,6 +47,9 @@ class FusedTrainer:
         self.log_stds = torch.tensor(list(target_log_stds), dtype=torch.float32, device=dev)
         self.loss = torch.zeros(1, device=dev)
         self.step_count = 0
+        self._graph = None
+        self._seed_dev = None
+        self.grad_hook = None  # called with the flat gradient between backward and clip (DP all_reduce)
 
     def set_lr(self, lr: float, sigma_lr: Optional[float] = None) -> None:
         self.opt.param_groups[0]["lr"] = lr
@@ -72,8 +75,76 @@ class FusedTrainer:
     def step(self, batch, seed: Optional[int] = None) -> torch.Tensor:
         if seed is None:
             seed = int(torch.randint(0, 2**62, (1,)).item())
+        if self._graph is not None and self._graph[2] is batch:
+            return self._replay(seed)
         loss = self.forward_backward(batch, seed)
-        torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
-        self.opt.step()
+        if self.grad_hook is not None:
+            self.grad_hook(self.st.grad)
+        self._clip_and_update()
         self.step_count += 1
         return loss
+
+    def _clip_and_update(self) -> None:
+        torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
+        self.opt.step()
+
+    # --------------------------------------------------------------------------------------------
+    # HIP-graph mode: the step (jitter, forward, loss, backward | clip, AdamW: ~300 kernels) is
+    # captured once for a fixed batch as two graphs and replayed — no per-kernel host work and no
+    # launch gaps.  ``grad_hook`` (e.g. the data-parallel all_reduce) runs eagerly between the two.
+    # Randomness stays per step: the kernels read a device step seed (ops.set_step_seed) that
+    # step() updates before each replay.  The learning rate is baked in at capture.
+    # --------------------------------------------------------------------------------------------
+    def capture(self, batch) -> None:
+        """Capture the training step on ``batch`` (which must stay alive with unchanged shapes; its
+        tensors may be refilled in place).  Model and optimizer state are left as they were."""
+        dev = self.st.flat.device
+        if self._seed_dev is None:
+            self._seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        ops.set_step_seed(self._seed_dev)
+        batch_cache(batch)
+        # warm-up (allocations, optimizer state) on a side stream, then restore the state
+        snap = self._snapshot()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.forward_backward(batch, 0)
+                self._clip_and_update()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        profiling.clear()  # roofline probes (bench.py): keep only the launches captured below
+        g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            self.forward_backward(batch, 0)
+        with torch.cuda.graph(g_up, pool=g_fb.pool()):
+            self._clip_and_update()
+        torch.cuda.synchronize(dev)
+        self._restore(snap)
+        self._graph = (g_fb, g_up, batch)
+
+    def _replay(self, seed: int) -> torch.Tensor:
+        self._seed_dev.fill_(int(seed) & (2**63 - 1))
+        self._graph[0].replay()
+        if self.grad_hook is not None:
+            self.grad_hook(self.st.grad)
+        self._graph[1].replay()
+        self.step_count += 1
+        return self.loss
+
+    def _snapshot(self):
+        opt_state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                     for p, st in self.opt.state.items()}
+        return self.st.flat.clone(), opt_state
+
+    def _restore(self, snap) -> None:
+        flat, opt_state = snap
+        self.st.flat.copy_(flat)
+        for p, st in self.opt.state.items():
+            saved = opt_state.get(id(p))
+            for k, v in st.items():
+                if torch.is_tensor(v):
+                    if saved is not None and k in saved:
+                        v.copy_(saved[k])
+                    else:
+                        v.zero_()

@@ -59,15 +59,32 @@ __device__ __forceinline__ float dropout_mul(uint64_t seed, uint64_t idx, uint32
   return hash_u32(seed, idx) >= thresh ? inv_keep : 0.0f;
 }
 
+// Device-resident step seed registered by alignn_set_step_seed (NULL: host seeds only).
+extern const uint64_t* g_step_seed;
+
+__device__ __forceinline__ uint64_t mix_seed(uint64_t site, const uint64_t* sptr) {
+  if (!sptr) return site;
+  uint64_t x = (*sptr + 0x632BE59BD9B4E019ULL) * 0x9E3779B97F4A7C15ULL;
+  x ^= x >> 31;
+  return site ^ x;
+}
+
 struct DropParams {
   uint64_t seed;
   uint32_t thresh;   // p * 2^32
   float inv_keep;    // 1/(1-p)
   int active;
+  const uint64_t* sptr;  // step seed (mixed in once per thread: resolve_drop)
 };
+// Call once at kernel entry: folds the device step seed into d.seed.
+__device__ __forceinline__ void resolve_drop(DropParams& d) {
+  d.seed = mix_seed(d.seed, d.sptr);
+  d.sptr = nullptr;
+}
 inline DropParams make_drop(float p, uint64_t seed) {
   DropParams d;
   d.seed = seed;
+  d.sptr = g_step_seed;
   d.active = p > 0.0f ? 1 : 0;
   double t = (double)p * 4294967296.0;
   d.thresh = p > 0.0f ? (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t) : 0u;

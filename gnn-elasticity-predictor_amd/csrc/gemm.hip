@@ -41,6 +41,7 @@ struct GemmParams {
   float* ws;
   int vecA, vecB;
   int reduce_batch;  // sum the batch into one output: K loop runs over (batch, k), K % BK == 0
+  const int32_t* c_rows;  // optional scatter of C rows
 };
 
 // Loads one operand tile (ROWS x BK) into registers.  KC: load along k (general strides,
@@ -125,10 +126,14 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ lds, int row
   }
 }
 
+__device__ __forceinline__ int64_t c_row(const GemmParams& p, int64_t row) {
+  return p.c_rows ? (int64_t)p.c_rows[row] : row;
+}
+
 __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, int64_t row, int64_t col, float acc) {
   float v = p.alpha * acc;
   float* Cb = p.C + b * p.scb;
-  if (p.beta != 0.f) v += p.beta * Cb[row * p.scm + col * p.scn];
+  if (p.beta != 0.f) v += p.beta * Cb[c_row(p, row) * p.scm + col * p.scn];
   if (p.bias) v += p.bias[b * p.sbias_b + col];
   if (p.rowscale) v += p.rowscale[b * p.srs_b + row * p.srs_m] * p.bias2[b * p.sb2_b + col];
   if (p.relu) v = fmaxf(v, 0.f);
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         if (p.split_k > 1) {
           p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
         } else {
-          p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
+          p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
         }
       }
     }
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
     }
     for (int j = 0; k < p.split_k; ++k, ++j) s[j] += w[(int64_t)k * stride];
     const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-    p.C[b * p.scb + row * p.scm + col * p.scn] = epilogue_value(p, b, row, col, t);
+    p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, t);
   }
 }
 
@@ -265,9 +270,86 @@ static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, 
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
 
+static int g_cus = 0;
+static int device_cus() {
+  if (g_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_cus = n;
+  }
+  return g_cus;
+}
+
+struct GemmPlan {
+  int bm, bn, split;
+  int64_t kchunk;
+};
+
+// Tile shape: minimise (tile waves over the CUs) x (tile area) x (per-flop cost of the shape), so a
+// launch of 1.4 waves of 128x128 tiles loses to 2.8 waves of 128x64.  Split-K only when the grid
+// stays under half the CUs and K is long (>= 1024): each split keeps >= 256 of K, and the grid aims
+// at one workgroup per CU.  Small-K GEMMs never split (the reduce would cost more than it saves).
+static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int requested, int tile) {
+  const int cus = device_cus();
+  static const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  static const double eff[4] = {1.0, 1.1, 1.1, 1.35};
+  GemmPlan pl{64, 64, 1, 0};
+  double best = -1.0;
+  int64_t best_tiles = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int bm = cand[c][0], bn = cand[c][1];
+    if (tile >= 1 && tile <= 4 && c != tile - 1) continue;
+    if (tile == 0 && ((bm == 128 && M <= 64) || (bn == 128 && N <= 64))) continue;
+    const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * nb;
+    const double cost = (double)((tiles + cus - 1) / cus) * bm * bn * eff[c];
+    if (best < 0 || cost < best) {
+      best = cost;
+      pl.bm = bm;
+      pl.bn = bn;
+      best_tiles = tiles;
+    }
+  }
+  int split = requested;
+  if (split <= 0) {
+    split = 1;
+    if (best_tiles * 2 < cus && Ktot >= 1024) {
+      const int64_t want = (cus + best_tiles - 1) / best_tiles;
+      const int64_t maxs = Ktot / 256;
+      split = (int)std::max<int64_t>(1, std::min(want, maxs));
+    }
+  }
+  if (Ktot == 0) split = 1;
+  int64_t kchunk = (Ktot + split - 1) / split;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  if (kchunk == 0) kchunk = BK;
+  split = (int)((Ktot + kchunk - 1) / kchunk);
+  if (split < 1) split = 1;
+  pl.split = split;
+  pl.kchunk = kchunk;
+  return pl;
+}
+
+static bool plan_args(const AlignnGemmArgs* a, GemmPlan& pl, int64_t& ktot, int64_t& nb_out) {
+  if (!a || a->M < 0 || a->N < 0 || a->K < 0 || a->batch < 1) return false;
+  const bool rb = a->reduce_batch && a->batch > 1;
+  ktot = rb ? a->K * a->batch : a->K;
+  nb_out = rb ? 1 : a->batch;
+  pl = make_plan(a->M, a->N, ktot, nb_out, a->split_k, a->tile);
+  return true;
+}
+
 }  // namespace alignn
 
 using namespace alignn;
+
+extern "C" int64_t alignn_gemm_workspace(const AlignnGemmArgs* a) {
+  GemmPlan pl;
+  int64_t ktot, nb;
+  if (!plan_args(a, pl, ktot, nb)) return -1;
+  return pl.split > 1 ? (int64_t)pl.split * nb * a->M * a->N : 0;
+}
 
 extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (!a || a->M < 0 || a->N < 0 || a->K < 0 || a->batch < 1) {
@@ -291,14 +373,14 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   p.mask = a->mask; p.smk_m = a->smk_m; p.smk_n = a->smk_n;
   p.alpha = a->alpha; p.beta = a->beta; p.relu = a->relu;
   p.reduce_batch = a->reduce_batch && a->batch > 1;
+  p.c_rows = a->c_rows;
   if (p.reduce_batch && a->K % BK != 0) {
     set_error("gemm: reduce_batch needs K %% %d == 0 (K=%lld)", BK, (long long)a->K);
     return ALIGNN_E_UNSUPPORTED;
   }
-  const int64_t Ktot = p.reduce_batch ? a->K * a->batch : a->K;
-  const int64_t nbatch_out = p.reduce_batch ? 1 : a->batch;
-  int split = a->split_k < 1 ? 1 : a->split_k;
-  if (a->K == 0) split = 1;
+  GemmPlan pl;
+  int64_t Ktot, nbatch_out;
+  plan_args(a, pl, Ktot, nbatch_out);
   // A is "k-contiguous" unless it is contiguous along m only.
   const bool akc = !(a->sam == 1 && a->sak != 1);
   const bool bkc = !(a->sbn == 1 && a->sbk != 1);
@@ -306,29 +388,22 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
                : (a->sak % 4 == 0 && a->sab % 4 == 0 && aligned16(a->A));
   p.vecB = bkc ? (a->sbk == 1 && a->sbn % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B))
                : (a->sbk % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B));
-  int64_t kchunk = (Ktot + split - 1) / split;
-  kchunk = (kchunk + BK - 1) / BK * BK;
-  if (kchunk == 0) kchunk = BK;
-  split = (int)((Ktot + kchunk - 1) / kchunk);
-  if (split < 1) split = 1;
-  p.kchunk = kchunk;
-  p.split_k = split;
+  p.kchunk = pl.kchunk;
+  p.split_k = pl.split;
   p.ws = a->workspace;
-  if (split > 1 && (!a->workspace || a->workspace_elems < (int64_t)split * nbatch_out * a->M * a->N)) {
-    set_error("gemm: split_k=%d needs %lld workspace floats", split, (long long)split * nbatch_out * a->M * a->N);
+  if (pl.split > 1 && (!a->workspace || a->workspace_elems < (int64_t)pl.split * nbatch_out * a->M * a->N)) {
+    set_error("gemm: split_k=%d needs %lld workspace floats", pl.split,
+              (long long)pl.split * nbatch_out * a->M * a->N);
     return ALIGNN_E_WORKSPACE;
   }
-  // Tile choice: 128x128 for large problems, 64-wide on a small dimension.
-  const int bm = a->M >= 128 ? 128 : 64;
-  const int bn = a->N >= 128 ? 128 : 64;
-  const int64_t tiles = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
-  dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * split));
-  if (bm == 128 && bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, s);
-  else if (bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, s);
-  else if (bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, s);
+  const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
+  dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
+  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, s);
+  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, s);
+  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, s);
   else dispatch_layout<64, 64>(p, akc, bkc, grid, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
-  if (split > 1) {
+  if (pl.split > 1) {
     int64_t total = nbatch_out * a->M * a->N;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);

@@ -123,6 +123,17 @@ __global__ void gather_rows_kernel(const float* __restrict__ in, int64_t ld_in, 
   }
 }
 
+__global__ void scatter_rows_kernel(const float* __restrict__ in, int64_t ld_in, const int32_t* __restrict__ idx,
+                                    int64_t rows, int64_t cols, float* __restrict__ out, int64_t ld_out, int acc) {
+  const int64_t total = rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i / cols, c = i % cols;
+    float* o = out + (int64_t)idx[r] * ld_out + c;
+    const float v = in[r * ld_in + c];
+    *o = acc ? *o + v : v;
+  }
+}
+
 static int grid_for(int64_t work, int block = 256, int64_t cap = 8192) {
   int64_t g = (work + block - 1) / block;
   if (g < 1) g = 1;
@@ -184,5 +195,16 @@ extern "C" int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int3
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
                      out, ld_out);
   ALIGNN_LAUNCH_CHECK("gather_rows_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows, int64_t cols,
+                                       float* out, int64_t ld_out, int32_t accumulate, void* stream) {
+  if (rows < 0 || cols < 0) return ALIGNN_E_BAD_SHAPE;
+  if (rows == 0 || cols == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
+                     out, ld_out, accumulate);
+  ALIGNN_LAUNCH_CHECK("scatter_rows_kernel");
   return ALIGNN_OK;
 }

@@ -9,6 +9,7 @@
 namespace alignn {
 
 static thread_local char g_err[512] = "";
+const uint64_t* g_step_seed = nullptr;
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -48,6 +49,7 @@ struct GateFwdParams {
 
 template <int VPL>
 __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
+  resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= p.n) return;
@@ -118,6 +120,7 @@ struct GateBwdParams {
 
 template <int VPL>
 __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
+  resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int D = p.D, j0 = lane * VPL;
@@ -221,6 +224,7 @@ static int vpl_for(int D) {
 __global__ void readout_fwd_kernel(int64_t B, int D, const float* __restrict__ h, const int64_t* __restrict__ ptr,
                                    const float* __restrict__ gx, int gdim, const float* __restrict__ sg, int sgdim,
                                    float* __restrict__ feats, DropParams drop) {
+  resolve_drop(drop);
   const int64_t b = blockIdx.x;
   const int W = D + gdim + sgdim;
   const int64_t s = ptr[b], e = ptr[b + 1];
@@ -244,6 +248,7 @@ __global__ void readout_fwd_kernel(int64_t B, int D, const float* __restrict__ h
 __global__ void pool_bwd_kernel(int64_t N, int D, const float* __restrict__ dfeats, int64_t ldf,
                                 const int64_t* __restrict__ ptr, const int64_t* __restrict__ batch,
                                 float* __restrict__ dh, int acc, DropParams drop) {
+  resolve_drop(drop);
   const int64_t total = N * D;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t node = i / D;
@@ -258,6 +263,7 @@ __global__ void pool_bwd_kernel(int64_t N, int D, const float* __restrict__ dfea
 
 __global__ void dropout_kernel(int64_t rows, int64_t cols, const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
                                int64_t ldy, const float* __restrict__ ref, int64_t ldr, DropParams drop) {
+  resolve_drop(drop);
   const int64_t total = rows * cols;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cols, c = i % cols;
@@ -300,7 +306,8 @@ __global__ __launch_bounds__(256) void hetero_nll_kernel(int64_t B, int T, const
   if (threadIdx.x == 0) *loss = red[0] * inv;
 }
 
-__global__ void add_noise_kernel(int64_t n, float* __restrict__ x, float stdv, uint64_t seed) {
+__global__ void add_noise_kernel(int64_t n, float* __restrict__ x, float stdv, uint64_t seed, const uint64_t* sptr) {
+  seed = mix_seed(seed, sptr);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t a = hash_u32(seed, 2 * (uint64_t)i), b = hash_u32(seed, 2 * (uint64_t)i + 1);
     const float u1 = ((float)a + 1.0f) * 2.3283064e-10f;  // (0, 1]
@@ -428,7 +435,9 @@ extern "C" int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64
 extern "C" int alignn_add_noise_f32(int64_t n, float* x, float stdv, uint64_t seed, void* stream) {
   if (n == 0 || stdv == 0.f) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, x, stdv, seed);
+  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, x, stdv, seed, g_step_seed);
   ALIGNN_LAUNCH_CHECK("add_noise_kernel");
   return ALIGNN_OK;
 }
+
+extern "C" void alignn_set_step_seed(const uint64_t* device_ptr) { alignn::g_step_seed = device_ptr; }

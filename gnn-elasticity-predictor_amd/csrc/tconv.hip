@@ -32,7 +32,10 @@ namespace alignn {
 // operands of the next group are in flight while the current one computes, and the PF*H (or
 // 2*PF*H) per-head dot products of a group are reduced across the wave together (reduce_bcast).
 // ---------------------------------------------------------------------------------------------
-constexpr int PF = 4;
+#ifndef ALIGNN_PF
+#define ALIGNN_PF 4
+#endif
+constexpr int PF = ALIGNN_PF;
 
 struct Sched {
   const int32_t* light;
@@ -162,7 +165,7 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = p.off[d], end = p.off[d + 1];
+  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
 
   float accS[H][VPL], accV[VPL];
   float m[H], s[H], sa[H];
@@ -205,8 +208,8 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
       ring[j].xr = 0.f;
       const int32_t t = first + j;
       if (t < end)
-        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[t],
-                           p.feat_row ? (int64_t)p.feat_row[t] : t, j0, act, lane);
+        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[t]),
+                           p.feat_row ? (int64_t)uni(p.feat_row[t]) : t, j0, act, lane);
     }
     for (int32_t tb = first; tb < end; tb += stride) {
       if constexpr (KM > 0) enc_group<VPL, KM>(ew, D, j0, ring);
@@ -260,8 +263,8 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
         if (tn < end)
-          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[tn],
-                             p.feat_row ? (int64_t)p.feat_row[tn] : tn, j0, act, lane);
+          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[tn]),
+                             p.feat_row ? (int64_t)uni(p.feat_row[tn]) : tn, j0, act, lane);
       }
     }
   }
@@ -343,6 +346,7 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
 
 template <int VPL, int H, int KM>
 __global__ TCONV_ATTR void tconv_fwd_kernel(FwdParams p, Sched sc, EncParams en) {
+  resolve_drop(p.drop);
   constexpr int MERGE = fwd_merge_floats<VPL, H>();
   constexpr int ENCW = KM > 0 ? (KM + 1) * 64 * VPL : 0;
   __shared__ float smem[MERGE + ENCW];
@@ -368,10 +372,10 @@ __global__ TCONV_ATTR void tconv_fwd_kernel(FwdParams p, Sched sc, EncParams en)
       }
     }
     if (it < sc.n_heavy) {
-      fwd_node<VPL, H, KM>(p, en, ew, smem, (int64_t)sc.heavy[it], wave, 4, true);
+      fwd_node<VPL, H, KM>(p, en, ew, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) fwd_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)sc.light[i] : i, 0, 1, false);
+      if (i < sc.n_light) fwd_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false);
     }
   }
 }
@@ -424,7 +428,7 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = p.off[d], end = p.off[d + 1];
+  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
   const bool do_dF = KM == 0 && p.dF != nullptr;
 
   float sz[H][VPL], sgz[H], dqa[VPL];
@@ -487,8 +491,8 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
       const int32_t t = first + j;
       rows[j] = 0;
       if (t < end) {
-        rows[j] = p.feat_row ? p.feat_row[t] : t;
-        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[t], rows[j], j0, act, lane);
+        rows[j] = p.feat_row ? uni(p.feat_row[t]) : t;
+        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[t]), rows[j], j0, act, lane);
         if constexpr (KM == 0)
           if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
       }
@@ -565,8 +569,8 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
         }
         const int32_t tn = tb + stride + j;
         if (tn < end) {
-          rows[j] = p.feat_row ? p.feat_row[tn] : tn;
-          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)p.src_at[tn], rows[j], j0, act,
+          rows[j] = p.feat_row ? uni(p.feat_row[tn]) : tn;
+          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[tn]), rows[j], j0, act,
                              lane);
           if constexpr (KM == 0)
             if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
@@ -615,6 +619,7 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
 template <int VPL, int H, int KM>
 __global__ TCONV_ATTR void tconv_bwd_dst_kernel(BwdDstParams p, Sched sc, EncParams en,
                                                             float* __restrict__ part) {
+  resolve_drop(p.drop);
   constexpr int MERGE = bwd_merge_floats<VPL, H, KM>();
   constexpr int ENCW = KM > 0 ? (KM + 1) * 64 * VPL : 0;
   __shared__ float smem[MERGE + ENCW];
@@ -631,11 +636,11 @@ __global__ TCONV_ATTR void tconv_bwd_dst_kernel(BwdDstParams p, Sched sc, EncPar
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      bwd_dst_node<VPL, H, KM>(p, en, ew, smem, (int64_t)sc.heavy[it], wave, 4, true, ea);
+      bwd_dst_node<VPL, H, KM>(p, en, ew, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true, ea);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
       if (i < sc.n_light)
-        bwd_dst_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)sc.light[i] : i, 0, 1, false, ea);
+        bwd_dst_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false, ea);
     }
   }
   if constexpr (KM > 0) {

@@ -55,6 +55,10 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
+// Wave-uniform value (index loaded from memory at a uniform address) moved to an SGPR, so the
+// addresses derived from it are scalar (global_load with SGPR base + one shared VGPR offset).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 __device__ __forceinline__ float f_bits(unsigned u) { return __builtin_bit_cast(float, u); }
 __device__ __forceinline__ unsigned u_bits(float f) { return __builtin_bit_cast(unsigned, f); }
 

@@ -28,6 +28,13 @@ extern "C" {
 int alignn_version(void);
 const char* alignn_last_error(void);
 
+/* Dropout / jitter randomness: every call site passes a 64-bit site seed; masks are a counter hash
+ * of (seed, element), so the backward regenerates them.  alignn_set_step_seed(ptr) registers a
+ * device-resident uint64 that kernels launched afterwards mix into their site seed when they run:
+ * a step captured once in a HIP graph draws fresh masks on every replay after the caller updates
+ * *ptr (NULL = host seeds only).  Process-wide setting. */
+void alignn_set_step_seed(const uint64_t* device_ptr);
+
 /* ------------------------------------------------------------------------------------------
  * Dense projections (MFMA f32 32x32x2, exact fp32).  Replaces every nn.Linear / PyG Linear
  * addmm+mm on the path: encoders train.py:350-364, TransformerConv lin_query/key/value/skip/
@@ -39,7 +46,8 @@ const char* alignn_last_error(void);
  * with A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn], C(m,n) = C[m*scm + n*scn].
  * Fast path: (sak == 1 or sam == 1) and (sbk == 1 or sbn == 1); others fall back to scalar loads.
  * split_k > 1 accumulates fp32 partial slabs in `workspace` (>= split_k*batch*M*N floats) and
- * reduces them in a second kernel in fixed order.  reduce_batch = 1 sums the batch into C itself
+ * reduces them in a second kernel in fixed order; split_k = 0 lets the library choose tile shape
+ * and split (alignn_gemm_workspace gives the workspace that choice needs).  reduce_batch = 1 sums the batch into C itself
  * (used for weights shared by all layers, e.g. the folded angle-encoder projection).
  * ---------------------------------------------------------------------------------------- */
 typedef struct AlignnGemmArgs {
@@ -56,10 +64,16 @@ typedef struct AlignnGemmArgs {
   int32_t split_k;
   float* workspace; int64_t workspace_elems;
   int32_t reduce_batch;   /* 1: C = sum over the batch (one output; K % 16 == 0) */
-  int32_t reserved;
+  int32_t tile;           /* 0: automatic; 1: 128x128, 2: 128x64, 3: 64x128, 4: 64x64 (tuning) */
+  const int32_t* c_rows;  /* optional: logical row r of C is stored at row c_rows[r] (scatter; beta
+                             reads the same row).  bias/rowscale/mask stay indexed by r. */
 } AlignnGemmArgs;
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
+
+/* Workspace floats alignn_gemm_f32 needs for these arguments (split_k = 0: the automatic plan on
+ * the current device); 0 when no split is used, -1 for invalid shapes. */
+int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
  * Two-stage, fixed order.  workspace >= 256*N floats. */
@@ -87,6 +101,11 @@ int alignn_graph_prep(const int64_t* edge_index, int64_t m, int64_t n,
  * in target-sorted order (lg_edge_attr, train.py:553-554) once per batch. */
 int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows,
                            int64_t cols, float* out, int64_t ld_out, void* stream);
+
+/* out[idx[i], :] (+)= in[i, :] (idx distinct).  Scatters rows computed on the compacted set of
+ * active nodes (nodes with line-graph edges) back to all nodes. */
+int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows,
+                            int64_t cols, float* out, int64_t ld_out, int32_t accumulate, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused TransformerConv attention (PyG 2.7.0 TransformerConv.message/aggregate + utils.softmax,

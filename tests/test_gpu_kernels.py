@@ -73,6 +73,41 @@ def test_gemm_split_k_deterministic():
     assert _rel(out1, ref) < 5e-6
 
 
+@pytest.mark.parametrize("M,N,K,batch", [(2580, 768, 256, 1), (23040, 256, 256, 1), (64, 256, 2580, 4),
+                                         (2580, 64, 256, 4), (256, 11, 253440, 1), (64, 1, 23040, 4)])
+def test_gemm_auto_plan_shapes(M, N, K, batch):
+    """The step's GEMM shapes under the library's automatic tile/split-K plan (all four tile shapes,
+    split and unsplit) vs fp64."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + batch)
+    A = torch.randn(batch, K, M, generator=g).to(DEV).transpose(1, 2)   # m-contiguous A (weight-grad layout)
+    B = torch.randn(batch, K, N, generator=g).to(DEV)
+    C = torch.empty(batch, M, N, device=DEV)
+    ops.gemm(A, B, C)
+    ref = A.double() @ B.double()
+    assert _rel(C, ref) < 5e-6
+
+
+def test_gemm_c_rows_scatter():
+    ops = _ops()
+    torch.manual_seed(3)
+    n, na, K, N = 5000, 700, 768, 256
+    rows = torch.randperm(n)[:na].sort().values.to(torch.int32).to(DEV)
+    A = torch.randn(na, K, device=DEV)
+    W = torch.randn(K, N, device=DEV)
+    C0 = torch.randn(n, N, device=DEV)
+    C = C0.clone()
+    ops.gemm(A, W, C, beta=1.0, c_rows=rows)
+    ref = C0.double().clone()
+    ref[rows.long()] += A.double() @ W.double()
+    assert _rel(C, ref) < 2e-6
+    # scatter / gather row helpers
+    out = torch.zeros(n, N, device=DEV)
+    ops.scatter_rows(A[:, :N].contiguous(), rows, out)
+    assert torch.equal(out[rows.long()], A[:, :N]) and float(out.abs().sum()) == float(A[:, :N].abs().sum())
+    assert torch.equal(ops.gather_rows(out, rows), A[:, :N])
+
+
 def test_colsum():
     ops = _ops()
     X = torch.randn(100003, 300, device=DEV)

@@ -90,7 +90,7 @@ print("rows as lg source", float(err[srcdeg > 0].max()), "never source", float(e
 worst = int(err.argmax()); print("worst row", worst, "deg", int(deg[worst]), "srcdeg", int(srcdeg[worst]))
 c = CTX[0].edge[0]
 D = 256
-R = c.QKVR[:, 3 * D:]
+R = c.R
 y = c.beta[:, None] * R + (1 - c.beta[:, None]) * c.outp
 mu = y.mean(1)
 var = ((y - mu[:, None]) ** 2).mean(1)

@@ -1,0 +1,108 @@
+"""GEMM plan tuning: records every ops.gemm call of one training step (bench workload), then replays
+each distinct call under forced plans (tile shape x split-K) and the automatic plan, timing each with
+HIP events (median of R reps).  Prints per-shape times and the best plan, plus the step totals.
+
+usage: python tools/gemm_bench.py [--reps 15] [--json out.json]
+"""
+import argparse
+import collections
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gnn-elasticity-predictor_amd"))
+import alignn_mi355x as A  # noqa: E402
+from alignn_mi355x import ops  # noqa: E402
+from alignn_mi355x.synthetic import mp_like_batch  # noqa: E402
+
+TILES = {1: "128x128", 2: "128x64", 3: "64x128", 4: "64x64"}
+
+
+def timeit(fn, reps):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    fn()
+    torch.cuda.synchronize()
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+    return ts[len(ts) // 2]
+
+
+def sig(c):
+    A, B, C = c["A"], c["B"], c["C"]
+    return (tuple(A.shape), tuple(A.stride()), tuple(B.shape), tuple(B.stride()), tuple(C.shape), tuple(C.stride()),
+            c["beta"] != 0, c["reduce_batch"], c["c_rows"] is not None)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    dev = "cuda"
+    torch.manual_seed(0)
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(dev)
+    tr = A.FusedTrainer(model)
+    b = mp_like_batch(a.batch).to(dev)
+    tr.forward_backward(b, 1)
+    torch.cuda.synchronize()
+    ops.GEMM_TRACE = []
+    tr.forward_backward(b, 2)
+    torch.cuda.synchronize()
+    calls = ops.GEMM_TRACE
+    ops.GEMM_TRACE = None
+    groups = collections.OrderedDict()
+    for c in calls:
+        groups.setdefault(sig(c), []).append(c)
+    print(f"{len(calls)} gemm calls, {len(groups)} distinct", flush=True)
+    res = []
+    tot_auto = tot_best = 0.0
+    for key, cs in groups.items():
+        c = cs[0]
+        C_save = c["C"].clone()
+
+        def run(tile=0, split=None, c=c):
+            ops.gemm(c["A"], c["B"], c["C"], alpha=c["alpha"], beta=c["beta"], bias=c["bias"], rowscale=c["rowscale"],
+                     bias2=c["bias2"], relu=c["relu"], mask=c["mask"], reduce_batch=c["reduce_batch"],
+                     c_rows=c["c_rows"], split_k=split, tile=tile)
+
+        t_auto = timeit(lambda: run(), a.reps)
+        trials = {}
+        for tile in (1, 2, 3, 4):
+            for split in (1, 2, 4, 8, 16, 32, 64):
+                try:
+                    trials[(tile, split)] = timeit(lambda: run(tile, split), a.reps)
+                except Exception as e:  # noqa: BLE001 - workspace or shape limits
+                    trials[(tile, split)] = float("inf")
+        c["C"].copy_(C_save)
+        best = min(trials, key=trials.get)
+        n = len(cs)
+        tot_auto += t_auto * n
+        tot_best += trials[best] * n
+        Ash, Bsh, Csh = key[0], key[2], key[4]
+        M, K = Ash[-2], Ash[-1]
+        N = Bsh[-1]
+        bt = max(len(Ash) == 3 and Ash[0] or 1, len(Csh) == 3 and Csh[0] or 1, len(Bsh) == 3 and Bsh[0] or 1)
+        fl = 2.0 * M * N * K * bt
+        row = {"M": M, "N": N, "K": K, "batch": bt, "A_stride": key[1], "B_stride": key[3], "calls": n,
+               "auto_us": t_auto, "best": [TILES[best[0]], best[1]], "best_us": trials[best],
+               "auto_tflops": fl / t_auto / 1e6, "best_tflops": fl / trials[best] / 1e6,
+               "trials": {f"{TILES[k[0]]}/s{k[1]}": v for k, v in trials.items()}}
+        res.append(row)
+        print(f"M{M:6d} N{N:5d} K{K:6d} b{bt} x{n:2d} A{key[1]} B{key[3]}: auto {t_auto:7.1f}us "
+              f"({row['auto_tflops']:5.1f} TF)  best {TILES[best[0]]}/s{best[1]} {trials[best]:7.1f}us "
+              f"({row['best_tflops']:5.1f} TF)", flush=True)
+    print(f"step gemm total: auto {tot_auto:.0f} us, best {tot_best:.0f} us")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
