@@ -98,6 +98,7 @@ def main():
 
     import alignn_mi355x as A
     from alignn_mi355x import profiling
+    from alignn_mi355x.dp import grad_allreduce_hook, max_over_ranks, rank_graphs
     from alignn_mi355x.synthetic import mp_like_batch
 
     B = args.batch
@@ -105,12 +106,9 @@ def main():
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                       args.dropout), 2).to(dev)
     trainer = A.FusedTrainer(model)
-    batch = mp_like_batch(B, first=rank * B, lg_offset=args.lg_offset).to(dev)
+    batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=args.lg_offset).to(dev)
     if world > 1:
-        def allreduce(grad):  # the data-parallel exchange: one all_reduce of the flat gradient
-            dist.all_reduce(grad)
-            grad.mul_(1.0 / world)
-        trainer.grad_hook = allreduce
+        trainer.grad_hook = grad_allreduce_hook(world)  # the DP exchange: one all_reduce of the flat gradient
 
     def step(i):
         trainer.step(batch, seed=1000003 * rank + i)
@@ -166,9 +164,7 @@ def main():
     dt = time.perf_counter() - t0
     profiling.disable()
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = max_over_ranks(dt, dev)
     if probe_in_graph:
         try:  # the event nodes hold the last replay's times
             s_ = profiling.summary()[dominant]
