@@ -286,12 +286,16 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
 
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
-                   dwbar: Optional[torch.Tensor] = None, enc_grads=None) -> None:
+                   dwbar: Optional[torch.Tensor] = None, enc_grads=None,
+                   side: Optional[torch.cuda.Stream] = None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
     (c.wbar set) the gradients of M and w̄ are written to dM / dwbar for :func:`proj_grads`.
-    With an in-kernel edge encoder (c.enc), enc_grads = (dW1, db1) receive its gradients (+=)."""
+    With an in-kernel edge encoder (c.enc), enc_grads = (dW1, db1) receive its gradients (+=).
+    side: a second stream for the weight-gradient products (dM, dw̄, dW, db), which nothing
+    downstream in the backward reads; they overlap the next block's latency-bound attention.  The
+    caller joins the side stream before reading those gradients."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -325,28 +329,60 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
     Oh = dout_a.view(na, H, C).permute(1, 2, 0)
     dQv = dQKV[:, :D].view(na, H, C).transpose(0, 1)
+    Mt = c.M.view(H, C, D).transpose(1, 2)
+    # critical path: dQ (+ its edge-projection terms), then dX
     if c.with_proj:
-        ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0, rowscale=sigz.t(),
-                 bias2=c.wbar.view(H, C))
-        ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
-        ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
-        ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
-        ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
+        ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0, rowscale=sigz.t(), bias2=c.wbar.view(H, C))
     else:
-        ops.gemm(Sz.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), dQv, beta=1.0)
-        ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
-        ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
+        ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0)
     if rows is None:
         ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
-        ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
-        ops.colsum(dQKVR, gv.bqkvr)
     else:
         ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                    # residual + skip projection
         ops.gemm(dQKV, cv.Wqkvr[:3 * D], dX, beta=1.0, c_rows=rows)     # + Q/K/V projections (active rows)
-        ops.gemm(dR.t(), c.X, gv.Wqkvr[3 * D:])
-        ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D])
-        ops.colsum(dR, gv.bqkvr[3 * D:])
-        ops.colsum(dQKV, gv.bqkvr[:3 * D])
+    # weight gradients: off the critical path
+    with _side_work(side, (c.QKV, dout_a, Sz, sigz, c.S, c.sumA, dQKV, dR, c.X, c.Xa)):
+        if c.with_proj:
+            ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
+            ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
+            ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
+            ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
+        else:
+            ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
+            ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
+        if rows is None:
+            ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
+            ops.colsum(dQKVR, gv.bqkvr)
+        else:
+            ops.gemm(dR.t(), c.X, gv.Wqkvr[3 * D:])
+            ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D])
+            ops.colsum(dR, gv.bqkvr[3 * D:])
+            ops.colsum(dQKV, gv.bqkvr[:3 * D])
+
+
+class _side_work:
+    """Runs the enclosed launches on ``side`` after everything already queued on the current
+    stream (no-op context without a side stream).  The tensors are marked as used by the side
+    stream so the caching allocator does not hand their memory to the main stream early."""
+
+    def __init__(self, side: Optional[torch.cuda.Stream], tensors):
+        self.side, self.tensors, self.ctx = side, tensors, None
+
+    def __enter__(self):
+        if self.side is None:
+            return self
+        self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+        for t in self.tensors:
+            if t is not None:
+                t.record_stream(self.side)
+        self.ctx = torch.cuda.stream(self.side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
 
 
 # ------------------------------------------------------------------------------------------------
@@ -363,6 +399,8 @@ class AlignnEngine:
         # recompute the angle hidden layer inside the line convs (kin <= 16) instead of materialising
         # it: measured slower than streaming the materialised rows so far (occupancy-bound), so off
         self.recompute_angle = False
+        # weight-gradient products on a second stream, overlapping the next block's attention
+        self.overlap = True
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -518,6 +556,7 @@ class AlignnEngine:
             dM_all = torch.empty(L, D, D, device=dev)
             dwbar_all = torch.empty(L, D, device=dev)
         line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
+        side = ops.side_stream(dev) if self.overlap else None
         if line_proj:
             dMl_all = torch.empty(L, D, D, device=dev)
             dwl_all = torch.empty(L, D, device=dev)
@@ -526,7 +565,7 @@ class AlignnEngine:
             if self.debug is not None:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
-                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l])
+                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -536,23 +575,27 @@ class AlignnEngine:
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
-                                   enc_grads=enc_grads)
+                                   enc_grads=enc_grads, side=side)
                 else:
-                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags)
+                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side)
                 da_written = True
         if self.debug is not None:
             self.debug["de0"] = de.clone()
-        if E > 0 and L > 0:
-            proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
-        if line_proj:
-            proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all, dwl_all,
-                              G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
-        # encoders
-        if ctx.has_angle and da_written and ctx.angle_enc is None:
-            ops.gemm(da.t(), bc.xa, G.enc("angle", 0, "weight"))  # da is the masked hidden-layer gradient
-            ops.colsum(da, G.enc("angle", 0, "bias"))
+        # projection chain rules and the angle encoder's first layer: side stream (after the
+        # per-layer dM/dw̄ there), overlapping the edge/node encoder backward below
+        with _side_work(side, (da,)):
+            if E > 0 and L > 0:
+                proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
+            if line_proj:
+                proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all,
+                                  dwl_all, G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
+            if ctx.has_angle and da_written and ctx.angle_enc is None:
+                ops.gemm(da.t(), bc.xa, G.enc("angle", 0, "weight"))  # da is the masked hidden-layer gradient
+                ops.colsum(da, G.enc("angle", 0, "bias"))
         if ctx.h1e is not None:
             self._mlp_bwd(de, ctx.edge_attr, ctx.h1e, P.enc("edge", 2, "weight"), G.enc("edge", 0, "weight"),
                           G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))
         self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
                       G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))
+        if side is not None:
+            torch.cuda.current_stream(dev).wait_stream(side)  # join: every gradient is written

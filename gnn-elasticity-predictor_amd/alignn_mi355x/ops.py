@@ -32,15 +32,30 @@ def _require(t: torch.Tensor, name: str, dtype=torch.float32):
 # Workspace (grown on demand, reused; allocate before any graph capture)
 # ------------------------------------------------------------------------------------------------
 class _Workspace:
+    """Scratch buffers per (purpose, device, dtype, stream): kernels on different streams never
+    share one, and a buffer is only reused in its stream's order."""
+
     def __init__(self):
         self.buf = {}
 
     def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
-        cur = self.buf.get((key, device, dtype))
+        k = (key, str(device), dtype, torch.cuda.current_stream(device).cuda_stream)
+        cur = self.buf.get(k)
         if cur is None or cur.numel() < n:
             cur = torch.empty(max(n, 1), device=device, dtype=dtype)
-            self.buf[(key, device, dtype)] = cur
+            self.buf[k] = cur
         return cur
+
+
+_SIDE = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """A second stream per device for work off the critical path (weight gradients)."""
+    key = str(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
 
 
 WS = _Workspace()

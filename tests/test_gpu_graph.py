@@ -51,3 +51,15 @@ def test_graph_step_seed_changes_masks():
     torch.cuda.synchronize()
     assert not torch.equal(g1, g2)
     ops.set_step_seed(None)
+
+
+def test_side_stream_overlap_is_bitwise_neutral():
+    """Weight-gradient work on the side stream gives the same bits as all on one stream."""
+    _, tr1, b1 = _setup()
+    _, tr2, b2 = _setup()
+    tr2.model._engine.overlap = False
+    l1 = tr1.forward_backward(b1, 7)
+    l2 = tr2.forward_backward(b2, 7)
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2)
+    assert torch.equal(tr1.st.grad, tr2.st.grad)
