@@ -309,9 +309,38 @@ def _enc_ws_elems(D: int, H: int, kin: int) -> int:
     return _ENC_WS[key]
 
 
+def _check_tconv(g: GraphCSR, D: int, H: int, QKVR, F, feat_row, enc, node_out=(), node_heads=(), edge_heads=()):
+    """Host check that every operand covers what the kernels index (n target/source rows, m edge
+    rows) before a launch: an undersized buffer would be an out-of-bounds device access."""
+    n, m = g.n, g.m
+    if QKVR.size(0) < n or QKVR.size(1) < 3 * D or QKVR.stride(1) != 1:
+        raise ValueError(f"tconv: QKVR {tuple(QKVR.shape)} must cover [{n}, >= {3 * D}] row-major")
+    if enc is None:
+        if F is None or F.size(1) < D or F.stride(1) != 1:
+            raise ValueError("tconv: edge features F [m, D] row-major required")
+        if m > 0 and F.size(0) < (m if feat_row is None else int(feat_row.numel())):
+            raise ValueError(f"tconv: F has {F.size(0)} rows, the graph has {m} edges")
+        if feat_row is not None and feat_row.numel() < m:
+            raise ValueError("tconv: feat_row must have one entry per edge")
+    elif enc.x.size(0) < m:
+        raise ValueError(f"tconv: encoder inputs have {enc.x.size(0)} rows, the graph has {m} edges")
+    for t in node_out:
+        if t is not None and t.numel() < n * D:
+            raise ValueError(f"tconv: per-node operand {tuple(t.shape)} smaller than [{n}, {D}]")
+    for t in node_heads:
+        if t is not None and t.numel() < n * H:
+            raise ValueError(f"tconv: per-node stats {tuple(t.shape)} smaller than [{n}, {H}]")
+    for t in edge_heads:
+        if t is not None and t.numel() < m * H:
+            raise ValueError(f"tconv: per-edge stats {tuple(t.shape)} smaller than [{m}, {H}]")
+
+
 def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, wbar: Optional[torch.Tensor],
               F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float,
               seed: int, enc: Optional[EdgeEncoder] = None):
+    _check_tconv(g, D, H, QKVR, F, feat_row, enc, node_out=(aggV,), node_heads=(sumA, mstat, den))
+    if U.numel() < g.n * H * D or S.numel() < g.n * H * D:
+        raise ValueError("tconv_fwd: U and S must be [n, H, D]")
     es = None if enc is None else enc.struct()
     profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd", enc.kin if enc else 0),
                      lambda: check(_lib.lib().alignn_tconv_fwd(
@@ -327,6 +356,12 @@ def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, d
                   enc: Optional[EdgeEncoder] = None):
     """accumulate_dF: bit 0 add into dF, bit 1 apply the ReLU mask (F > 0) to the result.  With an
     edge encoder, F/dF are unused and the encoder gradients go to enc.dw1/enc.db1."""
+    _check_tconv(g, D, H, QKVR, F, feat_row, enc, node_out=(dout, outp), node_heads=(mstat, den, sigz),
+                 edge_heads=(dz_e, alpha_e))
+    if U.numel() < g.n * H * D or Vd.numel() < g.n * H * D or Sz.numel() < g.n * H * D or dq.size(0) < g.n:
+        raise ValueError("tconv_bwd_dst: U, Vd, Sz must be [n, H, D] and dq [n, >= D]")
+    if enc is None and dF is not None and dF.size(0) < F.size(0):
+        raise ValueError("tconv_bwd_dst: dF must cover the rows of F")
     es = None if enc is None else enc.struct(D, H, backward=True)
     profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0,
                      _tconv_bytes(g.n, g.m, D, H, "bwd_dst", enc.kin if enc else 0),
@@ -342,6 +377,9 @@ def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, d
 
 
 def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):
+    if (QKVR.size(0) < g.n or dout.numel() < g.n * D or dKV.size(0) < g.n or dKV.size(1) < 2 * D
+            or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H):
+        raise ValueError("tconv_bwd_src: operands do not cover the graph's n nodes / m edges")
     profiling.launch(f"tconv_bwd_src n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_src"), lambda: check(_lib.lib().alignn_tconv_bwd_src(g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(),
                                           g.dst_at.data_ptr(), QKVR.data_ptr(), QKVR.stride(0), dout.data_ptr(),
                                           dz_e.data_ptr(), alpha_e.data_ptr(), dKV.data_ptr(), dKV.stride(0),

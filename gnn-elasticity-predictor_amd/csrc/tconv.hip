@@ -531,6 +531,7 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
           const float dzl = pick<H>(dz, hl);
 #pragma unroll
           for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, ring[j].k[i], dqa[i]);
+#ifndef ALIGNN_NO_ENC_ACC
           if constexpr (KM > 0) {
             // g = relu'(.) * sum_h (dz u + alpha' Vd); dW1 += g x^T, db1 += g
             float g[VPL];
@@ -548,7 +549,9 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
 #pragma unroll
               for (int i = 0; i < VPL; ++i) ea.w[k][i] = fmaf(xk, g[i], ea.w[k][i]);
             }
-          } else {
+          } else
+#endif
+          if constexpr (KM == 0) {
             if (do_dF && act) {
               float df[VPL];
 #pragma unroll

@@ -80,3 +80,21 @@ def test_collate_matches_oracle(mode):
               "batch", "ptr"):
         assert torch.equal(getattr(b, k), getattr(r, k)), k
     assert b.num_graphs == 3
+
+
+def test_tconv_host_shape_checks_reject_undersized_operands():
+    """The attention wrappers refuse (ValueError) operands smaller than the graph before any launch."""
+    import types
+    from alignn_mi355x import ops
+    g = types.SimpleNamespace(n=10, m=40)
+    D, H = 64, 4
+    ok = dict(QKVR=torch.zeros(10, 3 * D), F=torch.zeros(40, D))
+    ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None, None)
+    with pytest.raises(ValueError):
+        ops._check_tconv(g, D, H, ok["QKVR"], torch.zeros(39, D), None, None)     # F short of m rows
+    with pytest.raises(ValueError):
+        ops._check_tconv(g, D, H, torch.zeros(9, 3 * D), ok["F"], None, None)     # QKVR short of n rows
+    with pytest.raises(ValueError):
+        ops._check_tconv(g, D, H, ok["QKVR"], None, None, None)                    # no edge features
+    with pytest.raises(ValueError):
+        ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None, None, edge_heads=(torch.zeros(40, 3),))

@@ -31,6 +31,10 @@ def timeit(fn, reps):
 
 def run_graph(name, g, n, m, D, H, F, enc, reps, out):
     dev = "cuda"
+    # shapes the kernels assume (checked on the host before any launch)
+    assert g.n == n and g.m == m, (g.n, n, g.m, m)
+    assert F is None or F.size(0) >= m, (F.size(0), m)
+    assert enc is None or enc.x.size(0) >= m
     gen = torch.Generator(device=dev).manual_seed(0)
     r = lambda *s: torch.randn(*s, device=dev, generator=gen) * 0.5
     QKVR, U, Vd = r(n, 4 * D), r(n, H, D), r(n, H, D)
@@ -68,15 +72,17 @@ def main():
     for lg_offset in ("num_nodes", "num_edges"):
         b = mp_like_batch(a.batch, lg_offset=lg_offset).to("cuda")
         E, T = b.edge_index.size(1), b.lg_edge_index.size(1)
-        lg = ops.GraphCSR(b.lg_edge_index, E)
+        from alignn_mi355x.engine import BatchCache
+        lg = BatchCache._compact(ops.GraphCSR(b.lg_edge_index, E), b.lg_edge_index, E)
+        nl = lg.n  # line-graph nodes after compaction to the bonds with line-graph edges
         xa = torch.empty_like(b.lg_edge_attr)
         ops.gather_rows(b.lg_edge_attr, lg.perm_dst, xa)
         w1 = torch.randn(D, xa.size(1), device="cuda") * 0.3
         b1 = torch.randn(D, device="cuda") * 0.1
         enc = ops.EdgeEncoder(xa, w1, b1)
-        run_graph(f"line/{lg_offset}/enc", lg, E, T, D, H, None, enc, a.reps, out)
+        run_graph(f"line/{lg_offset}/enc", lg, nl, T, D, H, None, enc, a.reps, out)
         F = torch.relu(xa @ w1.t() + b1)
-        run_graph(f"line/{lg_offset}/F", lg, E, T, D, H, F, None, a.reps, out)
+        run_graph(f"line/{lg_offset}/F", lg, nl, T, D, H, F, None, a.reps, out)
         if lg_offset == "num_nodes":
             N = b.x.size(0)
             ag = ops.GraphCSR(b.edge_index, N)
