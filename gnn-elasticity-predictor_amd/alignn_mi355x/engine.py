@@ -227,7 +227,7 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
 
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
-                  seed_blk: int, enc: Optional[ops.EdgeEncoder] = None):
+                  seed_blk: int, enc: Optional[ops.EdgeEncoder] = None, side: Optional[torch.cuda.Stream] = None):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     enc: edge features recomputed in-kernel from raw inputs (then F is None).
 
@@ -254,7 +254,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
         c.QKV = torch.empty(na, 3 * D, device=dev)
         ops.gemm(c.Xa, cv.Wqkvr[:3 * D].t(), c.QKV, bias=cv.bqkvr[:3 * D])
         c.R = torch.empty(n, D, device=dev)
-        ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+        with _side_work(side, (X, c.R)):   # skip projection of all rows, concurrent with the attention
+            ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
     c.U = torch.empty(na, H, D, device=dev)
     ops.gemm(c.QKV[:, :D].view(na, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
     c.outp_a = torch.empty(na, D, device=dev)
@@ -275,6 +276,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     else:
         c.outp = torch.zeros(n, D, device=dev)
         ops.scatter_rows(c.outp_a, rows, c.outp)
+    if side is not None and rows is not None:
+        torch.cuda.current_stream(dev).wait_stream(side)
     X_new = torch.empty(n, D, device=dev)
     c.beta = torch.empty(n, device=dev)
     c.mu = torch.empty(n, device=dev)
@@ -401,6 +404,9 @@ class AlignnEngine:
         self.recompute_angle = False
         # weight-gradient products on a second stream, overlapping the next block's attention
         self.overlap = True
+        # forward: the line blocks' skip projection on the second stream beside the attention
+        # (off by default until measured on MI355X)
+        self.overlap_forward = False
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -458,6 +464,7 @@ class AlignnEngine:
             a = torch.zeros(T, D, device=dev)
         ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
+        side = ops.side_stream(dev) if (self.overlap and self.overlap_forward) else None
         if T > 0 and E > 0 and L > 0 and ctx.has_angle:
             W2, b2 = P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias")
             ctx.Ml_all, ctx.wl_all = proj_weights(P.edge_We, W2.expand(L, D, D), b2.expand(L, D))
@@ -468,7 +475,8 @@ class AlignnEngine:
             if T > 0 and E > 0:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
-                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), enc=ctx.angle_enc)
+                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), enc=ctx.angle_enc,
+                                     side=side)
             else:
                 c = None
             ctx.edge.append(c)

@@ -3,27 +3,27 @@
 // Replaces the cuBLAS addmm/mm behind every nn.Linear / PyG Linear of the reference's hot path
 // (SURVEY §2 implicit-kernel table) and their autograd backward products.
 //
-// Tiling: BM x BN block (64 or 128 each), BK = 16, 256 threads = 4 waves in a 2x2 grid, each wave
-// owns (BM/2)x(BN/2) = MI x NI subtiles of 32x32.  One K-tile per iteration, double-buffered LDS
-// with register prefetch of the next tile (issue global loads before the MFMAs, write LDS after).
+// Tiling: BM x BN block (64 or 128 each), K stage BKT = 16 or 32 (two 16-deep slices), 256 threads
+// = 4 waves in a 2x2 grid, each wave owns (BM/2)x(BN/2) = MI x NI subtiles of 32x32.  One stage per
+// iteration, double-buffered LDS with register prefetch of the next stage (issue global loads
+// before the MFMAs, write LDS after); a 32-deep stage halves the barriers per MFMA.
 //
 // k-slot assignment: an MFMA 32x32x2 sums over two k-slots, lane half h = lane>>5 supplying slot h.
-// Over the 8 MFMAs of a 16-deep K-tile, step s uses k = 8h + s for lane half h, so a lane's eight
+// Over the 8 MFMAs of a 16-deep slice, step s uses k = 8h + s for lane half h, so a lane's eight
 // k-values are contiguous: one pair of ds_read_b128 per subtile when the LDS image is [row][k],
 // eight ds_read_b32 when it is [k][row].  Both operands use the same assignment, so the sum over
 // k is complete (in a permuted order — still an exact per-product-rounded fp32 chain).
 //
 // LDS images follow global contiguity (no transposes while staging):
-//   operand contiguous along k   -> [row][BK+4]   (80-B rows: ds_read_b128 conflict-free)
-//   operand contiguous along row -> [BK][ROWS+4]
+//   operand contiguous along k   -> [row][BKT+4]
+//   operand contiguous along row -> [BKT][ROWS+4]
 #include "common.h"
 
 namespace alignn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 16;
-constexpr int KPAD = BK + 4;
+constexpr int BK = 16;  // split-K chunk granularity
 
 struct GemmParams {
   int64_t M, N, K, batch;
@@ -44,11 +44,12 @@ struct GemmParams {
   const int32_t* c_rows;  // optional scatter of C rows
 };
 
-// Loads one operand tile (ROWS x BK) into registers.  KC: load along k (general strides,
+// Loads one operand tile (ROWS x BKT) into registers.  KC: load along k (general strides,
 // float4 when stride_k==1 and aligned); !KC: load along rows (stride_row == 1).
-template <int ROWS, bool KC>
+template <int ROWS, bool KC, int BKT>
 struct TileLoader {
-  static constexpr int F4 = ROWS * BK / 4 / 256;  // float4 per thread (1 or 2)
+  static constexpr int F4 = ROWS * BKT / 4 / 256;  // float4 per thread
+  static constexpr int KP = BKT + 4;               // padded k-row of the [row][k] image
   float4 r[F4];
 
   __device__ __forceinline__ void load(const float* __restrict__ P, int64_t srow, int64_t sk, int64_t row0,
@@ -58,8 +59,8 @@ struct TileLoader {
       int idx = threadIdx.x + 256 * i;
       int64_t gr, gk;
       if (KC) {
-        gr = row0 + (idx >> 2);
-        gk = k0 + (idx & 3) * 4;
+        gr = row0 + (idx / (BKT / 4));
+        gk = k0 + (idx % (BKT / 4)) * 4;
       } else {
         gk = k0 + (idx / (ROWS / 4));
         gr = row0 + (idx % (ROWS / 4)) * 4;
@@ -97,8 +98,8 @@ struct TileLoader {
     for (int i = 0; i < F4; ++i) {
       int idx = threadIdx.x + 256 * i;
       if (KC) {
-        int rr = idx >> 2, kk = (idx & 3) * 4;
-        *reinterpret_cast<float4*>(lds + rr * KPAD + kk) = r[i];
+        int rr = idx / (BKT / 4), kk = (idx % (BKT / 4)) * 4;
+        *reinterpret_cast<float4*>(lds + rr * KP + kk) = r[i];
       } else {
         int kk = idx / (ROWS / 4), rr = (idx % (ROWS / 4)) * 4;
         *reinterpret_cast<float4*>(lds + kk * (ROWS + 4) + rr) = r[i];
@@ -107,22 +108,24 @@ struct TileLoader {
   }
 };
 
-template <int ROWS, bool KC>
+template <int ROWS, bool KC, int BKT>
 constexpr int lds_floats() {
-  return KC ? ROWS * KPAD : BK * (ROWS + 4);
+  return KC ? ROWS * (BKT + 4) : BKT * (ROWS + 4);
 }
 
-// Reads the 8 k-values of lane half h for subtile row `row` (0..ROWS-1).
-template <int ROWS, bool KC>
-__device__ __forceinline__ void read_frag(const float* __restrict__ lds, int row, int h, float (&f)[8]) {
+// Reads the 8 k-values of lane half h in 16-deep slice `sub` for subtile row `row`:
+// k = 16*sub + 8*h + s, s = 0..7 (the MFMA k-slot assignment, identical for A and B).
+template <int ROWS, bool KC, int BKT>
+__device__ __forceinline__ void read_frag(const float* __restrict__ lds, int row, int h, int sub, float (&f)[8]) {
   if (KC) {
-    float4 a = *reinterpret_cast<const float4*>(lds + row * KPAD + 8 * h);
-    float4 b = *reinterpret_cast<const float4*>(lds + row * KPAD + 8 * h + 4);
+    const float* q = lds + row * (BKT + 4) + 16 * sub + 8 * h;
+    float4 a = *reinterpret_cast<const float4*>(q);
+    float4 b = *reinterpret_cast<const float4*>(q + 4);
     f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
     f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
   } else {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) f[s] = lds[(8 * h + s) * (ROWS + 4) + row];
+    for (int s = 0; s < 8; ++s) f[s] = lds[(16 * sub + 8 * h + s) * (ROWS + 4) + row];
   }
 }
 
@@ -141,10 +144,10 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, 
   return v;
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC>
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
-  constexpr int LA = lds_floats<BM, A_KC>(), LB = lds_floats<BN, B_KC>();
+  constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
@@ -174,8 +177,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  TileLoader<BM, A_KC> la;
-  TileLoader<BN, B_KC> lb;
+  TileLoader<BM, A_KC, BKT> la;
+  TileLoader<BN, B_KC, BKT> lb;
   // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
   la.load(tileA(kb), p.sam, p.sak, m0, p.M, kloc(kb), kend(kb), p.vecA);
   lb.load(tileB(kb), p.sbn, p.sbk, n0, p.N, kloc(kb), kend(kb), p.vecB);
@@ -184,26 +187,29 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   __syncthreads();
 
   int cur = 0;
-  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
-    const bool more = k0 + BK < ke;
+  for (int64_t k0 = kb; k0 < ke; k0 += BKT) {
+    const bool more = k0 + BKT < ke;
     if (more) {
-      la.load(tileA(k0 + BK), p.sam, p.sak, m0, p.M, kloc(k0 + BK), kend(k0 + BK), p.vecA);
-      lb.load(tileB(k0 + BK), p.sbn, p.sbk, n0, p.N, kloc(k0 + BK), kend(k0 + BK), p.vecB);
+      la.load(tileA(k0 + BKT), p.sam, p.sak, m0, p.M, kloc(k0 + BKT), kend(k0 + BKT), p.vecA);
+      lb.load(tileB(k0 + BKT), p.sbn, p.sbk, n0, p.N, kloc(k0 + BKT), kend(k0 + BKT), p.vecB);
     }
     const float* As = smem + cur * (LA + LB);
     const float* Bs = As + LA;
-    float fa[MI][8], fb[NI][8];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) read_frag<BM, A_KC>(As, wm * (BM / 2) + i * 32 + l32, h, fa[i]);
+    for (int sub = 0; sub < BKT / 16; ++sub) {
+      float fa[MI][8], fb[NI][8];
 #pragma unroll
-    for (int j = 0; j < NI; ++j) read_frag<BN, B_KC>(Bs, wn * (BN / 2) + j * 32 + l32, h, fb[j]);
+      for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, BKT>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+      for (int j = 0; j < NI; ++j) read_frag<BN, B_KC, BKT>(Bs, wn * (BN / 2) + j * 32 + l32, h, sub, fb[j]);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+    }
     if (more) {
       float* nxt = smem + (cur ^ 1) * (LA + LB);
       la.store(nxt);
@@ -256,16 +262,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC>
-static void launch(const GemmParams& p, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC>), grid, dim3(256), 0, s, p);
+static void launch(const GemmParams& p, dim3 grid, int bk, hipStream_t s) {
+  if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16>), grid, dim3(256), 0, s, p);
 }
 
 template <int BM, int BN>
-static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, hipStream_t s) {
-  if (akc && bkc) launch<BM, BN, true, true>(p, grid, s);
-  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, s);
-  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, s);
-  else launch<BM, BN, false, false>(p, grid, s);
+static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, hipStream_t s) {
+  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, s);
+  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, s);
+  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, s);
+  else launch<BM, BN, false, false>(p, grid, bk, s);
 }
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -283,7 +290,7 @@ static int device_cus() {
 }
 
 struct GemmPlan {
-  int bm, bn, split;
+  int bm, bn, split, bk;
   int64_t kchunk;
 };
 
@@ -295,13 +302,14 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   const int cus = device_cus();
   static const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
   static const double eff[4] = {1.0, 1.1, 1.1, 1.35};
-  GemmPlan pl{64, 64, 1, 0};
+  GemmPlan pl{64, 64, 1, 16, 0};
   double best = -1.0;
   int64_t best_tiles = 0;
   for (int c = 0; c < 4; ++c) {
     const int bm = cand[c][0], bn = cand[c][1];
-    if (tile >= 1 && tile <= 4 && c != tile - 1) continue;
-    if (tile == 0 && ((bm == 128 && M <= 64) || (bn == 128 && N <= 64))) continue;
+    const int shape = tile & 15;
+    if (shape >= 1 && shape <= 4 && c != shape - 1) continue;
+    if (shape == 0 && ((bm == 128 && M <= 64) || (bn == 128 && N <= 64))) continue;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * nb;
     const double cost = (double)((tiles + cus - 1) / cus) * bm * bn * eff[c];
     if (best < 0 || cost < best) {
@@ -328,6 +336,9 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   if (split < 1) split = 1;
   pl.split = split;
   pl.kchunk = kchunk;
+  // K depth of a pipeline stage (tile bit 4 selects 32: half the barriers per flop; the automatic
+  // plan keeps 16 until the 32-deep stage has been measured on MI355X)
+  pl.bk = (tile & 16) ? 32 : 16;
   return pl;
 }
 
@@ -337,6 +348,9 @@ static bool plan_args(const AlignnGemmArgs* a, GemmPlan& pl, int64_t& ktot, int6
   ktot = rb ? a->K * a->batch : a->K;
   nb_out = rb ? 1 : a->batch;
   pl = make_plan(a->M, a->N, ktot, nb_out, a->split_k, a->tile);
+  // a stage must not straddle two batch entries of a batch-reduced product, nor a split chunk
+  if (rb && a->K % pl.bk != 0) pl.bk = 16;
+  if (pl.split > 1 && pl.kchunk % pl.bk != 0) pl.bk = 16;
   return true;
 }
 
@@ -398,10 +412,10 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   }
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
-  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, s);
-  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, s);
-  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, s);
-  else dispatch_layout<64, 64>(p, akc, bkc, grid, s);
+  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, s);
+  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, s);
+  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, s);
+  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {
     int64_t total = nbatch_out * a->M * a->N;

@@ -17,20 +17,30 @@ import alignn_mi355x as A  # noqa: E402
 from alignn_mi355x import ops  # noqa: E402
 from alignn_mi355x.synthetic import mp_like_batch  # noqa: E402
 
-TILES = {1: "128x128", 2: "128x64", 3: "64x128", 4: "64x64"}
+TILES = {b + k: f"{s}/bk{bk}" for k, s in ((1, "128x128"), (2, "128x64"), (3, "64x128"), (4, "64x64"))
+         for b, bk in ((0, "auto"), (16, 32), (32, 16))}
 
 
 def timeit(fn, reps):
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    """Device time per call: ``reps`` calls captured in one HIP graph (no host launch cost in the
+    measurement), replayed 3 times between two events; median replay / reps."""
     fn()
     torch.cuda.synchronize()
-    for a, b in ev:
-        a.record()
-        fn()
-        b.record()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
-    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
-    return ts[len(ts) // 2]
+    ts = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / reps)
+    return sorted(ts)[1]
 
 
 def sig(c):
@@ -74,7 +84,7 @@ def main():
 
         t_auto = timeit(lambda: run(), a.reps)
         trials = {}
-        for tile in (1, 2, 3, 4):
+        for tile in (1, 2, 3, 4, 17, 18, 19, 20, 33, 34, 35, 36):
             for split in (1, 2, 4, 8, 16, 32, 64):
                 try:
                     trials[(tile, split)] = timeit(lambda: run(tile, split), a.reps)

@@ -17,16 +17,25 @@ from alignn_mi355x.synthetic import mp_like_batch  # noqa: E402
 
 
 def timeit(fn, reps):
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    """Device time per call: ``reps`` calls captured in one HIP graph, replayed 3 times between two
+    events; median replay / reps."""
     fn()
     torch.cuda.synchronize()
-    for a, b in ev:
-        a.record()
-        fn()
-        b.record()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
-    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
-    return ts[len(ts) // 2]
+    ts = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / reps)
+    return sorted(ts)[1]
 
 
 def run_graph(name, g, n, m, D, H, F, enc, reps, out):
