@@ -349,8 +349,7 @@ static bool plan_args(const AlignnGemmArgs* a, GemmPlan& pl, int64_t& ktot, int6
   nb_out = rb ? 1 : a->batch;
   pl = make_plan(a->M, a->N, ktot, nb_out, a->split_k, a->tile);
   // a stage must not straddle two batch entries of a batch-reduced product, nor a split chunk
-  if (rb && a->K % pl.bk != 0) pl.bk = 16;
-  if (pl.split > 1 && pl.kchunk % pl.bk != 0) pl.bk = 16;
+  if (rb && (a->K % pl.bk != 0 || (pl.split > 1 && pl.kchunk % pl.bk != 0))) pl.bk = 16;
   return true;
 }
 
