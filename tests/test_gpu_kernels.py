@@ -88,30 +88,6 @@ def test_gemm_auto_plan_shapes(M, N, K, batch):
     assert _rel(C, ref) < 5e-6
 
 
-@pytest.mark.parametrize("shape", [1, 2, 3, 4])
-@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
-def test_gemm_bk32_stage(shape, layout):
-    """32-deep K stage (tile bit 4) on every tile shape and operand layout, unsplit and split-K."""
-    ops = _ops()
-    g = torch.Generator(device="cpu").manual_seed(shape * 11 + len(layout))
-    M, N, K = 300, 257, 1000
-    A = torch.randn(M, K, generator=g).to(DEV)
-    B = torch.randn(K, N, generator=g).to(DEV)
-    Av = A if layout[0] == "n" else A.t().contiguous().t()
-    Bv = B if layout[1] == "n" else B.t().contiguous().t()
-    ref = A.double() @ B.double()
-    for split in (1, 3):
-        C = torch.empty(M, N, device=DEV)
-        ops.gemm(Av, Bv, C, tile=16 + shape, split_k=split)
-        assert _rel(C, ref) < 5e-6, (split,)
-    # batch-reduced (shared weights): K multiple of 32 keeps the 32-deep stage inside one batch entry
-    Ab = torch.randn(4, 64, 256, generator=g).to(DEV)
-    Bb = torch.randn(4, 256, 96, generator=g).to(DEV)
-    Cb = torch.empty(64, 96, device=DEV)
-    ops.gemm(Ab, Bb, Cb, reduce_batch=True, tile=16 + shape)
-    assert _rel(Cb, (Ab.double() @ Bb.double()).sum(0)) < 5e-6
-
-
 def test_gemm_c_rows_scatter():
     ops = _ops()
     torch.manual_seed(3)
