@@ -1,0 +1,173 @@
+"""Deep-ensemble inference on the MI355X engine.
+
+Reference: ``ensemble_collect`` / ``ensemble_collect_embeddings`` (scripts/train.py:849-927),
+``_fit_affine_debias`` / ``conformal_calibration`` / ``apply_conformal_intervals``
+(train.py:1013-1076) and ``predict.ensemble_predict`` (scripts/predict.py:582-653).
+
+MI355X design: the M members share one batch preparation (CSR lists, line-graph compaction); their
+forwards (eval mode, no autograd) run concurrently, one HIP stream per member — the attention
+kernels are latency-bound, so members overlap on the CUs — and one kernel
+(``alignn_ensemble_moments``) does the moment mix and the log-normal conversion.  Calibration
+(affine debias, conformal quantile) runs on the host over the collected [n, T] predictions, as in
+the reference.  Members on different GPUs: run one ``EnsemblePredictor`` of one member per rank and
+gather the [B, 2T] heads.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import MIN_LOGVAR_FLOOR, batch_cache
+from .ops import stream_ptr
+from .synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS
+
+Z_SCORE_90 = 1.6448536269514722  # predict.py:63
+
+
+class EnsemblePredictor:
+    def __init__(self, models: Sequence, min_logvar_floor: float = MIN_LOGVAR_FLOOR,
+                 target_log_means: Sequence[float] = TARGET_LOG_MEANS,
+                 target_log_stds: Sequence[float] = TARGET_LOG_STDS, concurrent: bool = True):
+        if not models:
+            raise ValueError("EnsemblePredictor needs at least one member")
+        self.models = list(models)
+        self.floor = float(min_logvar_floor)
+        self.concurrent = concurrent
+        self._streams: List[torch.cuda.Stream] = []
+        self._log_means = list(target_log_means)
+        self._log_stds = list(target_log_stds)
+        self._lm = self._ls = None
+
+    def _member_streams(self, dev) -> List[Optional[torch.cuda.Stream]]:
+        if not self.concurrent:
+            return [None] * len(self.models)
+        while len(self._streams) < len(self.models):
+            self._streams.append(torch.cuda.Stream(device=dev))
+        return self._streams[:len(self.models)]
+
+    def member_outputs(self, batch, mode: str = "hetero") -> torch.Tensor:
+        """[M, B, 2T] heads (hetero) or [M, B, D] embeddings, members in eval mode (dropout off)."""
+        bc = batch_cache(batch)
+        dev = batch.x.device
+        main = torch.cuda.current_stream(dev)
+        x, gx = batch.x.contiguous().float(), batch.global_x.contiguous().float()
+        outs = []
+        for m, s in zip(self.models, self._member_streams(dev)):
+            st = m._ensure_flat()
+            if s is None:
+                out, _ = m._engine.forward(st.P, batch, bc, False, 0, x, gx, mode)
+            else:
+                s.wait_stream(main)
+                with torch.cuda.stream(s):
+                    out, _ = m._engine.forward(st.P, batch, bc, False, 0, x, gx, mode)
+                out.record_stream(main)
+            outs.append(out)
+        for s in self._member_streams(dev):
+            if s is not None:
+                main.wait_stream(s)
+        return torch.stack(outs, 0)
+
+    def _moments(self, heads: torch.Tensor, convert: bool) -> Dict[str, torch.Tensor]:
+        M, B, W = heads.shape
+        T = W // 2
+        dev = heads.device
+        if self._lm is None or self._lm.device != dev:
+            self._lm = torch.tensor(self._log_means, dtype=torch.float32, device=dev)
+            self._ls = torch.tensor(self._log_stds, dtype=torch.float32, device=dev)
+        names = ("mean_z", "std_z") + (("mean_orig", "std_lin", "lo90", "hi90") if convert else ())
+        res = {k: torch.empty(B, T, device=dev) for k in names}
+        ptr = lambda k: res[k].data_ptr() if k in res else None  # noqa: E731
+        h = heads.contiguous()
+        _lib.check(_lib.lib().alignn_ensemble_moments(
+            M, B, T, h.data_ptr(), h.stride(0), h.stride(1), self.floor,
+            self._lm.data_ptr() if convert else None, self._ls.data_ptr() if convert else None,
+            ptr("mean_z"), ptr("std_z"), ptr("mean_orig"), ptr("std_lin"), ptr("lo90"), ptr("hi90"),
+            stream_ptr()), "alignn_ensemble_moments")
+        return res
+
+    def predict_batch(self, batch) -> Dict[str, torch.Tensor]:
+        """predict.ensemble_predict for one batch (device tensors, [B, T] each): mean_z, std_z
+        (standardized log space), mean_orig (= mu), std_lin (= sigma), lo90/hi90 (ci90)."""
+        return self._moments(self.member_outputs(batch), convert=True)
+
+    def collect(self, batches) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """ensemble_collect (hetero): (mean_z [n,T], targets [n,T], std_z [n,T]) on the host."""
+        means, stds, ys = [], [], []
+        for b in batches:
+            r = self._moments(self.member_outputs(b), convert=False)
+            means.append(r["mean_z"].cpu())
+            stds.append(r["std_z"].cpu())
+            ys.append(b.y.view(b.num_graphs, -1).float().cpu())
+        if not means:
+            raise ValueError("No batches produced predictions.")
+        return torch.cat(means), torch.cat(ys), torch.cat(stds)
+
+    def embed(self, batches) -> torch.Tensor:
+        """ensemble_collect_embeddings: member-mean of embed() per graph, host [n, D]."""
+        out = []
+        for b in batches:
+            e = self.member_outputs(b, mode="embed").contiguous()
+            M = e.size(0)
+            mean = torch.empty(e.shape[1:], device=e.device)
+            _lib.check(_lib.lib().alignn_member_mean_f32(M, mean.numel(), e.data_ptr(), e.stride(0),
+                                                         mean.data_ptr(), stream_ptr()), "alignn_member_mean_f32")
+            out.append(mean.cpu())
+        if not out:
+            raise ValueError("No batches produced embeddings.")
+        return torch.cat(out)
+
+
+# ------------------------------------------------------------------------------------------------
+# Calibration on the collected predictions (host, as in the reference)
+# ------------------------------------------------------------------------------------------------
+def fit_affine_debias(pred_z: torch.Tensor, target_z: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """train.py:1013-1026: per-target least squares target_z ~ a * pred_z + b (float64 solve)."""
+    p = pred_z.detach().float().cpu().numpy()
+    t = target_z.detach().float().cpu().numpy()
+    a = np.zeros(p.shape[1])
+    b = np.zeros(p.shape[1])
+    for k in range(p.shape[1]):
+        X = np.stack([p[:, k], np.ones_like(p[:, k])], axis=1)
+        sol = np.linalg.lstsq(X, t[:, k], rcond=None)[0]
+        a[k], b[k] = sol[0], sol[1]
+    return (torch.from_numpy(a).to(pred_z.device, pred_z.dtype), torch.from_numpy(b).to(pred_z.device, pred_z.dtype))
+
+
+def _to_z(targets: torch.Tensor, log_means, log_stds) -> torch.Tensor:
+    m = torch.as_tensor(log_means, dtype=targets.dtype).view(1, -1)
+    s = torch.as_tensor(log_stds, dtype=targets.dtype).view(1, -1)
+    return (torch.log(torch.clamp(targets, min=1e-12)) - m) / s
+
+
+def conformal_calibration(mean_z, std_z, targets, alpha: float, method: str,
+                          log_means=TARGET_LOG_MEANS, log_stds=TARGET_LOG_STDS) -> Dict:
+    """train.py:1029-1051: split-conformal quantile of |target_z - mean_z| (/ std_z if 'scaled')."""
+    tz = _to_z(targets, log_means, log_stds) if log_means is not None else targets
+    if method == "scaled" and std_z is not None:
+        s = (tz - mean_z).abs() / torch.clamp(std_z, min=1e-12)
+    else:
+        s = (tz - mean_z).abs()
+        method = "absolute"
+    n = s.size(0)
+    q_level = min(max(math.ceil((n + 1) * (1 - alpha)) / n, 0.0), 1.0)
+    return {"q": torch.quantile(s, q_level, dim=0), "method": method, "alpha": alpha}
+
+
+def apply_conformal_intervals(mean_z, std_z, conf: Dict, log_means=TARGET_LOG_MEANS, log_stds=TARGET_LOG_STDS):
+    """train.py:1054-1076: (mean, lower, upper) on the target scale."""
+    q = conf["q"].to(mean_z)
+    if conf.get("method") == "scaled" and std_z is not None:
+        lo, hi = mean_z - q * std_z.to(mean_z), mean_z + q * std_z.to(mean_z)
+    else:
+        lo, hi = mean_z - q, mean_z + q
+    if log_means is None:
+        return mean_z, lo, hi
+    m = torch.as_tensor(log_means, dtype=mean_z.dtype, device=mean_z.device).view(1, -1)
+    s = torch.as_tensor(log_stds, dtype=mean_z.dtype, device=mean_z.device).view(1, -1)
+    inv = lambda z: torch.exp(z * s + m)  # noqa: E731  (LogTransformer.inverse_transform_tensor)
+    return inv(mean_z), inv(lo), inv(hi)

@@ -233,6 +233,25 @@ int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64_t ldh, con
 /* Feature jitter (train.py:641-646): x += std * N(0,1) from a counter-based generator. */
 int alignn_add_noise_f32(int64_t n, float* x, float std, uint64_t seed, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Deep-ensemble inference: moment-matched mixture of M heteroscedastic members,
+ * ensemble_collect train.py:875-894, and predict.ensemble_predict's log-normal conversion and
+ * 90% interval, predict.py:604-640.
+ *   heads: member j's [B, 2T] output (mean | logvar) at heads + j*member_stride, row stride ldh.
+ *   var_j = exp(max(logvar_j, floor)); mean = E[mu]; var = E[var_j] + E[mu^2] - mean^2;
+ *   std_z = sqrt(max(var, 1e-12)).  With log_means/log_stds [T] (LogTransformer): mean_orig =
+ *   exp(mean*s+m), std_lin = sqrt(max((exp(ls^2)-1) exp(2lm+ls^2), 0)), lo90/hi90 = mean_orig -/+
+ *   1.6448536269514722 std_lin (lo clipped at 0).  Outputs [B, T]; any may be NULL.
+ * ---------------------------------------------------------------------------------------- */
+int alignn_ensemble_moments(int32_t M, int64_t B, int32_t T, const float* heads, int64_t member_stride,
+                            int64_t ldh, float min_logvar_floor, const float* log_means, const float* log_stds,
+                            float* mean_z, float* std_z, float* mean_orig, float* std_lin, float* lo90,
+                            float* hi90, void* stream);
+
+/* out[i] = mean over M members of x[j*member_stride + i], i < n (ensemble embeddings,
+ * ensemble_collect_embeddings train.py:907-927). */
+int alignn_member_mean_f32(int32_t M, int64_t n, const float* x, int64_t member_stride, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
