@@ -84,6 +84,9 @@ _SIGNATURES = {
     "alignn_ensemble_moments": ([c_i32, c_i64, c_i32, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_vp, c_vp], c_i32),
     "alignn_member_mean_f32": ([c_i32, c_i64, c_vp, c_i64, c_vp, c_vp], c_i32),
+    "alignn_grad_norm_f32": ([c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
+    "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_f32,
+                          c_vp, c_vp], c_i32),
 }
 
 EXPORTED = tuple(_SIGNATURES.keys())

@@ -443,3 +443,27 @@ def hetero_nll(heads, y, log_means, log_stds, floor, l2, loss, dheads):
 def add_noise(x: torch.Tensor, std: float, seed: int):
     check(_lib.lib().alignn_add_noise_f32(x.numel(), x.data_ptr(), float(std), int(seed) & (2**64 - 1),
                                           stream_ptr()), "alignn_add_noise_f32")
+
+
+# ------------------------------------------------------------------------------------------------
+# Optimizer (clip_grad_norm_ + AdamW over the flat buffers)
+# ------------------------------------------------------------------------------------------------
+def grad_norm(g: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    _require(g, "g")
+    ws = WS.get("gnorm", 1024, g.device)
+    check(_lib.lib().alignn_grad_norm_f32(g.data_ptr(), g.numel(), out.data_ptr(), ws.data_ptr(), stream_ptr()),
+          "alignn_grad_norm_f32")
+    return out
+
+
+def adamw_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, split: int, lr0: float,
+               lr1: float, weight_decay: float, betas=(0.9, 0.999), eps: float = 1e-8,
+               norm: Optional[torch.Tensor] = None, max_norm: float = 5.0, step: torch.Tensor = None) -> None:
+    for t, n in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
+        _require(t, n)
+        if not t.is_contiguous() or t.numel() != p.numel():
+            raise ValueError(f"adamw_step: {n} must be contiguous with {p.numel()} elements")
+    check(_lib.lib().alignn_adamw_f32(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), int(split),
+                                      float(lr0), float(lr1), float(weight_decay), float(betas[0]), float(betas[1]),
+                                      float(eps), _p(norm), float(max_norm), step.data_ptr(), stream_ptr()),
+          "alignn_adamw_f32")

@@ -24,7 +24,8 @@ class FusedTrainer:
                  sigma_lr: Optional[float] = 3e-4, max_norm: float = 5.0, log_sigma_l2: float = 0.1,
                  feature_jitter_std: float = 0.1, min_logvar_floor: float = MIN_LOGVAR_FLOOR,
                  target_log_means: Sequence[float] = TARGET_LOG_MEANS,
-                 target_log_stds: Sequence[float] = TARGET_LOG_STDS, fused_adamw: bool = True):
+                 target_log_stds: Sequence[float] = TARGET_LOG_STDS, fused_adamw: bool = True,
+                 optimizer: str = "torch"):
         self.model = model
         st = model._ensure_flat()
         self.st = st
@@ -38,6 +39,17 @@ class FusedTrainer:
         kw = {"fused": True, "capturable": True} if (fused_adamw and st.flat.is_cuda) else {}
         self.opt = torch.optim.AdamW([{"params": [self.p_base], "lr": lr}, {"params": [self.p_sigma], "lr": sigma_lr}],
                                      lr=lr, weight_decay=weight_decay, **kw)
+        # optimizer="hip": clip + AdamW in libalignn_hip over the flat buffers (alignn_adamw_f32), the
+        # same update as torch's fused AdamW (betas (0.9, 0.999), eps 1e-8, decoupled decay)
+        if optimizer not in ("torch", "hip"):
+            raise ValueError("optimizer must be 'torch' or 'hip'")
+        self.optimizer = optimizer
+        self.lr, self.sigma_lr, self.weight_decay = lr, sigma_lr, weight_decay
+        if optimizer == "hip":
+            self.exp_avg = torch.zeros_like(st.flat)
+            self.exp_avg_sq = torch.zeros_like(st.flat)
+            self.hip_step = torch.zeros(1, device=st.flat.device)
+            self.gnorm = torch.zeros(1, device=st.flat.device)
         self.max_norm = max_norm
         self.l2 = log_sigma_l2
         self.jitter = feature_jitter_std
@@ -54,6 +66,7 @@ class FusedTrainer:
     def set_lr(self, lr: float, sigma_lr: Optional[float] = None) -> None:
         self.opt.param_groups[0]["lr"] = lr
         self.opt.param_groups[1]["lr"] = lr if sigma_lr is None else sigma_lr
+        self.lr, self.sigma_lr = lr, (lr if sigma_lr is None else sigma_lr)
 
     def forward_backward(self, batch, seed: int, training: bool = True) -> torch.Tensor:
         """Forward + loss + backward into the flat gradient buffer; returns the loss (device)."""
@@ -85,6 +98,12 @@ class FusedTrainer:
         return loss
 
     def _clip_and_update(self) -> None:
+        if self.optimizer == "hip":
+            st = self.st
+            ops.grad_norm(st.grad, self.gnorm)
+            ops.adamw_step(st.flat, st.grad, self.exp_avg, self.exp_avg_sq, st.P.sigma_start, self.lr, self.sigma_lr,
+                           self.weight_decay, norm=self.gnorm, max_norm=self.max_norm, step=self.hip_step)
+            return
         torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
         self.opt.step()
 
@@ -135,11 +154,18 @@ class FusedTrainer:
     def _snapshot(self):
         opt_state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
                      for p, st in self.opt.state.items()}
-        return self.st.flat.clone(), opt_state
+        hip = None
+        if self.optimizer == "hip":
+            hip = (self.exp_avg.clone(), self.exp_avg_sq.clone(), self.hip_step.clone())
+        return self.st.flat.clone(), opt_state, hip
 
     def _restore(self, snap) -> None:
-        flat, opt_state = snap
+        flat, opt_state, hip = snap
         self.st.flat.copy_(flat)
+        if hip is not None:
+            self.exp_avg.copy_(hip[0])
+            self.exp_avg_sq.copy_(hip[1])
+            self.hip_step.copy_(hip[2])
         for p, st in self.opt.state.items():
             saved = opt_state.get(id(p))
             for k, v in st.items():

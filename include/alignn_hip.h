@@ -252,6 +252,21 @@ int alignn_ensemble_moments(int32_t M, int64_t B, int32_t T, const float* heads,
  * ensemble_collect_embeddings train.py:907-927). */
 int alignn_member_mean_f32(int32_t M, int64_t n, const float* x, int64_t member_stride, float* out, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Optimizer step over the flat buffers: clip_grad_norm_(5.0) + fused AdamW with
+ * the reference's two param groups (train.py:693-699, :1516-1542).
+ * alignn_grad_norm_f32: *norm = ||g||_2 (fixed-order two-stage sum; workspace >= 1024 floats).
+ * alignn_adamw_f32: *step += 1; c = min(max_norm / (*norm + 1e-6), 1) (norm NULL: c = 1); g *= c
+ * (in place, as clip_grad_norm_); then for i < split lr = lr0 else lr1:
+ *   p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+ *   p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps).
+ * norm and step are device scalars (graph-capturable).
+ * ---------------------------------------------------------------------------------------- */
+int alignn_grad_norm_f32(const float* g, int64_t n, float* norm, float* workspace, void* stream);
+int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, float lr0, float lr1,
+                     float weight_decay, float beta1, float beta2, float eps, const float* norm, float max_norm,
+                     float* step, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
