@@ -85,6 +85,9 @@ _SIGNATURES = {
                                  c_vp, c_vp, c_vp], c_i32),
     "alignn_member_mean_f32": ([c_i32, c_i64, c_vp, c_i64, c_vp, c_vp], c_i32),
     "alignn_grad_norm_f32": ([c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
+    "alignn_collate_rows_f32": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
+    "alignn_collate_index_i64": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp], c_i32),
+    "alignn_collate_batchvec": ([c_i32, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_f32,
                           c_vp, c_vp], c_i32),
 }

@@ -1,0 +1,90 @@
+// collate.hip — batch assembly from a dataset resident in HBM.
+//
+// Replaces PyG's Collater / Batch.from_data_list over the reference's per-sample
+// `.pt` loads (train.py:132): the whole dataset lives in HBM as flat per-field arrays with per-graph
+// row ranges, and a batch is a set of segmented copies.  Index fields (edge_index, lg_edge_index:
+// two rows each) get the per-graph increment added — the caller passes PyG's increments, including
+// the lg_edge_index-by-num_nodes rule, so the batch is bit-identical to PyG's.
+#include "common.h"
+
+namespace alignn {
+
+// grid (chunks, G): graph g's segment [src_start[g], +count[g]) * width -> [dst_start[g], ...)
+__global__ void collate_rows_kernel(const float* __restrict__ src, int64_t width, const int64_t* __restrict__ src_start,
+                                    const int64_t* __restrict__ dst_start, const int64_t* __restrict__ count,
+                                    float* __restrict__ dst) {
+  const int g = blockIdx.y;
+  const int64_t n = count[g] * width;
+  const float* s = src + src_start[g] * width;
+  float* d = dst + dst_start[g] * width;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = s[i];
+}
+
+// Two-row int64 index field: row r of graph g's segment, plus add[g].
+__global__ void collate_index_kernel(const int64_t* __restrict__ src, int64_t src_ld,
+                                     const int64_t* __restrict__ src_start, const int64_t* __restrict__ dst_start,
+                                     const int64_t* __restrict__ count, const int64_t* __restrict__ add,
+                                     int64_t* __restrict__ dst, int64_t dst_ld) {
+  const int g = blockIdx.y;
+  const int64_t n = count[g];
+  const int64_t a = add[g];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    dst[dst_start[g] + i] = src[src_start[g] + i] + a;
+    dst[dst_ld + dst_start[g] + i] = src[src_ld + src_start[g] + i] + a;
+  }
+}
+
+// batch vector: nodes of graph g get g
+__global__ void collate_batchvec_kernel(const int64_t* __restrict__ dst_start, const int64_t* __restrict__ count,
+                                        int64_t* __restrict__ batch) {
+  const int g = blockIdx.y;
+  const int64_t n = count[g];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    batch[dst_start[g] + i] = g;
+}
+
+static dim3 seg_grid(int64_t max_count_elems, int G) {
+  int64_t chunks = (max_count_elems + 1023) / 1024;
+  if (chunks < 1) chunks = 1;
+  if (chunks > 64) chunks = 64;
+  return dim3((unsigned)chunks, (unsigned)G);
+}
+
+}  // namespace alignn
+
+using namespace alignn;
+
+extern "C" int alignn_collate_rows_f32(int32_t G, const float* src, int64_t width, const int64_t* src_start,
+                                       const int64_t* dst_start, const int64_t* count, int64_t max_count,
+                                       float* dst, void* stream) {
+  if (G < 0 || width < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
+  if (G == 0 || width == 0 || max_count == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(collate_rows_kernel, seg_grid(max_count * width, G), dim3(256), 0, s, src, width, src_start,
+                     dst_start, count, dst);
+  ALIGNN_LAUNCH_CHECK("collate_rows_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_collate_index_i64(int32_t G, const int64_t* src, int64_t src_ld, const int64_t* src_start,
+                                        const int64_t* dst_start, const int64_t* count, const int64_t* add,
+                                        int64_t max_count, int64_t* dst, int64_t dst_ld, void* stream) {
+  if (G < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
+  if (G == 0 || max_count == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(collate_index_kernel, seg_grid(max_count, G), dim3(256), 0, s, src, src_ld, src_start, dst_start,
+                     count, add, dst, dst_ld);
+  ALIGNN_LAUNCH_CHECK("collate_index_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, const int64_t* count, int64_t max_count,
+                                       int64_t* batch, void* stream) {
+  if (G < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
+  if (G == 0 || max_count == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(collate_batchvec_kernel, seg_grid(max_count, G), dim3(256), 0, s, dst_start, count, batch);
+  ALIGNN_LAUNCH_CHECK("collate_batchvec_kernel");
+  return ALIGNN_OK;
+}

@@ -267,6 +267,25 @@ int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t 
                      float weight_decay, float beta1, float beta2, float eps, const float* norm, float max_norm,
                      float* step, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Batch assembly from a dataset resident in HBM (replaces PyG Collater /
+ * Batch.from_data_list, SURVEY §8a A9, over per-sample .pt loads, train.py:132).  All offset
+ * arrays are device int64 [G]; graph g's segment src[src_start[g] .. +count[g]) goes to
+ * dst[dst_start[g] ..); max_count = max_g count[g] (sizes the grid).
+ *   rows:  float rows of `width` values (x, edge_attr, lg_edge_attr, global_x, sg_one_hot, y)
+ *   index: two int64 rows (src row stride src_ld, dst row stride dst_ld), + add[g] (PyG's
+ *          increment: cumulative num_nodes for edge_index AND lg_edge_index)
+ *   batchvec: batch[dst_start[g] + i] = g for i < count[g] (nodes).
+ * ---------------------------------------------------------------------------------------- */
+int alignn_collate_rows_f32(int32_t G, const float* src, int64_t width, const int64_t* src_start,
+                            const int64_t* dst_start, const int64_t* count, int64_t max_count, float* dst,
+                            void* stream);
+int alignn_collate_index_i64(int32_t G, const int64_t* src, int64_t src_ld, const int64_t* src_start,
+                             const int64_t* dst_start, const int64_t* count, const int64_t* add, int64_t max_count,
+                             int64_t* dst, int64_t dst_ld, void* stream);
+int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, const int64_t* count, int64_t max_count,
+                            int64_t* batch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
