@@ -78,7 +78,7 @@ _SIGNATURES = {
     "alignn_readout_pool_bwd": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp],
                                 c_i32),
     "alignn_dropout_f32": ([c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_u64, c_vp], c_i32),
-    "alignn_hetero_nll": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp],
+    "alignn_hetero_nll": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp],
                           c_i32),
     "alignn_add_noise_f32": ([c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_ensemble_moments": ([c_i32, c_i64, c_i32, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

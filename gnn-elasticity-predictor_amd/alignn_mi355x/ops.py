@@ -432,12 +432,16 @@ def dropout(x, y, relu_ref=None, drop_p=0.0, seed=0):
     return y
 
 
-def hetero_nll(heads, y, log_means, log_stds, floor, l2, loss, dheads):
+def hetero_nll(heads, y, log_means, log_stds, floor, l2, loss, dheads, weights: Optional[torch.Tensor] = None):
+    """weights: per-graph KNN sample weights [B] (train.py:660-674) or None."""
     B = heads.size(0)
     T = heads.size(1) // 2
-    check(_lib.lib().alignn_hetero_nll(B, T, heads.data_ptr(), heads.stride(0), y.data_ptr(), log_means.data_ptr(),
-                                       log_stds.data_ptr(), float(floor), float(l2), loss.data_ptr(),
-                                       dheads.data_ptr(), dheads.stride(0), stream_ptr()), "alignn_hetero_nll")
+    if weights is not None and (weights.numel() != B or weights.dtype != torch.float32 or not weights.is_contiguous()):
+        raise ValueError("hetero_nll: weights must be a contiguous float32 [B] tensor")
+    check(_lib.lib().alignn_hetero_nll(B, T, heads.data_ptr(), heads.stride(0), y.data_ptr(), _p(weights),
+                                       log_means.data_ptr(), log_stds.data_ptr(), float(floor), float(l2),
+                                       loss.data_ptr(), dheads.data_ptr(), dheads.stride(0), stream_ptr()),
+          "alignn_hetero_nll")
 
 
 def add_noise(x: torch.Tensor, std: float, seed: int):

@@ -68,8 +68,10 @@ class FusedTrainer:
         self.opt.param_groups[1]["lr"] = lr if sigma_lr is None else sigma_lr
         self.lr, self.sigma_lr = lr, (lr if sigma_lr is None else sigma_lr)
 
-    def forward_backward(self, batch, seed: int, training: bool = True) -> torch.Tensor:
-        """Forward + loss + backward into the flat gradient buffer; returns the loss (device)."""
+    def forward_backward(self, batch, seed: int, training: bool = True,
+                         sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Forward + loss + backward into the flat gradient buffer; returns the loss (device).
+        sample_weights: per-graph KNN weights [B] (train.py:660-674), or None."""
         model, st = self.model, self.st
         bc = batch_cache(batch)
         x, gx = batch.x, batch.global_x
@@ -81,16 +83,16 @@ class FusedTrainer:
         out, ctx = model._engine.forward(st.P, batch, bc, training, seed, x, gx, "hetero")
         dout = torch.empty_like(out)
         ops.hetero_nll(out, batch.y.contiguous().float(), self.log_means, self.log_stds, self.floor, self.l2,
-                       self.loss, dout)
+                       self.loss, dout, weights=sample_weights)
         model._engine.backward(st.P, st.G, ctx, dout)
         return self.loss
 
-    def step(self, batch, seed: Optional[int] = None) -> torch.Tensor:
+    def step(self, batch, seed: Optional[int] = None, sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         if seed is None:
             seed = int(torch.randint(0, 2**62, (1,)).item())
-        if self._graph is not None and self._graph[2] is batch:
+        if self._graph is not None and self._graph[2] is batch and sample_weights is None:
             return self._replay(seed)
-        loss = self.forward_backward(batch, seed)
+        loss = self.forward_backward(batch, seed, sample_weights=sample_weights)
         if self.grad_hook is not None:
             self.grad_hook(self.st.grad)
         self._clip_and_update()

@@ -276,7 +276,8 @@ __global__ void dropout_kernel(int64_t rows, int64_t cols, const float* __restri
 
 // Hetero NLL forward+gradient, single block (B*T is small).
 __global__ __launch_bounds__(256) void hetero_nll_kernel(int64_t B, int T, const float* __restrict__ heads, int64_t ldh,
-                                                         const float* __restrict__ y, const float* __restrict__ lm,
+                                                         const float* __restrict__ y, const float* __restrict__ w,
+                                                         const float* __restrict__ lm,
                                                          const float* __restrict__ ls, float floor, float l2,
                                                          float* __restrict__ loss, float* __restrict__ dh, int64_t lddh) {
   __shared__ float red[256];
@@ -292,9 +293,10 @@ __global__ __launch_bounds__(256) void hetero_nll_kernel(int64_t B, int T, const
     const float yz = (logf(y[b * T + t]) - lm[t]) / ls[t];
     const float var = expf(lv);
     const float diff = mu - yz;
-    acc += 0.5f * (lv + diff * diff / var) + l2 * (0.5f * lv) * (0.5f * lv);
-    dh[b * lddh + t] = inv * diff / var;
-    const float dlv = inv * (0.5f * (1.0f - diff * diff / var) + l2 * 0.5f * lv);
+    const float wb = w ? w[b] : 1.0f;  // KNN sample weight (train.py:660-674): scales the NLL term only
+    acc += wb * (0.5f * (lv + diff * diff / var)) + l2 * (0.5f * lv) * (0.5f * lv);
+    dh[b * lddh + t] = inv * wb * diff / var;
+    const float dlv = inv * (wb * 0.5f * (1.0f - diff * diff / var) + l2 * 0.5f * lv);
     dh[b * lddh + T + t] = lvr >= floor ? dlv : 0.f;
   }
   red[threadIdx.x] = acc;
@@ -422,12 +424,12 @@ extern "C" int alignn_dropout_f32(int64_t rows, int64_t cols, const float* x, in
 }
 
 extern "C" int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
-                                 const float* log_means, const float* log_stds, float floor, float l2, float* loss,
-                                 float* dheads, int64_t lddh, void* stream) {
+                                 const float* weights, const float* log_means, const float* log_stds, float floor,
+                                 float l2, float* loss, float* dheads, int64_t lddh, void* stream) {
   if (B <= 0 || T <= 0) return ALIGNN_E_BAD_SHAPE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(hetero_nll_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, log_means, log_stds, floor, l2,
-                     loss, dheads, lddh);
+  hipLaunchKernelGGL(hetero_nll_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, weights, log_means, log_stds,
+                     floor, l2, loss, dheads, lddh);
   ALIGNN_LAUNCH_CHECK("hetero_nll_kernel");
   return ALIGNN_OK;
 }

@@ -223,11 +223,12 @@ int alignn_readout_pool_bwd(int64_t B, int64_t N, int32_t D, const float* dfeats
 int alignn_dropout_f32(int64_t rows, int64_t cols, const float* x, int64_t ldx, float* y, int64_t ldy,
                        const float* relu_ref, int64_t ldr, float drop_p, uint64_t seed, void* stream);
 
-/* Hetero Gaussian NLL (train.py:656-681, no KNN weights), forward + gradient in one launch:
- * loss = mean_b mean_t 0.5(lv + (mu-y)^2/e^lv) + l2 * mean((lv/2)^2), lv = clamp(logvar, floor).
- * heads [B, ldh] hold mean at col 0..T-1 and logvar at T..2T-1; y_z = (log y - m)/s. */
+/* Hetero Gaussian NLL (train.py:656-681), forward + gradient in one launch:
+ * loss = mean_b mean_t w_b 0.5(lv + (mu-y)^2/e^lv) + l2 * mean((lv/2)^2), lv = clamp(logvar, floor).
+ * heads [B, ldh] hold mean at col 0..T-1 and logvar at T..2T-1; y_z = (log y - m)/s.
+ * weights [B]: KNN sample weights (train.py:660-674), NULL = 1. */
 int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
-                      const float* log_means, const float* log_stds, float floor, float l2,
+                      const float* weights, const float* log_means, const float* log_stds, float floor, float l2,
                       float* loss, float* dheads, int64_t lddh, void* stream);
 
 /* Feature jitter (train.py:641-646): x += std * N(0,1) from a counter-based generator. */

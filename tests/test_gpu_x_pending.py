@@ -114,3 +114,27 @@ def test_fused_trainer_hip_optimizer_vs_reference_golden(golden):
         if k.endswith("lin_key.bias"):
             continue
         assert rel_err(v.cpu(), g[f"f32/post/{k}"]) < 1e-4, k
+
+
+def test_hetero_nll_with_knn_sample_weights():
+    """Weighted NLL (train.py:660-674: nll * w per graph, L2 term unweighted) vs torch fp64 autograd."""
+    ops = _ops()
+    torch.manual_seed(8)
+    B, T = 16, 2
+    heads = torch.randn(B, 2 * T, device=DEV)
+    y = torch.rand(B * T, device=DEV) * 299 + 1
+    w = torch.rand(B, device=DEV) * 2
+    lm = torch.tensor([4.3228, 3.5567], device=DEV)
+    ls = torch.tensor([0.9051, 0.9405], device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    dh = torch.empty_like(heads)
+    ops.hetero_nll(heads, y, lm, ls, -2.9, 0.1, loss, dh, weights=w)
+    h = heads.double().clone().requires_grad_(True)
+    mean, logvar = h[:, :T], h[:, T:]
+    tz = (torch.log(y.double().view(B, T)) - lm.double()) / ls.double()
+    lv = torch.clamp(logvar, min=-2.9)
+    nll = 0.5 * (lv + (mean - tz) ** 2 / torch.exp(lv)) * w.double().view(-1, 1)
+    ref = nll.mean(1).mean() + 0.1 * (0.5 * lv).pow(2).mean()
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-5 * abs(float(ref))
+    assert _rel(dh, h.grad) < 1e-5
