@@ -287,6 +287,25 @@ int alignn_collate_index_i64(int32_t G, const int64_t* src, int64_t src_ld, cons
 int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, const int64_t* count, int64_t max_count,
                             int64_t* batch, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * KNN density weights over graph embeddings (compute_global_knn_weights,
+ * train.py:930-1010).  Column standardisation (population std, floor 1e-8) from column sums:
+ *   alignn_col_center_sq_f32: out = (Z - colsum/n)^2 (feed to alignn_colsum_f32 for ssq)
+ *   alignn_standardize_f32:   out = (Z - colsum/n) / max(sqrt(ssq/n), 1e-8)
+ *   alignn_row_sqnorm_f32:    r_i = |Zs_i|^2
+ * alignn_knn_select_weights: for query rows row0..row0+rows-1 with G = Zs[rows] Zs^T ([rows, ldg]):
+ *   the k nearest j != i by d2 = r_i + r_j - 2 G (ties by index), nbr [rows, k] (may be NULL),
+ *   w_raw[i] = (k / (sum sqrt(d2) + eps))^-alpha / (1 + beta * mean_t var_k(Y[nbr, t])).
+ *   Y [n, T] (raw targets, as the reference); 1 <= k <= min(64, n-1).
+ * ---------------------------------------------------------------------------------------- */
+int alignn_col_center_sq_f32(const float* Z, int64_t n, int32_t D, const float* colsum, float* out, void* stream);
+int alignn_standardize_f32(const float* Z, int64_t n, int32_t D, const float* colsum, const float* ssq, float* out,
+                           void* stream);
+int alignn_row_sqnorm_f32(const float* Zs, int64_t n, int32_t D, float* r, void* stream);
+int alignn_knn_select_weights(const float* G, int64_t ldg, const float* r, int64_t n, int64_t row0, int64_t rows,
+                              int32_t k, const float* Y, int32_t T, float eps, float alpha, float beta, int64_t* nbr,
+                              float* w_raw, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
