@@ -42,7 +42,11 @@ class GemmArgs(ctypes.Structure):
 
 
 class Schedule(ctypes.Structure):
-    _fields_ = [("light", c_vp), ("n_light", c_i64), ("heavy", c_vp), ("n_heavy", c_i64)]
+    _fields_ = [("light", c_vp), ("n_light", c_i64), ("heavy", c_vp), ("n_heavy", c_i64),
+                ("flags", c_i32), ("reserved", c_i32)]
+
+
+SCHED_COMPACT_REGS = 1
 
 
 class EdgeEncoder(ctypes.Structure):

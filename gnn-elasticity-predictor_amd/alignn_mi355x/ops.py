@@ -181,6 +181,7 @@ class GraphCSR:
                  "n_full")
 
     HEAVY_THRESHOLD = 32  # in-degree above which a target node gets a 4-wave workgroup
+    COMPACT_REGS = False  # attention kernel variant with row-distributed softmax state (opt-in)
 
     def __init__(self, edge_index: torch.Tensor, n: int):
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
@@ -222,6 +223,7 @@ class GraphCSR:
             sc = _lib.Schedule()
             sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
             sc.heavy, sc.n_heavy = (heavy.data_ptr() if heavy.numel() else None), heavy.numel()
+            sc.flags = _lib.SCHED_COMPACT_REGS if self.COMPACT_REGS else 0
             self._sched = (sc, light, heavy)
         return self._sched[0]
 

@@ -710,6 +710,513 @@ __global__ __launch_bounds__(1024) void enc_grad_reduce(const float* __restrict_
 }
 
 // =============================================================================================
+// Version 2 kernels (schedule flag ALIGNN_SCHED_COMPACT_REGS; materialised edge features only).
+//
+// Same arithmetic as above with a smaller register footprint, for more waves per SIMD on the
+// latency-bound edge stream:
+//  * per-(edge, head) softmax quantities stay ROW-DISTRIBUTED — after the transpose-reduction
+//    (reduce_rows) row j of value register h holds (edge j, head h) — so a group needs H registers
+//    per quantity instead of PF*H broadcast copies; group max/sums over the PF rows are two xor-16/32
+//    shuffles; single (edge, head) values are read back as scalars (v_readlane) where they scale a
+//    feature vector;
+//  * the node's per-head vectors (u, and Vd in the backward) are staged in LDS, one copy per wave,
+//    and read one head at a time.
+// The LDS of the node vectors and of the heavy-node merge alias (a barrier separates them).
+// =============================================================================================
+
+// Transpose-reduction without the broadcast: value r*(P/4)+i ends in row r of b[i] (P = N rounded up
+// to a multiple of 4), replicated over the row's 16 lanes.
+template <int N>
+__device__ __forceinline__ void reduce_rows(const float (&v)[N], float (&b)[(N + 3) / 4]) {
+  constexpr int P = (N + 3) / 4 * 4;
+  float a[P / 2];
+#pragma unroll
+  for (int i = 0; i < P / 2; ++i) {
+    const float x = i < N ? v[i] : 0.f;
+    const float y = (i + P / 2) < N ? v[i + P / 2] : 0.f;
+    const auto r = __builtin_amdgcn_permlane32_swap(u_bits(x), u_bits(y), false, false);
+    a[i] = f_bits(r[0]) + f_bits(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < P / 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u_bits(a[i]), u_bits(a[i + P / 4]), false, false);
+    b[i] = row_sum16(f_bits(r[0]) + f_bits(r[1]));
+  }
+}
+
+// Over the four rows of a row-replicated value (VALU lane swaps, no LDS crossbar):
+// permlane32_swap(x, x) pairs lane l with l^32, permlane16_swap(x, x) row 2k with 2k+1.
+__device__ __forceinline__ float rows_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(u_bits(x), u_bits(x), false, false);
+  x = f_bits(r[0]) + f_bits(r[1]);
+  r = __builtin_amdgcn_permlane16_swap(u_bits(x), u_bits(x), false, false);
+  return f_bits(r[0]) + f_bits(r[1]);
+}
+__device__ __forceinline__ float rows_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(u_bits(x), u_bits(x), false, false);
+  x = fmaxf(f_bits(r[0]), f_bits(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(u_bits(x), u_bits(x), false, false);
+  return fmaxf(f_bits(r[0]), f_bits(r[1]));
+}
+
+template <int VPL, int H>
+constexpr int fwd2_lds_floats() { return cmax(fwd_merge_floats<VPL, H>(), 4 * H * 64 * VPL); }
+
+template <int VPL, int H>
+__device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64_t d, int wsub, int nw, bool heavy) {
+  static_assert(PF == 4, "row-distributed layout assumes one edge per row");
+  constexpr int NS = 3 * H + H * VPL + VPL;
+  constexpr int RS = 64 * VPL;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row = lane >> 4;
+  const int D = p.D, C = D / H;
+  const int j0 = lane * VPL;
+  const bool act = j0 < D;
+  const int hl = act ? j0 / C : 0;
+  const float scale = 1.0f / sqrtf((float)C);
+  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
+  float* uv = smem + wave * H * RS;  // this wave's copy of u[h]
+
+  float accS[H][VPL], accV[VPL];
+  float m[H], s[H], sa[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    m[h] = -INFINITY;
+    s[h] = 0.f;
+    sa[h] = 0.f;
+    vzero(accS[h]);
+  }
+  vzero(accV);
+
+  const int32_t first = beg + wsub * PF, stride = nw * PF;
+  if (first < end) {
+    float q[VPL];
+    vzero(q);
+    if (act) {
+      vload(p.QKVR + d * p.ldq + j0, q);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float t[VPL];
+        vload(p.U + (d * H + h) * D + j0, t);
+        vstore(uv + h * RS + j0, t);
+      }
+    }
+    float c[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) c[h] = 0.f;
+    if (p.wbar) {
+      float wb[VPL];
+      vzero(wb);
+      if (act) vload(p.wbar + j0, wb);
+      const float part = vdot(wb, q);
+#pragma unroll
+      for (int h = 0; h < H; ++h) c[h] = (h == hl) ? part : 0.f;
+      reduce_bcast<H>(c, lane);
+    }
+    EdgeSlot<VPL> ring[PF];
+    const EncParams no_enc{nullptr, 0, 0, nullptr, nullptr};
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
+      ring[j].xr = 0.f;
+      const int32_t t = first + j;
+      if (t < end)
+        load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[t]),
+                          p.feat_row ? (int64_t)uni(p.feat_row[t]) : t, j0, act, lane);
+    }
+    for (int32_t tb = first; tb < end; tb += stride) {
+      asm volatile("" ::: "memory");  // keep the u reads in the loop (registers are the point)
+      float pr[PF * H];
+      {
+        float qk[PF];
+#pragma unroll
+        for (int j = 0; j < PF; ++j) qk[j] = vdot(q, ring[j].k);
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          float u[VPL];
+          vload(uv + h * RS + j0, u);
+#pragma unroll
+          for (int j = 0; j < PF; ++j) pr[j * H + h] = vdot(u, ring[j].f) + ((h == hl) ? qk[j] : 0.f);
+        }
+      }
+      float b[H];
+      reduce_rows<PF * H>(pr, b);  // row j: b[h] = score partial of (edge tb + j, head h)
+      const bool rv = tb + row < end;
+      float mine = 1.0f;
+      if (p.drop.active && lane < PF * H)
+        mine = dropout_mul(p.drop.seed, (uint64_t)(tb + lane / H) * H + (lane % H), p.drop.thresh, p.drop.inv_keep);
+      float corr[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float z = rv ? (b[h] + c[h]) * scale : -INFINITY;
+        const float mn = fmaxf(m[h], rows_max(z));
+        corr[h] = __expf(m[h] - mn);
+        m[h] = mn;
+        const float ex = __expf(z - mn);  // 0 on rows past the segment end
+        const float mul = p.drop.active ? __shfl(mine, row * H + h, 64) : 1.0f;
+        const float ed = ex * mul;
+        s[h] = s[h] * corr[h] + rows_sum(ex);
+        sa[h] = sa[h] * corr[h] + rows_sum(ed);
+        b[h] = ed;  // row-distributed alpha' numerators
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) accS[h][i] *= corr[h];
+      }
+      {
+        const float cl = pick_r<H>(corr, hl);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) accV[i] *= cl;
+      }
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        float e[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          e[h] = readlane_f(b[h], 16 * j);
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(e[h], ring[j].f[i], accS[h][i]);
+        }
+        const float el = pick_r<H>(e, hl);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
+        const int32_t tn = tb + stride + j;
+        if (tn < end)
+          load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[tn]),
+                            p.feat_row ? (int64_t)uni(p.feat_row[tn]) : tn, j0, act, lane);
+      }
+    }
+  }
+
+  if (heavy) {
+    __syncthreads();  // every wave is done with its u copy (the merge buffer aliases it)
+    float* my = smem + (wave * 64 + lane) * NS;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      my[h] = m[h];
+      my[H + h] = s[h];
+      my[2 * H + h] = sa[h];
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) my[3 * H + h * VPL + i] = accS[h][i];
+    }
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) my[3 * H + H * VPL + i] = accV[i];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float mt = -INFINITY;
+        for (int v = 0; v < 4; ++v) mt = fmaxf(mt, smem[(v * 64 + lane) * NS + h]);
+        s[h] = 0.f;
+        sa[h] = 0.f;
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) accS[h][i] = 0.f;
+        for (int v = 0; v < 4; ++v) {
+          const float* o = smem + (v * 64 + lane) * NS;
+          const float f = (o[h] == -INFINITY) ? 0.f : __expf(o[h] - mt);
+          s[h] = fmaf(o[H + h], f, s[h]);
+          sa[h] = fmaf(o[2 * H + h], f, sa[h]);
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(o[3 * H + h * VPL + i], f, accS[h][i]);
+        }
+        m[h] = mt;
+      }
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) accV[i] = 0.f;
+      for (int v = 0; v < 4; ++v) {
+        const float* o = smem + (v * 64 + lane) * NS;
+        const float mh = o[hl];
+        const float f = (mh == -INFINITY) ? 0.f : __expf(mh - pick_r<H>(m, hl));
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) accV[i] = fmaf(o[3 * H + H * VPL + i], f, accV[i]);
+      }
+    }
+  }
+
+  if (!heavy || wave == 0) {
+    float inv[H], dn[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      dn[h] = s[h] + 1e-16f;
+      inv[h] = 1.0f / dn[h];
+    }
+    if (act) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float o[VPL];
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) o[i] = accS[h][i] * inv[h];
+        vstore(p.S + (d * H + h) * D + j0, o);
+      }
+      const float il = pick_r<H>(inv, hl);
+      float o[VPL];
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) o[i] = accV[i] * il;
+      vstore(p.aggV + d * D + j0, o);
+    }
+    if (lane < H) {
+      p.sumA[d * H + lane] = pick_r<H>(sa, lane) * pick_r<H>(inv, lane);
+      p.mstat[d * H + lane] = pick_r<H>(m, lane);
+      p.den[d * H + lane] = pick_r<H>(dn, lane);
+    }
+  }
+  if (heavy) __syncthreads();  // merge buffer / u copies free for the next item
+}
+
+template <int VPL, int H>
+__global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
+  resolve_drop(p.drop);
+  __shared__ float smem[fwd2_lds_floats<VPL, H>()];
+  const int wave = threadIdx.x >> 6;
+  const int64_t items = sc.items();
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    if (it < sc.n_heavy) {
+      fwd2_node<VPL, H>(p, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true);
+    } else {
+      const int64_t i = (it - sc.n_heavy) * 4 + wave;
+      if (i < sc.n_light) fwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false);
+    }
+  }
+}
+
+template <int VPL, int H>
+constexpr int bwd2_lds_floats() { return cmax(bwd_merge_floats<VPL, H, 0>(), 4 * 2 * H * 64 * VPL); }
+
+template <int VPL, int H>
+__device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, int64_t d, int wsub, int nw, bool heavy) {
+  static_assert(PF == 4, "row-distributed layout assumes one edge per row");
+  constexpr int NS = H + H * VPL + VPL;
+  constexpr int RS = 64 * VPL;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row = lane >> 4;
+  const int D = p.D, C = D / H;
+  const int j0 = lane * VPL;
+  const bool act = j0 < D;
+  const int hl = act ? j0 / C : 0;
+  const float scale = 1.0f / sqrtf((float)C);
+  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
+  float* uv = smem + wave * 2 * H * RS;  // this wave's u[h] (h < H) and Vd[h] (H + h)
+  const bool do_dF = p.dF != nullptr;
+
+  float sz[H][VPL], sgz[H], dqa[VPL];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    vzero(sz[h]);
+    sgz[h] = 0.f;
+  }
+  vzero(dqa);
+
+  const int32_t first = beg + wsub * PF, stride = nw * PF;
+  if (first < end) {
+    float q[VPL], go[VPL];
+    vzero(q);
+    vzero(go);
+    float c[3 * H];
+    {
+      float op[VPL], wb[VPL];
+      vzero(op);
+      vzero(wb);
+      if (act) {
+        vload(p.QKVR + d * p.ldq + j0, q);
+        vload(p.dout + d * D + j0, go);
+        vload(p.outp + d * D + j0, op);
+        if (p.wbar) vload(p.wbar + j0, wb);
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          float t[VPL];
+          vload(p.U + (d * H + h) * D + j0, t);
+          vstore(uv + h * RS + j0, t);
+          vload(p.Vd + (d * H + h) * D + j0, t);
+          vstore(uv + (H + h) * RS + j0, t);
+        }
+      }
+      const float pc = vdot(wb, q), pc2 = vdot(wb, go), pdl = vdot(go, op);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        c[h] = (h == hl) ? pc : 0.f;
+        c[H + h] = (h == hl) ? pc2 : 0.f;
+        c[2 * H + h] = (h == hl) ? pdl : 0.f;
+      }
+      reduce_bcast<3 * H>(c, lane);
+    }
+    float mst[H], inv_den[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      mst[h] = p.mstat[d * H + h];
+      inv_den[h] = 1.0f / p.den[d * H + h];
+    }
+    EdgeSlot<VPL> ring[PF];
+    float old[PF][VPL];
+    int64_t rows_[PF];
+    const EncParams no_enc{nullptr, 0, 0, nullptr, nullptr};
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
+      ring[j].xr = 0.f;
+      vzero(old[j]);
+      const int32_t t = first + j;
+      rows_[j] = 0;
+      if (t < end) {
+        rows_[j] = p.feat_row ? uni(p.feat_row[t]) : t;
+        load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[t]), rows_[j], j0, act,
+                          lane);
+        if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
+      }
+    }
+    for (int32_t tb = first; tb < end; tb += stride) {
+      asm volatile("" ::: "memory");  // keep the u / Vd reads in the loop
+      float bs[H], bd[H];
+      {
+        float ps[PF * H], pd[PF * H];
+        float qk[PF], gv[PF];
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+          qk[j] = vdot(q, ring[j].k);
+          gv[j] = vdot(go, ring[j].v);
+        }
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          float u[VPL], vd[VPL];
+          vload(uv + h * RS + j0, u);
+          vload(uv + (H + h) * RS + j0, vd);
+#pragma unroll
+          for (int j = 0; j < PF; ++j) {
+            ps[j * H + h] = vdot(u, ring[j].f) + ((h == hl) ? qk[j] : 0.f);
+            pd[j * H + h] = vdot(vd, ring[j].f) + ((h == hl) ? gv[j] : 0.f);
+          }
+        }
+        reduce_rows<PF * H>(ps, bs);
+        reduce_rows<PF * H>(pd, bd);
+      }
+      const bool rv = tb + row < end;
+      float mine = 1.0f;
+      if (p.drop.active && lane < PF * H)
+        mine = dropout_mul(p.drop.seed, (uint64_t)(tb + lane / H) * H + (lane % H), p.drop.thresh, p.drop.inv_keep);
+      // row-distributed dz (= dL/dz / sqrt(C)) in bs, alpha' in bd
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float mul = p.drop.active ? __shfl(mine, row * H + h, 64) : 1.0f;
+        const float z = (bs[h] + c[h]) * scale;
+        const float alpha = __expf(z - mst[h]) * inv_den[h];
+        const float al = alpha * mul;
+        const float dal = (bd[h] + c[H + h]) * mul;
+        const float dz = alpha * (dal - c[2 * H + h]) * scale;
+        bs[h] = rv ? dz : 0.f;
+        bd[h] = rv ? al : 0.f;
+        sgz[h] += rows_sum(bs[h]);
+      }
+      {
+        const int col = lane & 15;
+        if (col < H && rv) {
+          const int64_t t = (int64_t)(tb + row);
+          p.dz_e[t * H + col] = pick_r<H>(bs, col);
+          p.alpha_e[t * H + col] = pick_r<H>(bd, col);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        float e[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          e[h] = readlane_f(bs[h], 16 * j);
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(e[h], ring[j].f[i], sz[h][i]);
+        }
+        const float dzl = pick_r<H>(e, hl);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, ring[j].k[i], dqa[i]);
+      }
+      if (do_dF) {
+        // dF[row(t)] (+)= sum_h dz u_h + alpha' Vd_h, one head at a time from LDS
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          float u[VPL], vd[VPL];
+          vload(uv + h * RS + j0, u);
+          vload(uv + (H + h) * RS + j0, vd);
+#pragma unroll
+          for (int j = 0; j < PF; ++j) {
+            const float ez = readlane_f(bs[h], 16 * j), ea = readlane_f(bd[h], 16 * j);
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) old[j][i] = fmaf(ez, u[i], fmaf(ea, vd[i], old[j][i]));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+          if (tb + j < end && act) {
+            float df[VPL];
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) df[i] = (p.acc_dF & 2) ? (ring[j].f[i] > 0.f ? old[j][i] : 0.f) : old[j][i];
+            vstore(p.dF + rows_[j] * p.lddf + j0, df);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int32_t tn = tb + stride + j;
+        vzero(old[j]);
+        if (tn < end) {
+          rows_[j] = p.feat_row ? uni(p.feat_row[tn]) : tn;
+          load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[tn]), rows_[j], j0,
+                            act, lane);
+          if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
+        }
+      }
+    }
+  }
+  if (heavy) {
+    __syncthreads();  // u / Vd copies are dead before the merge buffer (aliased) is written
+    float* my = smem + (wave * 64 + lane) * NS;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      my[h] = sgz[h];
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) my[H + h * VPL + i] = sz[h][i];
+    }
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) my[H + H * VPL + i] = dqa[i];
+    __syncthreads();
+    if (wave == 0) {
+      for (int v = 1; v < 4; ++v) {
+        const float* o = smem + (v * 64 + lane) * NS;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          sgz[h] += o[h];
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) sz[h][i] += o[H + h * VPL + i];
+        }
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) dqa[i] += o[H + H * VPL + i];
+      }
+    }
+  }
+  if (!heavy || wave == 0) {
+    if (act) {
+      vstore(p.dq + d * p.lddq + j0, dqa);
+#pragma unroll
+      for (int h = 0; h < H; ++h) vstore(p.Sz + (d * H + h) * D + j0, sz[h]);
+    }
+    if (lane < H) p.sigz[d * H + lane] = pick_r<H>(sgz, lane);
+  }
+  if (heavy) __syncthreads();
+}
+
+template <int VPL, int H>
+__global__ TCONV_ATTR void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
+  resolve_drop(p.drop);
+  __shared__ float smem[bwd2_lds_floats<VPL, H>()];
+  const int wave = threadIdx.x >> 6;
+  const int64_t items = sc.items();
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    if (it < sc.n_heavy) {
+      bwd2_node<VPL, H>(p, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true);
+    } else {
+      const int64_t i = (it - sc.n_heavy) * 4 + wave;
+      if (i < sc.n_light) bwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false);
+    }
+  }
+}
+
+// =============================================================================================
 // Backward, source side: dK, dV per source node over the by-source CSR (no atomics)
 // =============================================================================================
 struct BwdSrcParams {
@@ -835,10 +1342,15 @@ static int64_t bwd_grid_cap() {
 }
 
 template <int VPL, int H>
-static void launch_fwd(const FwdParams& p, const Sched& sc, const EncParams& en, int km, hipStream_t s) {
+static void launch_fwd(const FwdParams& p, const Sched& sc, const EncParams& en, int km, hipStream_t s,
+                       int flags = 0) {
   const int64_t items = sc.items();
   if (items == 0) return;
   const dim3 grid((unsigned)items), block(256);
+  if (km == 0 && (flags & ALIGNN_SCHED_COMPACT_REGS)) {
+    hipLaunchKernelGGL((tconv_fwd2_kernel<VPL, H>), grid, block, 0, s, p, sc);
+    return;
+  }
   switch (km) {
     case 0: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 0>), grid, block, 0, s, p, sc, en); break;
     case 8: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 8>), grid, block, 0, s, p, sc, en); break;
@@ -849,8 +1361,13 @@ static void launch_fwd(const FwdParams& p, const Sched& sc, const EncParams& en,
 
 template <int VPL, int H, int KM>
 static int launch_bwd_dst_km(const BwdDstParams& p, const Sched& sc, const EncParams& en,
-                             const AlignnEdgeEncoder* enc, hipStream_t s) {
+                             const AlignnEdgeEncoder* enc, hipStream_t s, int flags = 0) {
   const int64_t items = sc.items();
+  if (KM == 0 && (flags & ALIGNN_SCHED_COMPACT_REGS)) {
+    if (items > 0)
+      hipLaunchKernelGGL((tconv_bwd_dst2_kernel<VPL, H>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+    return ALIGNN_OK;
+  }
   if (KM == 0) {
     if (items > 0)
       hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, 0>), dim3((unsigned)items), dim3(256), 0, s, p, sc, en,
@@ -877,9 +1394,9 @@ static int launch_bwd_dst_km(const BwdDstParams& p, const Sched& sc, const EncPa
 
 template <int VPL, int H>
 static int launch_bwd_dst(const BwdDstParams& p, const Sched& sc, const EncParams& en, const AlignnEdgeEncoder* enc,
-                          int km, hipStream_t s) {
+                          int km, hipStream_t s, int flags) {
   switch (km) {
-    case 0: return launch_bwd_dst_km<VPL, H, 0>(p, sc, en, enc, s);
+    case 0: return launch_bwd_dst_km<VPL, H, 0>(p, sc, en, enc, s, flags);
     case 8: return launch_bwd_dst_km<VPL, H, 8>(p, sc, en, enc, s);
     case 12: return launch_bwd_dst_km<VPL, H, 12>(p, sc, en, enc, s);
     default: return launch_bwd_dst_km<VPL, H, 16>(p, sc, en, enc, s);
@@ -970,7 +1487,8 @@ extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, cons
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
   const Sched sc = make_sched(sched, n);
-  ALIGNN_DISPATCH_VH(vpl, H, launch_fwd, p, sc, en, km, s);
+  const int flags = sched ? sched->flags : 0;
+  ALIGNN_DISPATCH_VH(vpl, H, launch_fwd, p, sc, en, km, s, flags);
   ALIGNN_LAUNCH_CHECK("tconv_fwd_kernel");
   return ALIGNN_OK;
 }
@@ -1016,6 +1534,7 @@ extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, 
     set_error("tconv_bwd_dst: edge encoder gradients dw1/db1 are required");
     return ALIGNN_E_BAD_SHAPE;
   }
+  const int flags = sched ? sched->flags : 0;
   BwdDstParams p{n, m, D, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den,
                  dq, lddq, Sz, sigz, dz_e, alpha_e, enc ? nullptr : dF, lddf, accumulate_dF,
                  make_drop(drop_p, seed)};
@@ -1023,7 +1542,7 @@ extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, 
   const int vpl = vpl_for(D);
   const Sched sc = make_sched(sched, n);
   int lrc = ALIGNN_OK;
-#define ALIGNN_BWD(V_, H_) lrc = launch_bwd_dst<V_, H_>(p, sc, en, enc, km, s)
+#define ALIGNN_BWD(V_, H_) lrc = launch_bwd_dst<V_, H_>(p, sc, en, enc, km, s, flags)
   if (vpl == 1 && H == 1) ALIGNN_BWD(1, 1);
   else if (vpl == 1 && H == 2) ALIGNN_BWD(1, 2);
   else if (vpl == 1 && H == 4) ALIGNN_BWD(1, 4);

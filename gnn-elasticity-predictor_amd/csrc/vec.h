@@ -117,4 +117,20 @@ __device__ __forceinline__ float pick(const float (&a)[H], int idx) {
   return r;
 }
 
+// pick<H> with every candidate laundered through an empty asm: the optimizer otherwise folds the
+// select chain into a dynamically indexed load of the array, which forces the array into scratch
+// memory (private segment) — observed on the attention kernels' per-head state arrays.
+__device__ __forceinline__ float launder(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <int H>
+__device__ __forceinline__ float pick_r(const float (&a)[H], int idx) {
+  float r = launder(a[0]);
+#pragma unroll
+  for (int h = 1; h < H; ++h) r = (idx == h) ? launder(a[h]) : r;
+  return r;
+}
+
 }  // namespace alignn

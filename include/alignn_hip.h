@@ -129,7 +129,10 @@ int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, 
 typedef struct AlignnSchedule {
   const int32_t* light; int64_t n_light;
   const int32_t* heavy; int64_t n_heavy;
+  int32_t flags;     /* ALIGNN_SCHED_COMPACT_REGS: the compact-register kernel variants (no encoder) */
+  int32_t reserved;
 } AlignnSchedule;
+#define ALIGNN_SCHED_COMPACT_REGS 1
 
 /* Edge encoder (optional, replaces F): the edge features are the hidden layer of a
  * Linear->ReLU edge encoder, f_t = relu(W1 x[row(t)] + b1) — the angle encoder's first Linear
