@@ -138,3 +138,84 @@ def test_hetero_nll_with_knn_sample_weights():
     ref.backward()
     assert abs(float(loss) - float(ref)) < 1e-5 * abs(float(ref))
     assert _rel(dh, h.grad) < 1e-5
+
+
+def _tconv_case(D, H, n, deg_hi, seed, with_wbar, feat_row):
+    """Random graph with ragged in-degrees (some 0, some above the heavy threshold) and operands."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(seed)
+    degs = torch.randint(0, deg_hi, (n,), generator=g)
+    degs[::7] = 0
+    dst = torch.repeat_interleave(torch.arange(n), degs)
+    src = torch.randint(0, n, (dst.numel(),), generator=g)
+    ei = torch.stack([src, dst]).to(DEV)
+    csr = ops.GraphCSR(ei, n)
+    m = dst.numel()
+    r = lambda *s: (torch.randn(*s, generator=g) * 0.5).to(DEV)  # noqa: E731
+    t = dict(QKVR=r(n, 4 * D), U=r(n, H, D), Vd=r(n, H, D), F=r(max(m, 1), D), dout=r(n, D),
+             wbar=r(D) if with_wbar else None, dF0=r(max(m, 1), D),
+             feat_row=(torch.randperm(max(m, 1), generator=g)[:m].to(torch.int32).to(DEV) if feat_row else None))
+    return csr, m, t
+
+
+def _run_tconv(csr, m, t, D, H, drop, compact):
+    ops = _ops()
+    n = csr.n
+    csr._sched = None
+    ops.GraphCSR.COMPACT_REGS = compact
+    try:
+        outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
+        sumA, mstat, den = (torch.empty(n, H, device=DEV) for _ in range(3))
+        ops.tconv_fwd(csr, D, H, t["QKVR"], t["U"], t["wbar"], t["F"], t["feat_row"], outp, S, sumA, mstat, den,
+                      drop, 77)
+        dq = torch.empty(n, D, device=DEV)
+        Sz, sigz = torch.empty(n, H, D, device=DEV), torch.empty(n, H, device=DEV)
+        dz, al = torch.empty(max(m, 1), H, device=DEV), torch.empty(max(m, 1), H, device=DEV)
+        dF = t["dF0"].clone()
+        ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], t["feat_row"], t["dout"], outp,
+                          mstat, den, dq, Sz, sigz, dz, al, dF, 3, drop, 77)
+    finally:
+        ops.GraphCSR.COMPACT_REGS = False
+        csr._sched = None
+    torch.cuda.synchronize()
+    return dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz[:m], al=al[:m],
+                dF=dF)
+
+
+@pytest.mark.parametrize("D,H", [(256, 4), (128, 2), (64, 1), (32, 4), (512, 8)])
+@pytest.mark.parametrize("drop", [0.0, 0.15])
+def test_compact_register_attention_kernels_match_v1(D, H, drop):
+    """The row-distributed (COMPACT_REGS) attention kernels vs the default ones: same math, softmax
+    sums in a different order -> 1e-5 relative; per-edge dz / alpha' and the dF rows agree too."""
+    for seed, (with_wbar, feat_row) in enumerate([(True, False), (False, True)]):
+        csr, m, t = _tconv_case(D, H, 300, 70, 10 + seed, with_wbar, feat_row)
+        a = _run_tconv(csr, m, t, D, H, drop, False)
+        b = _run_tconv(csr, m, t, D, H, drop, True)
+        for k in a:
+            assert _rel(b[k], a[k]) < 1e-5, (k, D, H, drop, seed)
+
+
+@pytest.mark.parametrize("lg_offset", ["num_nodes", "num_edges"])
+def test_compact_register_kernels_full_model_vs_oracle(lg_offset):
+    import alignn_mi355x as A
+    from alignn_mi355x import ops
+    from alignn_mi355x.synthetic import mp_like_batch
+    from oracle import model_ref
+    from oracle.pyg_ref import RefData
+    torch.manual_seed(5)
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
+    st = {k: v.detach().clone().double() for k, v in model.state_dict().items()}
+    cpu_batch = mp_like_batch(3, lg_offset=lg_offset)
+    ref_b = RefData(**{k: getattr(cpu_batch, k) for k in cpu_batch.keys()})
+    for k in ("x", "edge_attr", "lg_edge_attr", "global_x", "sg_one_hot", "y"):
+        setattr(ref_b, k, getattr(ref_b, k).double())
+    ref_b.num_graphs = 3
+    rmean, rlogvar = model_ref.hetero_forward(st, ref_b, 4)
+    ops.GraphCSR.COMPACT_REGS = True
+    try:
+        model.to(DEV)
+        mean, logvar = model(cpu_batch.to(DEV))
+    finally:
+        ops.GraphCSR.COMPACT_REGS = False
+    assert _rel(mean.detach().cpu(), rmean) < 1e-4
+    assert _rel(logvar.detach().cpu(), rlogvar) < 1e-4
