@@ -242,7 +242,7 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
         for (int i = 0; i < VPL; ++i) accS[h][i] *= corr[h];
       }
       {
-        const float cl = pick<H>(corr, hl);
+        const float cl = pick_r<H>(corr, hl);
 #pragma unroll
         for (int i = 0; i < VPL; ++i) accV[i] *= cl;
       }
@@ -258,7 +258,7 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
 #pragma unroll
           for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(ed[h], ring[j].f[i], accS[h][i]);
         }
-        const float el = pick<H>(ed, hl);
+        const float el = pick_r<H>(ed, hl);
 #pragma unroll
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
@@ -307,7 +307,7 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
       for (int v = 0; v < 4; ++v) {
         const float* o = merge + (v * 64 + lane) * NS;
         const float mh = o[hl];
-        const float f = (mh == -INFINITY) ? 0.f : __expf(mh - pick<H>(m, hl));
+        const float f = (mh == -INFINITY) ? 0.f : __expf(mh - pick_r<H>(m, hl));
 #pragma unroll
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(o[3 * H + H * VPL + i], f, accV[i]);
       }
@@ -329,16 +329,16 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
         for (int i = 0; i < VPL; ++i) o[i] = accS[h][i] * inv[h];
         vstore(p.S + (d * H + h) * D + j0, o);
       }
-      const float il = pick<H>(inv, hl);
+      const float il = pick_r<H>(inv, hl);
       float o[VPL];
 #pragma unroll
       for (int i = 0; i < VPL; ++i) o[i] = accV[i] * il;
       vstore(p.aggV + d * D + j0, o);
     }
     if (lane < H) {
-      p.sumA[d * H + lane] = pick<H>(sa, lane) * pick<H>(inv, lane);
-      p.mstat[d * H + lane] = pick<H>(m, lane);
-      p.den[d * H + lane] = pick<H>(dn, lane);
+      p.sumA[d * H + lane] = pick_r<H>(sa, lane) * pick_r<H>(inv, lane);
+      p.mstat[d * H + lane] = pick_r<H>(m, lane);
+      p.den[d * H + lane] = pick_r<H>(dn, lane);
     }
   }
   if (heavy) __syncthreads();  // merge buffer free for the next item
@@ -528,7 +528,7 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
 #pragma unroll
             for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(dz[h], ring[j].f[i], sz[h][i]);
           }
-          const float dzl = pick<H>(dz, hl);
+          const float dzl = pick_r<H>(dz, hl);
 #pragma unroll
           for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, ring[j].k[i], dqa[i]);
 #ifndef ALIGNN_NO_ENC_ACC
@@ -566,8 +566,8 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
             }
           }
           if (lane < H) {
-            p.dz_e[(int64_t)t * H + lane] = pick<H>(dz, lane);
-            p.alpha_e[(int64_t)t * H + lane] = pick<H>(al, lane);
+            p.dz_e[(int64_t)t * H + lane] = pick_r<H>(dz, lane);
+            p.alpha_e[(int64_t)t * H + lane] = pick_r<H>(al, lane);
           }
         }
         const int32_t tn = tb + stride + j;
@@ -612,7 +612,7 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
 #pragma unroll
       for (int h = 0; h < H; ++h) vstore(p.Sz + (d * H + h) * D + j0, sz[h]);
     }
-    if (lane < H) p.sigz[d * H + lane] = pick<H>(sgz, lane);
+    if (lane < H) p.sigz[d * H + lane] = pick_r<H>(sgz, lane);
   }
   if (heavy) __syncthreads();
 }
