@@ -115,6 +115,7 @@ def main():
 
     # pick the dominant kernel (untimed eager probe step with events around every launch)
     dominant = None
+    step_work = None
     if not args.no_roofline:
         step(0)
         torch.cuda.synchronize()
@@ -124,6 +125,10 @@ def main():
         summ = profiling.summary()
         profiling.disable()
         dominant = max(summ, key=lambda k: summ[k]["total_ms"])
+        # whole-step algorithmic work of this formulation (one probe step): GEMM flops, attention bytes
+        step_work = {"gemm_gflop": sum(v["flops_per_launch"] * v["count"] for v in summ.values()) / 1e9,
+                     "tconv_gbyte": sum(v["bytes_per_launch"] * v["count"] for k, v in summ.items()
+                                        if k.startswith("tconv")) / 1e9}
         if args.dump_probes and rank == 0:
             with open(args.dump_probes, "w") as f:
                 json.dump(dict(sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"])), f, indent=1)
@@ -218,6 +223,13 @@ def main():
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
                        "dropout": args.dropout, "launch": launch_mode},
             "roofline": roof, "cpu_baseline": cpu,
+            # whole-step view: this formulation's GEMM flops and attention bytes per
+            # graph and the fraction of the fp32 MFMA / HBM peaks they imply at the measured rate
+            "step_roofline": None if step_work is None else {
+                "gemm_gflop_per_graph": round(step_work["gemm_gflop"] / B, 4),
+                "mfma_frac": round(step_work["gemm_gflop"] / B * (value / world) / (FP32_MFMA_TFLOPS * 1e3), 4),
+                "tconv_mbyte_per_graph": round(step_work["tconv_gbyte"] * 1e3 / B, 2),
+                "hbm_frac": round(step_work["tconv_gbyte"] / B * value / world / HBM_PEAK_GBS, 4)},
         }
         print(json.dumps(result), flush=True)
     if world > 1:
