@@ -129,7 +129,13 @@ class BatchCache:
         la = batch.lg_edge_attr
         self.angle_dim = int(la.size(-1)) if la.dim() == 2 else 0
         if self.T > 0 and la.numel() > 0:
-            self.xa = ops.gather_rows(la.contiguous().float(), self.lg.perm_dst[: self.T])
+            # target-sorted angle inputs, rows padded to a multiple of 4 floats (16-byte aligned rows:
+            # the encoder GEMMs read them with float4 loads; the pad column is never read)
+            a = la.contiguous().float()
+            ld = (a.size(1) + 3) // 4 * 4
+            buf = torch.empty(self.T, ld, device=a.device)
+            self.xa = buf[:, :a.size(1)]
+            ops.gather_rows(a, self.lg.perm_dst[: self.T], self.xa)
         else:
             self.xa = None
         if hasattr(batch, "batch") and batch.batch is not None:
