@@ -6,6 +6,11 @@ reference's clip_grad_norm_(5.0) + AdamW, which then run identically on every ra
 The reference trains on one device (scripts/train.py:607-723); with the PyG lg_edge_index offset
 rule a rank's batch is collated on its own, so DP parity means: every rank's
 gradient equals the reference's on that rank's batch, and the update uses their mean.
+
+Ensemble sharding: the reference trains its members one after the other
+(scripts/train.py:2052-2093, member i has seed ``seed + 1007 i`` and fold ``i % num_folds``); here
+member i lives on rank ``i % world`` with no per-step communication, and inference gathers every
+member's [B, 2T] heads to rank 0 (one gather per batch) for the moment mix.
 """
 from __future__ import annotations
 
@@ -37,3 +42,51 @@ def max_over_ranks(seconds: float, device) -> float:
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ------------------------------------------------------------------------------------------------
+# Ensemble sharding: one (or more) members per rank
+# ------------------------------------------------------------------------------------------------
+def member_seed(base_seed: int, member: int) -> int:
+    """Seed of ensemble member ``member`` (train.py:2053)."""
+    return int(base_seed) + int(member) * 1007
+
+
+def member_fold(member: int, num_folds: int) -> int:
+    """Cross-validation fold member ``member`` trains against (train.py:2054)."""
+    return int(member) % int(num_folds)
+
+
+def members_of_rank(num_members: int, world: int, rank: int) -> List[int]:
+    """Members placed on ``rank``: i % world == rank (5 members on 8 GPUs -> ranks 0-4 one each,
+    ranks 5-7 none)."""
+    if num_members < 1 or world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad placement: members={num_members} world={world} rank={rank}")
+    return list(range(rank, num_members, world))
+
+
+def gather_member_heads(local: torch.Tensor, num_members: int, dst: int = 0, group=None) -> Optional[torch.Tensor]:
+    """Gathers every rank's member outputs ``local [m_rank, B, W]`` (its members in
+    :func:`members_of_rank` order) to ``dst`` and returns them there as ``[num_members, B, W]`` in
+    member order (``None`` on the other ranks).  Ranks pad to the same slot count so one fixed-size
+    gather suffices (RCCL gather over xGMI; B x 2T x 4 bytes per member)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    mine = members_of_rank(num_members, world, rank) if rank < num_members else []
+    if local.size(0) != len(mine):
+        raise ValueError(f"rank {rank} holds members {mine} but passed {local.size(0)} outputs")
+    slots = -(-num_members // world)
+    buf = local.new_zeros((slots,) + tuple(local.shape[1:]))
+    if len(mine):
+        buf[:len(mine)].copy_(local)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, parts, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.stack([parts[i % world][i // world] for i in range(num_members)], 0)
+
+
+def broadcast_(tensors: Sequence[torch.Tensor], src: int = 0, group=None) -> None:
+    """Broadcast in place (e.g. the target normalizer stats, scaler_state, before training)."""
+    for t in tensors:
+        dist.broadcast(t, src=src, group=group)

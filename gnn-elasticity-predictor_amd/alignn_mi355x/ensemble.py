@@ -10,11 +10,10 @@ kernels are latency-bound, so members overlap on the CUs — and one kernel
 (``alignn_ensemble_moments``) does the moment mix and the log-normal conversion.  Calibration
 (affine debias, conformal quantile) runs on the host over the collected [n, T] predictions, as in
 the reference.  Members on different GPUs: run one ``EnsemblePredictor`` of one member per rank and
-gather the [B, 2T] heads.
+gather the [B, 2T] heads to one rank (:class:`ShardedEnsemble`).
 """
 from __future__ import annotations
 
-import ctypes
 import math
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -72,23 +71,15 @@ class EnsemblePredictor:
                 main.wait_stream(s)
         return torch.stack(outs, 0)
 
-    def _moments(self, heads: torch.Tensor, convert: bool) -> Dict[str, torch.Tensor]:
-        M, B, W = heads.shape
-        T = W // 2
-        dev = heads.device
+    def _stats(self, dev):
         if self._lm is None or self._lm.device != dev:
             self._lm = torch.tensor(self._log_means, dtype=torch.float32, device=dev)
             self._ls = torch.tensor(self._log_stds, dtype=torch.float32, device=dev)
-        names = ("mean_z", "std_z") + (("mean_orig", "std_lin", "lo90", "hi90") if convert else ())
-        res = {k: torch.empty(B, T, device=dev) for k in names}
-        ptr = lambda k: res[k].data_ptr() if k in res else None  # noqa: E731
-        h = heads.contiguous()
-        _lib.check(_lib.lib().alignn_ensemble_moments(
-            M, B, T, h.data_ptr(), h.stride(0), h.stride(1), self.floor,
-            self._lm.data_ptr() if convert else None, self._ls.data_ptr() if convert else None,
-            ptr("mean_z"), ptr("std_z"), ptr("mean_orig"), ptr("std_lin"), ptr("lo90"), ptr("hi90"),
-            stream_ptr()), "alignn_ensemble_moments")
-        return res
+        return self._lm, self._ls
+
+    def _moments(self, heads: torch.Tensor, convert: bool) -> Dict[str, torch.Tensor]:
+        lm, ls = self._stats(heads.device)
+        return ensemble_moments(heads, self.floor, lm if convert else None, ls if convert else None)
 
     def predict_batch(self, batch) -> Dict[str, torch.Tensor]:
         """predict.ensemble_predict for one batch (device tensors, [B, T] each): mean_z, std_z
@@ -111,12 +102,112 @@ class EnsemblePredictor:
         """ensemble_collect_embeddings: member-mean of embed() per graph, host [n, D]."""
         out = []
         for b in batches:
-            e = self.member_outputs(b, mode="embed").contiguous()
-            M = e.size(0)
-            mean = torch.empty(e.shape[1:], device=e.device)
-            _lib.check(_lib.lib().alignn_member_mean_f32(M, mean.numel(), e.data_ptr(), e.stride(0),
-                                                         mean.data_ptr(), stream_ptr()), "alignn_member_mean_f32")
-            out.append(mean.cpu())
+            out.append(member_mean(self.member_outputs(b, mode="embed")).cpu())
+        if not out:
+            raise ValueError("No batches produced embeddings.")
+        return torch.cat(out)
+
+
+def ensemble_moments(heads: torch.Tensor, floor: float, log_means: Optional[torch.Tensor] = None,
+                     log_stds: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    """One kernel over member heads ``[M, B, 2T]`` (mean | logvar): mean_z, std_z
+    (train.py:875-902); with the target stats on the device also mean_orig, std_lin, lo90, hi90
+    (predict.py:616-640)."""
+    M, B, W = heads.shape
+    T = W // 2
+    dev = heads.device
+    convert = log_means is not None
+    names = ("mean_z", "std_z") + (("mean_orig", "std_lin", "lo90", "hi90") if convert else ())
+    res = {k: torch.empty(B, T, device=dev) for k in names}
+    ptr = lambda k: res[k].data_ptr() if k in res else None  # noqa: E731
+    h = heads.contiguous()
+    _lib.check(_lib.lib().alignn_ensemble_moments(
+        M, B, T, h.data_ptr(), h.stride(0), h.stride(1), float(floor),
+        log_means.data_ptr() if convert else None, log_stds.data_ptr() if convert else None,
+        ptr("mean_z"), ptr("std_z"), ptr("mean_orig"), ptr("std_lin"), ptr("lo90"), ptr("hi90"),
+        stream_ptr()), "alignn_ensemble_moments")
+    return res
+
+
+def member_mean(outs: torch.Tensor) -> torch.Tensor:
+    """Mean over members of ``[M, B, D]`` (ensemble_collect_embeddings, train.py:907-927)."""
+    e = outs.contiguous()
+    mean = torch.empty(e.shape[1:], device=e.device)
+    _lib.check(_lib.lib().alignn_member_mean_f32(e.size(0), mean.numel(), e.data_ptr(), e.stride(0),
+                                                 mean.data_ptr(), stream_ptr()), "alignn_member_mean_f32")
+    return mean
+
+
+class ShardedEnsemble:
+    """Members spread over the ranks of a process group (one member per GPU).
+
+    Rank r runs the members ``dp.members_of_rank(num_members, world, r)`` (``local_models``, in that
+    order; an empty list on ranks without members) concurrently on its GPU; every batch ends with one
+    gather of the [m_r, B, W] outputs to ``dst``, which does the moment mix.  Same results as an
+    :class:`EnsemblePredictor` holding all members on one device; the methods return ``None`` on
+    ranks other than ``dst``.  Every rank must call them with the same batches (same graph counts)."""
+
+    def __init__(self, local_models: Sequence, num_members: int, target_dim: int = 2, hidden: int = 256,
+                 dst: int = 0, group=None, min_logvar_floor: float = MIN_LOGVAR_FLOOR,
+                 target_log_means: Sequence[float] = TARGET_LOG_MEANS,
+                 target_log_stds: Sequence[float] = TARGET_LOG_STDS, concurrent: bool = True):
+        from . import dp
+        import torch.distributed as dist
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        mine = dp.members_of_rank(num_members, self.world, self.rank)
+        if len(local_models) != len(mine):
+            raise ValueError(f"rank {self.rank} must hold members {mine}, got {len(local_models)} models")
+        self.num_members, self.dst, self.group = int(num_members), int(dst), group
+        self.widths = {"hetero": 2 * int(target_dim), "embed": int(hidden)}
+        self.local = (EnsemblePredictor(local_models, min_logvar_floor, target_log_means, target_log_stds, concurrent)
+                      if local_models else None)
+        self.floor = float(min_logvar_floor)
+        self._log_means, self._log_stds = list(target_log_means), list(target_log_stds)
+
+    def _gathered(self, batch, mode: str) -> Optional[torch.Tensor]:
+        from . import dp
+        if self.local is not None:
+            out = self.local.member_outputs(batch, mode)
+        else:
+            out = torch.empty(0, int(batch.num_graphs), self.widths[mode], device=batch.x.device)
+        return dp.gather_member_heads(out, self.num_members, dst=self.dst, group=self.group)
+
+    def _mix(self, heads: torch.Tensor, convert: bool) -> Dict[str, torch.Tensor]:
+        if not convert:
+            return ensemble_moments(heads, self.floor)
+        dev = heads.device
+        lm = torch.tensor(self._log_means, dtype=torch.float32, device=dev)
+        ls = torch.tensor(self._log_stds, dtype=torch.float32, device=dev)
+        return ensemble_moments(heads, self.floor, lm, ls)
+
+    def predict_batch(self, batch) -> Optional[Dict[str, torch.Tensor]]:
+        heads = self._gathered(batch, "hetero")
+        return None if heads is None else self._mix(heads, convert=True)
+
+    def collect(self, batches) -> Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        means, stds, ys = [], [], []
+        for b in batches:
+            heads = self._gathered(b, "hetero")
+            if heads is None:
+                continue
+            r = self._mix(heads, convert=False)
+            means.append(r["mean_z"].cpu())
+            stds.append(r["std_z"].cpu())
+            ys.append(b.y.view(b.num_graphs, -1).float().cpu())
+        if self.rank != self.dst:
+            return None
+        if not means:
+            raise ValueError("No batches produced predictions.")
+        return torch.cat(means), torch.cat(ys), torch.cat(stds)
+
+    def embed(self, batches) -> Optional[torch.Tensor]:
+        out = []
+        for b in batches:
+            e = self._gathered(b, "embed")
+            if e is not None:
+                out.append(member_mean(e).cpu())
+        if self.rank != self.dst:
+            return None
         if not out:
             raise ValueError("No batches produced embeddings.")
         return torch.cat(out)

@@ -65,3 +65,46 @@ def test_dp_allreduce_clip_adamw_world2(tmp_path):
     assert torch.allclose(r[0]["new"], ref, rtol=1e-6, atol=1e-7)
     assert r[0]["t"] == r[1]["t"] == 1.5
     assert r[0]["graphs"] == list(range(0, 32)) and r[1]["graphs"] == list(range(32, 64))
+
+
+# ------------------------------------------------------------------------------------------------
+# Ensemble sharding: members placed i % world, heads gathered to rank 0 in member order
+# ------------------------------------------------------------------------------------------------
+def _member_heads(member, B=3, W=4):
+    return torch.randn(B, W, generator=torch.Generator().manual_seed(500 + member))
+
+
+def _ens_worker(rank, world, port, out_dir, num_members):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = dp.members_of_rank(num_members, world, rank)
+        local = torch.stack([_member_heads(i) for i in mine], 0) if mine else torch.empty(0, 3, 4)
+        got = dp.gather_member_heads(local, num_members)
+        stats = torch.tensor([4.32, 3.56]) if rank == 0 else torch.zeros(2)
+        dp.broadcast_([stats])
+        torch.save({"got": got, "mine": mine, "stats": stats}, os.path.join(out_dir, f"e{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("world,num_members", [(2, 5), (3, 2)])
+def test_ensemble_member_gather(tmp_path, world, num_members):
+    mp.spawn(_ens_worker, args=(world, _free_port(), str(tmp_path), num_members), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"e{i}.pt", weights_only=True) for i in range(world)]
+    want = torch.stack([_member_heads(i) for i in range(num_members)], 0)
+    assert torch.equal(r[0]["got"], want)
+    assert all(x["got"] is None for x in r[1:])
+    assert sorted(i for x in r for i in x["mine"]) == list(range(num_members))
+    assert all(torch.equal(x["stats"], torch.tensor([4.32, 3.56])) for x in r)
+
+
+def test_member_placement_and_seeds():
+    # train.py:2053-2054: seed + 1007 i, fold i % num_folds; C4: 5 members over 8 ranks
+    assert [dp.member_seed(42, i) for i in range(3)] == [42, 1049, 2056]
+    assert [dp.member_fold(i, 5) for i in range(7)] == [0, 1, 2, 3, 4, 0, 1]
+    assert [dp.members_of_rank(5, 8, r) for r in range(8)] == [[0], [1], [2], [3], [4], [], [], []]
+    assert dp.members_of_rank(5, 2, 0) == [0, 2, 4] and dp.members_of_rank(5, 2, 1) == [1, 3]
+    with pytest.raises(ValueError):
+        dp.members_of_rank(5, 2, 2)

@@ -69,3 +69,30 @@ def test_concurrent_members_equal_sequential_bitwise(ens):
     h2 = ep2.member_outputs(b2[1])
     torch.cuda.synchronize()
     assert torch.equal(h1, h2)
+
+
+def test_sharded_ensemble_world1_matches_reference(ens):
+    """ShardedEnsemble (members over ranks, RCCL gather to rank 0) in a 1-rank group holds all three
+    members; its collect/embed are the reference's.  Multi-rank placement and gather order are
+    covered by tests/test_dp_gloo.py."""
+    import torch.distributed as dist
+    from alignn_mi355x.ensemble import ShardedEnsemble
+    ep, batches = _setup(ens)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+    try:
+        se = ShardedEnsemble(ep.models, 3, target_dim=2, hidden=int(ens["meta/dims"][4]),
+                             min_logvar_floor=float(ens["meta/min_logvar_floor"]),
+                             target_log_means=ens["meta/target_log_means"].tolist(),
+                             target_log_stds=ens["meta/target_log_stds"].tolist())
+        mean_z, targets, std_z = se.collect(batches)
+        emb = se.embed(batches)
+        r = se.predict_batch(batches[0])
+    finally:
+        dist.destroy_process_group()
+    assert rel_err(mean_z, ens["out/mean_z"]) < TOL
+    assert rel_err(std_z, ens["out/std_z"]) < TOL
+    assert torch.equal(targets, torch.from_numpy(ens["out/targets"]))
+    assert rel_err(emb, ens["out/embed"]) < TOL
+    r0 = ep.predict_batch(batches[0])
+    for k in r0:
+        assert torch.equal(r[k], r0[k]), k
