@@ -30,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "graphs/sec fwd+bwd (ALIGNN, ~60-atom MP crystals) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
+BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 
 
 def parse():
@@ -47,6 +48,9 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--dump-probes", default="", help="write the per-op probe summary (JSON) to this path")
+    p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                   help="GEMM arithmetic: fp32 (BASELINE config 2, the default) or bf16 matrix-core inputs with "
+                        "fp32 accumulation (config 3's autocast precision; a secondary line, never the fp32 number)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as HIP graphs (ROCm disallows external event nodes, so the roofline "
                         "probe then runs in 2 eager steps after the timed region)")
@@ -105,7 +109,8 @@ def main():
     torch.manual_seed(1234)  # identical initial weights on every rank
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                       args.dropout), 2).to(dev)
-    trainer = A.FusedTrainer(model)
+    trainer = A.FusedTrainer(model, precision=args.precision)
+    mfma_peak = BF16_MFMA_TFLOPS if args.precision == "bf16" else FP32_MFMA_TFLOPS
     batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=args.lg_offset).to(dev)
     if world > 1:
         trainer.grad_hook = grad_allreduce_hook(world)  # the DP exchange: one all_reduce of the flat gradient
@@ -201,8 +206,8 @@ def main():
             avg_s = s["avg_ms"] / 1e3
             if s["flops_per_launch"] > 0:
                 ach = s["flops_per_launch"] / avg_s / 1e12
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(ach / FP32_MFMA_TFLOPS, 4), "traffic": None, "kernel": dominant,
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": mfma_peak, "unit": "TFLOP/s",
+                        "frac": round(ach / mfma_peak, 4), "traffic": None, "kernel": dominant,
                         "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
                         "flops_per_launch": s["flops_per_launch"], "timing": probe_src}
             else:
@@ -217,17 +222,17 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16-gemm/f32", "data": "synthetic",
             "config": {"workload": f"B={B} synthetic MP-like graphs per GPU (60 atoms/720 bonds/7920 triplets), "
                                    f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
-                       "dropout": args.dropout, "launch": launch_mode},
+                       "dropout": args.dropout, "launch": launch_mode, "precision": args.precision},
             "roofline": roof, "cpu_baseline": cpu,
             # whole-step view: this formulation's GEMM flops and attention bytes per
             # graph and the fraction of the fp32 MFMA / HBM peaks they imply at the measured rate
             "step_roofline": None if step_work is None else {
                 "gemm_gflop_per_graph": round(step_work["gemm_gflop"] / B, 4),
-                "mfma_frac": round(step_work["gemm_gflop"] / B * (value / world) / (FP32_MFMA_TFLOPS * 1e3), 4),
+                "mfma_frac": round(step_work["gemm_gflop"] / B * (value / world) / (mfma_peak * 1e3), 4),
                 "tconv_mbyte_per_graph": round(step_work["tconv_gbyte"] * 1e3 / B, 2),
                 "hbm_frac": round(step_work["tconv_gbyte"] / B * value / world / HBM_PEAK_GBS, 4)},
         }

@@ -413,6 +413,10 @@ class AlignnEngine:
         # forward: the line blocks' skip projection on the second stream beside the attention
         # (off by default until measured on MI355X)
         self.overlap_forward = False
+        # GEMM arithmetic: "fp32" (the reference's CPU path; exact fp32 MFMA) or "bf16" (bf16 MFMA
+        # inputs, fp32 accumulation — the reference's CUDA autocast);
+        # attention, softmax, LayerNorm and all storage stay fp32 either way
+        self.precision = "fp32"
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -432,6 +436,16 @@ class AlignnEngine:
 
     def forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
                 x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
+        with ops.gemm_precision(self.precision):
+            return self._forward(P, batch, bc, training, seed, x, global_x, mode)
+
+    def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
+        """Writes d(loss)/d(param) for every parameter into G (see _backward)."""
+        with ops.gemm_precision(self.precision):
+            self._backward(P, G, ctx, dout)
+
+    def _forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
+                 x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
         cfg = self.cfg
         D, H, L = cfg.hidden, cfg.heads, cfg.layers
         p_drop = cfg.dropout if training else 0.0
@@ -521,7 +535,7 @@ class AlignnEngine:
         ops.gemm(ctx.shared, P.Wout.t(), out, bias=P.bout)
         return out, ctx
 
-    def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
+    def _backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
         """Writes d(loss)/d(param) for every parameter into G (overwrites; head grads are zero in
         'embed' mode).  ``dout`` is the gradient of the forward's output."""
         cfg = self.cfg

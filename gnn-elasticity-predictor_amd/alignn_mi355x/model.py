@@ -225,6 +225,15 @@ class _ModelFn(torch.autograd.Function):
 class _EngineModelMixin:
     _hetero: bool = True
 
+    def set_precision(self, precision: str):
+        """GEMM arithmetic of this model's forward/backward: "fp32" (default; the reference's CPU
+        path) or "bf16" (bf16 matrix-core inputs, fp32 accumulation and storage — the reference's
+        CUDA autocast GEMMs, train.py:632-636).  Returns self."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self._engine.precision = precision
+        return self
+
     def _flat_params(self) -> Dict[str, nn.Parameter]:
         named = dict(self.named_parameters())
         _, total, _ = offsets(self.config, self._hetero)

@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+from contextlib import contextmanager
 from typing import Optional
 
 import torch
@@ -73,6 +74,23 @@ def _as3(t: torch.Tensor):
 
 
 GEMM_TRACE: Optional[list] = None
+_GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
+GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
+
+
+@contextmanager
+def gemm_precision(precision: str):
+    """GEMMs issued inside run with "fp32" (exact fp32 MFMA) or "bf16" arithmetic (bf16-rounded
+    inputs on v_mfma_f32_32x32x16_bf16, fp32 accumulation and output: ALIGNN_GEMM_BF16)."""
+    global _GEMM_FLAGS
+    if precision not in ("fp32", "bf16"):
+        raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+    prev = _GEMM_FLAGS
+    _GEMM_FLAGS = GEMM_BF16 if precision == "bf16" else 0
+    try:
+        yield
+    finally:
+        _GEMM_FLAGS = prev
 
 _STEP_SEED: Optional[torch.Tensor] = None
 
@@ -135,7 +153,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if c_rows is not None:
         a.c_rows = c_rows.data_ptr()
     a.split_k = 0 if split_k is None else int(split_k)   # 0: the library plans tile shape and split-K
-    a.tile = int(tile)
+    a.tile = int(tile) | _GEMM_FLAGS
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
     if need < 0:
         raise ValueError("gemm: invalid shape")

@@ -14,6 +14,11 @@
 // eight ds_read_b32 when it is [k][row].  Both operands use the same assignment, so the sum over
 // k is complete (in a permuted order — still an exact per-product-rounded fp32 chain).
 //
+// bf16 compute (ALIGNN_GEMM_BF16): v_mfma_f32_32x32x16_bf16 takes, on lane half h, k = 8h + j
+// (j = 0..7) of a 16-deep slice — the same eight k-values the f32 path feeds to its 8 MFMAs — so
+// the tiles and LDS images are unchanged: the fragments are rounded to bf16 (v_cvt_pk_bf16_f32,
+// RNE) after the LDS read and one MFMA replaces eight.
+//
 // LDS images follow global contiguity (no transposes while staging):
 //   operand contiguous along k   -> [row][BKT+4]
 //   operand contiguous along row -> [BKT][ROWS+4]
@@ -22,6 +27,7 @@
 namespace alignn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BK = 16;  // split-K chunk granularity
 
@@ -144,7 +150,7 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, 
   return v;
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC, int BKT>
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
   constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
@@ -202,13 +208,30 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, BKT>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
 #pragma unroll
       for (int j = 0; j < NI; ++j) read_frag<BN, B_KC, BKT>(Bs, wn * (BN / 2) + j * 32 + l32, h, sub, fb[j]);
+      if constexpr (BF) {
+        bf16x8 ha[MI], hb[NI];
 #pragma unroll
-      for (int s = 0; s < 8; ++s)
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int s = 0; s < 8; ++s) ha[i][s] = (__bf16)fa[i][s];
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int s = 0; s < 8; ++s) hb[j][s] = (__bf16)fb[j][s];
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], hb[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      }
     }
     if (more) {
       float* nxt = smem + (cur ^ 1) * (LA + LB);
@@ -262,17 +285,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC>
-static void launch(const GemmParams& p, dim3 grid, int bk, hipStream_t s) {
-  if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32>), grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16>), grid, dim3(256), 0, s, p);
+static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
+  if (bf) {
+    if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
+  } else {
+    if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
+  }
 }
 
 template <int BM, int BN>
-static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, hipStream_t s) {
-  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, s);
-  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, s);
-  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, s);
-  else launch<BM, BN, false, false>(p, grid, bk, s);
+static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, bool bf, hipStream_t s) {
+  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, bf, s);
+  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, bf, s);
+  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, bf, s);
+  else launch<BM, BN, false, false>(p, grid, bk, bf, s);
 }
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -307,7 +335,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   int64_t best_tiles = 0;
   for (int c = 0; c < 4; ++c) {
     const int bm = cand[c][0], bn = cand[c][1];
-    const int shape = tile & 15;
+    const int shape = tile & 15;  // bits 16/32: stage depth, bit 64: bf16 compute
     if (shape >= 1 && shape <= 4 && c != shape - 1) continue;
     if (shape == 0 && ((bm == 128 && M <= 64) || (bn == 128 && N <= 64))) continue;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * nb;
@@ -338,7 +366,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   pl.kchunk = kchunk;
   // K depth of a pipeline stage (tile bit 4 selects 32: half the barriers per flop; the automatic
   // plan keeps 16 until the 32-deep stage has been measured on MI355X)
-  pl.bk = (tile & 16) ? 32 : 16;
+  pl.bk = (tile & ALIGNN_GEMM_BK32) ? 32 : 16;
   return pl;
 }
 
@@ -411,10 +439,11 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   }
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
-  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, s);
-  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, s);
-  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, s);
-  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, s);
+  const bool bf = (a->tile & ALIGNN_GEMM_BF16) != 0;
+  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, bf, s);
+  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, bf, s);
+  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, bf, s);
+  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {
     int64_t total = nbatch_out * a->M * a->N;
