@@ -40,3 +40,34 @@ def test_library_is_gfx950():
     from alignn_mi355x import _lib
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_gemm_plan_workspace_query_on_host():
+    """alignn_gemm_workspace runs the C-side plan without touching a GPU (no device: 256 CUs
+    assumed, the MI355X count): split-K only for long K with a small tile grid."""
+    import ctypes
+    from alignn_mi355x import _lib
+    lib = _lib.load()
+
+    def ws(M, N, K, batch=1, split=0, reduce_batch=0, tile=0):
+        a = _lib.GemmArgs()
+        a.M, a.N, a.K, a.batch = M, N, K, batch
+        a.sam, a.sak, a.sbk, a.sbn, a.scm, a.scn = K, 1, 1, K, N, 1
+        a.split_k, a.reduce_batch, a.tile = split, reduce_batch, tile
+        return lib.alignn_gemm_workspace(ctypes.byref(a))
+
+    # dW of a line-graph projection: 4 tiles of 64x64, K = 23040 -> 63 chunks of 368
+    assert ws(64, 256, 23040) == 63 * 64 * 256
+    assert ws(256, 256, 256) == 0                    # short K never splits
+    assert ws(2580, 768, 256) == 0                   # enough tiles
+    assert ws(256, 256, 4096, split=4) == 4 * 256 * 256
+    assert ws(256, 256, 4096, split=1) == 0
+    assert ws(64, 64, 4096, tile=4 | 64) == ws(64, 64, 4096, tile=4)   # bf16 flag leaves the plan alone
+    assert ws(-1, 4, 4) == -1
+
+
+def test_precision_flags_match_header():
+    from alignn_mi355x import ops
+    src = open(HEADER).read()
+    assert re.search(rf"#define ALIGNN_GEMM_BF16 {ops.GEMM_BF16}\b", src)
+    assert re.search(r"#define ALIGNN_GEMM_BK32 16\b", src)
