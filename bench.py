@@ -51,6 +51,10 @@ def parse():
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM arithmetic: fp32 (BASELINE config 2, the default) or bf16 matrix-core inputs with "
                         "fp32 accumulation (config 3's autocast precision; a secondary line, never the fp32 number)")
+    p.add_argument("--e2e", type=int, default=0, metavar="GRAPHS",
+                   help="also time the end-to-end loop over an HBM-resident dataset of this many graphs per rank: "
+                        "device collate of a random batch + CSR/compaction + step (SURVEY §8d's 'including collate' "
+                        "number; reported as a separate field, never as value)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as HIP graphs (ROCm disallows external event nodes, so the roofline "
                         "probe then runs in 2 eager steps after the timed region)")
@@ -87,6 +91,48 @@ def cpu_baseline(args, B):
     return {"value": round(B * args.cpu_steps / dt, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
             "sample": f"{args.cpu_steps} steps x {B} graphs (fp32 fwd+bwd+clip+AdamW, dropout 0) after 1 warm-up; "
                       f"{cpu_model}"}
+
+
+def end_to_end(args, trainer, dev, rank, world):
+    """Training loop over a dataset resident in HBM (store.GraphStore): per step a random batch is
+    collated on the device and its CSR lists / line-graph compaction are built, then the step runs."""
+    import numpy as np
+    from alignn_mi355x.data import Data
+    from alignn_mi355x.dp import max_over_ranks
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_graph
+
+    keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+    first = rank * args.e2e
+    t_build = time.perf_counter()
+    graphs = [mp_like_graph(first + g) for g in range(args.e2e)]
+    store = GraphStore.from_data_list([Data(**{k: getattr(d, k) for k in keys}) for d in graphs], dev)
+    del graphs
+    t_build = time.perf_counter() - t_build
+    rng = np.random.default_rng(1234 + rank)
+    B = args.batch
+
+    def e2e_step(i):
+        batch = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset)
+        trainer.step(batch, seed=7919 * rank + i)
+
+    for i in range(args.warmup):
+        e2e_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        e2e_step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dt = max_over_ranks(dt, dev)
+    return {"value": round(B * world * args.steps / dt, 2), "unit": "graphs/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "dataset_graphs_per_rank": args.e2e, "store_build_s": round(t_build, 1),
+            "includes": "device collate of a random batch + CSR/compaction + fwd/NLL/bwd/clip/AdamW"}
 
 
 def main():
@@ -194,6 +240,10 @@ def main():
         profiling.disable()
         trainer._graph = saved
 
+    e2e = None
+    if args.e2e > 0:
+        e2e = end_to_end(args, trainer, dev, rank, world)
+
     probe_src = ("hip events in the captured step (last timed replay)" if probe_in_graph else
                  "hip events around each launch, timed region" if launch_mode == "eager" else
                  "hip events, 2 eager steps after the timed region")
@@ -227,7 +277,7 @@ def main():
                                    f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
                        "dropout": args.dropout, "launch": launch_mode, "precision": args.precision},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "e2e": e2e,
             # whole-step view: this formulation's GEMM flops and attention bytes per
             # graph and the fraction of the fp32 MFMA / HBM peaks they imply at the measured rate
             "step_roofline": None if step_work is None else {
