@@ -3,10 +3,11 @@
 // Replaces the cuBLAS addmm/mm behind every nn.Linear / PyG Linear of the reference's hot path
 // (SURVEY §2 implicit-kernel table) and their autograd backward products.
 //
-// Tiling: BM x BN block (64 or 128 each), K stage BKT = 16 or 32 (two 16-deep slices), 256 threads
+// Tiling: BM x BN block (64 or 128 each), K stage BKT = 16, 32 or 64 (16-deep slices), 256 threads
 // = 4 waves in a 2x2 grid, each wave owns (BM/2)x(BN/2) = MI x NI subtiles of 32x32.  One stage per
 // iteration, double-buffered LDS with register prefetch of the next stage (issue global loads
-// before the MFMAs, write LDS after); a 32-deep stage halves the barriers per MFMA.
+// before the MFMAs, write LDS after); a 32-deep stage halves the barriers per MFMA, a 64-deep one
+// quarters the stages of a small-grid long-K product (latency-bound: one global round trip each).
 //
 // k-slot assignment: an MFMA 32x32x2 sums over two k-slots, lane half h = lane>>5 supplying slot h.
 // Over the 8 MFMAs of a 16-deep slice, step s uses k = 8h + s for lane half h, so a lane's eight
@@ -287,10 +288,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 template <int BM, int BN, bool A_KC, bool B_KC>
 static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
   if (bf) {
-    if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
+    if (bk == 64) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
   } else {
-    if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
+    if (bk == 64) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
   }
 }
@@ -366,7 +369,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   pl.kchunk = kchunk;
   // K depth of a pipeline stage (tile bit 4 selects 32: half the barriers per flop; the automatic
   // plan keeps 16 until the 32-deep stage has been measured on MI355X)
-  pl.bk = (tile & ALIGNN_GEMM_BK32) ? 32 : 16;
+  pl.bk = (tile & ALIGNN_GEMM_BK64) ? 64 : (tile & ALIGNN_GEMM_BK32) ? 32 : 16;
   return pl;
 }
 

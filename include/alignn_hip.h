@@ -65,13 +65,14 @@ typedef struct AlignnGemmArgs {
   float* workspace; int64_t workspace_elems;
   int32_t reduce_batch;   /* 1: C = sum over the batch (one output; K % 16 == 0) */
   int32_t tile;           /* 0: automatic; 1: 128x128, 2: 128x64, 3: 64x128, 4: 64x64 (tuning);
-                             + ALIGNN_GEMM_BK32 / ALIGNN_GEMM_BK16 (stage depth), + ALIGNN_GEMM_BF16 */
+                             + ALIGNN_GEMM_BK32 / BK16 / BK64 (stage depth), + ALIGNN_GEMM_BF16 */
   const int32_t* c_rows;  /* optional: logical row r of C is stored at row c_rows[r] (scatter; beta
                              reads the same row).  bias/rowscale/mask stay indexed by r. */
 } AlignnGemmArgs;
 
 #define ALIGNN_GEMM_BK32 16
 #define ALIGNN_GEMM_BK16 32
+#define ALIGNN_GEMM_BK64 128   /* 64-deep stages: 4x fewer global round trips (small grids, long K) */
 /* bf16 compute (the reference's CUDA autocast precision, train.py:632-636):
  * A and B are rounded to bf16 (round-to-nearest-even) as they enter the matrix cores
  * (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate); accumulation, epilogue and storage stay fp32. */

@@ -28,10 +28,12 @@ def _setup(seed=0):
     return model, tr, b
 
 
+@pytest.mark.parametrize("stage", [16, 128])
 @pytest.mark.parametrize("shape", [1, 2, 3, 4])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
-def test_gemm_bk32_stage(shape, layout):
-    """32-deep K stage (tile bit 4) on every tile shape and operand layout, unsplit and split-K."""
+def test_gemm_bk32_stage(shape, layout, stage):
+    """32-deep (ALIGNN_GEMM_BK32 = 16) and 64-deep (ALIGNN_GEMM_BK64 = 128) K stages on every tile
+    shape and operand layout, unsplit and split-K (K = 1000: a partial last stage)."""
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(shape * 11 + len(layout))
     M, N, K = 300, 257, 1000
@@ -42,13 +44,13 @@ def test_gemm_bk32_stage(shape, layout):
     ref = A.double() @ B.double()
     for split in (1, 3):
         C = torch.empty(M, N, device=DEV)
-        ops.gemm(Av, Bv, C, tile=16 + shape, split_k=split)
+        ops.gemm(Av, Bv, C, tile=stage + shape, split_k=split)
         assert _rel(C, ref) < 5e-6, (split,)
     # batch-reduced (shared weights): K multiple of 32 keeps the 32-deep stage inside one batch entry
     Ab = torch.randn(4, 64, 256, generator=g).to(DEV)
     Bb = torch.randn(4, 256, 96, generator=g).to(DEV)
     Cb = torch.empty(64, 96, device=DEV)
-    ops.gemm(Ab, Bb, Cb, reduce_batch=True, tile=16 + shape)
+    ops.gemm(Ab, Bb, Cb, reduce_batch=True, tile=stage + shape)
     assert _rel(Cb, (Ab.double() @ Bb.double()).sum(0)) < 5e-6
 
 

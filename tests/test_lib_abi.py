@@ -71,3 +71,4 @@ def test_precision_flags_match_header():
     src = open(HEADER).read()
     assert re.search(rf"#define ALIGNN_GEMM_BF16 {ops.GEMM_BF16}\b", src)
     assert re.search(r"#define ALIGNN_GEMM_BK32 16\b", src)
+    assert re.search(r"#define ALIGNN_GEMM_BK64 128\b", src)

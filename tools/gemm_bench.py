@@ -18,7 +18,7 @@ from alignn_mi355x import ops  # noqa: E402
 from alignn_mi355x.synthetic import mp_like_batch  # noqa: E402
 
 TILES = {b + k: f"{s}/bk{bk}" for k, s in ((1, "128x128"), (2, "128x64"), (3, "64x128"), (4, "64x64"))
-         for b, bk in ((0, "auto"), (16, 32), (32, 16))}
+         for b, bk in ((0, "auto"), (16, 32), (32, 16), (128, 64))}
 
 
 def timeit(fn, reps):
@@ -84,7 +84,9 @@ def main():
 
         t_auto = timeit(lambda: run(), a.reps)
         trials = {}
-        for tile in (1, 2, 3, 4, 17, 18, 19, 20, 33, 34, 35, 36):
+        for tile in sorted(TILES):
+            if tile < 16:
+                continue
             for split in (1, 2, 4, 8, 16, 32, 64):
                 try:
                     trials[(tile, split)] = timeit(lambda: run(tile, split), a.reps)
