@@ -97,6 +97,11 @@ _SIGNATURES = {
     "alignn_row_sqnorm_f32": ([c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
     "alignn_knn_select_weights": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_i32, c_f32, c_f32, c_f32,
                                    c_vp, c_vp, c_vp], c_i32),
+    "alignn_linear_smallk_f32": ([c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp],
+                                 c_i32),
+    "alignn_gemm_tn_smalln_workspace": ([c_i64, c_i64, c_i32], c_i64),
+    "alignn_gemm_tn_smalln_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp,
+                                   c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_f32,
                           c_vp, c_vp], c_i32),
 }

@@ -417,6 +417,9 @@ class AlignnEngine:
         # inputs, fp32 accumulation — the reference's CUDA autocast);
         # attention, softmax, LayerNorm and all storage stay fp32 either way
         self.precision = "fp32"
+        # the angle encoder's first Linear (11 inputs, T rows) and its weight/bias gradients as
+        # streamed HBM-rate kernels (skinny.hip) instead of MFMA tiles (off until measured)
+        self.skinny_encoder = False
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -479,7 +482,11 @@ class AlignnEngine:
             ctx.angle_enc = ops.EdgeEncoder(bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"))
         elif ctx.has_angle:
             a = torch.empty(T, D, device=dev)
-            ops.gemm(bc.xa, P.enc("angle", 0, "weight").t(), a, bias=P.enc("angle", 0, "bias"), relu=True)
+            W1, b1 = P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias")
+            if self.skinny_encoder and ops.linear_smallk_ok(bc.xa, W1, a):
+                ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
+            else:
+                ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
         else:
             a = torch.zeros(T, D, device=dev)
         ctx.h1a = ctx.a = a
@@ -618,8 +625,12 @@ class AlignnEngine:
                 proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all,
                                   dwl_all, G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
             if ctx.has_angle and da_written and ctx.angle_enc is None:
-                ops.gemm(da.t(), bc.xa, G.enc("angle", 0, "weight"))  # da is the masked hidden-layer gradient
-                ops.colsum(da, G.enc("angle", 0, "bias"))
+                # da is the masked hidden-layer gradient
+                if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLN_MAX:
+                    ops.gemm_tn_smalln(da, bc.xa, G.enc("angle", 0, "weight"), colsum=G.enc("angle", 0, "bias"))
+                else:
+                    ops.gemm(da.t(), bc.xa, G.enc("angle", 0, "weight"))
+                    ops.colsum(da, G.enc("angle", 0, "bias"))
         if ctx.h1e is not None:
             self._mlp_bwd(de, ctx.edge_attr, ctx.h1e, P.enc("edge", 2, "weight"), G.enc("edge", 0, "weight"),
                           G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))

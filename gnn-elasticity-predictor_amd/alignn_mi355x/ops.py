@@ -189,6 +189,47 @@ def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torc
     return out
 
 
+SMALLK_MAX = 16   # alignn_linear_smallk_f32: K <= 16
+SMALLN_MAX = 16   # alignn_gemm_tn_smalln_f32: N <= 16
+
+
+def linear_smallk_ok(X: torch.Tensor, W: torch.Tensor, out: torch.Tensor) -> bool:
+    """Shapes alignn_linear_smallk_f32 takes (else use gemm)."""
+    return (X.dim() == 2 and X.stride(1) == 1 and W.dim() == 2 and W.stride(1) == 1 and out.stride(1) == 1
+            and W.size(1) == X.size(1) <= SMALLK_MAX and out.size(1) == W.size(0) and out.size(0) == X.size(0)
+            and W.size(0) % 4 == 0 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0)
+
+
+def linear_smallk(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor,
+                  relu: bool = False) -> torch.Tensor:
+    """out = act(X W^T + bias) for K = X.size(1) <= 16, streamed (HBM-bound) instead of tiled."""
+    if not linear_smallk_ok(X, W, out):
+        raise ValueError(f"linear_smallk: unsupported shapes X{tuple(X.shape)} W{tuple(W.shape)} out{tuple(out.shape)}")
+    check(_lib.lib().alignn_linear_smallk_f32(X.data_ptr(), X.stride(0), X.size(0), X.size(1), W.data_ptr(),
+                                              W.stride(0), None if bias is None else bias.data_ptr(), W.size(0),
+                                              int(bool(relu)), out.data_ptr(), out.stride(0), stream_ptr()),
+          "alignn_linear_smallk_f32")
+    return out
+
+
+def gemm_tn_smalln(A: torch.Tensor, X: torch.Tensor, C: torch.Tensor, colsum: Optional[torch.Tensor] = None,
+                   accumulate: bool = False) -> torch.Tensor:
+    """C (+)= A^T X and colsum (+)= A.sum(0) in one pass over A [K, M] (X [K, N], N <= 16): the
+    weight and bias gradients of a Linear with few inputs."""
+    K, M = A.shape
+    N = X.size(1)
+    if (A.stride(1) != 1 or X.stride(1) != 1 or C.stride(1) != 1 or X.size(0) != K or tuple(C.shape) != (M, N)
+            or N > SMALLN_MAX or (colsum is not None and (colsum.numel() != M or not colsum.is_contiguous()))):
+        raise ValueError(f"gemm_tn_smalln: unsupported shapes A{tuple(A.shape)} X{tuple(X.shape)} C{tuple(C.shape)}")
+    lib = _lib.lib()
+    need = int(lib.alignn_gemm_tn_smalln_workspace(K, M, N))
+    ws = WS.get("smalln", need, A.device)
+    check(lib.alignn_gemm_tn_smalln_f32(A.data_ptr(), A.stride(0), K, M, X.data_ptr(), X.stride(0), N, C.data_ptr(),
+                                        C.stride(0), None if colsum is None else colsum.data_ptr(), int(accumulate),
+                                        ws.data_ptr(), ws.numel(), stream_ptr()), "alignn_gemm_tn_smalln_f32")
+    return C
+
+
 # ------------------------------------------------------------------------------------------------
 # Graph preparation
 # ------------------------------------------------------------------------------------------------

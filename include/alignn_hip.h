@@ -84,6 +84,26 @@ int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
  * the current device); 0 when no split is used, -1 for invalid shapes. */
 int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
 
+/* ----------------------------------------------------------------------------------------
+ * Skinny products (skinny.hip), streamed at HBM rate: the angle encoder's first Linear over the
+ * T line-graph edges (train.py:358-364 and its autograd backward) — K or N is the 11 raw angle
+ * features.
+ *
+ *   alignn_linear_smallk_f32:  out[r][c] = act(sum_k X[r][k] W[c][k] + bias[c])   (K <= 16,
+ *       N % 4 == 0, out 16-byte aligned with ldo % 4 == 0; otherwise ALIGNN_E_UNSUPPORTED and the
+ *       caller uses alignn_gemm_f32).  relu = 1 applies ReLU.
+ *   alignn_gemm_tn_smalln_f32: C[m][n] (+)= sum_k A[k][m] X[k][n] (N <= 16) and, when colsum is
+ *       not NULL, colsum[m] (+)= sum_k A[k][m]: one pass over A (the weight and bias gradients of
+ *       a Linear from its [K, M] output gradient).  Two fixed-order stages (deterministic);
+ *       workspace floats from alignn_gemm_tn_smalln_workspace.
+ * ---------------------------------------------------------------------------------------- */
+int alignn_linear_smallk_f32(const float* X, int64_t ldx, int64_t M, int32_t K, const float* W, int64_t ldw,
+                             const float* bias, int64_t N, int32_t relu, float* out, int64_t ldo, void* stream);
+int64_t alignn_gemm_tn_smalln_workspace(int64_t K, int64_t M, int32_t N);
+int alignn_gemm_tn_smalln_f32(const float* A, int64_t lda, int64_t K, int64_t M, const float* X, int64_t ldx,
+                              int32_t N, float* C, int64_t ldc, float* colsum, int32_t accumulate, float* workspace,
+                              int64_t workspace_elems, void* stream);
+
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
  * Two-stage, fixed order.  workspace >= 256*N floats. */
 int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
