@@ -9,6 +9,21 @@
 
 namespace alignn {
 
+// Index of this thread's wavefront in its workgroup, as a wave-uniform (SGPR) value.  Plain
+// threadIdx.x >> 6 is uniform per wave64 too, but the compiler's divergence analysis cannot see
+// it: every address derived from it then stays in VGPRs, index loads become vector loads, and the
+// s_waitcnt vmcnt(0) that guards each dependent load also waits for every prefetch in flight
+// (measured in the attention kernels' ISA: one full memory round trip per edge).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
+// Load of a kernel-invariant value at a wave-uniform address through the constant address space,
+// so it is a scalar (s_load) load: its s_waitcnt lgkmcnt does not wait for the vector loads in
+// flight.  Only for arrays no kernel thread writes (CSR offsets, index lists).
+template <typename T>
+__device__ __forceinline__ T sld(const T* p, int64_t i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
 // ---------------------------------------------------------------------------------------------
 // Error handling (no exceptions cross the ABI)
 // ---------------------------------------------------------------------------------------------

@@ -66,7 +66,7 @@ __global__ void csr_fill(const K* __restrict__ keys, int64_t m, int64_t n, int32
 __global__ __launch_bounds__(256) void csr_sort_segments(const int32_t* __restrict__ off, int64_t n,
                                                          int32_t* __restrict__ perm) {
   __shared__ int32_t buf[4][1024];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = wave_id(), lane = threadIdx.x & 63;
   const int64_t seg = blockIdx.x * 4 + wave;
   if (seg >= n) return;
   const int32_t b = off[seg], e = off[seg + 1], len = e - b;

@@ -34,7 +34,7 @@ __global__ void standardize_kernel(const float* __restrict__ Z, int64_t n, int D
 }
 
 __global__ void row_sqnorm_kernel(const float* __restrict__ Zs, int64_t n, int D, float* __restrict__ r) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
   if (row >= n) return;
   float s = 0.f;
   for (int c = threadIdx.x & 63; c < D; c += 64) {
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float* __restrict
                                                          float eps, float alpha, float beta,
                                                          int64_t* __restrict__ nbr, float* __restrict__ w_raw) {
   const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave_id();
   if (q >= rows) return;
   const int64_t i = row0 + q;
   const float ri = r[i];

@@ -51,7 +51,7 @@ template <int VPL>
 __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
   if (row >= p.n) return;
   const int D = p.D, j0 = lane * VPL;
   const bool act = j0 < D;
@@ -122,7 +122,7 @@ template <int VPL>
 __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
   resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wid = blockIdx.x * 4 + wave_id();
   const int D = p.D, j0 = lane * VPL;
   const bool act = j0 < D;
   float w1[VPL], w2[VPL], w3[VPL], g[VPL], bb[VPL];

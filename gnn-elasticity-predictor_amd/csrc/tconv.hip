@@ -159,13 +159,13 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
                                          int64_t d, int wsub, int nw, bool heavy) {
   constexpr int NS = 3 * H + H * VPL + VPL;  // per-lane merge state: m, s, sa, accS, accV
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
+  const int32_t beg = uni(sld(p.off, d)), end = uni(sld(p.off, d + 1));
 
   float accS[H][VPL], accV[VPL];
   float m[H], s[H], sa[H];
@@ -208,8 +208,8 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
       ring[j].xr = 0.f;
       const int32_t t = first + j;
       if (t < end)
-        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[t]),
-                           p.feat_row ? (int64_t)uni(p.feat_row[t]) : t, j0, act, lane);
+        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(sld(p.src_at, t)),
+                           p.feat_row ? (int64_t)uni(sld(p.feat_row, t)) : t, j0, act, lane);
     }
     for (int32_t tb = first; tb < end; tb += stride) {
       if constexpr (KM > 0) enc_group<VPL, KM>(ew, D, j0, ring);
@@ -263,8 +263,8 @@ __device__ __forceinline__ void fwd_node(const FwdParams& p, const EncParams& en
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
         if (tn < end)
-          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[tn]),
-                             p.feat_row ? (int64_t)uni(p.feat_row[tn]) : tn, j0, act, lane);
+          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(sld(p.src_at, tn)),
+                             p.feat_row ? (int64_t)uni(sld(p.feat_row, tn)) : tn, j0, act, lane);
       }
     }
   }
@@ -351,7 +351,7 @@ __global__ TCONV_ATTR void tconv_fwd_kernel(FwdParams p, Sched sc, EncParams en)
   constexpr int ENCW = KM > 0 ? (KM + 1) * 64 * VPL : 0;
   __shared__ float smem[MERGE + ENCW];
   float* ew = smem + MERGE;
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int64_t items = sc.items();
   bool staged = false;
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
@@ -372,10 +372,10 @@ __global__ TCONV_ATTR void tconv_fwd_kernel(FwdParams p, Sched sc, EncParams en)
       }
     }
     if (it < sc.n_heavy) {
-      fwd_node<VPL, H, KM>(p, en, ew, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true);
+      fwd_node<VPL, H, KM>(p, en, ew, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) fwd_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false);
+      if (i < sc.n_light) fwd_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
     }
   }
 }
@@ -422,13 +422,13 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
                                              EncAcc<VPL, KM>& ea) {
   constexpr int NS = H + H * VPL + VPL;  // per-lane merge state: sigz, Sz, dq
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
+  const int32_t beg = uni(sld(p.off, d)), end = uni(sld(p.off, d + 1));
   const bool do_dF = KM == 0 && p.dF != nullptr;
 
   float sz[H][VPL], sgz[H], dqa[VPL];
@@ -491,8 +491,8 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
       const int32_t t = first + j;
       rows[j] = 0;
       if (t < end) {
-        rows[j] = p.feat_row ? uni(p.feat_row[t]) : t;
-        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[t]), rows[j], j0, act, lane);
+        rows[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
+        load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(sld(p.src_at, t)), rows[j], j0, act, lane);
         if constexpr (KM == 0)
           if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
       }
@@ -572,8 +572,8 @@ __device__ __forceinline__ void bwd_dst_node(const BwdDstParams& p, const EncPar
         }
         const int32_t tn = tb + stride + j;
         if (tn < end) {
-          rows[j] = p.feat_row ? uni(p.feat_row[tn]) : tn;
-          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(p.src_at[tn]), rows[j], j0, act,
+          rows[j] = p.feat_row ? uni(sld(p.feat_row, tn)) : tn;
+          load_edge<VPL, KM>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, en, (int64_t)uni(sld(p.src_at, tn)), rows[j], j0, act,
                              lane);
           if constexpr (KM == 0)
             if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows[j] * p.lddf + j0, old[j]);
@@ -628,7 +628,7 @@ __global__ TCONV_ATTR void tconv_bwd_dst_kernel(BwdDstParams p, Sched sc, EncPar
   __shared__ float smem[MERGE + ENCW];
   float* ew = smem + MERGE;
   if constexpr (KM > 0) stage_enc<VPL, KM>(ew, en, p.D);
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int lane = threadIdx.x & 63;
   EncAcc<VPL, KM> ea;
   if constexpr (KM > 0) {
@@ -639,11 +639,11 @@ __global__ TCONV_ATTR void tconv_bwd_dst_kernel(BwdDstParams p, Sched sc, EncPar
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      bwd_dst_node<VPL, H, KM>(p, en, ew, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true, ea);
+      bwd_dst_node<VPL, H, KM>(p, en, ew, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true, ea);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
       if (i < sc.n_light)
-        bwd_dst_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false, ea);
+        bwd_dst_node<VPL, H, KM>(p, en, ew, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false, ea);
     }
   }
   if constexpr (KM > 0) {
@@ -768,14 +768,14 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
   constexpr int NS = 3 * H + H * VPL + VPL;
   constexpr int RS = 64 * VPL;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int row = lane >> 4;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
+  const int32_t beg = uni(sld(p.off, d)), end = uni(sld(p.off, d + 1));
   float* uv = smem + wave * H * RS;  // this wave's copy of u[h]
 
   float accS[H][VPL], accV[VPL];
@@ -822,8 +822,8 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
       ring[j].xr = 0.f;
       const int32_t t = first + j;
       if (t < end)
-        load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[t]),
-                          p.feat_row ? (int64_t)uni(p.feat_row[t]) : t, j0, act, lane);
+        load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(sld(p.src_at, t)),
+                          p.feat_row ? (int64_t)uni(sld(p.feat_row, t)) : t, j0, act, lane);
     }
     for (int32_t tb = first; tb < end; tb += stride) {
       asm volatile("" ::: "memory");  // keep the u reads in the loop (registers are the point)
@@ -881,8 +881,8 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
         if (tn < end)
-          load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[tn]),
-                            p.feat_row ? (int64_t)uni(p.feat_row[tn]) : tn, j0, act, lane);
+          load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(sld(p.src_at, tn)),
+                            p.feat_row ? (int64_t)uni(sld(p.feat_row, tn)) : tn, j0, act, lane);
       }
     }
   }
@@ -966,14 +966,14 @@ template <int VPL, int H>
 __global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
   resolve_drop(p.drop);
   __shared__ float smem[fwd2_lds_floats<VPL, H>()];
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      fwd2_node<VPL, H>(p, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true);
+      fwd2_node<VPL, H>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) fwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false);
+      if (i < sc.n_light) fwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
     }
   }
 }
@@ -987,14 +987,14 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
   constexpr int NS = H + H * VPL + VPL;
   constexpr int RS = 64 * VPL;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int row = lane >> 4;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
   const bool act = j0 < D;
   const int hl = act ? j0 / C : 0;
   const float scale = 1.0f / sqrtf((float)C);
-  const int32_t beg = uni(p.off[d]), end = uni(p.off[d + 1]);
+  const int32_t beg = uni(sld(p.off, d)), end = uni(sld(p.off, d + 1));
   float* uv = smem + wave * 2 * H * RS;  // this wave's u[h] (h < H) and Vd[h] (H + h)
   const bool do_dF = p.dF != nullptr;
 
@@ -1057,8 +1057,8 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
       const int32_t t = first + j;
       rows_[j] = 0;
       if (t < end) {
-        rows_[j] = p.feat_row ? uni(p.feat_row[t]) : t;
-        load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[t]), rows_[j], j0, act,
+        rows_[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
+        load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(sld(p.src_at, t)), rows_[j], j0, act,
                           lane);
         if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
       }
@@ -1155,8 +1155,8 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
         const int32_t tn = tb + stride + j;
         vzero(old[j]);
         if (tn < end) {
-          rows_[j] = p.feat_row ? uni(p.feat_row[tn]) : tn;
-          load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(p.src_at[tn]), rows_[j], j0,
+          rows_[j] = p.feat_row ? uni(sld(p.feat_row, tn)) : tn;
+          load_edge<VPL, 0>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(sld(p.src_at, tn)), rows_[j], j0,
                             act, lane);
           if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
         }
@@ -1204,14 +1204,14 @@ template <int VPL, int H>
 __global__ TCONV_ATTR void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
   resolve_drop(p.drop);
   __shared__ float smem[bwd2_lds_floats<VPL, H>()];
-  const int wave = threadIdx.x >> 6;
+  const int wave = wave_id();
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      bwd2_node<VPL, H>(p, smem, (int64_t)uni(sc.heavy[it]), wave, 4, true);
+      bwd2_node<VPL, H>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) bwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sc.light[i]) : i, 0, 1, false);
+      if (i < sc.n_light) bwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
     }
   }
 }
@@ -1235,7 +1235,7 @@ struct BwdSrcParams {
 template <int VPL, int H>
 __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
   const int lane = threadIdx.x & 63;
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
   if (s >= p.n) return;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
   float dk[VPL], dv[VPL];
   vzero(dk);
   vzero(dv);
-  const int32_t beg = p.off_src[s], end = p.off_src[s + 1];
+  const int32_t beg = sld(p.off_src, s), end = sld(p.off_src, s + 1);
   if (act) {
     for (int32_t ib = beg; ib < end; ib += PF) {
       float qv[PF][VPL], gv[PF][VPL], dz[PF], al[PF];
@@ -1255,8 +1255,8 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
         dz[j] = 0.f;
         al[j] = 0.f;
         if (ib + j < end) {
-          const int64_t pos = p.pos_src[ib + j];
-          const int64_t dd = p.dst_at[pos];
+          const int64_t pos = sld(p.pos_src, ib + j);
+          const int64_t dd = sld(p.dst_at, pos);
           dz[j] = p.dz_e[pos * H + hl];
           al[j] = p.alpha_e[pos * H + hl];
           vload(p.QKVR + dd * p.ldq + j0, qv[j]);
