@@ -171,6 +171,7 @@ class BatchCache:
         gc = ops.GraphCSR(cmap[edge_index], na)
         gc.rows = rows.to(torch.int32)
         gc.n_full = n
+        gc.cmap = cmap.to(torch.int32)
         return gc
 
 
@@ -233,9 +234,12 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
 
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
-                  seed_blk: int, enc: Optional[ops.EdgeEncoder] = None, side: Optional[torch.cuda.Stream] = None):
+                  seed_blk: int, enc: Optional[ops.EdgeEncoder] = None, side: Optional[torch.cuda.Stream] = None,
+                  compact_gate: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     enc: edge features recomputed in-kernel from raw inputs (then F is None).
+    compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
+    (no zero-filled [n, D] copy; the backward writes the compacted dout directly).
 
     Compacted graphs (g.rows set: the graph's nodes are the active subset ``rows`` of X's rows, see
     BatchCache): Q/K/V, the attention and its per-node GEMMs run over the active rows only; the
@@ -277,8 +281,11 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     else:
         ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp_a.view(na, H, C).transpose(0, 1),
                  beta=1.0)
+    c.outp_rows = None
     if rows is None:
         c.outp = c.outp_a
+    elif compact_gate:
+        c.outp, c.outp_rows = c.outp_a, g.cmap
     else:
         c.outp = torch.zeros(n, D, device=dev)
         ops.scatter_rows(c.outp_a, rows, c.outp)
@@ -288,7 +295,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.beta = torch.empty(n, device=dev)
     c.mu = torch.empty(n, device=dev)
     c.rstd = torch.empty(n, device=dev)
-    ops.gate_ln_fwd(c.outp, c.R, cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop, seed_blk)
+    ops.gate_ln_fwd(c.outp, c.R, cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop, seed_blk,
+                    outp_rows=c.outp_rows)
     c.p, c.seed_att, c.seed_blk, c.H, c.with_proj = p_drop, seed_att, seed_blk, H, with_proj
     return X_new, c
 
@@ -312,7 +320,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     m = g.m
     rows = c.rows
     na = n if rows is None else g.n
-    dout = torch.empty(n, D, device=dev)
+    dout = torch.empty(n if c.outp_rows is None else na, D, device=dev)
     if rows is None:
         dQKVR = torch.empty(n, 4 * D, device=dev)
         dQKV, dR = dQKVR[:, :3 * D], dQKVR[:, 3 * D:]
@@ -320,8 +328,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         dQKV = torch.empty(na, 3 * D, device=dev)
         dR = torch.empty(n, D, device=dev)
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
-                    gv.lnb, c.p, c.seed_blk)
-    dout_a = dout if rows is None else ops.gather_rows(dout, rows)
+                    gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows)
+    dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
     Vd = torch.empty(na, H, D, device=dev)
     ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
     Sz = torch.empty(na, H, D, device=dev)
@@ -420,6 +428,9 @@ class AlignnEngine:
         # the angle encoder's first Linear (11 inputs, T rows) and its weight/bias gradients as
         # streamed HBM-rate kernels (skinny.hip) instead of MFMA tiles (off until measured)
         self.skinny_encoder = False
+        # line blocks on compacted graphs: gate/LayerNorm read the compacted conv output through the
+        # row map instead of a zero-filled full copy (off until measured)
+        self.compact_gate = False
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -503,7 +514,7 @@ class AlignnEngine:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), enc=ctx.angle_enc,
-                                     side=side)
+                                     side=side, compact_gate=self.compact_gate)
             else:
                 c = None
             ctx.edge.append(c)

@@ -237,7 +237,7 @@ class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
     __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
-                 "n_full")
+                 "n_full", "cmap")
 
     HEAVY_THRESHOLD = 32  # in-degree above which a target node gets a 4-wave workgroup
     COMPACT_REGS = False  # attention kernel variant with row-distributed softmax state (opt-in)
@@ -260,6 +260,7 @@ class GraphCSR:
         self._sched = None
         self.rows = None     # compacted graph: int32 ids of its nodes in the full node set
         self.n_full = n
+        self.cmap = None     # compacted graph: int32 [n_full] full row -> node id, -1 if inactive
         ws = WS.get("graph", 2 * n + 64, dev, torch.int32)
         check(_lib.lib().alignn_graph_prep(ei.data_ptr(), m, n, self.off_dst.data_ptr(), self.perm_dst.data_ptr(),
                                            self.src_at.data_ptr(), self.dst_at.data_ptr(), self.off_src.data_ptr(),
@@ -450,23 +451,41 @@ def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):
 # ------------------------------------------------------------------------------------------------
 # Row ops
 # ------------------------------------------------------------------------------------------------
-def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed):
-    n, D = outp.shape
-    check(_lib.lib().alignn_gate_ln_fwd(n, D, outp.data_ptr(), R.data_ptr(), R.stride(0), wbeta.data_ptr(),
-                                        X.data_ptr(), X.stride(0), ln_w.data_ptr(), ln_b.data_ptr(), Xnew.data_ptr(),
-                                        Xnew.stride(0), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),
-                                        float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_gate_ln_fwd")
+def _check_outp_rows(outp, outp_rows, n):
+    if outp_rows is None:
+        if outp.size(0) != n:
+            raise ValueError(f"gate_ln: outp has {outp.size(0)} rows, expected {n}")
+        return None
+    if outp_rows.dtype != torch.int32 or outp_rows.numel() != n or not outp_rows.is_contiguous():
+        raise ValueError("gate_ln: outp_rows must be contiguous int32 with one entry per row")
+    return outp_rows.data_ptr()
 
 
-def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_wbeta, d_ln_w, d_ln_b, drop_p, seed):
-    n, D = outp.shape
+def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed, outp_rows=None):
+    """outp_rows (int32 [n], -1 = zero row): o of row r is outp[outp_rows[r]] (compacted conv output)."""
+    n, D = X.shape
+    rp = _check_outp_rows(outp, outp_rows, n)
+    check(_lib.lib().alignn_gate_ln_fwd_rows(n, D, outp.data_ptr(), rp, R.data_ptr(), R.stride(0), wbeta.data_ptr(),
+                                             X.data_ptr(), X.stride(0), ln_w.data_ptr(), ln_b.data_ptr(),
+                                             Xnew.data_ptr(), Xnew.stride(0), beta.data_ptr(), mu.data_ptr(),
+                                             rstd.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+          "alignn_gate_ln_fwd")
+
+
+def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_wbeta, d_ln_w, d_ln_b, drop_p, seed,
+                outp_rows=None):
+    """outp_rows: as in gate_ln_fwd; dout then has outp's (compacted) rows and only those are written."""
+    n, D = R.shape
+    rp = _check_outp_rows(outp, outp_rows, n)
+    if dout.shape != outp.shape:
+        raise ValueError("gate_ln_bwd: dout must have outp's shape")
     ws = WS.get("gate_ln", 1024 * 5 * D, outp.device)
-    check(_lib.lib().alignn_gate_ln_bwd(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), R.data_ptr(),
-                                        R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
-                                        beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(), dout.data_ptr(),
-                                        dR.data_ptr(), dR.stride(0), d_wbeta.data_ptr(), d_ln_w.data_ptr(),
-                                        d_ln_b.data_ptr(), ws.data_ptr(), float(drop_p), int(seed) & (2**64 - 1),
-                                        stream_ptr()), "alignn_gate_ln_bwd")
+    check(_lib.lib().alignn_gate_ln_bwd_rows(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), rp,
+                                             R.data_ptr(), R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(),
+                                             ln_b.data_ptr(), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),
+                                             dout.data_ptr(), dR.data_ptr(), dR.stride(0), d_wbeta.data_ptr(),
+                                             d_ln_w.data_ptr(), d_ln_b.data_ptr(), ws.data_ptr(), float(drop_p),
+                                             int(seed) & (2**64 - 1), stream_ptr()), "alignn_gate_ln_bwd")
 
 
 def readout_feats_fwd(h, ptr, global_x, gdim, sg, sgdim, feats, drop_p, seed):

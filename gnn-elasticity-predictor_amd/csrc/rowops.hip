@@ -45,6 +45,7 @@ struct GateFwdParams {
   float* Xn; int64_t ldxn;
   float* beta; float* mu; float* rstd;
   DropParams drop;
+  const int32_t* orow;  // optional: row r of o is outp[orow[r]] (-1: o = 0) — compacted conv outputs
 };
 
 template <int VPL>
@@ -57,8 +58,9 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   const bool act = j0 < D;
   float o[VPL], r[VPL], w1[VPL], w2[VPL], w3[VPL];
   vzero(o); vzero(r); vzero(w1); vzero(w2); vzero(w3);
+  const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
   if (act) {
-    vload(p.outp + row * D + j0, o);
+    if (orow >= 0) vload(p.outp + orow * D + j0, o);
     vload(p.R + row * p.ldr + j0, r);
     vload(p.wbeta + j0, w1);
     vload(p.wbeta + D + j0, w2);
@@ -116,6 +118,7 @@ struct GateBwdParams {
   float* part;  // [nwaves][5*D]
   int nwaves;
   DropParams drop;
+  const int32_t* orow;  // optional: o and dout rows through this map (-1: o = 0, dout not written)
 };
 
 template <int VPL>
@@ -139,8 +142,9 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
   for (int64_t row = wid; row < p.n; row += p.nwaves) {
     float o[VPL], r[VPL], gx[VPL];
     vzero(o); vzero(r); vzero(gx);
+    const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
     if (act) {
-      vload(p.outp + row * D + j0, o);
+      if (orow >= 0) vload(p.outp + orow * D + j0, o);
       vload(p.R + row * p.ldr + j0, r);
       vload(p.dXn + row * p.lddx + j0, gx);
     }
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
         a_w2[i] = fmaf(dl, r[i], a_w2[i]);
         a_w3[i] = fmaf(dl, o[i] - r[i], a_w3[i]);
       }
-      vstore(p.dout + row * D + j0, dov);
+      if (orow >= 0) vstore(p.dout + orow * D + j0, dov);
       vstore(p.dR + row * p.lddr + j0, drv);
     }
   }
@@ -326,17 +330,18 @@ using namespace alignn;
 extern "C" int alignn_version(void) { return 1; }
 extern "C" const char* alignn_last_error(void) { return g_err; }
 
-extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const float* R, int64_t ldr,
-                                  const float* wbeta, const float* X, int64_t ldx, const float* ln_w,
-                                  const float* ln_b, float* Xnew, int64_t ldxn, float* beta, float* mu, float* rstd,
-                                  float drop_p, uint64_t seed, void* stream) {
+extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
+                                       const float* R, int64_t ldr, const float* wbeta, const float* X, int64_t ldx,
+                                       const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, float* beta,
+                                       float* mu, float* rstd, float drop_p, uint64_t seed, void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_fwd: unsupported hidden %d", D);
     return ALIGNN_E_UNSUPPORTED;
   }
   if (n == 0) return ALIGNN_OK;
-  GateFwdParams p{n, D, outp, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd, make_drop(drop_p, seed)};
+  GateFwdParams p{n, D, outp, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd, make_drop(drop_p, seed),
+                  outp_rows};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((n + 3) / 4));
   switch (vpl) {
@@ -349,11 +354,20 @@ extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const
   return ALIGNN_OK;
 }
 
-extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
-                                  const float* R, int64_t ldr, const float* wbeta, const float* ln_w, const float* ln_b,
-                                  const float* beta, const float* mu, const float* rstd, float* dout, float* dR,
-                                  int64_t lddr, float* d_wbeta, float* d_ln_w, float* d_ln_b, float* workspace,
+extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const float* R, int64_t ldr,
+                                  const float* wbeta, const float* X, int64_t ldx, const float* ln_w,
+                                  const float* ln_b, float* Xnew, int64_t ldxn, float* beta, float* mu, float* rstd,
                                   float drop_p, uint64_t seed, void* stream) {
+  return alignn_gate_ln_fwd_rows(n, D, outp, nullptr, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd,
+                                 drop_p, seed, stream);
+}
+
+extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                       const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
+                                       const float* ln_w, const float* ln_b, const float* beta, const float* mu,
+                                       const float* rstd, float* dout, float* dR, int64_t lddr, float* d_wbeta,
+                                       float* d_ln_w, float* d_ln_b, float* workspace, float drop_p, uint64_t seed,
+                                       void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_bwd: unsupported hidden %d", D);
@@ -362,7 +376,7 @@ extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int6
   if (n == 0) return ALIGNN_OK;
   const int nwaves = (int)std::min<int64_t>(1024, n);
   GateBwdParams p{n, D, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
-                  nwaves, make_drop(drop_p, seed)};
+                  nwaves, make_drop(drop_p, seed), outp_rows};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
   switch (vpl) {
@@ -388,6 +402,15 @@ extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int6
   }
   ALIGNN_LAUNCH_CHECK("gate_ln param-grad reduction");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                  const float* R, int64_t ldr, const float* wbeta, const float* ln_w, const float* ln_b,
+                                  const float* beta, const float* mu, const float* rstd, float* dout, float* dR,
+                                  int64_t lddr, float* d_wbeta, float* d_ln_w, float* d_ln_b, float* workspace,
+                                  float drop_p, uint64_t seed, void* stream) {
+  return alignn_gate_ln_bwd_rows(n, D, dXnew, lddx, outp, nullptr, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR,
+                                 lddr, d_wbeta, d_ln_w, d_ln_b, workspace, drop_p, seed, stream);
 }
 
 extern "C" int alignn_readout_feats_fwd(int64_t B, int32_t D, const float* h, const int64_t* ptr, const float* global_x,

@@ -239,6 +239,20 @@ int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int64_t lddx, c
                        float* dout, float* dR, int64_t lddr, float* d_wbeta, float* d_ln_w, float* d_ln_b,
                        float* workspace, float drop_p, uint64_t seed, void* stream);
 
+/* Compacted conv outputs (the line graph's active bonds): o of row r is
+ * outp[outp_rows[r]] (outp_rows[r] = -1: o = 0, the exact output of a node without in-edges), and
+ * the backward writes dout only at the compacted rows — no zero-filled [n, D] copy of o and no
+ * [n, D] dout to gather from.  outp_rows = NULL is the plain entry above. */
+int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows, const float* R,
+                            int64_t ldr, const float* wbeta, const float* X, int64_t ldx, const float* ln_w,
+                            const float* ln_b, float* Xnew, int64_t ldxn, float* beta, float* mu, float* rstd,
+                            float drop_p, uint64_t seed, void* stream);
+int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                            const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
+                            const float* ln_w, const float* ln_b, const float* beta, const float* mu,
+                            const float* rstd, float* dout, float* dR, int64_t lddr, float* d_wbeta, float* d_ln_w,
+                            float* d_ln_b, float* workspace, float drop_p, uint64_t seed, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Readout (train.py:562-586): global_mean_pool over ptr (PyG, train.py:562), concat with
  * global_x / sg_one_hot (train.py:563-572), dropout (train.py:573).

@@ -221,3 +221,17 @@ def test_compact_register_kernels_full_model_vs_oracle(lg_offset):
         ops.GraphCSR.COMPACT_REGS = False
     assert _rel(mean.detach().cpu(), rmean) < 1e-4
     assert _rel(logvar.detach().cpu(), rlogvar) < 1e-4
+
+
+def test_compact_gate_is_bitwise_neutral():
+    """Line blocks on the compacted graph with the gate reading the compacted conv output through
+    the row map (engine.compact_gate): same bits as the zero-filled full copy + gather."""
+    _, tr1, b1 = _setup()
+    _, tr2, b2 = _setup()
+    tr2.model._engine.compact_gate = True
+    l1 = tr1.forward_backward(b1, 11)
+    l2 = tr2.forward_backward(b2, 11)
+    torch.cuda.synchronize()
+    assert b1._alignn_cache.lg.cmap is not None      # the B=4 batch is compacted (PyG offset rule)
+    assert torch.equal(l1, l2)
+    assert torch.equal(tr1.st.grad, tr2.st.grad)
