@@ -58,7 +58,32 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="replay the step as HIP graphs (ROCm disallows external event nodes, so the roofline "
                         "probe then runs in 2 eager steps after the timed region)")
+    p.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
+                   help="engine option (engine.<attr>=0/1), trainer optimizer (optimizer=hip) or GEMM stage "
+                        "(gemm_stage=16|32|64); repeatable — for measuring opt-in paths")
     return p.parse_args()
+
+
+def apply_settings(args, model):
+    """--set KEY=VAL: opt-in engine paths for A/B measurement; returns the trainer kwargs."""
+    from alignn_mi355x import ops
+    kw = {}
+    for item in args.set:
+        k, v = item.split("=", 1)
+        if k.startswith("engine."):
+            attr = k.split(".", 1)[1]
+            if not hasattr(model._engine, attr):
+                raise ValueError(f"unknown engine option {attr}")
+            setattr(model._engine, attr, bool(int(v)))
+        elif k == "gemm_stage":
+            ops.GEMM_STAGE = {"16": 0, "32": 16, "64": 128}[v]
+        elif k == "compact_regs":
+            ops.GraphCSR.COMPACT_REGS = bool(int(v))
+        elif k == "optimizer":
+            kw["optimizer"] = v
+        else:
+            raise ValueError(f"unknown --set key {k}")
+    return kw
 
 
 def cpu_baseline(args, B):
@@ -155,7 +180,7 @@ def main():
     torch.manual_seed(1234)  # identical initial weights on every rank
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                       args.dropout), 2).to(dev)
-    trainer = A.FusedTrainer(model, precision=args.precision)
+    trainer = A.FusedTrainer(model, precision=args.precision, **apply_settings(args, model))
     mfma_peak = BF16_MFMA_TFLOPS if args.precision == "bf16" else FP32_MFMA_TFLOPS
     batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=args.lg_offset).to(dev)
     if world > 1:
@@ -276,7 +301,8 @@ def main():
             "config": {"workload": f"B={B} synthetic MP-like graphs per GPU (60 atoms/720 bonds/7920 triplets), "
                                    f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
-                       "dropout": args.dropout, "launch": launch_mode, "precision": args.precision},
+                       "dropout": args.dropout, "launch": launch_mode, "precision": args.precision,
+                       **({"settings": args.set} if args.set else {})},
             "roofline": roof, "cpu_baseline": cpu, "e2e": e2e,
             # whole-step view: this formulation's GEMM flops and attention bytes per
             # graph and the fraction of the fp32 MFMA / HBM peaks they imply at the measured rate

@@ -419,18 +419,18 @@ class AlignnEngine:
         # weight-gradient products on a second stream, overlapping the next block's attention
         self.overlap = True
         # forward: the line blocks' skip projection on the second stream beside the attention
-        # (off by default until measured on MI355X)
-        self.overlap_forward = False
+        # (measured +1.2 % graphs/s on MI355X, profiles/r01/v7_sweep.log)
+        self.overlap_forward = True
         # GEMM arithmetic: "fp32" (the reference's CPU path; exact fp32 MFMA) or "bf16" (bf16 MFMA
         # inputs, fp32 accumulation — the reference's CUDA autocast);
         # attention, softmax, LayerNorm and all storage stay fp32 either way
         self.precision = "fp32"
         # the angle encoder's first Linear (11 inputs, T rows) and its weight/bias gradients as
-        # streamed HBM-rate kernels (skinny.hip) instead of MFMA tiles (off until measured)
-        self.skinny_encoder = False
+        # streamed HBM-rate kernels (skinny.hip) instead of MFMA tiles (+3.2 %, v7_sweep.log)
+        self.skinny_encoder = True
         # line blocks on compacted graphs: gate/LayerNorm read the compacted conv output through the
-        # row map instead of a zero-filled full copy (off until measured)
-        self.compact_gate = False
+        # row map instead of a zero-filled full copy (+1.2 %, v7_sweep.log)
+        self.compact_gate = True
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden

@@ -25,7 +25,7 @@ class FusedTrainer:
                  feature_jitter_std: float = 0.1, min_logvar_floor: float = MIN_LOGVAR_FLOOR,
                  target_log_means: Sequence[float] = TARGET_LOG_MEANS,
                  target_log_stds: Sequence[float] = TARGET_LOG_STDS, fused_adamw: bool = True,
-                 optimizer: str = "torch", precision: Optional[str] = None):
+                 optimizer: str = "hip", precision: Optional[str] = None):
         self.model = model
         if precision is not None:
             model.set_precision(precision)

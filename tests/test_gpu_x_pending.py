@@ -14,8 +14,12 @@ def _ops():
 
 
 def _rel(a, b):
+    """Max-abs difference relative to max |b|; equal entries (incl. matching -inf softmax maxima
+    of zero in-degree targets) count as 0."""
     a, b = a.double(), b.double()
-    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+    d = torch.where(a == b, torch.zeros_like(a), a - b)
+    fin = b[torch.isfinite(b)]
+    return float(d.abs().max() / (fin.abs().max() if fin.numel() else torch.tensor(1.0)).clamp(min=1e-30))
 
 
 def _setup(seed=0):
@@ -59,6 +63,7 @@ def test_forward_side_stream_is_bitwise_neutral():
     """The line blocks' skip projection on the side stream (overlap_forward) changes no bits."""
     _, tr1, b1 = _setup()
     _, tr2, b2 = _setup()
+    tr1.model._engine.overlap_forward = False
     tr2.model._engine.overlap_forward = True
     l1 = tr1.forward_backward(b1, 9)
     l2 = tr2.forward_backward(b2, 9)
@@ -93,7 +98,13 @@ def test_hip_clip_adamw_matches_torch():
         assert abs(float(norm) - float(g.double().norm())) < 1e-5 * float(g.double().norm())
         ops.adamw_step(p, gg, m, v, split, 3e-4, 1e-4, 1e-4, norm=norm, max_norm=5.0, step=step)
         assert _rel(gg, torch.cat([pa.grad, pb.grad])) < 1e-6, it
-        assert _rel(p - p0, torch.cat([pa.detach(), pb.detach()]) - p0) < 1e-4, it
+        # parameters: both sides round p in fp32, so allow 2 ulp of |p| on top of 1e-4 of the update
+        pt = torch.cat([pa.detach(), pb.detach()])
+        tol = 1e-4 * (pt - p0).abs().max() + 2 * torch.finfo(torch.float32).eps * p.abs()
+        assert bool(((p - pt).abs() <= tol).all()), (it, float((p - pt).abs().max()))
+        mt = torch.cat([opt.state[pa]["exp_avg"], opt.state[pb]["exp_avg"]])
+        vt = torch.cat([opt.state[pa]["exp_avg_sq"], opt.state[pb]["exp_avg_sq"]])
+        assert _rel(m, mt) < 1e-5 and _rel(v, vt) < 1e-5, it
     assert float(step) == 3.0
 
 
@@ -164,6 +175,7 @@ def _run_tconv(csr, m, t, D, H, drop, compact):
     ops = _ops()
     n = csr.n
     csr._sched = None
+    prev = ops.GraphCSR.COMPACT_REGS
     ops.GraphCSR.COMPACT_REGS = compact
     try:
         outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
@@ -177,7 +189,7 @@ def _run_tconv(csr, m, t, D, H, drop, compact):
         ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], t["feat_row"], t["dout"], outp,
                           mstat, den, dq, Sz, sigz, dz, al, dF, 3, drop, 77)
     finally:
-        ops.GraphCSR.COMPACT_REGS = False
+        ops.GraphCSR.COMPACT_REGS = prev
         csr._sched = None
     torch.cuda.synchronize()
     return dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz[:m], al=al[:m],
@@ -213,12 +225,13 @@ def test_compact_register_kernels_full_model_vs_oracle(lg_offset):
         setattr(ref_b, k, getattr(ref_b, k).double())
     ref_b.num_graphs = 3
     rmean, rlogvar = model_ref.hetero_forward(st, ref_b, 4)
+    prev = ops.GraphCSR.COMPACT_REGS
     ops.GraphCSR.COMPACT_REGS = True
     try:
         model.to(DEV)
         mean, logvar = model(cpu_batch.to(DEV))
     finally:
-        ops.GraphCSR.COMPACT_REGS = False
+        ops.GraphCSR.COMPACT_REGS = prev
     assert _rel(mean.detach().cpu(), rmean) < 1e-4
     assert _rel(logvar.detach().cpu(), rlogvar) < 1e-4
 
@@ -228,6 +241,7 @@ def test_compact_gate_is_bitwise_neutral():
     the row map (engine.compact_gate): same bits as the zero-filled full copy + gather."""
     _, tr1, b1 = _setup()
     _, tr2, b2 = _setup()
+    tr1.model._engine.compact_gate = False
     tr2.model._engine.compact_gate = True
     l1 = tr1.forward_backward(b1, 11)
     l2 = tr2.forward_backward(b2, 11)
