@@ -55,6 +55,18 @@ class EdgeEncoder(ctypes.Structure):
                 ("workspace", c_vp), ("workspace_elems", c_i64)]
 
 
+ENCBWD_MAX_LAYERS = 8
+
+
+class EncBwdArgs(ctypes.Structure):
+    _fields_ = [("n", c_i64), ("T", c_i64), ("D", c_i32), ("H", c_i32), ("L", c_i32), ("kin", c_i32),
+                ("dst_at", c_vp), ("x", c_vp), ("ldx", c_i64), ("w1", c_vp), ("b1", c_vp),
+                ("U", c_vp * ENCBWD_MAX_LAYERS), ("Vd", c_vp * ENCBWD_MAX_LAYERS),
+                ("dz", c_vp * ENCBWD_MAX_LAYERS), ("alpha", c_vp * ENCBWD_MAX_LAYERS),
+                ("dW1", c_vp), ("db1", c_vp), ("accumulate", c_i32),
+                ("workspace", c_vp), ("workspace_elems", c_i64)]
+
+
 _SIGNATURES = {
     "alignn_version": ([], c_i32),
     "alignn_last_error": ([], ctypes.c_char_p),
@@ -106,6 +118,8 @@ _SIGNATURES = {
     "alignn_gemm_tn_smalln_workspace": ([c_i64, c_i64, c_i32], c_i64),
     "alignn_gemm_tn_smalln_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp,
                                    c_i64, c_vp], c_i32),
+    "alignn_enc_bwd_workspace": ([c_i32, c_i32], c_i64),
+    "alignn_enc_bwd_f32": ([ctypes.POINTER(EncBwdArgs), c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_f32,
                           c_vp, c_vp], c_i32),
 }

@@ -304,7 +304,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, enc_grads=None,
-                   side: Optional[torch.cuda.Stream] = None) -> None:
+                   side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -312,7 +312,9 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     With an in-kernel edge encoder (c.enc), enc_grads = (dW1, db1) receive its gradients (+=).
     side: a second stream for the weight-gradient products (dM, dw̄, dW, db), which nothing
     downstream in the backward reads; they overlap the next block's latency-bound attention.  The
-    caller joins the side stream before reading those gradients."""
+    caller joins the side stream before reading those gradients.
+    keep_edge_scalars: leave (Vd, dz_e, alpha_e) on ``c.edge_scalars`` for the deferred angle-encoder
+    backward (ops.enc_bwd; then dF is None)."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -343,6 +345,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
                       dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
     ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
+    if keep_edge_scalars:
+        c.edge_scalars = (Vd, dz_e, al_e)
     Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
     Oh = dout_a.view(na, H, C).permute(1, 2, 0)
     dQv = dQKV[:, :D].view(na, H, C).transpose(0, 1)
@@ -431,6 +435,9 @@ class AlignnEngine:
         # line blocks on compacted graphs: gate/LayerNorm read the compacted conv output through the
         # row map instead of a zero-filled full copy (+1.2 %, v7_sweep.log)
         self.compact_gate = True
+        # angle encoder backward deferred to one pass after the last line block (ops.enc_bwd): the
+        # line convs leave per-edge scalars instead of read-modify-writing a [T, D] gradient per layer
+        self.defer_angle_bwd = False  # on once measured on MI355X
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -595,7 +602,9 @@ class AlignnEngine:
         dh = torch.empty(N, D, device=dev)
         ops.readout_pool_bwd(dfeats, bc.ptr, bc.batch_vec, dh, False, p_drop, site_seed(seed, 4 * L))
         de = torch.zeros(E, D, device=dev)
-        da = torch.empty(T, D, device=dev) if (T > 0 and ctx.angle_enc is None) else None
+        defer = (self.defer_angle_bwd and ctx.has_angle and ctx.angle_enc is None and T > 0 and E > 0 and L > 0
+                 and ops.enc_bwd_ok(D, cfg.heads, L, bc.xa.size(1)))
+        da = torch.empty(T, D, device=dev) if (T > 0 and ctx.angle_enc is None and not defer) else None
         enc_grads = (G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias")) if ctx.angle_enc is not None else None
         da_written = False
         if E > 0 and L > 0:
@@ -621,7 +630,7 @@ class AlignnEngine:
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
-                                   enc_grads=enc_grads, side=side)
+                                   enc_grads=enc_grads, side=side, keep_edge_scalars=defer)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side)
                 da_written = True
@@ -629,13 +638,19 @@ class AlignnEngine:
             self.debug["de0"] = de.clone()
         # projection chain rules and the angle encoder's first layer: side stream (after the
         # per-layer dM/dw̄ there), overlapping the edge/node encoder backward below
-        with _side_work(side, (da,)):
+        kept = [t for c in ctx.edge for t in (c.U, *c.edge_scalars)] if defer else []
+        with _side_work(side, (da, *kept)):
             if E > 0 and L > 0:
                 proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
             if line_proj:
                 proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all,
                                   dwl_all, G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
-            if ctx.has_angle and da_written and ctx.angle_enc is None:
+            if defer:
+                ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
+                            [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
+                            [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
+                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
+            elif ctx.has_angle and da_written and ctx.angle_enc is None:
                 # da is the masked hidden-layer gradient
                 if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLN_MAX:
                     ops.gemm_tn_smalln(da, bc.xa, G.enc("angle", 0, "weight"), colsum=G.enc("angle", 0, "bias"))

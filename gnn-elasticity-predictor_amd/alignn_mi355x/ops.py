@@ -231,6 +231,48 @@ def gemm_tn_smalln(A: torch.Tensor, X: torch.Tensor, C: torch.Tensor, colsum: Op
     return C
 
 
+def enc_bwd_ok(D: int, H: int, L: int, kin: int) -> bool:
+    """Shapes alignn_enc_bwd_f32 takes (else the per-layer dF path)."""
+    return 0 < D <= 256 and D % 4 == 0 and 0 <= kin <= 16 and 1 <= L <= _lib.ENCBWD_MAX_LAYERS and H * L <= 16
+
+
+def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, Us, Vds, dzs, alphas,
+            dW1: torch.Tensor, db1: torch.Tensor, accumulate: bool = False) -> None:
+    """Deferred backward of the angle encoder's first Linear + ReLU over the line graph ``g``:
+    dW1/db1 (+)= sum_t dpre_t x_t^T / dpre_t with dpre_t = relu'(W1 x_t + b1) * sum_l,h
+    (dz_l u_l + alpha_l Vd_l) — see include/alignn_hip.h (alignn_enc_bwd_f32)."""
+    L = len(Us)
+    T, kin = x.shape
+    D = W1.size(0)
+    H = Us[0].size(1) if L else 1
+    if (not enc_bwd_ok(D, H, L, kin) or len(Vds) != L or len(dzs) != L or len(alphas) != L or T != g.m
+            or x.stride(1) != 1 or not W1.is_contiguous() or tuple(W1.shape) != (D, kin) or not dW1.is_contiguous()
+            or tuple(dW1.shape) != (D, kin) or b1.numel() != D or db1.numel() != D):
+        raise ValueError("enc_bwd: unsupported or inconsistent shapes")
+    for U, Vd, dz, al in zip(Us, Vds, dzs, alphas):
+        if (tuple(U.shape) != (g.n, H, D) or tuple(Vd.shape) != (g.n, H, D) or not U.is_contiguous()
+                or not Vd.is_contiguous() or dz.size(0) < T or al.size(0) < T or dz.size(-1) != H
+                or al.size(-1) != H or not dz.is_contiguous() or not al.is_contiguous()):
+            raise ValueError("enc_bwd: per-layer operand does not cover the graph")
+    lib = _lib.lib()
+    a = _lib.EncBwdArgs()
+    a.n, a.T, a.D, a.H, a.L, a.kin = g.n, T, D, H, L, kin
+    a.dst_at = g.dst_at.data_ptr()
+    a.x, a.ldx = x.data_ptr(), x.stride(0)
+    a.w1, a.b1 = W1.data_ptr(), b1.data_ptr()
+    for l in range(L):
+        a.U[l], a.Vd[l] = Us[l].data_ptr(), Vds[l].data_ptr()
+        a.dz[l], a.alpha[l] = dzs[l].data_ptr(), alphas[l].data_ptr()
+    a.dW1, a.db1, a.accumulate = dW1.data_ptr(), db1.data_ptr(), int(bool(accumulate))
+    need = int(lib.alignn_enc_bwd_workspace(D, kin))
+    ws = WS.get("enc_bwd", need, x.device)
+    a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
+    # compulsory bytes: x rows, targets, 2LH scalars per edge; U/Vd rows once per target
+    nbytes = 4.0 * (T * (kin + 1 + 2 * L * H) + 2 * L * g.n * H * D)
+    profiling.launch(f"enc_bwd T{T} L{L}", 0.0, nbytes,
+                     lambda: check(lib.alignn_enc_bwd_f32(ctypes.byref(a), stream_ptr()), "alignn_enc_bwd_f32"))
+
+
 # ------------------------------------------------------------------------------------------------
 # Graph preparation
 # ------------------------------------------------------------------------------------------------
@@ -317,16 +359,17 @@ def scatter_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, accumu
     return out
 
 
-def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, kin: int = 0) -> float:
+def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, kin: int = 0, dF_rw: int = 1) -> float:
     """Compulsory HBM bytes of one launch (every operand touched once, ideal caching).  kin > 0:
-    edge features recomputed from kin raw inputs per edge (no [m, D] feature / gradient rows)."""
+    edge features recomputed from kin raw inputs per edge (no [m, D] feature / gradient rows).
+    dF_rw: [m, D] edge-feature gradient rows moved by bwd_dst (0 none, 1 written, 2 read + written)."""
     f = 4.0
     feat = m * kin if kin else m * D
     if kind == "fwd":   # Q,K,V + U + edge features + CSR in; aggV + S + 3 stats out
         return f * (3 * n * D + n * H * D + feat + 2 * m + n + n * D + n * H * D + 3 * n * H)
     if kind == "bwd_dst":  # Q,K,V,U,Vd,dout,outp,features,stats in; dQ,Sz,sigz,dz,alpha(,dF) out
         return f * (3 * n * D + 2 * n * H * D + 2 * n * D + feat + 2 * n * H + 2 * m + n
-                    + n * D + n * H * D + n * H + 2 * m * H + (0 if kin else m * D))
+                    + n * D + n * H * D + n * H + 2 * m * H + (0 if kin else dF_rw * m * D))
     return f * (2 * n * D + 2 * m * H + 2 * m + n + 2 * n * D)  # bwd_src
 
 
@@ -427,7 +470,8 @@ def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, d
         raise ValueError("tconv_bwd_dst: dF must cover the rows of F")
     es = None if enc is None else enc.struct(D, H, backward=True)
     profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0,
-                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", enc.kin if enc else 0),
+                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", enc.kin if enc else 0,
+                                  0 if dF is None else (2 if accumulate_dF & 1 else 1)),
                      lambda: check(_lib.lib().alignn_tconv_bwd_dst(
                          g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
                          ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0),

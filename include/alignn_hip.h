@@ -104,6 +104,36 @@ int alignn_gemm_tn_smalln_f32(const float* A, int64_t lda, int64_t K, int64_t M,
                               int32_t N, float* C, int64_t ldc, float* colsum, int32_t accumulate, float* workspace,
                               int64_t workspace_elems, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Angle-encoder backward, deferred (encbwd.hip).  Replaces the autograd backward of the angle
+ * encoder's first Linear + ReLU (train.py:358-364) as it is reached from every EdgeUpdateBlock's
+ * TransformerConv (train.py:315): instead of each layer's attention backward accumulating the
+ * hidden-layer gradient into a [T, D] array (alignn_tconv_bwd_dst with dF), the layers leave their
+ * per-edge scalars dz_e / alpha_e and per-target U / Vd, and one pass forms per target-sorted edge t
+ *     dpre_t = [W1 x_t + b1 > 0] * sum_{l<L, h<H} dz_l[t,h] U_l[d,h] + alpha_l[t,h] Vd_l[d,h]
+ *     dW1 (+)= sum_t dpre_t x_t^T,   db1 (+)= sum_t dpre_t        (d = dst_at[t])
+ * The pre-activation uses alignn_linear_smallk_f32's fma order (the forward's ReLU mask exactly).
+ * Needs D <= 256 with D % 4 == 0, kin <= 16, H*L <= 16, L <= ALIGNN_ENCBWD_MAX_LAYERS
+ * (otherwise ALIGNN_E_UNSUPPORTED: the caller keeps the per-layer dF path).  Fixed grid and
+ * summation orders: deterministic.  workspace floats: alignn_enc_bwd_workspace(D, kin).
+ * ---------------------------------------------------------------------------------------- */
+#define ALIGNN_ENCBWD_MAX_LAYERS 8
+typedef struct AlignnEncBwdArgs {
+  int64_t n, T;                        /* line-graph nodes (targets) and edges */
+  int32_t D, H, L, kin;
+  const int32_t* dst_at;               /* [T] target of each target-sorted edge (alignn_graph_prep) */
+  const float* x; int64_t ldx;         /* [T, kin] raw angle features, target-sorted */
+  const float* w1; const float* b1;    /* [D, kin], [D] */
+  const float* U[ALIGNN_ENCBWD_MAX_LAYERS];      /* per layer [n, H, D] */
+  const float* Vd[ALIGNN_ENCBWD_MAX_LAYERS];     /* per layer [n, H, D] */
+  const float* dz[ALIGNN_ENCBWD_MAX_LAYERS];     /* per layer [T, H] (alignn_tconv_bwd_dst dz_e) */
+  const float* alpha[ALIGNN_ENCBWD_MAX_LAYERS];  /* per layer [T, H] (alignn_tconv_bwd_dst alpha_e) */
+  float* dW1; float* db1; int32_t accumulate;
+  float* workspace; int64_t workspace_elems;
+} AlignnEncBwdArgs;
+int64_t alignn_enc_bwd_workspace(int32_t D, int32_t kin);
+int alignn_enc_bwd_f32(const AlignnEncBwdArgs* args, void* stream);
+
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
  * Two-stage, fixed order.  workspace >= 256*N floats. */
 int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,

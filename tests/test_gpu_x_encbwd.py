@@ -1,0 +1,115 @@
+"""Deferred angle-encoder backward (encbwd.hip, alignn_enc_bwd_f32; the autograd backward of the
+angle encoder's first Linear + ReLU, train.py:358-364, as reached from every EdgeUpdateBlock):
+kernel vs an fp64 restatement on random line graphs (ragged and empty segments, target changes
+inside a chunk, H*L = 1..16, kin 1..16), accumulate mode and determinism; then the engine with
+``defer_angle_bwd`` on vs off (only the W1/b1 gradients may differ, by summation order)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+def _case(n, D, H, L, kin, seed):
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    deg = torch.randint(0, 300, (n,), generator=g)
+    deg[::5] = 0
+    deg[1] = 1000  # one segment spanning several chunks
+    dst = torch.repeat_interleave(torch.arange(n), deg)
+    src = torch.randint(0, n, (dst.numel(),), generator=g)
+    csr = ops.GraphCSR(torch.stack([src, dst]).to(DEV), n)
+    T = dst.numel()
+    ldx = (kin + 3) // 4 * 4
+    xb = torch.randn(T, max(ldx, 4), generator=g).to(DEV)
+    x = xb[:, :kin]
+    W1 = torch.randn(D, kin, generator=g).to(DEV) * 0.5
+    b1 = torch.randn(D, generator=g).to(DEV) * 0.5
+    U = [torch.randn(n, H, D, generator=g).to(DEV) for _ in range(L)]
+    Vd = [torch.randn(n, H, D, generator=g).to(DEV) for _ in range(L)]
+    dz = [torch.randn(max(T, 1), H, generator=g).to(DEV) for _ in range(L)]
+    al = [torch.randn(max(T, 1), H, generator=g).to(DEV) for _ in range(L)]
+    return csr, x, W1, b1, U, Vd, dz, al
+
+
+def _reference(csr, x, W1, b1, U, Vd, dz, al):
+    """fp64 restatement; the ReLU mask from the forward's own fp32 kernel (linear_smallk)."""
+    from alignn_mi355x import ops
+    T = x.size(0)
+    D = W1.size(0)
+    h1 = torch.empty(T, D, device=DEV)
+    ops.linear_smallk(x, W1, b1, h1, relu=True)
+    d = csr.dst_at[:T].long()
+    gsum = torch.zeros(T, D, dtype=torch.float64, device=DEV)
+    for Ul, Vl, zl, al_l in zip(U, Vd, dz, al):
+        gsum += torch.einsum("th,thd->td", zl[:T].double(), Ul[d].double())
+        gsum += torch.einsum("th,thd->td", al_l[:T].double(), Vl[d].double())
+    dpre = gsum * (h1 > 0).double()
+    return dpre.t() @ x.double(), dpre.sum(0)
+
+
+@pytest.mark.parametrize("n,D,H,L,kin", [(40, 256, 4, 4, 11), (33, 64, 4, 2, 7), (17, 32, 1, 1, 7),
+                                         (25, 256, 8, 2, 16), (30, 128, 2, 8, 1), (9, 256, 4, 4, 12)])
+def test_enc_bwd_matches_fp64(n, D, H, L, kin):
+    from alignn_mi355x import ops
+    csr, x, W1, b1, U, Vd, dz, al = _case(n, D, H, L, kin, seed=n * 31 + D + H + L + kin)
+    dW1 = torch.full((D, kin), float("nan"), device=DEV)
+    db1 = torch.full((D,), float("nan"), device=DEV)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1, db1)
+    rW, rb = _reference(csr, x, W1, b1, U, Vd, dz, al)
+    assert _rel(dW1, rW) < 1e-5 and _rel(db1, rb) < 1e-5
+    # accumulate adds exactly the same partial sums; repeated launches are bitwise equal
+    dW2, db2 = dW1.clone(), db1.clone()
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW2, db2, accumulate=True)
+    assert torch.equal(dW2, dW1 + dW1) and torch.equal(db2, db1 + db1)
+    dW3, db3 = torch.empty_like(dW1), torch.empty_like(db1)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW3, db3)
+    assert torch.equal(dW3, dW1) and torch.equal(db3, db1)
+
+
+def test_enc_bwd_empty_graph_and_rejects_unsupported():
+    from alignn_mi355x import ops
+    csr = ops.GraphCSR(torch.zeros(2, 0, dtype=torch.int64, device=DEV), 5)
+    x = torch.zeros(0, 11, device=DEV)
+    W1, b1 = torch.randn(64, 11, device=DEV), torch.randn(64, device=DEV)
+    U = [torch.randn(5, 4, 64, device=DEV)]
+    z = [torch.zeros(1, 4, device=DEV)]
+    dW1, db1 = torch.full((64, 11), 3.0, device=DEV), torch.full((64,), 3.0, device=DEV)
+    ops.enc_bwd(csr, x, W1, b1, U, U, z, z, dW1, db1)
+    assert torch.equal(dW1, torch.zeros_like(dW1)) and torch.equal(db1, torch.zeros_like(db1))
+    assert not ops.enc_bwd_ok(512, 4, 4, 11) and not ops.enc_bwd_ok(256, 4, 5, 11)
+    assert not ops.enc_bwd_ok(256, 4, 4, 17)
+
+
+@pytest.mark.parametrize("lg_offset", ["num_nodes", "num_edges"])
+def test_engine_deferred_angle_backward(lg_offset):
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_batch
+    res = []
+    for defer in (False, True):
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(DEV)
+        model._engine.defer_angle_bwd = defer
+        tr = A.FusedTrainer(model)
+        b = mp_like_batch(4, lg_offset=lg_offset).to(DEV)
+        loss = tr.forward_backward(b, 3).clone()
+        torch.cuda.synchronize()
+        res.append((loss, tr.st.grad.clone(), tr.st))
+    (l0, g0, st), (l1, g1, _) = res
+    assert torch.equal(l0, l1)
+    P = st.P
+    w1 = P.enc("angle", 0, "weight")
+    b1 = P.enc("angle", 0, "bias")
+    o_w, o_b = w1.storage_offset() - st.flat.storage_offset(), b1.storage_offset() - st.flat.storage_offset()
+    sl = [slice(o_w, o_w + w1.numel()), slice(o_b, o_b + b1.numel())]
+    for s_ in sl:
+        assert _rel(g1[s_], g0[s_]) < 1e-5
+    mask = torch.ones_like(g0, dtype=torch.bool)
+    for s_ in sl:
+        mask[s_] = False
+    assert torch.equal(g0[mask], g1[mask])

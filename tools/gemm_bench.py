@@ -17,8 +17,9 @@ import alignn_mi355x as A  # noqa: E402
 from alignn_mi355x import ops  # noqa: E402
 from alignn_mi355x.synthetic import mp_like_batch  # noqa: E402
 
-TILES = {b + k: f"{s}/bk{bk}" for k, s in ((1, "128x128"), (2, "128x64"), (3, "64x128"), (4, "64x64"))
-         for b, bk in ((0, "auto"), (16, 32), (32, 16), (128, 64))}
+TILES = {20: "auto"}
+TILES.update({b + k: f"{s}/bk{bk}" for k, s in ((1, "128x128"), (2, "128x64"), (3, "64x128"), (4, "64x64"))
+         for b, bk in ((0, "auto"), (16, 32), (32, 16), (128, 64))})
 
 
 def timeit(fn, reps):
@@ -54,6 +55,7 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json")
+    ap.add_argument("--quick", action="store_true", help="auto plan + torch.matmul (hipBLASLt/rocBLAS) only")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -72,7 +74,7 @@ def main():
         groups.setdefault(sig(c), []).append(c)
     print(f"{len(calls)} gemm calls, {len(groups)} distinct", flush=True)
     res = []
-    tot_auto = tot_best = 0.0
+    tot_auto = tot_best = tot_lib = 0.0
     for key, cs in groups.items():
         c = cs[0]
         C_save = c["C"].clone()
@@ -83,9 +85,18 @@ def main():
                      c_rows=c["c_rows"], split_k=split, tile=tile)
 
         t_auto = timeit(lambda: run(), a.reps)
+        # library reference: the same plain product through torch.matmul (no epilogue)
+        Am, Bm = c["A"], c["B"]
+        if c["reduce_batch"]:
+            Am = Am.transpose(0, 1).reshape(Am.shape[1], -1) if Am.dim() == 3 else Am
+            Bm = Bm.reshape(-1, Bm.shape[-1]) if Bm.dim() == 3 else Bm
+        try:
+            t_lib = timeit(lambda: torch.matmul(Am, Bm), a.reps)
+        except Exception:  # noqa: BLE001
+            t_lib = float("nan")
         trials = {}
-        for tile in sorted(TILES):
-            if tile < 16:
+        for tile in ([] if a.quick else sorted(TILES)):
+            if tile < 16 or tile == 20:
                 continue
             for split in (1, 2, 4, 8, 16, 32, 64):
                 try:
@@ -93,9 +104,12 @@ def main():
                 except Exception as e:  # noqa: BLE001 - workspace or shape limits
                     trials[(tile, split)] = float("inf")
         c["C"].copy_(C_save)
+        if not trials:
+            trials[(20, 0)] = t_auto
         best = min(trials, key=trials.get)
         n = len(cs)
         tot_auto += t_auto * n
+        tot_lib += t_lib * n
         tot_best += trials[best] * n
         Ash, Bsh, Csh = key[0], key[2], key[4]
         M, K = Ash[-2], Ash[-1]
@@ -109,8 +123,8 @@ def main():
         res.append(row)
         print(f"M{M:6d} N{N:5d} K{K:6d} b{bt} x{n:2d} A{key[1]} B{key[3]}: auto {t_auto:7.1f}us "
               f"({row['auto_tflops']:5.1f} TF)  best {TILES[best[0]]}/s{best[1]} {trials[best]:7.1f}us "
-              f"({row['best_tflops']:5.1f} TF)", flush=True)
-    print(f"step gemm total: auto {tot_auto:.0f} us, best {tot_best:.0f} us")
+              f"({row['best_tflops']:5.1f} TF)  torch.matmul {t_lib:7.1f}us ({fl / t_lib / 1e6:5.1f} TF)", flush=True)
+    print(f"step gemm total: auto {tot_auto:.0f} us, best {tot_best:.0f} us, torch.matmul {tot_lib:.0f} us")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
