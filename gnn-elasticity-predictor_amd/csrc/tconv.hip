@@ -801,6 +801,13 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
         vload(p.U + (d * H + h) * D + j0, t);
         vstore(uv + h * RS + j0, t);
       }
+    } else {
+      // lanes past D: zeros, so their (otherwise uninitialised) LDS slots cannot put a NaN into
+      // the cross-lane score reduction (0 * NaN)
+      float z[VPL];
+      vzero(z);
+#pragma unroll
+      for (int h = 0; h < H; ++h) vstore(uv + h * RS + j0, z);
     }
     float c[H];
 #pragma unroll
@@ -1029,6 +1036,11 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
           vload(p.Vd + (d * H + h) * D + j0, t);
           vstore(uv + (H + h) * RS + j0, t);
         }
+      } else {  // lanes past D: zeros (see tconv_fwd2)
+        float z[VPL];
+        vzero(z);
+#pragma unroll
+        for (int h = 0; h < 2 * H; ++h) vstore(uv + h * RS + j0, z);
       }
       const float pc = vdot(wb, q), pc2 = vdot(wb, go), pdl = vdot(go, op);
 #pragma unroll

@@ -196,7 +196,7 @@ def _run_tconv(csr, m, t, D, H, drop, compact):
                 dF=dF)
 
 
-@pytest.mark.parametrize("D,H", [(256, 4), (128, 2), (64, 1), (32, 4), (512, 8)])
+@pytest.mark.parametrize("D,H", [(256, 4), (128, 2), (64, 1), (32, 4), (32, 1), (512, 8)])
 @pytest.mark.parametrize("drop", [0.0, 0.15])
 def test_compact_register_attention_kernels_match_v1(D, H, drop):
     """The row-distributed (COMPACT_REGS) attention kernels vs the default ones: same math, softmax

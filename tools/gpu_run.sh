@@ -8,7 +8,8 @@ for step in "$@"; do
   case "$step" in
     tests) cmd=(timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 120 --timeout-method thread -p no:cacheprovider) ;;
     tests-core) cmd=(timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider --ignore-glob=tests/test_gpu_x_*) ;;
-    tests-x) cmd=(timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_x_bf16.py tests/test_gpu_x_ensemble.py tests/test_gpu_x_knn.py tests/test_gpu_x_pending.py tests/test_gpu_x_skinny.py tests/test_gpu_x_store.py) ;;
+    tests-x) cmd=(timeout -k 10 600 python -u -m pytest -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_x_*.py) ;;
+    tests-enc) cmd=(timeout -k 10 300 python -u -m pytest tests/test_gpu_x_encbwd.py -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider) ;;
     tests-all) cmd=(timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider) ;;
     smoke) cmd=(timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()") ;;
     bench) cmd=(timeout -k 10 600 python bench.py --steps 20 --warmup 5) ;;
