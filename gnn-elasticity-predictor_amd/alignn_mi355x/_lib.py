@@ -20,6 +20,7 @@ c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
 c_u64 = ctypes.c_uint64
 c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
 c_vp = ctypes.c_void_p
 
 
@@ -120,7 +121,7 @@ _SIGNATURES = {
                                    c_i64, c_vp], c_i32),
     "alignn_enc_bwd_workspace": ([c_i32, c_i32], c_i64),
     "alignn_enc_bwd_f32": ([ctypes.POINTER(EncBwdArgs), c_vp], c_i32),
-    "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_f32,
+    "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                           c_vp, c_vp], c_i32),
 }
 

@@ -1,11 +1,12 @@
 // optim.hip — gradient clipping + AdamW over the flat parameter buffer.
 //
 // Reference (scripts/train.py:693-699, :1532-1542): torch.nn.utils.clip_grad_norm_(params, 5.0)
-// then torch.optim.AdamW (fused, betas (0.9, 0.999), eps 1e-8, decoupled weight decay) over two
-// param groups — base + mean heads | logvar heads — which the flat layout keeps as two contiguous
-// segments [0, split) and [split, n) with their own learning rates.
+// then torch.optim.AdamW (betas (0.9, 0.999), eps 1e-8, decoupled weight decay; fused on a GPU,
+// the single-tensor loop on the CPU path this engine is held to) over two param groups — base +
+// mean heads | logvar heads — which the flat layout keeps as two contiguous segments [0, split)
+// and [split, n) with their own learning rates.
 //   clip:  norm = ||g||_2 ;  c = min(max_norm / (norm + 1e-6), 1) ;  g *= c
-//   AdamW: step += 1 ; p *= 1 - lr*wd ; m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
+//   AdamW: step += 1 ; p *= 1 - lr*wd ; m = lerp(m, g, 1-b1) ; v = b2 v + (1-b2) g^2 ;
 //          p -= (lr / (1 - b1^step)) * m / (sqrt(v) / sqrt(1 - b2^step) + eps)
 // The norm is a fixed-order two-stage reduction (deterministic); the step counter and the norm live
 // in device memory, so the update can sit inside a captured HIP graph.
@@ -46,24 +47,31 @@ __global__ __launch_bounds__(256) void sumsq_stage2(const float* __restrict__ pa
 __global__ void step_inc_kernel(float* step) { *step += 1.0f; }
 
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
-                                                    float* __restrict__ v, int64_t n, int64_t split, float lr0,
-                                                    float lr1, float wd, float b1, float b2, float eps,
+                                                    float* __restrict__ v, int64_t n, int64_t split, double lr0,
+                                                    double lr1, double wd, double b1, double b2, float eps,
                                                     const float* __restrict__ norm, float max_norm,
                                                     const float* __restrict__ step) {
-  const float t = *step;
-  const float bc1 = 1.0f - powf(b1, t);
-  const float bc2s = sqrtf(1.0f - powf(b2, t));
+  // The reference's CPU AdamW (torch _single_tensor_adam, decoupled decay) forms its scalars as
+  // Python doubles and rounds each to fp32 once where a tensor op consumes it: 1 - lr*wd, 1 - b1
+  // (lerp weight), 1 - b2 (addcmul value), lr / (1 - b1^t), sqrt(1 - b2^t).  Same here.
+  const double t = (double)*step;
+  const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2), fb2 = (float)b2;
+  const float bc2s = (float)sqrt(1.0 - pow(b2, t));
+  const double bc1 = 1.0 - pow(b1, t);
+  const float ss0 = (float)(lr0 / bc1), ss1 = (float)(lr1 / bc1);
+  const float dec0 = (float)(1.0 - lr0 * wd), dec1 = (float)(1.0 - lr1 * wd);
   float c = 1.0f;
   if (norm) c = fminf(max_norm / (*norm + 1e-6f), 1.0f);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float lr = i < split ? lr0 : lr1;
+    const bool g0 = i < split;
     const float gi = g[i] * c;
     g[i] = gi;  // clip_grad_norm_ scales the gradients in place
-    float pi = p[i] * (1.0f - lr * wd);
-    const float mi = b1 * m[i] + (1.0f - b1) * gi;
-    const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
-    pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2s + eps);
-    p[i] = pi;
+    const float pi = p[i] * (g0 ? dec0 : dec1);
+    const float m0 = m[i];
+    const float mi = m0 + omb1 * (gi - m0);            // lerp_(g, 1 - b1), weight < 0.5 branch
+    const float vi = v[i] * fb2 + omb2 * gi * gi;       // mul_(b2).addcmul_(g, g, value=1 - b2)
+    const float den = sqrtf(vi) / bc2s + eps;
+    p[i] = pi + (-(g0 ? ss0 : ss1)) * mi / den;        // addcdiv_(m, denom, value=-step_size)
     m[i] = mi;
     v[i] = vi;
   }
@@ -83,8 +91,8 @@ extern "C" int alignn_grad_norm_f32(const float* g, int64_t n, float* norm, floa
   return ALIGNN_OK;
 }
 
-extern "C" int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, float lr0,
-                                float lr1, float weight_decay, float beta1, float beta2, float eps,
+extern "C" int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, double lr0,
+                                double lr1, double weight_decay, double beta1, double beta2, double eps,
                                 const float* norm, float max_norm, float* step, void* stream) {
   if (n < 0 || split < 0 || split > n || !step) return ALIGNN_E_BAD_SHAPE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -92,7 +100,7 @@ extern "C" int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t 
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   if (n > 0)
     hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, split, lr0, lr1,
-                       weight_decay, beta1, beta2, eps, norm, max_norm, step);
+                       weight_decay, beta1, beta2, (float)eps, norm, max_norm, step);
   ALIGNN_LAUNCH_CHECK("adamw_kernel");
   return ALIGNN_OK;
 }

@@ -337,11 +337,14 @@ int alignn_member_mean_f32(int32_t M, int64_t n, const float* x, int64_t member_
  * (in place, as clip_grad_norm_); then for i < split lr = lr0 else lr1:
  *   p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
  *   p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps).
+ * The hyper-parameters are doubles, as the reference's Python floats are: each derived scalar
+ * (1 - lr*wd, 1 - b1, 1 - b2, lr / (1 - b1^step), sqrt(1 - b2^step)) is formed in double and rounded
+ * to fp32 once, as torch's single-tensor AdamW does (the reference's CPU optimizer).
  * norm and step are device scalars (graph-capturable).
  * ---------------------------------------------------------------------------------------- */
 int alignn_grad_norm_f32(const float* g, int64_t n, float* norm, float* workspace, void* stream);
-int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, float lr0, float lr1,
-                     float weight_decay, float beta1, float beta2, float eps, const float* norm, float max_norm,
+int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, double lr0, double lr1,
+                     double weight_decay, double beta1, double beta2, double eps, const float* norm, float max_norm,
                      float* step, void* stream);
 
 /* ------------------------------------------------------------------------------------------
