@@ -55,9 +55,11 @@ def parse():
                    help="also time the end-to-end loop over an HBM-resident dataset of this many graphs per rank: "
                         "device collate of a random batch + CSR/compaction + step (SURVEY §8d's 'including collate' "
                         "number; reported as a separate field, never as value)")
-    p.add_argument("--graph", action="store_true",
-                   help="replay the step as HIP graphs (ROCm disallows external event nodes, so the roofline "
-                        "probe then runs in 2 eager steps after the timed region)")
+    p.add_argument("--launch", choices=["eager", "plan", "graph"], default="plan",
+                   help="eager: Python issues every launch; plan: the step is recorded once as a native launch "
+                        "plan and re-issued from C++ (plan.hip; the roofline probe is a pair of plan timestamps "
+                        "in every replay); graph: ROCm HIP graphs of the same capture")
+    p.add_argument("--graph", action="store_true", help="alias of --launch graph")
     p.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
                    help="engine option (engine.<attr>=0/1), trainer optimizer (optimizer=hip) or GEMM stage "
                         "(gemm_stage=16|32|64); repeatable — for measuring opt-in paths")
@@ -209,22 +211,21 @@ def main():
             with open(args.dump_probes, "w") as f:
                 json.dump(dict(sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"])), f, indent=1)
 
-    # HIP graphs: capture with the dominant kernel's launches bracketed by (external) event nodes,
-    # so every replay re-times them; the timed region's last replay is read back afterwards.
+    # captured step: in a plan the dominant kernel's launches are bracketed by plan timestamps, so
+    # every replay re-times them; the timed region's last replay is read back afterwards
+    if args.graph:
+        args.launch = "graph"
     launch_mode = "eager"
     probe_in_graph = False
-    if args.graph:
-        try:
-            if dominant is not None:
-                profiling.enable(dominant)
-            trainer.capture(batch)
-            launch_mode, probe_in_graph = "hip_graph", dominant is not None
-        except Exception as e:  # noqa: BLE001 - fall back to a plain capture, probes run eagerly
-            print(f"[bench] capture with probes failed ({e}); capturing without", file=sys.stderr)
-            profiling.disable()
-            trainer._graph = None
-            trainer.capture(batch)
-            launch_mode = "hip_graph"
+    if args.launch != "eager":
+        mode = args.launch
+        # ROCm refuses external event nodes in a captured graph: graph mode probes eagerly after
+        # the timed region; a plan carries the probes as timestamps
+        if dominant is not None and mode == "plan":
+            profiling.enable(dominant)
+        trainer.capture(batch, mode=mode)
+        probe_in_graph = dominant is not None and mode == "plan"
+        launch_mode = "native_plan" if mode == "plan" else "hip_graph"
         profiling.disable()
 
     for i in range(args.warmup):
@@ -253,7 +254,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             print(f"[bench] graph event timing unavailable ({e}); probing eagerly", file=sys.stderr)
             probe_in_graph = False
-    if dominant is not None and launch_mode == "hip_graph" and not probe_in_graph:
+    if dominant is not None and launch_mode != "eager" and not probe_in_graph:
         # fallback: time the dominant kernel in two extra eager steps after the timed region
         saved = trainer._graph
         trainer._graph = None
@@ -269,7 +270,8 @@ def main():
     if args.e2e > 0:
         e2e = end_to_end(args, trainer, dev, rank, world)
 
-    probe_src = ("hip events in the captured step (last timed replay)" if probe_in_graph else
+    probe_src = ("plan timestamps in the replayed step (last timed replay)" if (probe_in_graph and launch_mode == "native_plan") else
+                 "hip events in the captured step (last timed replay)" if probe_in_graph else
                  "hip events around each launch, timed region" if launch_mode == "eager" else
                  "hip events, 2 eager steps after the timed region")
     result = None

@@ -121,6 +121,18 @@ _SIGNATURES = {
                                    c_i64, c_vp], c_i32),
     "alignn_enc_bwd_workspace": ([c_i32, c_i32], c_i64),
     "alignn_enc_bwd_f32": ([ctypes.POINTER(EncBwdArgs), c_vp], c_i32),
+    "alignn_plan_begin": ([c_vp], c_i32),
+    "alignn_plan_note_wait": ([c_vp, c_vp], c_i32),
+    "alignn_plan_end": ([], c_vp),
+    "alignn_plan_abort": ([], c_i32),
+    "alignn_plan_replay": ([c_vp, c_vp], c_i32),
+    "alignn_plan_info": ([c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "alignn_plan_destroy": ([c_vp], c_i32),
+    "alignn_plan_note_timestamp": ([c_vp], c_i32),
+    "alignn_plan_elapsed_ms": ([c_vp, c_i32, c_i32, c_vp], c_i32),
+    "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
+    "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
+    "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                           c_vp, c_vp], c_i32),
 }

@@ -287,10 +287,10 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     elif compact_gate:
         c.outp, c.outp_rows = c.outp_a, g.cmap
     else:
-        c.outp = torch.zeros(n, D, device=dev)
+        c.outp = ops.zeros(n, D, device=dev)
         ops.scatter_rows(c.outp_a, rows, c.outp)
     if side is not None and rows is not None:
-        torch.cuda.current_stream(dev).wait_stream(side)
+        ops.stream_wait(torch.cuda.current_stream(dev), side)
     X_new = torch.empty(n, D, device=dev)
     c.beta = torch.empty(n, device=dev)
     c.mu = torch.empty(n, device=dev)
@@ -392,7 +392,7 @@ class _side_work:
     def __enter__(self):
         if self.side is None:
             return self
-        self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+        ops.stream_wait(self.side, torch.cuda.current_stream(self.side.device))
         for t in self.tensors:
             if t is not None:
                 t.record_stream(self.side)
@@ -486,7 +486,7 @@ class AlignnEngine:
             ctx.h1e, e = self._mlp_fwd(edge_attr, P.enc("edge", 0, "weight"), P.enc("edge", 0, "bias"),
                                        P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
         else:
-            ctx.h1e, e = None, torch.zeros(E, D, device=dev)
+            ctx.h1e, e = None, ops.zeros(E, D, device=dev)
         # Angle encoder (train.py:553-554): only its hidden layer is materialised.  Its second Linear
         # (W2, b2) is folded into every line-graph conv's edge projection, M_l = W_edge,l W2 and
         # w̄_l = W_edge,l b2 — exact algebra, so the [T, D] x [D, D] GEMM and its two
@@ -506,7 +506,7 @@ class AlignnEngine:
             else:
                 ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
         else:
-            a = torch.zeros(T, D, device=dev)
+            a = ops.zeros(T, D, device=dev)
         ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
         side = ops.side_stream(dev) if (self.overlap and self.overlap_forward) else None
@@ -572,7 +572,7 @@ class AlignnEngine:
         p_drop, seed = ctx.p, ctx.seed
         pre = P.prefix
         g = G.named
-        G.flat.zero_()
+        ops.zero_(G.flat)
         dout = dout.contiguous()
         # heads (train.py:582-585)
         if ctx.mode == "embed":
@@ -597,11 +597,11 @@ class AlignnEngine:
         ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"])
         ops.colsum(dpre, g[pre + "feat_proj.0.bias"])
         Wfeat = ctx.feats.size(1)
-        dfeats = torch.zeros(B, Wfeat, device=dev)
+        dfeats = ops.zeros(B, Wfeat, device=dev)
         ops.gemm(dpre, Wf[:, :D], dfeats[:, :D])
         dh = torch.empty(N, D, device=dev)
         ops.readout_pool_bwd(dfeats, bc.ptr, bc.batch_vec, dh, False, p_drop, site_seed(seed, 4 * L))
-        de = torch.zeros(E, D, device=dev)
+        de = ops.zeros(E, D, device=dev)
         defer = (self.defer_angle_bwd and ctx.has_angle and ctx.angle_enc is None and T > 0 and E > 0 and L > 0
                  and ops.enc_bwd_ok(D, cfg.heads, L, bc.xa.size(1)))
         da = torch.empty(T, D, device=dev) if (T > 0 and ctx.angle_enc is None and not defer) else None
@@ -663,4 +663,4 @@ class AlignnEngine:
         self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
                       G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))
         if side is not None:
-            torch.cuda.current_stream(dev).wait_stream(side)  # join: every gradient is written
+            ops.stream_wait(torch.cuda.current_stream(dev), side)  # join: every gradient is written

@@ -62,6 +62,40 @@ def side_stream(device) -> torch.cuda.Stream:
 WS = _Workspace()
 
 
+def stream_wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
+    """dst waits for the work queued on src so far (torch's event wait), noted as an ordering
+    edge when a launch plan is being recorded (alignn_plan_note_wait)."""
+    dst.wait_stream(src)
+    check(_lib.lib().alignn_plan_note_wait(dst.cuda_stream, src.cuda_stream), "alignn_plan_note_wait")
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """t[...] = 0 by a library kernel (recordable in a launch plan, unlike torch's fill)."""
+    _require(t, "zero_")
+    if not t.is_contiguous():
+        raise ValueError("zero_: contiguous tensors only")
+    check(_lib.lib().alignn_fill_f32(t.data_ptr(), t.numel(), 0.0, stream_ptr()), "alignn_fill_f32")
+    return t
+
+
+def zeros(*shape, device) -> torch.Tensor:
+    return zero_(torch.empty(*shape, device=device))
+
+
+def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst[...] = src[...] (contiguous fp32, same element count) by a library kernel."""
+    _require(dst, "copy_ dst")
+    _require(src, "copy_ src")
+    if not (dst.is_contiguous() and src.is_contiguous()) or dst.numel() != src.numel():
+        raise ValueError("copy_: contiguous tensors with equal element counts only")
+    check(_lib.lib().alignn_copy_f32(dst.data_ptr(), src.data_ptr(), dst.numel(), stream_ptr()), "alignn_copy_f32")
+    return dst
+
+
+def clone(src: torch.Tensor) -> torch.Tensor:
+    return copy_(torch.empty_like(src, memory_format=torch.contiguous_format), src.contiguous())
+
+
 # ------------------------------------------------------------------------------------------------
 # GEMM
 # ------------------------------------------------------------------------------------------------

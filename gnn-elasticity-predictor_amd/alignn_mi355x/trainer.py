@@ -8,12 +8,14 @@ contiguous segments (base + mean heads | logvar heads).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence
 
 import torch
 from torch import nn
 
-from . import ops, profiling
+from . import _lib, ops, profiling
+from ._lib import check
 from .engine import MIN_LOGVAR_FLOOR, batch_cache, site_seed
 from .model import HeteroAlignnRegressor
 from .synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS
@@ -42,7 +44,7 @@ class FusedTrainer:
         self.opt = torch.optim.AdamW([{"params": [self.p_base], "lr": lr}, {"params": [self.p_sigma], "lr": sigma_lr}],
                                      lr=lr, weight_decay=weight_decay, **kw)
         # optimizer="hip": clip + AdamW in libalignn_hip over the flat buffers (alignn_adamw_f32), the
-        # same update as torch's fused AdamW (betas (0.9, 0.999), eps 1e-8, decoupled decay)
+        # update of the reference's CPU AdamW (betas (0.9, 0.999), eps 1e-8, decoupled decay)
         if optimizer not in ("torch", "hip"):
             raise ValueError("optimizer must be 'torch' or 'hip'")
         self.optimizer = optimizer
@@ -78,8 +80,8 @@ class FusedTrainer:
         bc = batch_cache(batch)
         x, gx = batch.x, batch.global_x
         if training and self.jitter > 0.0:
-            x = x.clone()
-            gx = gx.clone()
+            x = ops.clone(x)
+            gx = ops.clone(gx)
             ops.add_noise(x, self.jitter, site_seed(seed, 1 << 20))
             ops.add_noise(gx, self.jitter, site_seed(seed, (1 << 20) + 1))
         out, ctx = model._engine.forward(st.P, batch, bc, training, seed, x, gx, "hetero")
@@ -112,16 +114,27 @@ class FusedTrainer:
         self.opt.step()
 
     # --------------------------------------------------------------------------------------------
-    # HIP-graph mode: the step (jitter, forward, loss, backward | clip, AdamW: ~300 kernels) is
-    # captured once for a fixed batch as two graphs and replayed — no per-kernel host work and no
-    # launch gaps.  ``grad_hook`` (e.g. the data-parallel all_reduce) runs eagerly between the two.
+    # Captured step (fixed batch).  The step (jitter, forward, loss, backward | clip, AdamW: ~300
+    # kernels on two streams) is recorded once and re-issued without per-kernel Python work.
+    #   mode "plan" (default): two native launch plans (plan.hip) — every library launch and every
+    #     cross-stream edge of the step, replayed from C++ onto the same two streams.  Recorded
+    #     inside a torch graph capture, whose private memory pool keeps every buffer of the step at
+    #     its address; the captured graph's node census must match the plan (nothing foreign).
+    #   mode "graph": ROCm HIP graphs of the same capture (measured slower on MI355X: 5.5 vs 5.2 ms
+    #     eager, the two streams' branches lose concurrency).
+    # ``grad_hook`` (e.g. the data-parallel all_reduce) runs eagerly between the two phases.
     # Randomness stays per step: the kernels read a device step seed (ops.set_step_seed) that
     # step() updates before each replay.  The learning rate is baked in at capture.
     # --------------------------------------------------------------------------------------------
-    def capture(self, batch) -> None:
+    def capture(self, batch, mode: str = "plan") -> None:
         """Capture the training step on ``batch`` (which must stay alive with unchanged shapes; its
         tensors may be refilled in place).  Model and optimizer state are left as they were."""
+        if mode not in ("plan", "graph"):
+            raise ValueError("capture mode must be 'plan' or 'graph'")
+        if mode == "plan" and self.optimizer != "hip":
+            raise ValueError("plan capture needs optimizer='hip' (torch's AdamW launches outside the library)")
         dev = self.st.flat.device
+        self.release_capture()
         if self._seed_dev is None:
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         ops.set_step_seed(self._seed_dev)
@@ -137,21 +150,53 @@ class FusedTrainer:
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         profiling.clear()  # roofline probes (bench.py): keep only the launches captured below
-        g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
-            self.forward_backward(batch, 0)
-        with torch.cuda.graph(g_up, pool=g_fb.pool()):
-            self._clip_and_update()
+        keep = mode == "plan"
+        g_fb, g_up = torch.cuda.CUDAGraph(keep_graph=keep), torch.cuda.CUDAGraph(keep_graph=keep)
+        plans = []
+        for g, fn, pool in ((g_fb, lambda: self.forward_backward(batch, 0), None),
+                            (g_up, self._clip_and_update, "fb")):
+            with torch.cuda.graph(g, pool=(g_fb.pool() if pool else None)):
+                if keep:
+                    plans.append(_record_plan(fn))
+                else:
+                    fn()
         torch.cuda.synchronize(dev)
         self._restore(snap)
-        self._graph = (g_fb, g_up, batch)
+        if keep:
+            try:
+                for g, pl, what in ((g_fb, plans[0], "forward/backward"), (g_up, plans[1], "clip/AdamW")):
+                    _check_census(g, pl, what)
+            except Exception:
+                for pl in plans:
+                    _lib.lib().alignn_plan_destroy(pl)
+                raise
+        self._graph = (g_fb, g_up, batch, plans if keep else None)
+
+    def release_capture(self) -> None:
+        if self._graph is not None and self._graph[3]:
+            for pl in self._graph[3]:
+                _lib.lib().alignn_plan_destroy(pl)
+        self._graph = None
+
+    def __del__(self):
+        try:
+            self.release_capture()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
     def _replay(self, seed: int) -> torch.Tensor:
         self._seed_dev.fill_(int(seed) & (2**63 - 1))
-        self._graph[0].replay()
+        g_fb, g_up, _, plans = self._graph
+        if plans:
+            check(_lib.lib().alignn_plan_replay(plans[0], ops.stream_ptr()), "alignn_plan_replay")
+        else:
+            g_fb.replay()
         if self.grad_hook is not None:
             self.grad_hook(self.st.grad)
-        self._graph[1].replay()
+        if plans:
+            check(_lib.lib().alignn_plan_replay(plans[1], ops.stream_ptr()), "alignn_plan_replay")
+        else:
+            g_up.replay()
         self.step_count += 1
         return self.loss
 
@@ -178,3 +223,40 @@ class FusedTrainer:
                         v.copy_(saved[k])
                     else:
                         v.zero_()
+
+
+def _record_plan(fn) -> int:
+    """Runs fn (inside the caller's capture) while the library records a launch plan."""
+    lib = _lib.lib()
+    check(lib.alignn_plan_begin(ops.stream_ptr()), "alignn_plan_begin")
+    profiling.plan_recording(True)
+    try:
+        fn()
+    except BaseException:
+        lib.alignn_plan_abort()
+        raise
+    finally:
+        profiling.plan_recording(False)
+    plan = lib.alignn_plan_end()
+    if not plan:
+        check(-1, "alignn_plan_end")
+    profiling.bind_plan(plan)
+    return plan
+
+
+def plan_info(plan) -> dict:
+    v = [ctypes.c_int64() for _ in range(4)]
+    check(_lib.lib().alignn_plan_info(plan, *[ctypes.byref(x) for x in v]), "alignn_plan_info")
+    return dict(zip(("launches", "edges", "streams", "arg_bytes"), (x.value for x in v)))
+
+
+def _check_census(graph: torch.cuda.CUDAGraph, plan, what: str) -> None:
+    """Every kernel node of the captured graph must be a recorded launch and nothing else may be
+    in it (a torch op inside the step would run in the graph but not in the plan)."""
+    k, o = ctypes.c_int64(), ctypes.c_int64()
+    check(_lib.lib().alignn_graph_census(ctypes.c_void_p(graph.raw_cuda_graph()), ctypes.byref(k), ctypes.byref(o)),
+          "alignn_graph_census")
+    info = plan_info(plan)
+    if k.value != info["launches"] or o.value != 0:
+        raise RuntimeError(f"launch plan of the {what} phase is incomplete: the captured graph holds {k.value} "
+                           f"kernel and {o.value} other nodes, the plan {info['launches']} launches")

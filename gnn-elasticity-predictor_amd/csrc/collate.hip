@@ -61,7 +61,7 @@ extern "C" int alignn_collate_rows_f32(int32_t G, const float* src, int64_t widt
   if (G < 0 || width < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
   if (G == 0 || width == 0 || max_count == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(collate_rows_kernel, seg_grid(max_count * width, G), dim3(256), 0, s, src, width, src_start,
+  launch(collate_rows_kernel, seg_grid(max_count * width, G), dim3(256), 0, s, src, width, src_start,
                      dst_start, count, dst);
   ALIGNN_LAUNCH_CHECK("collate_rows_kernel");
   return ALIGNN_OK;
@@ -73,7 +73,7 @@ extern "C" int alignn_collate_index_i64(int32_t G, const int64_t* src, int64_t s
   if (G < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
   if (G == 0 || max_count == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(collate_index_kernel, seg_grid(max_count, G), dim3(256), 0, s, src, src_ld, src_start, dst_start,
+  launch(collate_index_kernel, seg_grid(max_count, G), dim3(256), 0, s, src, src_ld, src_start, dst_start,
                      count, add, dst, dst_ld);
   ALIGNN_LAUNCH_CHECK("collate_index_kernel");
   return ALIGNN_OK;
@@ -84,7 +84,7 @@ extern "C" int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, cons
   if (G < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
   if (G == 0 || max_count == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(collate_batchvec_kernel, seg_grid(max_count, G), dim3(256), 0, s, dst_start, count, batch);
+  launch(collate_batchvec_kernel, seg_grid(max_count, G), dim3(256), 0, s, dst_start, count, batch);
   ALIGNN_LAUNCH_CHECK("collate_batchvec_kernel");
   return ALIGNN_OK;
 }

@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+#include <type_traits>
+#include <utility>
+
 #include "../../include/alignn_hip.h"
 
 #define ALIGNN_WAVE 64
@@ -35,6 +39,33 @@ int hip_status(hipError_t e, const char* what);
     hipError_t _e = hipGetLastError();                            \
     if (_e != hipSuccess) return ::alignn::hip_status(_e, what);  \
   } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// Kernel launches.  Every kernel of the library goes through launch(): the arguments are
+// converted to the kernel's parameter types and passed by address to hipLaunchKernel.  While a
+// launch plan is being recorded (plan.hip, alignn_plan_begin), the launch is also appended to it —
+// kernel, grid, block, LDS bytes, stream and a copy of the argument bytes — so the plan can issue
+// the same step again from C++ (alignn_plan_replay) without any per-launch host work above HIP.
+// ---------------------------------------------------------------------------------------------
+extern bool g_recording;
+void record_launch(const void* func, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, void* const* args,
+                   const size_t* sizes, const size_t* aligns, int nargs);
+
+template <typename... P, typename... A>
+inline void launch(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, A&&... a) {
+  static_assert(sizeof...(P) == sizeof...(A), "launch: argument count differs from the kernel's");
+  std::tuple<std::decay_t<P>...> vals(static_cast<std::decay_t<P>>(a)...);
+  void* ptrs[sizeof...(P) + 1];
+  std::apply([&](auto&... v) { int i = 0; ((ptrs[i++] = (void*)&v), ...); }, vals);
+  if (g_recording) {
+    const size_t sizes[sizeof...(P) + 1] = {sizeof(std::decay_t<P>)..., 0};
+    const size_t aligns[sizeof...(P) + 1] = {alignof(std::decay_t<P>)..., 1};
+    record_launch(reinterpret_cast<const void*>(kernel), grid, block, shmem, s, ptrs, sizes, aligns,
+                  (int)sizeof...(P));
+  }
+  // a failure is left in hipGetLastError for the caller's ALIGNN_LAUNCH_CHECK
+  (void)hipLaunchKernel(reinterpret_cast<const void*>(kernel), grid, block, ptrs, shmem, s);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Wave-level reductions (64 lanes).  __shfl_xor lowers to DPP/ds_swizzle/bpermute as the

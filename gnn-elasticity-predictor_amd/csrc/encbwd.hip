@@ -213,16 +213,16 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
   p.part = a->workspace;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->T > 0) {
-    if (a->kin <= 8) hipLaunchKernelGGL(enc_bwd_kernel<8>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
-    else if (a->kin <= 12) hipLaunchKernelGGL(enc_bwd_kernel<12>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(enc_bwd_kernel<16>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
+    if (a->kin <= 8) launch(enc_bwd_kernel<8>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
+    else if (a->kin <= 12) launch(enc_bwd_kernel<12>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
+    else launch(enc_bwd_kernel<16>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("enc_bwd_kernel");
   } else {
     const hipError_t e = hipMemsetAsync(a->workspace, 0, sizeof(float) * EB_BLOCKS * (a->kin + 1) * a->D, s);
     if (e != hipSuccess) return hip_status(e, "enc_bwd memset");
   }
   const int n = (a->kin + 1) * a->D;
-  hipLaunchKernelGGL(enc_bwd_stage2, dim3((n + 255) / 256), dim3(256), 0, s, a->workspace, EB_BLOCKS, a->D, a->kin,
+  launch(enc_bwd_stage2, dim3((n + 255) / 256), dim3(256), 0, s, a->workspace, EB_BLOCKS, a->D, a->kin,
                      a->dW1, a->db1, (int)a->accumulate);
   ALIGNN_LAUNCH_CHECK("enc_bwd_stage2");
   return ALIGNN_OK;

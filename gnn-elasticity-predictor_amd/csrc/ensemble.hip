@@ -75,7 +75,7 @@ extern "C" int alignn_ensemble_moments(int32_t M, int64_t B, int32_t T, const fl
   if (B == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t n = B * T;
-  hipLaunchKernelGGL(ensemble_moments_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, B, T, heads,
+  launch(ensemble_moments_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, B, T, heads,
                      member_stride, ldh, min_logvar_floor, log_means, log_stds, mean_z, std_z, mean_orig, std_lin,
                      lo90, hi90);
   ALIGNN_LAUNCH_CHECK("ensemble_moments_kernel");
@@ -87,7 +87,7 @@ extern "C" int alignn_member_mean_f32(int32_t M, int64_t n, const float* x, int6
   if (M < 1 || n < 0) return ALIGNN_E_BAD_SHAPE;
   if (n == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(member_mean_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, n, x, member_stride,
+  launch(member_mean_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, n, x, member_stride,
                      out);
   ALIGNN_LAUNCH_CHECK("member_mean_kernel");
   return ALIGNN_OK;

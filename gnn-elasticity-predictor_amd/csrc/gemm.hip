@@ -288,13 +288,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 template <int BM, int BN, bool A_KC, bool B_KC>
 static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
   if (bf) {
-    if (bk == 64) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
+    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
+    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
   } else {
-    if (bk == 64) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
+    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
+    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
   }
 }
 
@@ -451,7 +451,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (pl.split > 1) {
     int64_t total = nbatch_out * a->M * a->N;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
+    launch(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");
   }
   return ALIGNN_OK;
@@ -502,13 +502,13 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
   nparts = (int)((M + rows_per - 1) / rows_per);
   if (nparts < 1) nparts = 1;
   if (M == 0) {
-    hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, 0, N, out, accumulate);
+    launch(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, 0, N, out, accumulate);
     ALIGNN_LAUNCH_CHECK("colsum_stage2");
     return ALIGNN_OK;
   }
-  hipLaunchKernelGGL(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
+  launch(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
   ALIGNN_LAUNCH_CHECK("colsum_stage1");
-  hipLaunchKernelGGL(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
+  launch(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
   ALIGNN_LAUNCH_CHECK("colsum_stage2");
   return ALIGNN_OK;
 }

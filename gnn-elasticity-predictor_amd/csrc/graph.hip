@@ -149,15 +149,15 @@ static int build_csr(const K* keys, int64_t m, int64_t n, int32_t* off, int32_t*
   hipError_t he = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)n, s);
   if (he != hipSuccess) return hip_status(he, "hipMemsetAsync");
   if (m > 0) {
-    hipLaunchKernelGGL(csr_count<K>, dim3(grid_for(m)), dim3(256), 0, s, keys, m, n, cnt, err);
+    launch(csr_count<K>, dim3(grid_for(m)), dim3(256), 0, s, keys, m, n, cnt, err);
     ALIGNN_LAUNCH_CHECK("csr_count");
   }
-  hipLaunchKernelGGL(csr_scan, dim3(1), dim3(1024), 0, s, cnt, n, off, cursor);
+  launch(csr_scan, dim3(1), dim3(1024), 0, s, cnt, n, off, cursor);
   ALIGNN_LAUNCH_CHECK("csr_scan");
   if (m > 0) {
-    hipLaunchKernelGGL(csr_fill<K>, dim3(grid_for(m)), dim3(256), 0, s, keys, m, n, cursor, perm);
+    launch(csr_fill<K>, dim3(grid_for(m)), dim3(256), 0, s, keys, m, n, cursor, perm);
     ALIGNN_LAUNCH_CHECK("csr_fill");
-    hipLaunchKernelGGL(csr_sort_segments, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, off, n, perm);
+    launch(csr_sort_segments, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, off, n, perm);
     ALIGNN_LAUNCH_CHECK("csr_sort_segments");
   }
   return ALIGNN_OK;
@@ -180,7 +180,7 @@ extern "C" int alignn_graph_prep(const int64_t* edge_index, int64_t m, int64_t n
   int rc = build_csr<int64_t>(dst, m, n, off_dst, perm_dst, workspace, err_flag, s);
   if (rc) return rc;
   if (m > 0) {
-    hipLaunchKernelGGL(csr_endpoints, dim3(grid_for(m)), dim3(256), 0, s, src, dst, perm_dst, off_dst, n, m, src_at, dst_at);
+    launch(csr_endpoints, dim3(grid_for(m)), dim3(256), 0, s, src, dst, perm_dst, off_dst, n, m, src_at, dst_at);
     ALIGNN_LAUNCH_CHECK("csr_endpoints");
   }
   // Source-side CSR over target-sorted positions: keys = src_at.
@@ -192,7 +192,7 @@ extern "C" int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int3
   if (rows < 0 || cols < 0) return ALIGNN_E_BAD_SHAPE;
   if (rows == 0 || cols == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
+  launch(gather_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
                      out, ld_out);
   ALIGNN_LAUNCH_CHECK("gather_rows_kernel");
   return ALIGNN_OK;
@@ -203,7 +203,7 @@ extern "C" int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int
   if (rows < 0 || cols < 0) return ALIGNN_E_BAD_SHAPE;
   if (rows == 0 || cols == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
+  launch(scatter_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
                      out, ld_out, accumulate);
   ALIGNN_LAUNCH_CHECK("scatter_rows_kernel");
   return ALIGNN_OK;

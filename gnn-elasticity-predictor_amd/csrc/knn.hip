@@ -121,7 +121,7 @@ extern "C" int alignn_col_center_sq_f32(const float* Z, int64_t n, int32_t D, co
                                         void* stream) {
   if (n < 0 || D <= 0) return ALIGNN_E_BAD_SHAPE;
   if (n == 0) return ALIGNN_OK;
-  hipLaunchKernelGGL(col_center_sq_kernel, dim3(knn_grid(n * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  launch(col_center_sq_kernel, dim3(knn_grid(n * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      Z, n, D, colsum, out);
   ALIGNN_LAUNCH_CHECK("col_center_sq_kernel");
   return ALIGNN_OK;
@@ -131,7 +131,7 @@ extern "C" int alignn_standardize_f32(const float* Z, int64_t n, int32_t D, cons
                                       float* out, void* stream) {
   if (n < 0 || D <= 0) return ALIGNN_E_BAD_SHAPE;
   if (n == 0) return ALIGNN_OK;
-  hipLaunchKernelGGL(standardize_kernel, dim3(knn_grid(n * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  launch(standardize_kernel, dim3(knn_grid(n * D)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      Z, n, D, colsum, ssq, out);
   ALIGNN_LAUNCH_CHECK("standardize_kernel");
   return ALIGNN_OK;
@@ -140,7 +140,7 @@ extern "C" int alignn_standardize_f32(const float* Z, int64_t n, int32_t D, cons
 extern "C" int alignn_row_sqnorm_f32(const float* Zs, int64_t n, int32_t D, float* r, void* stream) {
   if (n < 0 || D <= 0) return ALIGNN_E_BAD_SHAPE;
   if (n == 0) return ALIGNN_OK;
-  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+  launch(row_sqnorm_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), Zs, n, D, r);
   ALIGNN_LAUNCH_CHECK("row_sqnorm_kernel");
   return ALIGNN_OK;
@@ -154,7 +154,7 @@ extern "C" int alignn_knn_select_weights(const float* G, int64_t ldg, const floa
     return ALIGNN_E_BAD_SHAPE;
   }
   if (rows == 0) return ALIGNN_OK;
-  hipLaunchKernelGGL(knn_select_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+  launch(knn_select_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), G, ldg, r, n, row0, rows, k, Y, T, eps, alpha, beta, nbr,
                      w_raw);
   ALIGNN_LAUNCH_CHECK("knn_select_kernel");

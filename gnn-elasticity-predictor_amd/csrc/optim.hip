@@ -85,8 +85,8 @@ extern "C" int alignn_grad_norm_f32(const float* g, int64_t n, float* norm, floa
   if (n < 0 || !norm || !workspace) return ALIGNN_E_BAD_SHAPE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(kNormBlocks, (n + 4095) / 4096));
-  hipLaunchKernelGGL(sumsq_stage1, dim3(parts), dim3(256), 0, s, g, n, workspace);
-  hipLaunchKernelGGL(sumsq_stage2, dim3(1), dim3(256), 0, s, workspace, parts, norm);
+  launch(sumsq_stage1, dim3(parts), dim3(256), 0, s, g, n, workspace);
+  launch(sumsq_stage2, dim3(1), dim3(256), 0, s, workspace, parts, norm);
   ALIGNN_LAUNCH_CHECK("grad norm");
   return ALIGNN_OK;
 }
@@ -96,10 +96,10 @@ extern "C" int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t 
                                 const float* norm, float max_norm, float* step, void* stream) {
   if (n < 0 || split < 0 || split > n || !step) return ALIGNN_E_BAD_SHAPE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  launch(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   if (n > 0)
-    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, split, lr0, lr1,
+    launch(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, split, lr0, lr1,
                        weight_decay, beta1, beta2, (float)eps, norm, max_norm, step);
   ALIGNN_LAUNCH_CHECK("adamw_kernel");
   return ALIGNN_OK;

@@ -1,0 +1,271 @@
+// plan.hip — launch plans: a training step recorded once and re-issued from C++.
+//
+// The step is ~300 kernels on two streams (critical path + weight-gradient side stream).  Issued
+// from Python, each launch costs ~15 us of host work (tensor views, ctypes argument structs), which
+// is more than the GPU needs for most of them: the step ran host-bound (host 4.4 ms vs device
+// 4.45 ms critical path, profiles/r01/v10_diag_overlap.log).  ROCm's own graph replay of the same
+// capture ran slower on the device (5.5 ms: the two streams' branches lose their concurrency).
+//
+// A plan is recorded while the caller runs one step: every launch() of the library appends
+// (kernel, grid, block, LDS bytes, stream slot, argument bytes), and the caller notes each
+// cross-stream ordering edge (alignn_plan_note_wait, after its own event wait).  Replay walks the
+// entries: hipLaunchKernel with the stored arguments, hipEventRecord + hipStreamWaitEvent for the
+// edges, so the device sees the same kernels, order and stream concurrency as the eager step.
+// Stream slot 0 is the stream that was current at alignn_plan_begin; replay puts the caller's
+// stream there, every other slot keeps its recorded stream.  Buffers are referenced by address:
+// the caller keeps every tensor the step touched alive and in place (trainer.py records inside a
+// torch graph capture, whose private memory pool does that).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace alignn {
+
+bool g_recording = false;
+
+struct PlanEntry {
+  const void* func;     // kernel (nullptr: stream-ordering edge or timestamp)
+  dim3 grid, block;
+  uint32_t shmem;
+  int slot;             // stream slot (kernel) / waiting stream slot (edge)
+  int src;              // edge: slot whose work is waited for
+  int event;            // edge: index into Plan::events; timestamp: -1 - index into Plan::stamps
+  size_t arg0, nargs;   // kernel: first index into Plan::arg_off, count
+};
+
+struct Plan {
+  std::vector<PlanEntry> entries;
+  std::vector<unsigned char> args;   // argument bytes (each at its type's alignment, max 16)
+  std::vector<size_t> arg_off;
+  std::vector<hipStream_t> streams;  // recorded handles; [0] replaced by the replay stream
+  std::vector<hipEvent_t> events;
+  std::vector<hipEvent_t> stamps;    // timing events (roofline probes around chosen launches)
+  int launches = 0;
+};
+
+static Plan* g_plan = nullptr;
+
+}  // namespace alignn
+extern "C" int alignn_plan_destroy(void* plan);
+namespace alignn {
+
+static int slot_of(Plan* p, hipStream_t s) {
+  for (size_t i = 0; i < p->streams.size(); ++i)
+    if (p->streams[i] == s) return (int)i;
+  p->streams.push_back(s);
+  return (int)p->streams.size() - 1;
+}
+
+void record_launch(const void* func, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, void* const* args,
+                   const size_t* sizes, const size_t* aligns, int nargs) {
+  Plan* p = g_plan;
+  if (!p) return;
+  PlanEntry e{};
+  e.func = func;
+  e.grid = grid;
+  e.block = block;
+  e.shmem = shmem;
+  e.slot = slot_of(p, s);
+  e.arg0 = p->arg_off.size();
+  e.nargs = (size_t)nargs;
+  for (int i = 0; i < nargs; ++i) {
+    size_t off = p->args.size();
+    const size_t al = aligns[i] > 16 ? 16 : aligns[i];
+    off = (off + al - 1) / al * al;
+    p->args.resize(off + sizes[i]);
+    std::memcpy(p->args.data() + off, args[i], sizes[i]);
+    p->arg_off.push_back(off);
+  }
+  p->entries.push_back(e);
+  p->launches++;
+}
+
+__global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ x, int64_t n, float v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+
+__global__ __launch_bounds__(256) void copy_f32_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                       int64_t n) {
+  const int64_t n4 = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) ? 0 : n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+  for (int64_t i = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+static unsigned blocks_for(int64_t n) { return (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 255) / 256), 8192); }
+
+}  // namespace alignn
+
+using namespace alignn;
+
+extern "C" int alignn_plan_begin(void* stream) {
+  if (g_plan) {
+    set_error("plan_begin: a plan is already being recorded");
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  g_plan = new Plan();
+  g_plan->streams.push_back(reinterpret_cast<hipStream_t>(stream));
+  g_recording = true;
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_plan_note_wait(void* dst_stream, void* src_stream) {
+  if (!g_plan) return ALIGNN_OK;
+  Plan* p = g_plan;
+  PlanEntry e{};
+  e.func = nullptr;
+  e.slot = slot_of(p, reinterpret_cast<hipStream_t>(dst_stream));
+  e.src = slot_of(p, reinterpret_cast<hipStream_t>(src_stream));
+  e.event = (int)p->events.size();
+  p->events.push_back(nullptr);
+  p->entries.push_back(e);
+  return ALIGNN_OK;
+}
+
+// Timestamp entry on `stream` (replay records a timing event there); returns its index, or -1
+// when no plan is being recorded.
+extern "C" int alignn_plan_note_timestamp(void* stream) {
+  if (!g_plan) return -1;
+  Plan* p = g_plan;
+  PlanEntry e{};
+  e.func = nullptr;
+  e.slot = slot_of(p, reinterpret_cast<hipStream_t>(stream));
+  const int idx = (int)p->stamps.size();
+  e.event = -1 - idx;
+  p->stamps.push_back(nullptr);
+  p->entries.push_back(e);
+  return idx;
+}
+
+extern "C" void* alignn_plan_end(void) {
+  Plan* p = g_plan;
+  g_plan = nullptr;
+  g_recording = false;
+  if (!p) {
+    set_error("plan_end: no plan is being recorded");
+    return nullptr;
+  }
+  bool ok = true;
+  for (auto& ev : p->events) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+  for (auto& ev : p->stamps) ok = ok && hipEventCreate(&ev) == hipSuccess;
+  if (!ok) {
+    set_error("plan_end: event creation failed");
+    alignn_plan_destroy(p);
+    return nullptr;
+  }
+  return p;
+}
+
+extern "C" int alignn_plan_abort(void) {
+  delete g_plan;
+  g_plan = nullptr;
+  g_recording = false;
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_plan_info(const void* plan, int64_t* launches, int64_t* waits, int64_t* streams,
+                                int64_t* arg_bytes) {
+  const Plan* p = reinterpret_cast<const Plan*>(plan);
+  if (!p) return ALIGNN_E_BAD_SHAPE;
+  if (launches) *launches = p->launches;
+  if (waits) *waits = (int64_t)p->events.size();
+  if (streams) *streams = (int64_t)p->streams.size();
+  if (arg_bytes) *arg_bytes = (int64_t)p->args.size();
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_plan_replay(void* plan, void* stream) {
+  Plan* p = reinterpret_cast<Plan*>(plan);
+  if (!p) return ALIGNN_E_BAD_SHAPE;
+  if (g_recording) {
+    set_error("plan_replay: not allowed while a plan is being recorded");
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  p->streams[0] = reinterpret_cast<hipStream_t>(stream);
+  std::vector<void*> ptrs;
+  for (const PlanEntry& e : p->entries) {
+    if (e.func) {
+      ptrs.resize(e.nargs + 1);
+      for (size_t i = 0; i < e.nargs; ++i) ptrs[i] = p->args.data() + p->arg_off[e.arg0 + i];
+      hipError_t r = hipLaunchKernel(e.func, e.grid, e.block, ptrs.data(), e.shmem, p->streams[e.slot]);
+      if (r != hipSuccess) return hip_status(r, "plan_replay: hipLaunchKernel");
+    } else if (e.event < 0) {
+      hipError_t r = hipEventRecord(p->stamps[-1 - e.event], p->streams[e.slot]);
+      if (r != hipSuccess) return hip_status(r, "plan_replay: timestamp");
+    } else {
+      hipError_t r = hipEventRecord(p->events[e.event], p->streams[e.src]);
+      if (r == hipSuccess) r = hipStreamWaitEvent(p->streams[e.slot], p->events[e.event], 0);
+      if (r != hipSuccess) return hip_status(r, "plan_replay: stream edge");
+    }
+  }
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_plan_destroy(void* plan) {
+  Plan* p = reinterpret_cast<Plan*>(plan);
+  if (!p) return ALIGNN_OK;
+  for (auto& ev : p->events)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : p->stamps)
+    if (ev) (void)hipEventDestroy(ev);
+  delete p;
+  return ALIGNN_OK;
+}
+
+// Device time between two timestamps of the last replay (call after it has completed).
+extern "C" int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms) {
+  Plan* p = reinterpret_cast<Plan*>(plan);
+  if (!p || i0 < 0 || i1 < 0 || i0 >= (int)p->stamps.size() || i1 >= (int)p->stamps.size() || !ms)
+    return ALIGNN_E_BAD_SHAPE;
+  hipError_t r = hipEventElapsedTime(ms, p->stamps[i0], p->stamps[i1]);
+  if (r != hipSuccess) return hip_status(r, "plan_elapsed_ms");
+  return ALIGNN_OK;
+}
+
+// Node census of a captured HIP graph: kernel nodes and everything else (memcpy, memset, host,
+// child graphs ...; event and empty nodes are not counted).  A plan recorded during that capture
+// is complete when its launch count equals the kernel count and `other` is 0.
+extern "C" int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  hipError_t r = hipGraphGetNodes(g, nullptr, &n);
+  if (r != hipSuccess) return hip_status(r, "graph_census: hipGraphGetNodes");
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) {
+    r = hipGraphGetNodes(g, nodes.data(), &n);
+    if (r != hipSuccess) return hip_status(r, "graph_census: hipGraphGetNodes");
+  }
+  int64_t k = 0, o = 0;
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    r = hipGraphNodeGetType(nodes[i], &t);
+    if (r != hipSuccess) return hip_status(r, "graph_census: hipGraphNodeGetType");
+    if (t == hipGraphNodeTypeKernel) ++k;
+    else if (t != hipGraphNodeTypeEmpty && t != hipGraphNodeTypeWaitEvent && t != hipGraphNodeTypeEventRecord) ++o;
+  }
+  *kernels = k;
+  *other = o;
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_fill_f32(float* x, int64_t n, float value, void* stream) {
+  if (n < 0) return ALIGNN_E_BAD_SHAPE;
+  if (n == 0) return ALIGNN_OK;
+  launch(fill_f32_kernel, dim3(blocks_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, n, value);
+  ALIGNN_LAUNCH_CHECK("fill_f32_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream) {
+  if (n < 0) return ALIGNN_E_BAD_SHAPE;
+  if (n == 0) return ALIGNN_OK;
+  launch(copy_f32_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dst,
+         src, n);
+  ALIGNN_LAUNCH_CHECK("copy_f32_kernel");
+  return ALIGNN_OK;
+}

@@ -345,10 +345,10 @@ extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((n + 3) / 4));
   switch (vpl) {
-    case 1: hipLaunchKernelGGL(gate_ln_fwd_kernel<1>, g, dim3(256), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(gate_ln_fwd_kernel<2>, g, dim3(256), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(gate_ln_fwd_kernel<4>, g, dim3(256), 0, s, p); break;
-    default: hipLaunchKernelGGL(gate_ln_fwd_kernel<8>, g, dim3(256), 0, s, p); break;
+    case 1: launch(gate_ln_fwd_kernel<1>, g, dim3(256), 0, s, p); break;
+    case 2: launch(gate_ln_fwd_kernel<2>, g, dim3(256), 0, s, p); break;
+    case 4: launch(gate_ln_fwd_kernel<4>, g, dim3(256), 0, s, p); break;
+    default: launch(gate_ln_fwd_kernel<8>, g, dim3(256), 0, s, p); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_fwd_kernel");
   return ALIGNN_OK;
@@ -380,25 +380,25 @@ extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
   switch (vpl) {
-    case 1: hipLaunchKernelGGL(gate_ln_bwd_kernel<1>, g, dim3(256), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(gate_ln_bwd_kernel<2>, g, dim3(256), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(gate_ln_bwd_kernel<4>, g, dim3(256), 0, s, p); break;
-    default: hipLaunchKernelGGL(gate_ln_bwd_kernel<8>, g, dim3(256), 0, s, p); break;
+    case 1: launch(gate_ln_bwd_kernel<1>, g, dim3(256), 0, s, p); break;
+    case 2: launch(gate_ln_bwd_kernel<2>, g, dim3(256), 0, s, p); break;
+    case 4: launch(gate_ln_bwd_kernel<4>, g, dim3(256), 0, s, p); break;
+    default: launch(gate_ln_bwd_kernel<8>, g, dim3(256), 0, s, p); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
   // d_wbeta[3D] | d_ln_w[D] | d_ln_b[D]: one 5D-wide fixed-order reduction when the three are
   // adjacent in memory (the flat gradient layout), else three.
   const unsigned strips3 = (unsigned)((3 * D + 63) / 64), strips1 = (unsigned)((D + 63) / 64);
   if (d_ln_w == d_wbeta + 3 * D && d_ln_b == d_ln_w + D) {
-    hipLaunchKernelGGL(colsum_stage2<0>, dim3((unsigned)((5 * D + 63) / 64)), dim3(kColsumThreads), 0, s, workspace,
+    launch(colsum_stage2<0>, dim3((unsigned)((5 * D + 63) / 64)), dim3(kColsumThreads), 0, s, workspace,
                        nwaves,
                        (int64_t)5 * D, d_wbeta, 1);
   } else {
     // partial rows are 5D wide: view them through column offsets with row stride 5D via a
     // compacting pass is unnecessary — reduce each slice with its own launch on a shifted base.
-    hipLaunchKernelGGL(gate_ln_slice_reduce, dim3(strips3), dim3(256), 0, s, workspace, nwaves, 5 * D, 0, 3 * D, d_wbeta);
-    hipLaunchKernelGGL(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, nwaves, 5 * D, 3 * D, D, d_ln_w);
-    hipLaunchKernelGGL(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, nwaves, 5 * D, 4 * D, D, d_ln_b);
+    launch(gate_ln_slice_reduce, dim3(strips3), dim3(256), 0, s, workspace, nwaves, 5 * D, 0, 3 * D, d_wbeta);
+    launch(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, nwaves, 5 * D, 3 * D, D, d_ln_w);
+    launch(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, nwaves, 5 * D, 4 * D, D, d_ln_b);
   }
   ALIGNN_LAUNCH_CHECK("gate_ln param-grad reduction");
   return ALIGNN_OK;
@@ -418,7 +418,7 @@ extern "C" int alignn_readout_feats_fwd(int64_t B, int32_t D, const float* h, co
                                         uint64_t seed, void* stream) {
   if (B == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(readout_fwd_kernel, dim3((unsigned)B), dim3(256), 0, s, B, D, h, ptr, global_x, gdim, sg, sgdim,
+  launch(readout_fwd_kernel, dim3((unsigned)B), dim3(256), 0, s, B, D, h, ptr, global_x, gdim, sg, sgdim,
                      feats, make_drop(drop_p, seed));
   ALIGNN_LAUNCH_CHECK("readout_fwd_kernel");
   return ALIGNN_OK;
@@ -430,7 +430,7 @@ extern "C" int alignn_readout_pool_bwd(int64_t B, int64_t N, int32_t D, const fl
   (void)B;
   if (N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid_for(N * D)), dim3(256), 0, s, N, D, dfeats, ldf, ptr, batch, dh,
+  launch(pool_bwd_kernel, dim3(grid_for(N * D)), dim3(256), 0, s, N, D, dfeats, ldf, ptr, batch, dh,
                      accumulate, make_drop(drop_p, seed));
   ALIGNN_LAUNCH_CHECK("pool_bwd_kernel");
   return ALIGNN_OK;
@@ -440,7 +440,7 @@ extern "C" int alignn_dropout_f32(int64_t rows, int64_t cols, const float* x, in
                                   const float* relu_ref, int64_t ldr, float drop_p, uint64_t seed, void* stream) {
   if (rows * cols == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, rows, cols, x, ldx, y, ldy, relu_ref,
+  launch(dropout_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, rows, cols, x, ldx, y, ldy, relu_ref,
                      ldr, make_drop(drop_p, seed));
   ALIGNN_LAUNCH_CHECK("dropout_kernel");
   return ALIGNN_OK;
@@ -451,7 +451,7 @@ extern "C" int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64
                                  float l2, float* loss, float* dheads, int64_t lddh, void* stream) {
   if (B <= 0 || T <= 0) return ALIGNN_E_BAD_SHAPE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(hetero_nll_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, weights, log_means, log_stds,
+  launch(hetero_nll_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, weights, log_means, log_stds,
                      floor, l2, loss, dheads, lddh);
   ALIGNN_LAUNCH_CHECK("hetero_nll_kernel");
   return ALIGNN_OK;
@@ -460,7 +460,7 @@ extern "C" int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64
 extern "C" int alignn_add_noise_f32(int64_t n, float* x, float stdv, uint64_t seed, void* stream) {
   if (n == 0 || stdv == 0.f) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, x, stdv, seed, g_step_seed);
+  launch(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, x, stdv, seed, g_step_seed);
   ALIGNN_LAUNCH_CHECK("add_noise_kernel");
   return ALIGNN_OK;
 }

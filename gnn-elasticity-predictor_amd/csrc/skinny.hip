@@ -199,7 +199,7 @@ extern "C" int alignn_linear_smallk_f32(const float* X, int64_t ldx, int64_t M, 
   if (M == 0 || N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned blocks = (unsigned)((M + SK_ROWS - 1) / SK_ROWS);
-  hipLaunchKernelGGL(linear_smallk_kernel, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, N,
+  launch(linear_smallk_kernel, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, N,
                      (int)relu, out, ldo);
   ALIGNN_LAUNCH_CHECK("linear_smallk_kernel");
   return ALIGNN_OK;
@@ -234,7 +234,7 @@ extern "C" int alignn_gemm_tn_smalln_f32(const float* A, int64_t lda, int64_t K,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vec = (lda % 4 == 0 && M % 4 == 0 && aligned16p(A)) ? 1 : 0;
   if (K > 0) {
-    hipLaunchKernelGGL(tn_smalln_stage1, dim3((unsigned)chunks, (unsigned)((M + 255) / 256)), dim3(256), 0, s, A, lda,
+    launch(tn_smalln_stage1, dim3((unsigned)chunks, (unsigned)((M + 255) / 256)), dim3(256), 0, s, A, lda,
                        K, M, X, ldx, (int)N, rows_per, vec, workspace);
     ALIGNN_LAUNCH_CHECK("tn_smalln_stage1");
   } else {
@@ -243,7 +243,7 @@ extern "C" int alignn_gemm_tn_smalln_f32(const float* A, int64_t lda, int64_t K,
     chunks = 1;
   }
   const int64_t total = M * SN_SLOTS;
-  hipLaunchKernelGGL(tn_smalln_stage2, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, workspace, (int)chunks,
+  launch(tn_smalln_stage2, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, workspace, (int)chunks,
                      M, (int)N, C, ldc, colsum, (int)accumulate);
   ALIGNN_LAUNCH_CHECK("tn_smalln_stage2");
   return ALIGNN_OK;

@@ -1360,14 +1360,14 @@ static void launch_fwd(const FwdParams& p, const Sched& sc, const EncParams& en,
   if (items == 0) return;
   const dim3 grid((unsigned)items), block(256);
   if (km == 0 && (flags & ALIGNN_SCHED_COMPACT_REGS)) {
-    hipLaunchKernelGGL((tconv_fwd2_kernel<VPL, H>), grid, block, 0, s, p, sc);
+    launch((tconv_fwd2_kernel<VPL, H>), grid, block, 0, s, p, sc);
     return;
   }
   switch (km) {
-    case 0: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 0>), grid, block, 0, s, p, sc, en); break;
-    case 8: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 8>), grid, block, 0, s, p, sc, en); break;
-    case 12: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 12>), grid, block, 0, s, p, sc, en); break;
-    default: hipLaunchKernelGGL((tconv_fwd_kernel<VPL, H, 16>), grid, block, 0, s, p, sc, en); break;
+    case 0: launch((tconv_fwd_kernel<VPL, H, 0>), grid, block, 0, s, p, sc, en); break;
+    case 8: launch((tconv_fwd_kernel<VPL, H, 8>), grid, block, 0, s, p, sc, en); break;
+    case 12: launch((tconv_fwd_kernel<VPL, H, 12>), grid, block, 0, s, p, sc, en); break;
+    default: launch((tconv_fwd_kernel<VPL, H, 16>), grid, block, 0, s, p, sc, en); break;
   }
 }
 
@@ -1377,12 +1377,12 @@ static int launch_bwd_dst_km(const BwdDstParams& p, const Sched& sc, const EncPa
   const int64_t items = sc.items();
   if (KM == 0 && (flags & ALIGNN_SCHED_COMPACT_REGS)) {
     if (items > 0)
-      hipLaunchKernelGGL((tconv_bwd_dst2_kernel<VPL, H>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+      launch((tconv_bwd_dst2_kernel<VPL, H>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
     return ALIGNN_OK;
   }
   if (KM == 0) {
     if (items > 0)
-      hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, 0>), dim3((unsigned)items), dim3(256), 0, s, p, sc, en,
+      launch((tconv_bwd_dst_kernel<VPL, H, 0>), dim3((unsigned)items), dim3(256), 0, s, p, sc, en,
                          nullptr);
     return ALIGNN_OK;
   }
@@ -1396,10 +1396,10 @@ static int launch_bwd_dst_km(const BwdDstParams& p, const Sched& sc, const EncPa
               (long long)enc->workspace_elems, (long long)per);
     return ALIGNN_E_WORKSPACE;
   }
-  hipLaunchKernelGGL((tconv_bwd_dst_kernel<VPL, H, KM>), dim3((unsigned)G), dim3(256), 0, s, p, sc, en,
+  launch((tconv_bwd_dst_kernel<VPL, H, KM>), dim3((unsigned)G), dim3(256), 0, s, p, sc, en,
                      enc->workspace);
   const int64_t outs = (int64_t)(en.kin + 1) * p.D;
-  hipLaunchKernelGGL(enc_grad_reduce, dim3((unsigned)((outs + 63) / 64)), dim3(1024), 0, s, enc->workspace, (int)G,
+  launch(enc_grad_reduce, dim3((unsigned)((outs + 63) / 64)), dim3(1024), 0, s, enc->workspace, (int)G,
                      KM, p.D, en.kin, enc->dw1, enc->db1, enc->accumulate);
   return ALIGNN_OK;
 }
@@ -1427,7 +1427,7 @@ static int64_t bwd_ws_elems(int km, int D) {
 
 template <int VPL, int H>
 static void launch_bwd_src(const BwdSrcParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  launch((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
 }
 
 static Sched make_sched(const AlignnSchedule* sc, int64_t n) {

@@ -385,6 +385,39 @@ int alignn_knn_select_weights(const float* G, int64_t ldg, const float* r, int64
                               int32_t k, const float* Y, int32_t T, float eps, float alpha, float beta, int64_t* nbr,
                               float* w_raw, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Launch plans (native step executor).  Replaces the per-batch host loop of train_epoch_hetero
+ * (train.py:639-699: model(batch), loss.backward(), clip_grad_norm_, optimizer.step()) once the
+ * step has been recorded: the engine's ~300 launches are re-issued from C++, no Python in between.
+ * alignn_plan_begin(stream): start recording; every launch of this library is executed as usual
+ *   and appended to the plan; `stream` becomes slot 0 (replaced by the replay stream).
+ * alignn_plan_note_wait(dst, src): append the ordering edge "dst waits for src's work so far"
+ *   (the caller performs the wait itself while recording; no-op when not recording).
+ * alignn_plan_end(): finish, returns the plan (NULL on error). alignn_plan_abort(): drop it.
+ * alignn_plan_replay(plan, stream): issue the recorded launches and edges (slot 0 -> stream).
+ *   Every buffer the recorded step touched must still be allocated at the same address.
+ * alignn_plan_info: launches, edges, distinct streams, stored argument bytes.
+ * alignn_plan_note_timestamp(stream): while recording, append a timing-event record on `stream`
+ *   and return its index (-1 when not recording); alignn_plan_elapsed_ms(plan, i0, i1, &ms): the
+ *   device time between two timestamps of the last (completed) replay (roofline probes).
+ * alignn_graph_census(hipGraph_t, &kernels, &other): node counts of a captured graph, to check
+ *   that a plan recorded during that capture holds every kernel (other == 0).
+ * alignn_fill_f32 / alignn_copy_f32: x[0:n] = value; dst[0:n] = src[0:n] (plan-recordable
+ *   replacements for torch's zero_/copy_ inside the step).
+ * ---------------------------------------------------------------------------------------- */
+int alignn_plan_begin(void* stream);
+int alignn_plan_note_wait(void* dst_stream, void* src_stream);
+void* alignn_plan_end(void);
+int alignn_plan_abort(void);
+int alignn_plan_replay(void* plan, void* stream);
+int alignn_plan_info(const void* plan, int64_t* launches, int64_t* waits, int64_t* streams, int64_t* arg_bytes);
+int alignn_plan_destroy(void* plan);
+int alignn_plan_note_timestamp(void* stream);
+int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms);
+int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other);
+int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
+int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
