@@ -58,6 +58,30 @@ struct TileLoader {
   static constexpr int F4 = ROWS * BKT / 4 / 256;  // float4 per thread
   static constexpr int KP = BKT + 4;               // padded k-row of the [row][k] image
   float4 r[F4];
+  const float* base[F4];                           // fast path: this thread's float4 at k = kb
+
+  // Fast path (vectorisable operand, full stage): per-thread addresses are formed once; a stage
+  // is F4 plain float4 loads, no bounds branches.  KC: rows past the end are clamped to the last
+  // row (they only feed output rows that are never stored).  !KC: only for interior tiles
+  // (row0 + ROWS <= rows), the caller checks.
+  __device__ __forceinline__ void setup_fast(const float* __restrict__ P, int64_t srow, int64_t sk, int64_t row0,
+                                             int64_t rows, int64_t kb) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      if (KC) {
+        const int64_t gr = min(row0 + idx / (BKT / 4), rows - 1);
+        base[i] = P + gr * srow + kb + (idx % (BKT / 4)) * 4;
+      } else {
+        base[i] = P + (kb + idx / (ROWS / 4)) * sk + row0 + (idx % (ROWS / 4)) * 4;
+      }
+    }
+  }
+  // k0 - kb = koff; KC operands have sk == 1 on the fast path
+  __device__ __forceinline__ void load_fast(int64_t koff, int64_t sk) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) r[i] = *reinterpret_cast<const float4*>(base[i] + (KC ? koff : koff * sk));
+  }
 
   __device__ __forceinline__ void load(const float* __restrict__ P, int64_t srow, int64_t sk, int64_t row0,
                                        int64_t rows, int64_t k0, int64_t kend, int vec) {
@@ -151,7 +175,7 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, 
   return v;
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF>
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF, bool RB>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
   constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
@@ -160,19 +184,19 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int64_t tiles_n = (p.N + BN - 1) / BN;
   const int64_t tile = blockIdx.x;
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-  const int64_t b = p.reduce_batch ? 0 : blockIdx.z / p.split_k;
+  const int64_t b = RB ? 0 : blockIdx.z / p.split_k;
   const int sidx = blockIdx.z % p.split_k;
-  const int64_t Ktot = p.reduce_batch ? p.K * p.batch : p.K;
+  const int64_t Ktot = RB ? p.K * p.batch : p.K;
   const int64_t kb = (int64_t)sidx * p.kchunk;
   const int64_t ke = min(Ktot, kb + p.kchunk);
 
   const float* A = p.A + b * p.sab;
   const float* B = p.B + b * p.sbb;
-  // (batch, local k) of a global k index; identity unless the batch is reduced
-  auto tileA = [&](int64_t k0) { return p.reduce_batch ? p.A + (k0 / p.K) * p.sab : A; };
-  auto tileB = [&](int64_t k0) { return p.reduce_batch ? p.B + (k0 / p.K) * p.sbb : B; };
-  auto kloc = [&](int64_t k0) { return p.reduce_batch ? k0 % p.K : k0; };
-  auto kend = [&](int64_t k0) { return p.reduce_batch ? p.K : ke; };
+  // (batch, local k) of a global k index; identity unless the batch is reduced (RB)
+  auto tileA = [&](int64_t k0) { return RB ? p.A + (k0 / p.K) * p.sab : A; };
+  auto tileB = [&](int64_t k0) { return RB ? p.B + (k0 / p.K) * p.sbb : B; };
+  auto kloc = [&](int64_t k0) { return RB ? k0 % p.K : k0; };
+  auto kend = [&](int64_t k0) { return RB ? p.K : ke; };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
 
@@ -186,9 +210,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 
   TileLoader<BM, A_KC, BKT> la;
   TileLoader<BN, B_KC, BKT> lb;
-  // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
-  la.load(tileA(kb), p.sam, p.sak, m0, p.M, kloc(kb), kend(kb), p.vecA);
-  lb.load(tileB(kb), p.sbn, p.sbk, n0, p.N, kloc(kb), kend(kb), p.vecB);
+  // fast loads (block-uniform): vectorisable operand, not batch-reduced, interior tile for a
+  // row-contiguous operand; then every full stage [k0, k0 + BKT) <= ke takes them
+  const bool fastA = !RB && p.vecA && (A_KC || m0 + BM <= p.M);
+  const bool fastB = !RB && p.vecB && (B_KC || n0 + BN <= p.N);
+  if (fastA) la.setup_fast(A, p.sam, p.sak, m0, p.M, kb);
+  if (fastB) lb.setup_fast(B, p.sbn, p.sbk, n0, p.N, kb);
+  auto load_stage = [&](int64_t k0) {
+    const bool full = k0 + BKT <= ke;
+    // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
+    if (fastA && full) la.load_fast(k0 - kb, p.sak);
+    else la.load(tileA(k0), p.sam, p.sak, m0, p.M, kloc(k0), kend(k0), p.vecA);
+    if (fastB && full) lb.load_fast(k0 - kb, p.sbk);
+    else lb.load(tileB(k0), p.sbn, p.sbk, n0, p.N, kloc(k0), kend(k0), p.vecB);
+  };
+  load_stage(kb);
   la.store(smem);
   lb.store(smem + LA);
   __syncthreads();
@@ -196,10 +232,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   int cur = 0;
   for (int64_t k0 = kb; k0 < ke; k0 += BKT) {
     const bool more = k0 + BKT < ke;
-    if (more) {
-      la.load(tileA(k0 + BKT), p.sam, p.sak, m0, p.M, kloc(k0 + BKT), kend(k0 + BKT), p.vecA);
-      lb.load(tileB(k0 + BKT), p.sbn, p.sbk, n0, p.N, kloc(k0 + BKT), kend(k0 + BKT), p.vecB);
-    }
+    if (more) load_stage(k0 + BKT);
     const float* As = smem + cur * (LA + LB);
     const float* Bs = As + LA;
 #pragma unroll
@@ -285,17 +318,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
+template <int BM, int BN, bool A_KC, bool B_KC, bool RB>
+static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
+  if (bf) {
+    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true, RB>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true, RB>), grid, dim3(256), 0, s, p);
+    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true, RB>), grid, dim3(256), 0, s, p);
+  } else {
+    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false, RB>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false, RB>), grid, dim3(256), 0, s, p);
+    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false, RB>), grid, dim3(256), 0, s, p);
+  }
+}
+
 template <int BM, int BN, bool A_KC, bool B_KC>
 static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
-  if (bf) {
-    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
-    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
-  } else {
-    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
-    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
-  }
+  if (p.reduce_batch) launch_rb<BM, BN, A_KC, B_KC, true>(p, grid, bk, bf, s);
+  else launch_rb<BM, BN, A_KC, B_KC, false>(p, grid, bk, bf, s);
 }
 
 template <int BM, int BN>
