@@ -364,38 +364,33 @@ struct GemmPlan {
   int64_t kchunk;
 };
 
-// Tile shape: minimise (tile waves over the CUs) x (tile area) x (per-flop cost of the shape), so a
-// launch of 1.4 waves of 128x128 tiles loses to 2.8 waves of 128x64.  Split-K only when the grid
-// stays under half the CUs and K is long (>= 1024): each split keeps >= 256 of K, and the grid aims
-// at one workgroup per CU.  Small-K GEMMs never split (the reduce would cost more than it saves).
+// Automatic plan, fitted to a sweep of every product of the training step on MI355X
+// (tools/gemm_bench.py, profiles/r01/v11_gemm_sweep.log; all tiles x stage depths x splits):
+//  * tile 64x64 — it was the fastest tile for every one of the 52 shapes (these products are
+//    latency-bound at 1-20 us; more, smaller workgroups hide more of it);
+//  * split-K toward one workgroup per CU (tiles x split ~ CUs), each split >= 32 deep, when the
+//    product is long (K >= 512) or its grid tiny (< 32 tiles); short-K grids of >= 32 tiles do
+//    not split (the reduce costs more than it saves);
+//  * 64-deep stages (a quarter of the global round trips) when a split is >= 128 deep and the
+//    grid <= 2 x CUs; 16-deep otherwise (large grids keep more workgroups resident with them).
+// Explicit tile / stage bits (tuning) override the choice.
 static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int requested, int tile) {
   const int cus = device_cus();
   static const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
-  static const double eff[4] = {1.0, 1.1, 1.1, 1.35};
   GemmPlan pl{64, 64, 1, 16, 0};
-  double best = -1.0;
-  int64_t best_tiles = 0;
-  for (int c = 0; c < 4; ++c) {
-    const int bm = cand[c][0], bn = cand[c][1];
-    const int shape = tile & 15;  // bits 16/32: stage depth, bit 64: bf16 compute
-    if (shape >= 1 && shape <= 4 && c != shape - 1) continue;
-    if (shape == 0 && ((bm == 128 && M <= 64) || (bn == 128 && N <= 64))) continue;
-    const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * nb;
-    const double cost = (double)((tiles + cus - 1) / cus) * bm * bn * eff[c];
-    if (best < 0 || cost < best) {
-      best = cost;
-      pl.bm = bm;
-      pl.bn = bn;
-      best_tiles = tiles;
-    }
+  const int shape = tile & 15;  // bits 16/32/128: stage depth, bit 64: bf16 compute
+  if (shape >= 1 && shape <= 4) {
+    pl.bm = cand[shape - 1][0];
+    pl.bn = cand[shape - 1][1];
   }
+  const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn) * nb;
   int split = requested;
   if (split <= 0) {
     split = 1;
-    if (best_tiles * 2 < cus && Ktot >= 1024) {
-      const int64_t want = (cus + best_tiles - 1) / best_tiles;
-      const int64_t maxs = Ktot / 256;
-      split = (int)std::max<int64_t>(1, std::min(want, maxs));
+    if (Ktot >= 512 || tiles < 32) {
+      const int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
+      const int64_t maxs = std::max<int64_t>(1, Ktot / 32);
+      split = (int)std::min(want, maxs);
     }
   }
   if (Ktot == 0) split = 1;
@@ -406,9 +401,10 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   if (split < 1) split = 1;
   pl.split = split;
   pl.kchunk = kchunk;
-  // K depth of a pipeline stage (tile bit 4 selects 32: half the barriers per flop; the automatic
-  // plan keeps 16 until the 32-deep stage has been measured on MI355X)
-  pl.bk = (tile & ALIGNN_GEMM_BK64) ? 64 : (tile & ALIGNN_GEMM_BK32) ? 32 : 16;
+  if (tile & ALIGNN_GEMM_BK64) pl.bk = 64;
+  else if (tile & ALIGNN_GEMM_BK32) pl.bk = 32;
+  else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;
+  else pl.bk = (kchunk >= 128 && tiles * split <= 2 * (int64_t)cus) ? 64 : 16;
   return pl;
 }
 

@@ -44,7 +44,8 @@ def test_library_is_gfx950():
 
 def test_gemm_plan_workspace_query_on_host():
     """alignn_gemm_workspace runs the C-side plan without touching a GPU (no device: 256 CUs
-    assumed, the MI355X count): split-K only for long K with a small tile grid."""
+    assumed, the MI355X count): 64x64 tiles, split-K toward one workgroup per CU for long K or a
+    tiny grid, each split >= 32 deep (gemm.hip make_plan)."""
     import ctypes
     from alignn_mi355x import _lib
     lib = _lib.load()
@@ -58,8 +59,10 @@ def test_gemm_plan_workspace_query_on_host():
 
     # dW of a line-graph projection: 4 tiles of 64x64, K = 23040 -> 63 chunks of 368
     assert ws(64, 256, 23040) == 63 * 64 * 256
-    assert ws(256, 256, 256) == 0                    # short K never splits
+    assert ws(256, 256, 256) == 8 * 256 * 256        # 16 tiles: split to 8 chunks of 32
+    assert ws(512, 256, 256) == 0                    # short K on >= 32 tiles does not split
     assert ws(2580, 768, 256) == 0                   # enough tiles
+    assert ws(1920, 256, 1024) == 2 * 1920 * 256     # 120 tiles, long K: 2 splits
     assert ws(256, 256, 4096, split=4) == 4 * 256 * 256
     assert ws(256, 256, 4096, split=1) == 0
     assert ws(64, 64, 4096, tile=4 | 64) == ws(64, 64, 4096, tile=4)   # bf16 flag leaves the plan alone
