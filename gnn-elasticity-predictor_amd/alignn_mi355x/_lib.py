@@ -61,7 +61,7 @@ ENCBWD_MAX_LAYERS = 8
 
 class EncBwdArgs(ctypes.Structure):
     _fields_ = [("n", c_i64), ("T", c_i64), ("D", c_i32), ("H", c_i32), ("L", c_i32), ("kin", c_i32),
-                ("dst_at", c_vp), ("x", c_vp), ("ldx", c_i64), ("w1", c_vp), ("b1", c_vp),
+                ("dst_at", c_vp), ("off_dst", c_vp), ("x", c_vp), ("ldx", c_i64), ("w1", c_vp), ("b1", c_vp),
                 ("U", c_vp * ENCBWD_MAX_LAYERS), ("Vd", c_vp * ENCBWD_MAX_LAYERS),
                 ("dz", c_vp * ENCBWD_MAX_LAYERS), ("alpha", c_vp * ENCBWD_MAX_LAYERS),
                 ("dW1", c_vp), ("db1", c_vp), ("accumulate", c_i32),

@@ -437,7 +437,8 @@ class AlignnEngine:
         self.compact_gate = True
         # angle encoder backward deferred to one pass after the last line block (ops.enc_bwd): the
         # line convs leave per-edge scalars instead of read-modify-writing a [T, D] gradient per layer
-        self.defer_angle_bwd = False  # on once measured on MI355X
+        # (+4.0 % graphs/s on MI355X once enc_bwd was column-parallel, profiles/r01/v13_sweep.log)
+        self.defer_angle_bwd = True
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden

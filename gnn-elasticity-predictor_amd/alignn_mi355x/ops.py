@@ -267,7 +267,8 @@ def gemm_tn_smalln(A: torch.Tensor, X: torch.Tensor, C: torch.Tensor, colsum: Op
 
 def enc_bwd_ok(D: int, H: int, L: int, kin: int) -> bool:
     """Shapes alignn_enc_bwd_f32 takes (else the per-layer dF path)."""
-    return 0 < D <= 256 and D % 4 == 0 and 0 <= kin <= 16 and 1 <= L <= _lib.ENCBWD_MAX_LAYERS and H * L <= 16
+    return (0 < D <= 256 and D % 4 == 0 and 0 <= kin <= 16 and 1 <= L <= _lib.ENCBWD_MAX_LAYERS and H in (1, 2, 4, 8)
+            and H * L <= 16)
 
 
 def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, Us, Vds, dzs, alphas,
@@ -292,6 +293,7 @@ def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, 
     a = _lib.EncBwdArgs()
     a.n, a.T, a.D, a.H, a.L, a.kin = g.n, T, D, H, L, kin
     a.dst_at = g.dst_at.data_ptr()
+    a.off_dst = g.off_dst.data_ptr()
     a.x, a.ldx = x.data_ptr(), x.stride(0)
     a.w1, a.b1 = W1.data_ptr(), b1.data_ptr()
     for l in range(L):

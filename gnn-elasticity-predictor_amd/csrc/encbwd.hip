@@ -14,26 +14,31 @@
 // kernel (skinny.hip linear_smallk), so the ReLU mask is the forward's bit for bit.  Neither the
 // [T, D] gradient nor a read of the [T, D] hidden layer exists.
 //
-// Layout: one wave walks chunks of EB_CHUNK consecutive target-sorted edges; lane j owns feature
-// columns 4j..4j+3.  The per-target vectors of all (layer, head) pairs for the lane's columns stay
-// in registers while the target does not change (2 x 16 x 4 floats); the per-edge scalars and
-// x_t are wave-uniform scalar loads (prefetched one edge ahead).  dW1/db1 partials: registers per
-// lane -> LDS merge of the 4 waves in wave order -> one partial per workgroup -> a second kernel
-// sums the workgroup partials in workgroup order (deterministic: fixed grid, fixed orders).
+// Layout: one workgroup per target segment (grid-strided over segments in a fixed order); thread j
+// owns feature column j.  The segment's per-target vectors of all (layer, head) pairs stay in
+// registers (2 x H*L floats per thread) and thread j keeps W1[j, :] and b1[j]; the segment's edges
+// are staged in chunks of EB_CHUNK: their 2 x H*L per-edge scalars and kin raw inputs go to LDS with
+// coalesced loads, and every thread walks the chunk reading them as LDS broadcasts — no dependent
+// global load per edge (the previous one-wave-per-edge-stream form waited on scalar loads at every
+// edge: 863 us at B = 32; profiles/r01/v13_sweep.log).  dW1/db1 partials: registers per thread,
+// one partial row per workgroup, a second kernel sums the workgroup partials in workgroup order
+// (deterministic: fixed grid, fixed orders).
 #include "common.h"
 #include "vec.h"
 
 namespace alignn {
 
 constexpr int EB_HL = 16;       // max H * L
-constexpr int EB_CHUNK = 128;   // edges per wave work item
-constexpr int EB_BLOCKS = 256;  // fixed grid: the partial-sum order does not depend on the device
+constexpr int EB_CHUNK = 128;   // edges staged in LDS at a time
+// fixed grid (the partial-sum order does not depend on the device): 4 workgroups per CU of an
+// MI355X (22.5 KB LDS each), so segment-start loads of one hide behind the others' edge loops
+constexpr int EB_BLOCKS = 1024;
 constexpr int EB_LMAX = ALIGNN_ENCBWD_MAX_LAYERS;
 
 struct EncBwdParams {
   int64_t n, T;
   int D, H, L, kin;
-  const int32_t* dst_at;           // [T] target of each target-sorted edge
+  const int32_t* off_dst;          // [n + 1] target segments of the target-sorted edges
   const float* x; int64_t ldx;     // [T, kin] target-sorted raw angle inputs
   const float* w1;                 // [D, kin]
   const float* b1;                 // [D]
@@ -44,130 +49,120 @@ struct EncBwdParams {
   float* part;                     // [EB_BLOCKS, (kin + 1) * D]
 };
 
-template <int KM>
+template <int KM, int H>
 __global__ __launch_bounds__(256) void enc_bwd_kernel(EncBwdParams p) {
-  __shared__ __attribute__((aligned(16))) float ew[(KM + 1) * 256];   // W1^T (zero rows k >= kin) | b1
-  __shared__ __attribute__((aligned(16))) float red[256];
-  const int lane = threadIdx.x & 63, wave = wave_id();
-  const int D = p.D, H = p.H, kin = p.kin;
-  const int HL = H * p.L;
-  const int j0 = 4 * lane;
-  const bool act = j0 < D;
-  for (int i = threadIdx.x; i < (KM + 1) * D; i += 256) {
-    const int k = i / D, j = i - k * D;
-    ew[k * 256 + j] = k < KM ? (k < kin ? p.w1[(int64_t)j * kin + k] : 0.f) : p.b1[j];
-  }
-  __syncthreads();
+  // per staged edge: [dz (HL) | alpha' (HL) | x (KM)]
+  constexpr int ROW = 2 * EB_HL + KM;
+  constexpr int LM = EB_HL / H < EB_LMAX ? EB_HL / H : EB_LMAX;  // layers that fit
+  __shared__ __attribute__((aligned(16))) float es[EB_CHUNK * ROW];
+  const int D = p.D, kin = p.kin, L = p.L;
+  const int HL = H * L;
+  const int j = threadIdx.x;
+  const bool act = j < D;
+  float w[KM], bj = 0.f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) w[k] = (act && k < kin) ? p.w1[(int64_t)j * kin + k] : 0.f;
+  if (act) bj = p.b1[j];
 
-  float acc[KM][4], accb[4];
+  float acc[KM], accb = 0.f;
 #pragma unroll
-  for (int k = 0; k < KM; ++k)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[k][i] = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) accb[i] = 0.f;
+  for (int k = 0; k < KM; ++k) acc[k] = 0.f;
+  // slots of (layer, head) pairs past H*L are never written: zero once (ordered by the first
+  // chunk's barrier)
+  for (int i = threadIdx.x; i < EB_CHUNK * ROW; i += 256) es[i] = 0.f;
 
-  float P[EB_HL][2][4];
-  const int64_t nchunks = (p.T + EB_CHUNK - 1) / EB_CHUNK;
-  const int64_t wstride = (int64_t)gridDim.x * 4;
-  for (int64_t ch = (int64_t)blockIdx.x * 4 + wave; ch < nchunks; ch += wstride) {
-    const int64_t tb = ch * EB_CHUNK;
-    const int64_t te = tb + EB_CHUNK < p.T ? tb + EB_CHUNK : p.T;
-    int cur = -1;
-    for (int64_t t = tb; t < te; ++t) {
-      const int d = uni(sld(p.dst_at, t));
-      if (d != cur) {
-        cur = d;
+  float Pu[EB_HL], Pv[EB_HL];
+  for (int64_t d = blockIdx.x; d < p.n; d += gridDim.x) {
+    const int64_t t0 = p.off_dst[d], t1 = p.off_dst[d + 1];
+    if (t0 == t1) continue;
 #pragma unroll
-        for (int q = 0; q < EB_HL; ++q) {
-          if (q < HL && act) {
-            const int l = q / H, h = q - (q / H) * H;
-            vload(p.U[l] + ((int64_t)d * H + h) * D + j0, P[q][0]);
-            vload(p.Vd[l] + ((int64_t)d * H + h) * D + j0, P[q][1]);
-          } else {
+    for (int q = 0; q < EB_HL; ++q) {
+      Pu[q] = Pv[q] = 0.f;
+      if (q < HL && act) {
+        const int l = q / H, h = q % H;   // constants: q unrolled, H a template parameter
+        Pu[q] = p.U[l][(d * H + h) * D + j];
+        Pv[q] = p.Vd[l][(d * H + h) * D + j];
+      }
+    }
+    for (int64_t tc = t0; tc < t1; tc += EB_CHUNK) {
+      const int ne = (int)min<int64_t>(EB_CHUNK, t1 - tc);
+      __syncthreads();   // the previous chunk's readers are done with es
+      // per-edge scalars: layer l's [T, H] rows tc..tc+ne are contiguous
 #pragma unroll
-            for (int i = 0; i < 4; ++i) P[q][0][i] = P[q][1][i] = 0.f;
+      for (int l = 0; l < LM; ++l) {
+        if (l < L) {
+          const float* dz = p.dz[l] + tc * H;
+          const float* al = p.al[l] + tc * H;
+          for (int i = threadIdx.x; i < ne * H; i += 256) {
+            const int e = i / H, h = i % H;
+            es[e * ROW + l * H + h] = dz[i];
+            es[e * ROW + EB_HL + l * H + h] = al[i];
           }
         }
       }
-      // g = sum over (layer, head) of dz u + alpha' Vd
-      float g[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = threadIdx.x; i < ne * KM; i += 256) {
+        const int e = i / KM, k = i - e * KM;
+        es[e * ROW + 2 * EB_HL + k] = k < kin ? p.x[(tc + e) * p.ldx + k] : 0.f;
+      }
+      __syncthreads();
+      if (act) {
+        for (int e = 0; e < ne; ++e) {
+          const float* r = es + e * ROW;
+          // g = sum over (layer, head) of dz u + alpha' Vd
+          // unconditional over all EB_HL slots: slots q >= HL are 0 in LDS and in Pu/Pv (a runtime
+          // q < HL test here compiled to one LDS round trip and full wait per slot)
+          float gq[4] = {0.f, 0.f, 0.f, 0.f};   // four independent chains
 #pragma unroll
-      for (int q = 0; q < EB_HL; ++q) {
-        if (q < HL) {
-          const int l = q / H, h = q - (q / H) * H;
-          const float cz = sld(p.dz[l], t * H + h), ca = sld(p.al[l], t * H + h);
+          for (int q = 0; q < EB_HL; ++q) gq[q & 3] = fmaf(r[q], Pu[q], fmaf(r[EB_HL + q], Pv[q], gq[q & 3]));
+          const float g = (gq[0] + gq[1]) + (gq[2] + gq[3]);
+          // pre-activation in linear_smallk's order: fma chain over k from 0, then + b1
+          float pre = 0.f;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) g[i] = fmaf(cz, P[q][0][i], fmaf(ca, P[q][1][i], g[i]));
+          for (int k = 0; k < KM; ++k) pre = fmaf(r[2 * EB_HL + k], w[k], pre);
+          const float dp = (pre + bj) > 0.f ? g : 0.f;
+          accb += dp;
+#pragma unroll
+          for (int k = 0; k < KM; ++k) acc[k] = fmaf(dp, r[2 * EB_HL + k], acc[k]);
         }
-      }
-      // pre-activation in linear_smallk's order: fma chain over k from 0, then + b1
-      float xk[KM];
-#pragma unroll
-      for (int k = 0; k < KM; ++k) xk[k] = k < kin ? sld(p.x, t * p.ldx + k) : 0.f;
-      float pre[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < KM; ++k) {
-        float w[4];
-        vload(ew + k * 256 + j0, w);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pre[i] = fmaf(xk[k], w[i], pre[i]);
-      }
-      float b[4];
-      vload(ew + KM * 256 + j0, b);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float dp = (pre[i] + b[i]) > 0.f ? g[i] : 0.f;
-        accb[i] += dp;
-#pragma unroll
-        for (int k = 0; k < KM; ++k) acc[k][i] = fmaf(dp, xk[k], acc[k][i]);
       }
     }
   }
-
-  // merge the 4 waves in wave order (red = w0 + w1 + w2 + w3), one partial row per workgroup
-  float* part = p.part + (int64_t)blockIdx.x * (kin + 1) * D;
-  auto merge_row = [&](const float (&v)[4], int k) {
-    for (int w = 0; w < 4; ++w) {
-      if (wave == w && act) {
-        float o[4];
-        if (w == 0) {
+  if (act) {
+    float* part = p.part + (int64_t)blockIdx.x * (kin + 1) * D;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = v[i];
-        } else {
-          vload(red + j0, o);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] += v[i];
-        }
-        if (w == 3) vstore(part + (int64_t)k * D + j0, o);
-        else vstore(red + j0, o);
-      }
-      __syncthreads();
-    }
-  };
-#pragma unroll
-  for (int k = 0; k < KM; ++k)
-    if (k < kin) merge_row(acc[k], k);
-  merge_row(accb, kin);
+    for (int k = 0; k < KM; ++k)
+      if (k < kin) part[(int64_t)k * D + j] = acc[k];
+    part[(int64_t)kin * D + j] = accb;
+  }
 }
 
 // out (j, k): sum over workgroups b of part[b][k * D + j] in workgroup order (4 chains, fixed
 // combine) -> dW1[j, k] (k < kin) or db1[j] (k == kin), written or accumulated.
-__global__ __launch_bounds__(256) void enc_bwd_stage2(const float* __restrict__ part, int blocks, int D, int kin,
-                                                      float* __restrict__ dW1, float* __restrict__ db1, int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Block: 16 row-lanes x 64 outputs; thread (ty, tx) keeps four chains over workgroups ty, ty+16,
+// ty+32, ty+48 of every 64, then the 16 row-lanes are combined in lane order (fixed).
+__global__ __launch_bounds__(1024) void enc_bwd_stage2(const float* __restrict__ part, int blocks, int D, int kin,
+                                                       float* __restrict__ dW1, float* __restrict__ db1, int accumulate) {
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + tx;
   const int n = (kin + 1) * D;
-  if (i >= n) return;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = 0;
-  for (; b + 3 < blocks; b += 4) {
-    s0 += part[(int64_t)b * n + i];
-    s1 += part[(int64_t)(b + 1) * n + i];
-    s2 += part[(int64_t)(b + 2) * n + i];
-    s3 += part[(int64_t)(b + 3) * n + i];
+  if (i < n) {
+    int b = ty;
+    for (; b + 48 < blocks; b += 64) {
+      s0 += part[(int64_t)b * n + i];
+      s1 += part[(int64_t)(b + 16) * n + i];
+      s2 += part[(int64_t)(b + 32) * n + i];
+      s3 += part[(int64_t)(b + 48) * n + i];
+    }
+    for (; b < blocks; b += 16) s0 += part[(int64_t)b * n + i];
   }
-  for (; b < blocks; ++b) s0 += part[(int64_t)b * n + i];
-  const float t = (s0 + s1) + (s2 + s3);
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ty != 0 || i >= n) return;
+  float t = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t += red[r][tx];
   const int k = i / D, j = i - k * D;
   float* dst = k < kin ? dW1 + (int64_t)j * kin + k : db1 + j;
   *dst = accumulate ? *dst + t : t;
@@ -187,8 +182,11 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
     set_error("enc_bwd: bad shape");
     return ALIGNN_E_BAD_SHAPE;
   }
-  if (a->D > 256 || a->D % 4 != 0 || a->kin > 16 || a->H * a->L > EB_HL || a->L > EB_LMAX || a->ldx < a->kin) {
-    set_error("enc_bwd: needs D <= 256 (multiple of 4), kin <= 16, H*L <= %d, L <= %d (D=%d kin=%d H=%d L=%d)", EB_HL,
+  const bool h_ok = a->H == 1 || a->H == 2 || a->H == 4 || a->H == 8;
+  if (a->D > 256 || a->D % 4 != 0 || a->kin > 16 || !h_ok || a->H * a->L > EB_HL || a->L > EB_LMAX ||
+      a->ldx < a->kin) {
+    set_error("enc_bwd: needs D <= 256 (multiple of 4), kin <= 16, H in {1,2,4,8}, H*L <= %d, L <= %d "
+              "(D=%d kin=%d H=%d L=%d)", EB_HL,
               EB_LMAX, a->D, a->kin, a->H, a->L);
     return ALIGNN_E_UNSUPPORTED;
   }
@@ -198,7 +196,7 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
   }
   EncBwdParams p;
   p.n = a->n; p.T = a->T; p.D = a->D; p.H = a->H; p.L = a->L; p.kin = a->kin;
-  p.dst_at = a->dst_at; p.x = a->x; p.ldx = a->ldx; p.w1 = a->w1; p.b1 = a->b1;
+  p.off_dst = a->off_dst; p.x = a->x; p.ldx = a->ldx; p.w1 = a->w1; p.b1 = a->b1;
   for (int l = 0; l < EB_LMAX; ++l) {
     const bool in = l < a->L;
     p.U[l] = in ? a->U[l] : nullptr;
@@ -212,17 +210,34 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
   }
   p.part = a->workspace;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a->T > 0 && !a->off_dst) {
+    set_error("enc_bwd: off_dst missing");
+    return ALIGNN_E_BAD_SHAPE;
+  }
   if (a->T > 0) {
-    if (a->kin <= 8) launch(enc_bwd_kernel<8>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
-    else if (a->kin <= 12) launch(enc_bwd_kernel<12>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
-    else launch(enc_bwd_kernel<16>, dim3(EB_BLOCKS), dim3(256), 0, s, p);
+    const int km = a->kin <= 8 ? 8 : a->kin <= 12 ? 12 : 16;
+#define EB_LAUNCH_H(KM_)                                                                   \
+  switch (a->H) {                                                                          \
+    case 1: launch(enc_bwd_kernel<KM_, 1>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;    \
+    case 2: launch(enc_bwd_kernel<KM_, 2>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;    \
+    case 4: launch(enc_bwd_kernel<KM_, 4>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;    \
+    default: launch(enc_bwd_kernel<KM_, 8>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;   \
+  }
+    if (km == 8) {
+      EB_LAUNCH_H(8)
+    } else if (km == 12) {
+      EB_LAUNCH_H(12)
+    } else {
+      EB_LAUNCH_H(16)
+    }
+#undef EB_LAUNCH_H
     ALIGNN_LAUNCH_CHECK("enc_bwd_kernel");
   } else {
-    const hipError_t e = hipMemsetAsync(a->workspace, 0, sizeof(float) * EB_BLOCKS * (a->kin + 1) * a->D, s);
-    if (e != hipSuccess) return hip_status(e, "enc_bwd memset");
+    const int rc = alignn_fill_f32(a->workspace, (int64_t)EB_BLOCKS * (a->kin + 1) * a->D, 0.f, stream);
+    if (rc != ALIGNN_OK) return rc;
   }
   const int n = (a->kin + 1) * a->D;
-  launch(enc_bwd_stage2, dim3((n + 255) / 256), dim3(256), 0, s, a->workspace, EB_BLOCKS, a->D, a->kin,
+  launch(enc_bwd_stage2, dim3((n + 63) / 64), dim3(1024), 0, s, a->workspace, EB_BLOCKS, a->D, a->kin,
                      a->dW1, a->db1, (int)a->accumulate);
   ALIGNN_LAUNCH_CHECK("enc_bwd_stage2");
   return ALIGNN_OK;

@@ -122,6 +122,7 @@ typedef struct AlignnEncBwdArgs {
   int64_t n, T;                        /* line-graph nodes (targets) and edges */
   int32_t D, H, L, kin;
   const int32_t* dst_at;               /* [T] target of each target-sorted edge (alignn_graph_prep) */
+  const int32_t* off_dst;              /* [n + 1] target segment offsets (alignn_graph_prep) */
   const float* x; int64_t ldx;         /* [T, kin] raw angle features, target-sorted */
   const float* w1; const float* b1;    /* [D, kin], [D] */
   const float* U[ALIGNN_ENCBWD_MAX_LAYERS];      /* per layer [n, H, D] */
