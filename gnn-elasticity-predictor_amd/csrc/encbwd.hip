@@ -75,34 +75,61 @@ __global__ __launch_bounds__(256) void enc_bwd_kernel(EncBwdParams p) {
   for (int64_t d = blockIdx.x; d < p.n; d += gridDim.x) {
     const int64_t t0 = p.off_dst[d], t1 = p.off_dst[d + 1];
     if (t0 == t1) continue;
+    // Every global load of a segment / chunk is issued before any of its values is used (one
+    // memory round trip, not one per staging iteration): branch-free, absent layers and columns
+    // read a valid row and are masked to 0 afterwards.
+    const int jc = act ? j : 0;
 #pragma unroll
     for (int q = 0; q < EB_HL; ++q) {
-      Pu[q] = Pv[q] = 0.f;
-      if (q < HL && act) {
-        const int l = q / H, h = q % H;   // constants: q unrolled, H a template parameter
-        Pu[q] = p.U[l][(d * H + h) * D + j];
-        Pv[q] = p.Vd[l][(d * H + h) * D + j];
-      }
+      const int l = q / H, h = q % H;   // constants: q unrolled, H a template parameter
+      const int ls = l < L ? l : 0;
+      const float u = p.U[ls][(d * H + h) * D + jc], v = p.Vd[ls][(d * H + h) * D + jc];
+      Pu[q] = (q < HL && act) ? u : 0.f;
+      Pv[q] = (q < HL && act) ? v : 0.f;
     }
+    constexpr int PER_L = (EB_CHUNK * H + 255) / 256;   // per-layer scalars per thread
+    constexpr int PER_X = (EB_CHUNK * KM + 255) / 256;  // raw-input values per thread
     for (int64_t tc = t0; tc < t1; tc += EB_CHUNK) {
       const int ne = (int)min<int64_t>(EB_CHUNK, t1 - tc);
-      __syncthreads();   // the previous chunk's readers are done with es
+      float vz[LM][PER_L], va[LM][PER_L], vx[PER_X];
       // per-edge scalars: layer l's [T, H] rows tc..tc+ne are contiguous
 #pragma unroll
       for (int l = 0; l < LM; ++l) {
+        const float* dz = p.dz[l < L ? l : 0] + tc * H;
+        const float* al = p.al[l < L ? l : 0] + tc * H;
+#pragma unroll
+        for (int u = 0; u < PER_L; ++u) {
+          const int i = threadIdx.x + 256 * u;
+          const int ic = i < ne * H ? i : 0;
+          vz[l][u] = dz[ic];
+          va[l][u] = al[ic];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PER_X; ++u) {
+        const int i = threadIdx.x + 256 * u;
+        const int e = i / KM, k = i % KM;
+        vx[u] = (i < ne * KM && k < kin) ? p.x[(tc + e) * p.ldx + k] : 0.f;
+      }
+      __syncthreads();   // the previous chunk's readers are done with es
+#pragma unroll
+      for (int l = 0; l < LM; ++l) {
         if (l < L) {
-          const float* dz = p.dz[l] + tc * H;
-          const float* al = p.al[l] + tc * H;
-          for (int i = threadIdx.x; i < ne * H; i += 256) {
-            const int e = i / H, h = i % H;
-            es[e * ROW + l * H + h] = dz[i];
-            es[e * ROW + EB_HL + l * H + h] = al[i];
+#pragma unroll
+          for (int u = 0; u < PER_L; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < ne * H) {
+              const int e = i / H, h = i % H;
+              es[e * ROW + l * H + h] = vz[l][u];
+              es[e * ROW + EB_HL + l * H + h] = va[l][u];
+            }
           }
         }
       }
-      for (int i = threadIdx.x; i < ne * KM; i += 256) {
-        const int e = i / KM, k = i - e * KM;
-        es[e * ROW + 2 * EB_HL + k] = k < kin ? p.x[(tc + e) * p.ldx + k] : 0.f;
+#pragma unroll
+      for (int u = 0; u < PER_X; ++u) {
+        const int i = threadIdx.x + 256 * u;
+        if (i < ne * KM) es[(i / KM) * ROW + 2 * EB_HL + i % KM] = vx[u];
       }
       __syncthreads();
       if (act) {
