@@ -162,6 +162,18 @@ def end_to_end(args, trainer, dev, rank, world):
             "includes": "device collate of a random batch + CSR/compaction + fwd/NLL/bwd/clip/AdamW"}
 
 
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch of ``kernel_key`` from the committed PMC passes (profiles/pmc_dominant.json:
+    FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py), or None when that kernel/shape was not counted."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_dominant.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(kernel_key)
+    except (OSError, ValueError):
+        return None
+    return None if rec is None else rec["traffic_bytes"]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -290,7 +302,7 @@ def main():
             else:
                 ach = s["bytes_per_launch"] / avg_s / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dominant,
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dominant), "kernel": dominant,
                         "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
                         "bytes_per_launch": s["bytes_per_launch"], "timing": probe_src}
         cpu = None
