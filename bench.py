@@ -83,6 +83,8 @@ def apply_settings(args, model):
             ops.GraphCSR.COMPACT_REGS = bool(int(v))
         elif k == "optimizer":
             kw["optimizer"] = v
+        elif k == "main_priority":
+            args.main_priority = int(v)
         else:
             raise ValueError(f"unknown --set key {k}")
     return kw
@@ -194,7 +196,14 @@ def main():
     torch.manual_seed(1234)  # identical initial weights on every rank
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                       args.dropout), 2).to(dev)
+    args.main_priority = 0
     trainer = A.FusedTrainer(model, precision=args.precision, **apply_settings(args, model))
+    if args.main_priority:
+        # the step's critical-path stream at a higher HIP priority than the weight-gradient side
+        # stream (A/B option; priority -1 is the highest torch exposes)
+        hi = torch.cuda.Stream(device=dev, priority=-1)
+        hi.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(hi)
     mfma_peak = BF16_MFMA_TFLOPS if args.precision == "bf16" else FP32_MFMA_TFLOPS
     batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=args.lg_offset).to(dev)
     if world > 1:

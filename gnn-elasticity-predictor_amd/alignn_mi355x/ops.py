@@ -560,7 +560,7 @@ def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_w
     rp = _check_outp_rows(outp, outp_rows, n)
     if dout.shape != outp.shape:
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
-    ws = WS.get("gate_ln", 1024 * 5 * D, outp.device)
+    ws = WS.get("gate_ln", int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D)), outp.device)
     check(_lib.lib().alignn_gate_ln_bwd_rows(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), rp,
                                              R.data_ptr(), R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(),
                                              ln_b.data_ptr(), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),

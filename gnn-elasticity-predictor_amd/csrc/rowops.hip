@@ -362,6 +362,17 @@ extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const
                                  drop_p, seed, stream);
 }
 
+// Waves of the gate/LayerNorm backward (each walks n / waves rows; one partial row of parameter
+// gradients per wave).
+#ifndef ALIGNN_GATE_BWD_WAVES
+#define ALIGNN_GATE_BWD_WAVES 2048  // measured: 2048 +1.0 % step, 4096 +0 % (profiles/r01/v18_ab_gate_waves.log)
+#endif
+
+extern "C" int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D) {
+  if (n < 0 || D <= 0) return -1;
+  return std::max<int64_t>(1, std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n)) * 5 * D;
+}
+
 extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
                                        const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
                                        const float* ln_w, const float* ln_b, const float* beta, const float* mu,
@@ -374,7 +385,7 @@ extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew,
     return ALIGNN_E_UNSUPPORTED;
   }
   if (n == 0) return ALIGNN_OK;
-  const int nwaves = (int)std::min<int64_t>(1024, n);
+  const int nwaves = (int)std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n);
   GateBwdParams p{n, D, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
                   nwaves, make_drop(drop_p, seed), outp_rows};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

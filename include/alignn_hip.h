@@ -278,6 +278,8 @@ int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32
                             int64_t ldr, const float* wbeta, const float* X, int64_t ldx, const float* ln_w,
                             const float* ln_b, float* Xnew, int64_t ldxn, float* beta, float* mu, float* rstd,
                             float drop_p, uint64_t seed, void* stream);
+/* Workspace floats alignn_gate_ln_bwd(_rows) needs for n rows of width D (-1: bad shape). */
+int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D);
 int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
                             const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
                             const float* ln_w, const float* ln_b, const float* beta, const float* mu,

@@ -10,9 +10,10 @@ out=$root/gnn-elasticity-predictor_amd/alignn_mi355x/variants
 bdir=$src/build_$name
 mkdir -p "$out" "$bdir"
 pids=()
-for f in gemm graph tconv rowops ensemble optim collate knn; do
+for path in "$src"/*.hip; do
+  f=$(basename "$path" .hip)
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function "$@" \
-    -c "$src/$f.hip" -o "$bdir/$f.o" &
+    -c "$path" -o "$bdir/$f.o" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
