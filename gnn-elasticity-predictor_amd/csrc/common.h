@@ -139,16 +139,19 @@ inline DropParams make_drop(float p, uint64_t seed) {
 }
 
 // Fixed-order column reduction of a [rows, N] partial buffer: out[c] (+)= sum_r part[r*N + c].
-// Grid: ceil(N/64) blocks of 1024 threads (16 row-lanes x 64 columns); each thread keeps four
+// Grid: ceil(N/16) blocks of 256 threads (16 row-lanes x 16 columns); each thread keeps four
 // independent partial sums (rows ty, ty+16, ty+32, ty+48 of every 64-row stride) so 16 x 4 loads
-// per column are in flight; the 16 row-lanes are combined in lane order.
-constexpr int kColsumThreads = 1024;
+// per column are in flight; the 16 row-lanes are combined in lane order.  Blocks of 256 threads
+// (not 1024) find room on a CU beside a side-stream kernel that fills it (a 1024-thread block
+// waited up to 80 us on the critical path, profiles/r01/v15_kernel_stats.csv).
+constexpr int kColsumThreads = 256;
+constexpr int kColsumCols = 16;
 template <int kUnused = 0>
-__global__ __launch_bounds__(1024) void colsum_stage2(const float* __restrict__ part, int rows, int64_t N,
-                                                      float* __restrict__ out, int acc) {
-  __shared__ float red[16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int rows, int64_t N,
+                                                     float* __restrict__ out, int acc) {
+  __shared__ float red[16][kColsumCols];
+  const int tx = threadIdx.x % kColsumCols, ty = threadIdx.x / kColsumCols;
+  const int64_t col = (int64_t)blockIdx.x * kColsumCols + tx;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int r = ty;
@@ -169,5 +172,6 @@ __global__ __launch_bounds__(1024) void colsum_stage2(const float* __restrict__ 
     out[col] = acc ? out[col] + t : t;
   }
 }
+static inline unsigned colsum_blocks(int64_t N) { return (unsigned)((N + kColsumCols - 1) / kColsumCols); }
 
 }  // namespace alignn

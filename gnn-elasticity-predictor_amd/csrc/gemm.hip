@@ -537,13 +537,13 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
   nparts = (int)((M + rows_per - 1) / rows_per);
   if (nparts < 1) nparts = 1;
   if (M == 0) {
-    launch(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, 0, N, out, accumulate);
+    launch(colsum_stage2<0>, dim3(colsum_blocks(N)), dim3(kColsumThreads), 0, s, workspace, 0, N, out, accumulate);
     ALIGNN_LAUNCH_CHECK("colsum_stage2");
     return ALIGNN_OK;
   }
   launch(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
   ALIGNN_LAUNCH_CHECK("colsum_stage1");
-  launch(colsum_stage2<0>, dim3(strips), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
+  launch(colsum_stage2<0>, dim3(colsum_blocks(N)), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
   ALIGNN_LAUNCH_CHECK("colsum_stage2");
   return ALIGNN_OK;
 }
