@@ -304,7 +304,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, enc_grads=None,
-                   side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False) -> None:
+                   side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False,
+                   overlap_src: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -314,7 +315,9 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     downstream in the backward reads; they overlap the next block's latency-bound attention.  The
     caller joins the side stream before reading those gradients.
     keep_edge_scalars: leave (Vd, dz_e, alpha_e) on ``c.edge_scalars`` for the deferred angle-encoder
-    backward (ops.enc_bwd; then dF is None)."""
+    backward (ops.enc_bwd; then dF is None).
+    overlap_src: with a side stream, run the source-side attention backward on a third stream beside
+    the dQ products."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -344,7 +347,11 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         dF = None
     ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
                       dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
-    ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
+    # dK/dV (source side) and the dQ products below are independent: with an aux stream the
+    # source-side kernel runs beside them and the dX products wait for both
+    aux = ops.aux_stream(dev) if (side is not None and overlap_src) else None
+    with _side_work(aux, (c.QKV, dout_a, dz_e, al_e, dQKVR if rows is None else dQKV)):
+        ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
     if keep_edge_scalars:
         c.edge_scalars = (Vd, dz_e, al_e)
     Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
@@ -356,6 +363,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0, rowscale=sigz.t(), bias2=c.wbar.view(H, C))
     else:
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0)
+    if aux is not None:
+        ops.stream_wait(torch.cuda.current_stream(dev), aux)
     if rows is None:
         ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
     else:
@@ -439,6 +448,9 @@ class AlignnEngine:
         # line convs leave per-edge scalars instead of read-modify-writing a [T, D] gradient per layer
         # (+4.0 % graphs/s on MI355X once enc_bwd was column-parallel, profiles/r01/v13_sweep.log)
         self.defer_angle_bwd = True
+        # backward: source-side attention kernel on a third stream beside the dQ products (measured
+        # -1.1 %: the cross-queue sync costs more than the overlap saves, v23_sweep_overlap_src.log)
+        self.overlap_src = False
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -621,7 +633,8 @@ class AlignnEngine:
             if self.debug is not None:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
-                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side)
+                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
+                               overlap_src=self.overlap_src)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -631,9 +644,11 @@ class AlignnEngine:
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
-                                   enc_grads=enc_grads, side=side, keep_edge_scalars=defer)
+                                   enc_grads=enc_grads, side=side, keep_edge_scalars=defer,
+                                   overlap_src=self.overlap_src)
                 else:
-                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side)
+                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
+                                   overlap_src=self.overlap_src)
                 da_written = True
         if self.debug is not None:
             self.debug["de0"] = de.clone()

@@ -59,6 +59,18 @@ def side_stream(device) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
+_AUX = {}
+
+
+def aux_stream(device) -> torch.cuda.Stream:
+    """A third stream per device for short branches beside the critical path (the source-side
+    attention backward next to the dQ products)."""
+    key = str(device)
+    if key not in _AUX:
+        _AUX[key] = torch.cuda.Stream(device=device)
+    return _AUX[key]
+
+
 WS = _Workspace()
 
 

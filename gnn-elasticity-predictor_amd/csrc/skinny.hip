@@ -18,7 +18,10 @@
 
 namespace alignn {
 
-constexpr int SK_ROWS = 64;
+#ifndef ALIGNN_SK_ROWS
+#define ALIGNN_SK_ROWS 256  // measured +0.5 % step vs 64 (profiles/r01/v22_ab_sk_rows.log)
+#endif
+constexpr int SK_ROWS = ALIGNN_SK_ROWS;  // rows of x per workgroup (W's 4 x K columns loaded once per workgroup)
 constexpr int SK_KMAX = 16;   // linear_smallk: K <= 16
 constexpr int SN_NMAX = 16;   // tn_smalln: N <= 16
 constexpr int SN_SLOTS = SN_NMAX + 1;
