@@ -305,7 +305,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, enc_grads=None,
                    side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False,
-                   overlap_src: bool = False) -> None:
+                   overlap_src: bool = False, wbar_colsum: bool = True) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -375,8 +375,11 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         if c.with_proj:
             ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
             ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
-            ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
-            ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
+            if wbar_colsum:   # dw̄_h = Σ Q_h σz_h + dout_h ΣA_h in one weighted column-sum kernel
+                ops.wcolsum2(c.QKV[:, :D], sigz, dout_a, c.sumA, dwbar)
+            else:
+                ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
+                ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
         else:
             ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
             ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
@@ -451,6 +454,8 @@ class AlignnEngine:
         # backward: source-side attention kernel on a third stream beside the dQ products (measured
         # -1.1 %: the cross-queue sync costs more than the overlap saves, v23_sweep_overlap_src.log)
         self.overlap_src = False
+        # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
+        self.wbar_colsum = True
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -634,7 +639,7 @@ class AlignnEngine:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               overlap_src=self.overlap_src)
+                               overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -645,10 +650,10 @@ class AlignnEngine:
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
                                    enc_grads=enc_grads, side=side, keep_edge_scalars=defer,
-                                   overlap_src=self.overlap_src)
+                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
-                                   overlap_src=self.overlap_src)
+                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum)
                 da_written = True
         if self.debug is not None:
             self.debug["de0"] = de.clone()

@@ -236,6 +236,23 @@ def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torc
     return out
 
 
+def wcolsum2(X1: torch.Tensor, W1: torch.Tensor, X2: torch.Tensor, W2: torch.Tensor, out: torch.Tensor,
+             accumulate: bool = False) -> torch.Tensor:
+    """out[j] (+)= sum_r W1[r, j // C] X1[r, j] + W2[r, j // C] X2[r, j], C = N // W1.size(1): the
+    per-head w-bar gradient sum_n Q_nh sigz_nh + dout_nh sumA_nh (alignn_wcolsum2_f32)."""
+    M, N = X1.shape
+    Hh = W1.size(1)
+    if (tuple(X2.shape) != (M, N) or tuple(W1.shape) != (M, Hh) or tuple(W2.shape) != (M, Hh) or N % Hh
+            or X1.stride(1) != 1 or X2.stride(1) != 1 or W1.stride(1) != 1 or W2.stride(1) != 1 or out.numel() != N
+            or not out.is_contiguous()):
+        raise ValueError("wcolsum2: inconsistent shapes or strides")
+    ws = WS.get("colsum", 256 * N, X1.device)
+    check(_lib.lib().alignn_wcolsum2_f32(M, N, N // Hh, X1.data_ptr(), X1.stride(0), W1.data_ptr(), W1.stride(0),
+                                         X2.data_ptr(), X2.stride(0), W2.data_ptr(), W2.stride(0), out.data_ptr(),
+                                         int(accumulate), ws.data_ptr(), stream_ptr()), "alignn_wcolsum2_f32")
+    return out
+
+
 SMALLK_MAX = 16   # alignn_linear_smallk_f32: K <= 16
 SMALLN_MAX = 16   # alignn_gemm_tn_smalln_f32: N <= 16
 

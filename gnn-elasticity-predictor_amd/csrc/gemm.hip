@@ -521,6 +521,37 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ X
   __syncthreads();
   if (ty == 0 && col < N) part[(int64_t)blockIdx.x * N + col] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
+
+// Weighted column sums of two row-strided matrices, per-row weights per column group of width C:
+//   out[j] (+)= sum_r W1[r, j / C] X1[r, j] + W2[r, j / C] X2[r, j]
+// (the w-bar gradient of a TransformerConv with a folded edge projection: per head h,
+// sum_n Q_nh sigz_nh + dout_nh sumA_nh).  Same two fixed-order stages as colsum.
+__global__ __launch_bounds__(256) void wcolsum2_stage1(const float* __restrict__ X1, int64_t ld1,
+                                                       const float* __restrict__ W1, int64_t lw1,
+                                                       const float* __restrict__ X2, int64_t ld2,
+                                                       const float* __restrict__ W2, int64_t lw2, int64_t M,
+                                                       int64_t N, int C, int64_t rows_per, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.y * 64 + tx;
+  const int64_t h = col / C;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < N) {
+    int64_t r = r0 + ty;
+    for (; r + 12 < r1; r += 16) {
+      s0 = fmaf(W1[r * lw1 + h], X1[r * ld1 + col], fmaf(W2[r * lw2 + h], X2[r * ld2 + col], s0));
+      s1 = fmaf(W1[(r + 4) * lw1 + h], X1[(r + 4) * ld1 + col], fmaf(W2[(r + 4) * lw2 + h], X2[(r + 4) * ld2 + col], s1));
+      s2 = fmaf(W1[(r + 8) * lw1 + h], X1[(r + 8) * ld1 + col], fmaf(W2[(r + 8) * lw2 + h], X2[(r + 8) * ld2 + col], s2));
+      s3 = fmaf(W1[(r + 12) * lw1 + h], X1[(r + 12) * ld1 + col],
+                fmaf(W2[(r + 12) * lw2 + h], X2[(r + 12) * ld2 + col], s3));
+    }
+    for (; r < r1; r += 4) s0 = fmaf(W1[r * lw1 + h], X1[r * ld1 + col], fmaf(W2[r * lw2 + h], X2[r * ld2 + col], s0));
+  }
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ty == 0 && col < N) part[(int64_t)blockIdx.x * N + col] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+}
 }  // namespace alignn
 
 extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
@@ -543,6 +574,31 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
   }
   launch(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
   ALIGNN_LAUNCH_CHECK("colsum_stage1");
+  launch(colsum_stage2<0>, dim3(colsum_blocks(N)), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
+  ALIGNN_LAUNCH_CHECK("colsum_stage2");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_wcolsum2_f32(int64_t M, int64_t N, int32_t C, const float* X1, int64_t ld1, const float* W1,
+                                   int64_t lw1, const float* X2, int64_t ld2, const float* W2, int64_t lw2, float* out,
+                                   int32_t accumulate, float* workspace, void* stream) {
+  if (M < 0 || N < 0 || C <= 0 || N % C != 0) return ALIGNN_E_BAD_SHAPE;
+  if (N == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned strips = (unsigned)((N + 63) / 64);
+  // as alignn_colsum_f32: ~2 blocks per CU, >= 64 rows per chunk, <= 256 chunks
+  int64_t want = std::max<int64_t>(1, 512 / (int64_t)strips);
+  int nparts = (int)std::min<int64_t>({256, want, std::max<int64_t>(1, (M + 63) / 64)});
+  int64_t rows_per = std::max<int64_t>(1, (M + nparts - 1) / nparts);
+  nparts = (int)std::max<int64_t>(1, (M + rows_per - 1) / rows_per);
+  if (M == 0) {
+    launch(colsum_stage2<0>, dim3(colsum_blocks(N)), dim3(kColsumThreads), 0, s, workspace, 0, N, out, accumulate);
+    ALIGNN_LAUNCH_CHECK("colsum_stage2");
+    return ALIGNN_OK;
+  }
+  launch(wcolsum2_stage1, dim3(nparts, strips), dim3(256), 0, s, X1, ld1, W1, lw1, X2, ld2, W2, lw2, M, N, (int)C,
+         rows_per, workspace);
+  ALIGNN_LAUNCH_CHECK("wcolsum2_stage1");
   launch(colsum_stage2<0>, dim3(colsum_blocks(N)), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
   ALIGNN_LAUNCH_CHECK("colsum_stage2");
   return ALIGNN_OK;

@@ -140,6 +140,16 @@ int alignn_enc_bwd_f32(const AlignnEncBwdArgs* args, void* stream);
 int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
                       float* workspace, void* stream);
 
+/* Weighted column sums of two row-strided [M, N] matrices with per-row weights per column group
+ * of width C (N % C == 0; W rows hold N / C weights):
+ *   out[j] (+)= sum_r W1[r*lw1 + j/C] X1[r*ld1 + j] + W2[r*lw2 + j/C] X2[r*ld2 + j]
+ * The w-bar gradient of a TransformerConv whose edge features pass through a folded Linear
+ * (edge_proj, train.py:325/:333; the angle encoder's 2nd Linear, train.py:358-364): per head,
+ * sum_n Q_nh sigz_nh + dout_nh sumA_nh.  Two fixed-order stages; workspace >= 256*N floats. */
+int alignn_wcolsum2_f32(int64_t M, int64_t N, int32_t C, const float* X1, int64_t ld1, const float* W1, int64_t lw1,
+                        const float* X2, int64_t ld2, const float* W2, int64_t lw2, float* out, int32_t accumulate,
+                        float* workspace, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Graph preparation: CSR neighbour lists in HBM.  Replaces PyG MessagePassing.collect's
  * index_select by edge_index[0]/[1] and the scatter/ index_add by edge_index[1]

@@ -190,3 +190,25 @@ def test_add_noise_moments():
     ops.add_noise(x, 0.1, 99)
     assert abs(x.mean().item()) < 5e-4
     assert abs(x.std().item() - 0.1) < 5e-4
+
+
+@pytest.mark.parametrize("M,N,H", [(1, 64, 1), (37, 256, 4), (2580, 256, 4), (1920, 128, 2), (0, 256, 4)])
+def test_wcolsum2_matches_fp64(M, N, H):
+    """alignn_wcolsum2_f32 (the per-head w-bar gradient) vs fp64 torch, on strided row views."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(M + N + H)
+    X1 = torch.randn(M, 3 * N, generator=g).to(DEV)[:, :N]         # a QKV-like row stride
+    X2 = torch.randn(M, N, generator=g).to(DEV)
+    W1 = torch.randn(M, H, generator=g).to(DEV)
+    W2 = torch.randn(M, H, generator=g).to(DEV)
+    out = torch.full((N,), float("nan"), device=DEV)
+    ops.wcolsum2(X1, W1, X2, W2, out)
+    C = N // H
+    ref = (X1.double() * W1.double().repeat_interleave(C, 1) + X2.double() * W2.double().repeat_interleave(C, 1)).sum(0)
+    torch.cuda.synchronize()
+    scale = max(1.0, float(ref.abs().max()))
+    assert float((out.double() - ref).abs().max()) <= 1e-5 * scale * max(1, M) ** 0.5
+    base = out.clone()
+    ops.wcolsum2(X1, W1, X2, W2, out, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(out, 2 * base, rtol=1e-6, atol=1e-6)
