@@ -347,7 +347,11 @@ class GraphCSR:
     __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
                  "n_full", "cmap")
 
-    HEAVY_THRESHOLD = 32  # in-degree above which a target node gets a 4-wave workgroup
+    # in-degree above which a target node gets a 4-wave workgroup (LDS merge of the waves); below it
+    # one wave walks the node's edges.  256: every node of the MP-like line graph (in-degree <= 132
+    # under the PyG offset rule) takes the 1-wave path — measured +6.2 % step at B = 32, +8.7 % at
+    # B = 256 bf16 vs 32 (line bwd_dst 194 -> 159 us; profiles/r01/v27_sweep_heavy_threshold.log)
+    HEAVY_THRESHOLD = 256
     COMPACT_REGS = True  # attention kernels with row-distributed softmax state (+1 %, bwd_dst 249 -> 231 us)
 
     def __init__(self, edge_index: torch.Tensor, n: int):

@@ -198,11 +198,15 @@ def _run_tconv(csr, m, t, D, H, drop, compact):
                 dF=dF)
 
 
+@pytest.mark.parametrize("thr", [32, 256])
 @pytest.mark.parametrize("D,H", [(256, 4), (128, 2), (64, 1), (32, 4), (32, 1), (512, 8)])
 @pytest.mark.parametrize("drop", [0.0, 0.15])
-def test_compact_register_attention_kernels_match_v1(D, H, drop):
+def test_compact_register_attention_kernels_match_v1(D, H, drop, thr, monkeypatch):
     """The row-distributed (COMPACT_REGS) attention kernels vs the default ones: same math, softmax
-    sums in a different order -> 1e-5 relative; per-edge dz / alpha' and the dF rows agree too."""
+    sums in a different order -> 1e-5 relative; per-edge dz / alpha' and the dF rows agree too.
+    thr: heavy-node threshold (32: in-degrees up to 70 take both the 4-wave and the 1-wave path;
+    256, the default: all 1-wave)."""
+    monkeypatch.setattr(_ops().GraphCSR, "HEAVY_THRESHOLD", thr)
     for seed, (with_wbar, feat_row) in enumerate([(True, False), (False, True)]):
         csr, m, t = _tconv_case(D, H, 300, 70, 10 + seed, with_wbar, feat_row)
         a = _run_tconv(csr, m, t, D, H, drop, False)
