@@ -83,6 +83,8 @@ def apply_settings(args, model):
             ops.GraphCSR.COMPACT_REGS = bool(int(v))
         elif k == "optimizer":
             kw["optimizer"] = v
+        elif k == "sort_by_degree":
+            ops.GraphCSR.SORT_BY_DEGREE = bool(int(v))
         elif k == "heavy_threshold":
             ops.GraphCSR.HEAVY_THRESHOLD = int(v)
         elif k == "main_priority":

@@ -352,6 +352,7 @@ class GraphCSR:
     # under the PyG offset rule) takes the 1-wave path — measured +6.2 % step at B = 32, +8.7 % at
     # B = 256 bf16 vs 32 (line bwd_dst 194 -> 159 us; profiles/r01/v27_sweep_heavy_threshold.log)
     HEAVY_THRESHOLD = 256
+    SORT_BY_DEGREE = False  # work items in descending in-degree order (A/B option; within noise, slower bwd_dst)
     COMPACT_REGS = True  # attention kernels with row-distributed softmax state (+1 %, bwd_dst 249 -> 231 us)
 
     def __init__(self, edge_index: torch.Tensor, n: int):
@@ -390,8 +391,16 @@ class GraphCSR:
             # light list: nodes with in-edges first, in-degree-0 nodes last (the kernels skip
             # per-workgroup setup for items that start with an empty node)
             light_mask = ~heavy_mask
-            light = torch.cat([idx[light_mask & (deg > 0)], idx[light_mask & (deg == 0)]]).to(self.off_dst.device)
-            heavy = idx[heavy_mask].to(self.off_dst.device)
+            lit = idx[light_mask & (deg > 0)]
+            hv = idx[heavy_mask]
+            if self.SORT_BY_DEGREE:
+                # longest segments first (their waves start in the first round of resident
+                # workgroups) and similar degrees in one workgroup (its 4 waves finish together);
+                # each node is still one wave's work, so results do not change
+                lit = lit[torch.sort(deg[lit.long()], descending=True, stable=True).indices]
+                hv = hv[torch.sort(deg[hv.long()], descending=True, stable=True).indices]
+            light = torch.cat([lit, idx[light_mask & (deg == 0)]]).to(self.off_dst.device)
+            heavy = hv.to(self.off_dst.device)
             sc = _lib.Schedule()
             sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
             sc.heavy, sc.n_heavy = (heavy.data_ptr() if heavy.numel() else None), heavy.numel()
