@@ -305,7 +305,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, enc_grads=None,
                    side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False,
-                   overlap_src: bool = False, wbar_colsum: bool = True) -> None:
+                   overlap_src: bool = False, wbar_colsum: bool = True, overlap_skip: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -317,7 +317,9 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     keep_edge_scalars: leave (Vd, dz_e, alpha_e) on ``c.edge_scalars`` for the deferred angle-encoder
     backward (ops.enc_bwd; then dF is None).
     overlap_src: with a side stream, run the source-side attention backward on a third stream beside
-    the dQ products."""
+    the dQ products.
+    overlap_skip: on a compacted graph with a side stream, the skip projection's dX product (all n rows)
+    runs on a third stream beside the attention backward; dX accumulates in the same order."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -335,6 +337,10 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
                     gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows)
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
+    skip = ops.aux_stream(dev) if (side is not None and overlap_skip and rows is not None) else None
+    if skip is not None:
+        with _side_work(skip, (dR, dX)):
+            ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                # residual + skip projection
     Vd = torch.empty(na, H, D, device=dev)
     ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
     Sz = torch.empty(na, H, D, device=dev)
@@ -368,7 +374,10 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     if rows is None:
         ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
     else:
-        ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                    # residual + skip projection
+        if skip is None:
+            ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                # residual + skip projection
+        else:
+            ops.stream_wait(torch.cuda.current_stream(dev), skip)
         ops.gemm(dQKV, cv.Wqkvr[:3 * D], dX, beta=1.0, c_rows=rows)     # + Q/K/V projections (active rows)
     # weight gradients: off the critical path
     with _side_work(side, (c.QKV, dout_a, Sz, sigz, c.S, c.sumA, dQKV, dR, c.X, c.Xa)):
@@ -454,6 +463,8 @@ class AlignnEngine:
         # backward: source-side attention kernel on a third stream beside the dQ products (measured
         # -1.1 %: the cross-queue sync costs more than the overlap saves, v23_sweep_overlap_src.log)
         self.overlap_src = False
+        # line blocks: the skip projection's dX product beside the attention backward (third stream)
+        self.overlap_skip = False
         # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
         self.wbar_colsum = True
 
@@ -639,7 +650,8 @@ class AlignnEngine:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum)
+                               overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
+                               overlap_skip=self.overlap_skip)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -650,10 +662,12 @@ class AlignnEngine:
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
                                    enc_grads=enc_grads, side=side, keep_edge_scalars=defer,
-                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum)
+                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
+                                   overlap_skip=self.overlap_skip)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
-                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum)
+                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
+                                   overlap_skip=self.overlap_skip)
                 da_written = True
         if self.debug is not None:
             self.debug["de0"] = de.clone()

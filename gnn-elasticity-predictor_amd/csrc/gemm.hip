@@ -25,6 +25,11 @@
 //   operand contiguous along row -> [BKT][ROWS+4]
 #include "common.h"
 
+// XCD-contiguous tile order (below): same-box A/B +1.5 % step (profiles/r01/v30_ab_gemm_xcd.log)
+#ifndef ALIGNN_GEMM_XCD
+#define ALIGNN_GEMM_XCD 1
+#endif
+
 namespace alignn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -182,10 +187,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
-  const int64_t tile = blockIdx.x;
+#if ALIGNN_GEMM_XCD
+  // XCD-contiguous work order: workgroups are dispatched round-robin over the 8 XCDs, so the
+  // linear id lin lands on XCD lin % 8.  Give XCD x the contiguous range of (z, tile) items
+  // [x*q + min(x, r), ...) so the column tiles of one A row band share that XCD's L2.
+  const int64_t nlin = (int64_t)gridDim.x * gridDim.z;
+  const int64_t lin = (int64_t)blockIdx.z * gridDim.x + blockIdx.x;
+  const int64_t xq = nlin / 8, xr = nlin % 8, xcd = lin % 8;
+  const int64_t item = xcd * xq + min(xcd, xr) + lin / 8;
+  const int64_t tile = item % gridDim.x, zid = item / gridDim.x;
+#else
+  const int64_t tile = blockIdx.x, zid = blockIdx.z;
+#endif
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-  const int64_t b = RB ? 0 : blockIdx.z / p.split_k;
-  const int sidx = blockIdx.z % p.split_k;
+  const int64_t b = RB ? 0 : zid / p.split_k;
+  const int sidx = zid % p.split_k;
   const int64_t Ktot = RB ? p.K * p.batch : p.K;
   const int64_t kb = (int64_t)sidx * p.kchunk;
   const int64_t ke = min(Ktot, kb + p.kchunk);

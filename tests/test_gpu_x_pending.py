@@ -72,6 +72,20 @@ def test_forward_side_stream_is_bitwise_neutral():
     assert torch.equal(tr1.st.grad, tr2.st.grad)
 
 
+@pytest.mark.parametrize("flag", ["overlap_skip", "overlap_src"])
+def test_backward_third_stream_is_bitwise_neutral(flag):
+    """Backward branches on the third stream (the line blocks' skip-projection dX product, the
+    source-side attention backward) change no bits: dX accumulates in the same order."""
+    _, tr1, b1 = _setup()
+    _, tr2, b2 = _setup()
+    setattr(tr2.model._engine, flag, True)
+    l1 = tr1.forward_backward(b1, 9)
+    l2 = tr2.forward_backward(b2, 9)
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2)
+    assert torch.equal(tr1.st.grad, tr2.st.grad)
+
+
 def test_hip_clip_adamw_matches_torch():
     """alignn_grad_norm_f32 + alignn_adamw_f32 vs torch clip_grad_norm_ + the single-tensor AdamW (the
     reference's CPU optimizer, train.py:1537-1540 without fused=True), 3 steps, two param groups with
