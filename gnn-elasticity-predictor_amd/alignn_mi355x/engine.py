@@ -465,6 +465,8 @@ class AlignnEngine:
         self.overlap_src = False
         # line blocks: the skip projection's dX product beside the attention backward (third stream)
         self.overlap_skip = False
+        # deferred angle-encoder backward on a third stream (see _backward)
+        self.enc_bwd_aux = False  # measured -0.6 % (v31_sweep_enc_bwd_aux_rejected.log)
         # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
         self.wbar_colsum = True
 
@@ -674,6 +676,15 @@ class AlignnEngine:
         # projection chain rules and the angle encoder's first layer: side stream (after the
         # per-layer dM/dw̄ there), overlapping the edge/node encoder backward below
         kept = [t for c in ctx.edge for t in (c.U, *c.edge_scalars)] if defer else []
+        # the deferred angle-encoder backward (the longest branch of the tail) on a third stream,
+        # started as soon as the last line block is done instead of behind the side stream's queue
+        aux = ops.aux_stream(dev) if (defer and side is not None and self.enc_bwd_aux) else None
+        if aux is not None:
+            with _side_work(aux, kept):
+                ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
+                            [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
+                            [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
+                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
         with _side_work(side, (da, *kept)):
             if E > 0 and L > 0:
                 proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
@@ -681,10 +692,11 @@ class AlignnEngine:
                 proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all,
                                   dwl_all, G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
             if defer:
-                ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
-                            [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
-                            [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
-                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
+                if aux is None:
+                    ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
+                                [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
+                                [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
+                                G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
             elif ctx.has_angle and da_written and ctx.angle_enc is None:
                 # da is the masked hidden-layer gradient
                 if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLN_MAX:
@@ -699,3 +711,5 @@ class AlignnEngine:
                       G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))
         if side is not None:
             ops.stream_wait(torch.cuda.current_stream(dev), side)  # join: every gradient is written
+        if aux is not None:
+            ops.stream_wait(torch.cuda.current_stream(dev), aux)

@@ -26,6 +26,9 @@
 #include "common.h"
 
 // XCD-contiguous tile order (below): same-box A/B +1.5 % step (profiles/r01/v30_ab_gemm_xcd.log)
+#ifndef ALIGNN_GEMM_BK128
+#define ALIGNN_GEMM_BK128 0
+#endif
 #ifndef ALIGNN_GEMM_XCD
 #define ALIGNN_GEMM_XCD 1
 #endif
@@ -337,11 +340,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
 template <int BM, int BN, bool A_KC, bool B_KC, bool RB>
 static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
   if (bf) {
-    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true, RB>), grid, dim3(256), 0, s, p);
+    if (bk >= 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true, RB>), grid, dim3(256), 0, s, p);
     else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true, RB>), grid, dim3(256), 0, s, p);
     else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true, RB>), grid, dim3(256), 0, s, p);
   } else {
-    if (bk == 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false, RB>), grid, dim3(256), 0, s, p);
+#if ALIGNN_GEMM_BK128
+    if constexpr (BM == 64 && BN == 64 && !RB) {
+      if (bk == 128) {
+        launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 128, false, RB>), grid, dim3(256), 0, s, p);
+        return;
+      }
+    }
+#endif
+    if (bk >= 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false, RB>), grid, dim3(256), 0, s, p);
     else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false, RB>), grid, dim3(256), 0, s, p);
     else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false, RB>), grid, dim3(256), 0, s, p);
   }
@@ -421,6 +432,13 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   else if (tile & ALIGNN_GEMM_BK32) pl.bk = 32;
   else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;
   else pl.bk = (kchunk >= 128 && tiles * split <= 2 * (int64_t)cus) ? 64 : 16;
+#if ALIGNN_GEMM_BK128
+  // 128-deep stages (half the round trips of 64) for a long split on at most one workgroup per CU
+  // (the 139 KB double-buffered stage allows one per CU); fp32 64x64 only
+  if (!(tile & (ALIGNN_GEMM_BK64 | ALIGNN_GEMM_BK32 | ALIGNN_GEMM_BK16)) && !(tile & ALIGNN_GEMM_BF16) &&
+      pl.bm == 64 && pl.bn == 64 && kchunk >= 256 && tiles * split <= (int64_t)cus)
+    pl.bk = 128;
+#endif
   return pl;
 }
 
@@ -431,6 +449,7 @@ static bool plan_args(const AlignnGemmArgs* a, GemmPlan& pl, int64_t& ktot, int6
   nb_out = rb ? 1 : a->batch;
   pl = make_plan(a->M, a->N, ktot, nb_out, a->split_k, a->tile);
   // a stage must not straddle two batch entries of a batch-reduced product, nor a split chunk
+  if (rb && pl.bk > 64) pl.bk = 64;
   if (rb && (a->K % pl.bk != 0 || (pl.split > 1 && pl.kchunk % pl.bk != 0))) pl.bk = 16;
   return true;
 }
