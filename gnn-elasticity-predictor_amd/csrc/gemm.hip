@@ -27,7 +27,7 @@
 
 // XCD-contiguous tile order (below): same-box A/B +1.5 % step (profiles/r01/v30_ab_gemm_xcd.log)
 #ifndef ALIGNN_GEMM_BK128
-#define ALIGNN_GEMM_BK128 0
+#define ALIGNN_GEMM_BK128 0  // measured -4 % (1 workgroup/CU hides less latency; v32_ab_gemm_bk128_rejected.log)
 #endif
 #ifndef ALIGNN_GEMM_XCD
 #define ALIGNN_GEMM_XCD 1
