@@ -190,6 +190,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
+#ifndef ALIGNN_GEMM_XCD_SPLIT
+#define ALIGNN_GEMM_XCD_SPLIT 1  // also for split-K grids: 8,003 vs 7,969 without (v33_ab_gemm_xcd_nosplit.log)
+#endif
 #if ALIGNN_GEMM_XCD
   // XCD-contiguous work order: workgroups are dispatched round-robin over the 8 XCDs, so the
   // linear id lin lands on XCD lin % 8.  Give XCD x the contiguous range of (z, tile) items
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int64_t nlin = (int64_t)gridDim.x * gridDim.z;
   const int64_t lin = (int64_t)blockIdx.z * gridDim.x + blockIdx.x;
   const int64_t xq = nlin / 8, xr = nlin % 8, xcd = lin % 8;
-  const int64_t item = xcd * xq + min(xcd, xr) + lin / 8;
+  const int64_t item = (ALIGNN_GEMM_XCD_SPLIT || p.split_k == 1) ? xcd * xq + min(xcd, xr) + lin / 8 : lin;
   const int64_t tile = item % gridDim.x, zid = item / gridDim.x;
 #else
   const int64_t tile = blockIdx.x, zid = blockIdx.z;
