@@ -96,6 +96,9 @@ _SIGNATURES = {
                                  c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_gate_ln_bwd_rows": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_gate_ln_bwd_partials": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_gate_ln_bwd_reduce": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_readout_feats_fwd": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_f32, c_u64, c_vp],
                                  c_i32),
     "alignn_readout_pool_bwd": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp],

@@ -305,7 +305,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, enc_grads=None,
                    side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False,
-                   overlap_src: bool = False, wbar_colsum: bool = True, overlap_skip: bool = False) -> None:
+                   overlap_src: bool = False, wbar_colsum: bool = True, overlap_skip: bool = False,
+                   gate_reduce_side: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -319,7 +320,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     overlap_src: with a side stream, run the source-side attention backward on a third stream beside
     the dQ products.
     overlap_skip: on a compacted graph with a side stream, the skip projection's dX product (all n rows)
-    runs on a third stream beside the attention backward; dX accumulates in the same order."""
+    runs on a third stream beside the attention backward; dX accumulates in the same order.
+    gate_reduce_side: the gate/LayerNorm parameter-gradient reduction on the side stream."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -335,7 +337,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         dQKV = torch.empty(na, 3 * D, device=dev)
         dR = torch.empty(n, D, device=dev)
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
-                    gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows)
+                    gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None)
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
     skip = ops.aux_stream(dev) if (side is not None and overlap_skip and rows is not None) else None
     if skip is not None:
@@ -465,6 +467,8 @@ class AlignnEngine:
         self.overlap_src = False
         # line blocks: the skip projection's dX product beside the attention backward (third stream)
         self.overlap_skip = False
+        # gate/LayerNorm parameter-gradient reduction on the side stream (off the critical path)
+        self.gate_reduce_side = True  # +0.3 % (v34_sweep_gate_reduce_side.log)
         # deferred angle-encoder backward on a third stream (see _backward)
         self.enc_bwd_aux = False  # measured -0.6 % (v31_sweep_enc_bwd_aux_rejected.log)
         # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
@@ -653,7 +657,7 @@ class AlignnEngine:
             if c is not None:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
                                overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
-                               overlap_skip=self.overlap_skip)
+                               overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -665,11 +669,11 @@ class AlignnEngine:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
                                    enc_grads=enc_grads, side=side, keep_edge_scalars=defer,
                                    overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
-                                   overlap_skip=self.overlap_skip)
+                                   overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
-                                   overlap_skip=self.overlap_skip)
+                                   overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
                 da_written = True
         if self.debug is not None:
             self.debug["de0"] = de.clone()

@@ -596,13 +596,30 @@ def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, see
 
 
 def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_wbeta, d_ln_w, d_ln_b, drop_p, seed,
-                outp_rows=None):
-    """outp_rows: as in gate_ln_fwd; dout then has outp's (compacted) rows and only those are written."""
+                outp_rows=None, reduce_stream: Optional[torch.cuda.Stream] = None):
+    """outp_rows: as in gate_ln_fwd; dout then has outp's (compacted) rows and only those are written.
+    reduce_stream: run the parameter-gradient reduction (d_wbeta, d_ln_w, d_ln_b) there, after the
+    row kernel, off the current stream (nothing on it reads those gradients)."""
     n, D = R.shape
     rp = _check_outp_rows(outp, outp_rows, n)
     if dout.shape != outp.shape:
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
-    ws = WS.get("gate_ln", int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D)), outp.device)
+    wsize = int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D))
+    if reduce_stream is not None:
+        ws = torch.empty(max(wsize, 1), device=outp.device)   # its own buffer: read later on reduce_stream
+        check(_lib.lib().alignn_gate_ln_bwd_partials(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), rp,
+                                                     R.data_ptr(), R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(),
+                                                     ln_b.data_ptr(), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),
+                                                     dout.data_ptr(), dR.data_ptr(), dR.stride(0), ws.data_ptr(),
+                                                     float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+              "alignn_gate_ln_bwd_partials")
+        stream_wait(reduce_stream, torch.cuda.current_stream(outp.device))
+        ws.record_stream(reduce_stream)
+        check(_lib.lib().alignn_gate_ln_bwd_reduce(n, D, ws.data_ptr(), d_wbeta.data_ptr(), d_ln_w.data_ptr(),
+                                                   d_ln_b.data_ptr(), reduce_stream.cuda_stream),
+              "alignn_gate_ln_bwd_reduce")
+        return
+    ws = WS.get("gate_ln", wsize, outp.device)
     check(_lib.lib().alignn_gate_ln_bwd_rows(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), rp,
                                              R.data_ptr(), R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(),
                                              ln_b.data_ptr(), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),

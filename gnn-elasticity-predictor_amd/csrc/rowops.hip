@@ -395,12 +395,11 @@ extern "C" int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D) {
   return std::max<int64_t>(1, std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n)) * 5 * D;
 }
 
-extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
-                                       const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
-                                       const float* ln_w, const float* ln_b, const float* beta, const float* mu,
-                                       const float* rstd, float* dout, float* dR, int64_t lddr, float* d_wbeta,
-                                       float* d_ln_w, float* d_ln_b, float* workspace, float drop_p, uint64_t seed,
-                                       void* stream) {
+extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                           const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
+                                           const float* ln_w, const float* ln_b, const float* beta, const float* mu,
+                                           const float* rstd, float* dout, float* dR, int64_t lddr, float* workspace,
+                                           float drop_p, uint64_t seed, void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_bwd: unsupported hidden %d", D);
@@ -419,21 +418,44 @@ extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew,
     default: launch(gate_ln_bwd_kernel<8>, g, dim3(256), 0, s, p); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_bwd_reduce(int64_t n, int32_t D, const float* workspace, float* d_wbeta, float* d_ln_w,
+                                         float* d_ln_b, void* stream) {
+  if (!vpl_for(D)) {
+    set_error("gate_ln_bwd: unsupported hidden %d", D);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  if (n == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nwaves = (int)std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n);
+  const int parts = (nwaves + 3) / 4;  // one partial row per workgroup of the partials kernel
   // d_wbeta[3D] | d_ln_w[D] | d_ln_b[D]: one 5D-wide fixed-order reduction when the three are
-  // adjacent in memory (the flat gradient layout), else three.
+  // adjacent in memory (the flat gradient layout), else one per slice of the 5D-wide partial rows.
   const unsigned strips3 = (unsigned)((3 * D + 63) / 64), strips1 = (unsigned)((D + 63) / 64);
   if (d_ln_w == d_wbeta + 3 * D && d_ln_b == d_ln_w + D) {
-    launch(colsum_stage2<0>, dim3(colsum_blocks(5 * D)), dim3(kColsumThreads), 0, s, workspace, (int)g.x,
+    launch(colsum_stage2<0>, dim3(colsum_blocks(5 * D)), dim3(kColsumThreads), 0, s, workspace, parts,
            (int64_t)5 * D, d_wbeta, 1);
   } else {
-    // partial rows are 5D wide: view them through column offsets with row stride 5D via a
-    // compacting pass is unnecessary — reduce each slice with its own launch on a shifted base.
-    launch(gate_ln_slice_reduce, dim3(strips3), dim3(256), 0, s, workspace, (int)g.x, 5 * D, 0, 3 * D, d_wbeta);
-    launch(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, (int)g.x, 5 * D, 3 * D, D, d_ln_w);
-    launch(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, (int)g.x, 5 * D, 4 * D, D, d_ln_b);
+    launch(gate_ln_slice_reduce, dim3(strips3), dim3(256), 0, s, workspace, parts, 5 * D, 0, 3 * D, d_wbeta);
+    launch(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, parts, 5 * D, 3 * D, D, d_ln_w);
+    launch(gate_ln_slice_reduce, dim3(strips1), dim3(256), 0, s, workspace, parts, 5 * D, 4 * D, D, d_ln_b);
   }
   ALIGNN_LAUNCH_CHECK("gate_ln param-grad reduction");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                       const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
+                                       const float* ln_w, const float* ln_b, const float* beta, const float* mu,
+                                       const float* rstd, float* dout, float* dR, int64_t lddr, float* d_wbeta,
+                                       float* d_ln_w, float* d_ln_b, float* workspace, float drop_p, uint64_t seed,
+                                       void* stream) {
+  int rc = alignn_gate_ln_bwd_partials(n, D, dXnew, lddx, outp, outp_rows, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd,
+                                       dout, dR, lddr, workspace, drop_p, seed, stream);
+  if (rc != ALIGNN_OK) return rc;
+  return alignn_gate_ln_bwd_reduce(n, D, workspace, d_wbeta, d_ln_w, d_ln_b, stream);
 }
 
 extern "C" int alignn_gate_ln_bwd(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,

@@ -295,6 +295,17 @@ int alignn_gate_ln_bwd_rows(int64_t n, int32_t D, const float* dXnew, int64_t ld
                             const float* ln_w, const float* ln_b, const float* beta, const float* mu,
                             const float* rstd, float* dout, float* dR, int64_t lddr, float* d_wbeta, float* d_ln_w,
                             float* d_ln_b, float* workspace, float drop_p, uint64_t seed, void* stream);
+/* alignn_gate_ln_bwd_rows in two halves, so the parameter-gradient reduction can run on another
+ * stream (the caller orders it after the partials and keeps the workspace alive until it ran):
+ * _partials writes dout, dR and the per-workgroup partial rows into workspace; _reduce adds the
+ * fixed-order sums of those rows to d_wbeta / d_ln_w / d_ln_b (same n, D). */
+int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
+                                const float* ln_w, const float* ln_b, const float* beta, const float* mu,
+                                const float* rstd, float* dout, float* dR, int64_t lddr, float* workspace,
+                                float drop_p, uint64_t seed, void* stream);
+int alignn_gate_ln_bwd_reduce(int64_t n, int32_t D, const float* workspace, float* d_wbeta, float* d_ln_w,
+                              float* d_ln_b, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Readout (train.py:562-586): global_mean_pool over ptr (PyG, train.py:562), concat with
