@@ -469,6 +469,8 @@ class AlignnEngine:
         self.overlap_skip = False
         # gate/LayerNorm parameter-gradient reduction on the side stream (off the critical path)
         self.gate_reduce_side = True  # +0.3 % (v34_sweep_gate_reduce_side.log)
+        # projection chain rules on the main stream after the encoder MLP backward (see _backward)
+        self.proj_main = False  # measured -0.3 % (with enc_bwd_aux -1.6 %; v35_sweep_proj_main_rejected.log)
         # deferred angle-encoder backward on a third stream (see _backward)
         self.enc_bwd_aux = False  # measured -0.6 % (v31_sweep_enc_bwd_aux_rejected.log)
         # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
@@ -689,12 +691,18 @@ class AlignnEngine:
                             [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                             [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
                             G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
-        with _side_work(side, (da, *kept)):
+        proj_main = self.proj_main and side is not None
+
+        def projections():
             if E > 0 and L > 0:
                 proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
             if line_proj:
                 proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all,
                                   dwl_all, G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
+
+        with _side_work(side, (da, *kept)):
+            if not proj_main:
+                projections()
             if defer:
                 if aux is None:
                     ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
@@ -713,6 +721,10 @@ class AlignnEngine:
                           G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))
         self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
                       G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))
+        if proj_main:
+            # after the encoder MLPs: wait for the side stream's per-layer dM / dw̄, then the chain rules
+            ops.stream_wait(torch.cuda.current_stream(dev), side)
+            projections()
         if side is not None:
             ops.stream_wait(torch.cuda.current_stream(dev), side)  # join: every gradient is written
         if aux is not None:

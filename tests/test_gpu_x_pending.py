@@ -72,7 +72,7 @@ def test_forward_side_stream_is_bitwise_neutral():
     assert torch.equal(tr1.st.grad, tr2.st.grad)
 
 
-@pytest.mark.parametrize("flag", ["overlap_skip", "overlap_src", "enc_bwd_aux", "gate_reduce_side"])
+@pytest.mark.parametrize("flag", ["overlap_skip", "overlap_src", "enc_bwd_aux", "gate_reduce_side", "proj_main"])
 def test_backward_third_stream_is_bitwise_neutral(flag):
     """Backward branches on the third stream (the line blocks' skip-projection dX product, the
     source-side attention backward) change no bits: dX accumulates in the same order."""
