@@ -1244,8 +1244,16 @@ struct BwdSrcParams {
   float* dKV; int64_t lddkv;
 };
 
+#ifndef ALIGNN_SRC_PF
+#define ALIGNN_SRC_PF 16  // 4 -> 16: +1.2 % same-box (8 gives +0.6 %, 24 drops to 1 wave/SIMD; v36_ab_bwd_src_pf.log)
+#endif
+// edges in flight per wave: 2,580 line-graph sources give only ~2.5 waves per SIMD, so the
+// memory-level parallelism has to come from each wave's own group depth
+constexpr int SRC_PF = ALIGNN_SRC_PF;
+
 template <int VPL, int H>
 __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
+  constexpr int PF = SRC_PF;
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
   if (s >= p.n) return;
