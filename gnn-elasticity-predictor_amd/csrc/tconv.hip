@@ -35,6 +35,9 @@ namespace alignn {
 #ifndef ALIGNN_PF
 #define ALIGNN_PF 4
 #endif
+#ifndef ALIGNN_BWD_RING2
+#define ALIGNN_BWD_RING2 0  // two groups in flight in bwd_dst: 245 VGPRs + SGPR spills, -1.4 % (v38_ab_bwd_dst_ring2_rejected.log)
+#endif
 constexpr int PF = ALIGNN_PF;
 
 struct Sched {
@@ -1075,6 +1078,23 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
         if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
       }
     }
+#if ALIGNN_BWD_RING2
+    // second group in flight: its K/V/F rows load while the current group is processed
+    EdgeSlot<VPL> ring2[PF];
+    int64_t rows2[PF];
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      vzero(ring2[j].k); vzero(ring2[j].v); vzero(ring2[j].f);
+      ring2[j].xr = 0.f;
+      const int32_t t = first + stride + j;
+      rows2[j] = 0;
+      if (t < end) {
+        rows2[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
+        load_edge<VPL, 0>(ring2[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(sld(p.src_at, t)), rows2[j], j0,
+                          act, lane);
+      }
+    }
+#endif
     for (int32_t tb = first; tb < end; tb += stride) {
       asm volatile("" ::: "memory");  // keep the u / Vd reads in the loop
       float bs[H], bd[H];
@@ -1162,6 +1182,21 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
           }
         }
       }
+#if ALIGNN_BWD_RING2
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int32_t tn = tb + stride + j, tn2 = tn + stride;
+        ring[j] = ring2[j];
+        rows_[j] = rows2[j];
+        vzero(old[j]);
+        if (tn < end && act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
+        if (tn2 < end) {
+          rows2[j] = p.feat_row ? uni(sld(p.feat_row, tn2)) : tn2;
+          load_edge<VPL, 0>(ring2[j], p.QKVR, p.ldq, D, p.F, p.ldf, no_enc, (int64_t)uni(sld(p.src_at, tn2)),
+                            rows2[j], j0, act, lane);
+        }
+      }
+#else
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         const int32_t tn = tb + stride + j;
@@ -1173,6 +1208,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
           if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
         }
       }
+#endif
     }
   }
   if (heavy) {
