@@ -26,6 +26,9 @@
 #include "common.h"
 
 // XCD-contiguous tile order (below): same-box A/B +1.5 % step (profiles/r01/v30_ab_gemm_xcd.log)
+#ifndef ALIGNN_GEMM_SPLIT_FLOOR
+#define ALIGNN_GEMM_SPLIT_FLOOR 0  // within noise in the step (8,046 vs 8,042; v39_ab_gemm_split_floor_neutral.log)
+#endif
 #ifndef ALIGNN_GEMM_BK128
 #define ALIGNN_GEMM_BK128 0  // measured -4 % (1 workgroup/CU hides less latency; v32_ab_gemm_bk128_rejected.log)
 #endif
@@ -418,7 +421,12 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   if (split <= 0) {
     split = 1;
     if (Ktot >= 512 || tiles < 32) {
+#if ALIGNN_GEMM_SPLIT_FLOOR
+      // never past one wave of workgroups: 164 tiles stay unsplit (26.0 vs 30.3 us split in two)
+      const int64_t want = std::max<int64_t>(1, cus / std::max<int64_t>(tiles, 1));
+#else
       const int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
+#endif
       const int64_t maxs = std::max<int64_t>(1, Ktot / 32);
       split = (int)std::min(want, maxs);
     }
