@@ -1281,7 +1281,7 @@ struct BwdSrcParams {
 };
 
 #ifndef ALIGNN_SRC_PF
-#define ALIGNN_SRC_PF 16  // 4 -> 16: +1.2 % same-box (8 gives +0.6 %, 24 drops to 1 wave/SIMD; v36_ab_bwd_src_pf.log)
+#define ALIGNN_SRC_PF 16  // 4 -> 16: +1.2 % same-box (8: +0.6 %; 12, 3 waves/SIMD: -0.4 % vs 16; 24 drops to 1 wave/SIMD; v36, v41)
 #endif
 // edges in flight per wave: 2,580 line-graph sources give only ~2.5 waves per SIMD, so the
 // memory-level parallelism has to come from each wave's own group depth
