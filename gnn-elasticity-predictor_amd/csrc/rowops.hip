@@ -387,7 +387,7 @@ extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const
 // Waves of the gate/LayerNorm backward (each walks n / waves rows; one partial row of parameter
 // gradients per wave).
 #ifndef ALIGNN_GATE_BWD_WAVES
-#define ALIGNN_GATE_BWD_WAVES 2048  // measured: 2048 +1.0 % step, 4096 +0 % (profiles/r01/v18_ab_gate_waves.log)
+#define ALIGNN_GATE_BWD_WAVES 4096  // 2048: +1.0 % (v18); 4096 once the parameter reduction left the main stream: +0.5 % (v43_ab_gate_waves_4096.log)
 #endif
 
 extern "C" int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D) {
