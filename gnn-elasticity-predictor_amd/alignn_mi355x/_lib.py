@@ -136,6 +136,7 @@ _SIGNATURES = {
     "alignn_plan_destroy": ([c_vp], c_i32),
     "alignn_plan_note_timestamp": ([c_vp], c_i32),
     "alignn_plan_elapsed_ms": ([c_vp, c_i32, c_i32, c_vp], c_i32),
+    "alignn_plan_check_ptrs": ([c_vp, c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
     "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),

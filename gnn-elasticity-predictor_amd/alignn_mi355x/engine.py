@@ -439,6 +439,8 @@ class AlignnEngine:
     def __init__(self, cfg: AlignnConfig):
         cfg.validate()
         self.cfg = cfg
+        # workspaces, side/aux streams and device step seed of this engine's launches (ops.ExecContext)
+        self.ctx = ops.ExecContext("engine")
         self.debug = None  # dict -> backward stores intermediate gradients (diagnostics only)
         # recompute the angle hidden layer inside the line convs (kin <= 16) instead of materialising
         # it: measured slower than streaming the materialised rows so far (occupancy-bound), so off
@@ -494,12 +496,13 @@ class AlignnEngine:
 
     def forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
                 x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
-        with ops.gemm_precision(self.precision):
+        with ops.using(self.ctx), ops.gemm_precision(self.precision):
             return self._forward(P, batch, bc, training, seed, x, global_x, mode)
 
     def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
         """Writes d(loss)/d(param) for every parameter into G (see _backward)."""
-        with ops.gemm_precision(self.precision):
+        with ops.using(self.ctx), ops.gemm_precision(self.precision):
+            self.ctx.new_pass()
             self._backward(P, G, ctx, dout)
 
     def _forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,

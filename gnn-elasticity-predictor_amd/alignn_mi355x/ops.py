@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import threading
 from contextlib import contextmanager
 from typing import Optional
 
@@ -30,48 +31,151 @@ def _require(t: torch.Tensor, name: str, dtype=torch.float32):
 
 
 # ------------------------------------------------------------------------------------------------
-# Workspace (grown on demand, reused; allocate before any graph capture)
+# Execution context: scratch workspaces, auxiliary streams and the device step seed of one engine
 # ------------------------------------------------------------------------------------------------
-class _Workspace:
-    """Scratch buffers per (purpose, device, dtype, stream): kernels on different streams never
-    share one, and a buffer is only reused in its stream's order."""
+def _dkey(device) -> str:
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return str(d)
 
-    def __init__(self):
+
+class ExecContext:
+    """What the launches of one engine (model) share: per-purpose scratch buffers, the side / aux
+    streams for work off the critical path, and the device step seed its dropout kernels read.
+
+    Buffers are keyed by (purpose, device, dtype, stream role) — role "main" (whatever stream is
+    current), "side" or "aux" (this context's own streams) — so kernels on different streams never
+    share one, and a buffer is reused only in its stream's order.  A buffer grows on demand while
+    nothing is being recorded; during a launch-plan recording (:func:`recording`) growth is refused,
+    because earlier recorded launches hold the old buffer's address.  The trainer sizes them with
+    uncaptured warm-up steps of the same shapes first and owns them for as long as its plans live.
+
+    ``fresh(purpose, ...)`` hands out a distinct buffer per call within one backward pass (reset by
+    :meth:`new_pass`): for data written on one stream and read later on another (the gate/LayerNorm
+    parameter-gradient partials, reduced on the side stream)."""
+
+    def __init__(self, name: str = "engine", owned: bool = True):
+        self.name = name
+        self.owned = owned
         self.buf = {}
+        self._cursor = {}
+        self._side = {}
+        self._aux = {}
+        self.step_seed: Optional[torch.Tensor] = None
 
-    def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
-        k = (key, str(device), dtype, torch.cuda.current_stream(device).cuda_stream)
+    def side(self, device) -> torch.cuda.Stream:
+        """A second stream per device for work off the critical path (weight gradients)."""
+        key = _dkey(device)
+        if key not in self._side:
+            self._side[key] = torch.cuda.Stream(device=device)
+        return self._side[key]
+
+    def aux(self, device) -> torch.cuda.Stream:
+        """A third stream per device for short branches beside the critical path."""
+        key = _dkey(device)
+        if key not in self._aux:
+            self._aux[key] = torch.cuda.Stream(device=device)
+        return self._aux[key]
+
+    def _role(self, device) -> str:
+        if torch.device(device).type != "cuda":
+            return "main"
+        cur = torch.cuda.current_stream(device).cuda_stream
+        key = _dkey(device)
+        if key in self._side and self._side[key].cuda_stream == cur:
+            return "side"
+        if key in self._aux and self._aux[key].cuda_stream == cur:
+            return "aux"
+        return "main"
+
+    def _take(self, k, n: int, device, dtype) -> torch.Tensor:
         cur = self.buf.get(k)
         if cur is None or cur.numel() < n:
+            if _RECORDING:
+                raise RuntimeError(
+                    f"workspace {k[0]!r} ({self.name}) would grow to {n} elements while a launch plan is being "
+                    f"recorded (earlier recorded launches hold the old buffer): run an uncaptured step of the same "
+                    f"shapes first")
             cur = torch.empty(max(n, 1), device=device, dtype=dtype)
             self.buf[k] = cur
         return cur
 
+    def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
+        if _RECORDING and not self.owned:
+            raise RuntimeError("launch-plan recording needs an engine-owned execution context (ops.using)")
+        return self._take((key, _dkey(device), dtype, self._role(device)), n, device, dtype)
 
-_SIDE = {}
+    def fresh(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
+        if not self.owned:   # shared default context: a new allocation (eager use only)
+            if _RECORDING:
+                raise RuntimeError("launch-plan recording needs an engine-owned execution context (ops.using)")
+            return torch.empty(max(n, 1), device=device, dtype=dtype)
+        i = self._cursor.get(key, 0)
+        self._cursor[key] = i + 1
+        return self._take((key, _dkey(device), dtype, ("fresh", i)), n, device, dtype)
+
+    def new_pass(self) -> None:
+        self._cursor.clear()
+
+    def tensors(self):
+        return list(self.buf.values())
+
+
+_TLS = threading.local()
+_DEFAULT = ExecContext("default", owned=False)
+_RECORDING = False
+
+
+def current() -> ExecContext:
+    st = getattr(_TLS, "stack", None)
+    return st[-1] if st else _DEFAULT
+
+
+@contextmanager
+def using(ctx: ExecContext):
+    """Launches inside run with ``ctx``'s workspaces, streams and device step seed."""
+    st = getattr(_TLS, "stack", None)
+    if st is None:
+        st = _TLS.stack = []
+    prev = current()
+    st.append(ctx)
+    _lib.lib().alignn_set_step_seed(None if ctx.step_seed is None else ctx.step_seed.data_ptr())
+    try:
+        yield ctx
+    finally:
+        st.pop()
+        _lib.lib().alignn_set_step_seed(None if prev.step_seed is None else prev.step_seed.data_ptr())
+
+
+@contextmanager
+def recording():
+    """Marks a launch-plan recording: workspaces may not grow, the default context may not be used."""
+    global _RECORDING
+    prev = _RECORDING
+    _RECORDING = True
+    try:
+        yield
+    finally:
+        _RECORDING = prev
 
 
 def side_stream(device) -> torch.cuda.Stream:
-    """A second stream per device for work off the critical path (weight gradients)."""
-    key = str(device)
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=device)
-    return _SIDE[key]
-
-
-_AUX = {}
+    return current().side(device)
 
 
 def aux_stream(device) -> torch.cuda.Stream:
-    """A third stream per device for short branches beside the critical path (the source-side
-    attention backward next to the dQ products)."""
-    key = str(device)
-    if key not in _AUX:
-        _AUX[key] = torch.cuda.Stream(device=device)
-    return _AUX[key]
+    return current().aux(device)
 
 
-WS = _Workspace()
+class _WSProxy:
+    """``WS.get`` = the current context's workspace (kept for the tools/ scripts)."""
+
+    def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
+        return current().get(key, n, device, dtype)
+
+
+WS = _WSProxy()
 
 
 def stream_wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
@@ -139,17 +243,13 @@ def gemm_precision(precision: str):
     finally:
         _GEMM_FLAGS = prev
 
-_STEP_SEED: Optional[torch.Tensor] = None
-
-
 def set_step_seed(t: Optional[torch.Tensor]) -> None:
-    """Register a device int64[1] that every dropout / jitter kernel launched afterwards mixes into
-    its site seed at run time (alignn_set_step_seed): a captured HIP graph then draws fresh masks on
-    each replay once the caller updates ``t``.  None: host seeds only."""
-    global _STEP_SEED
+    """Register a device int64[1] on the current context that every dropout / jitter kernel launched
+    afterwards (in it) mixes into its site seed at run time (alignn_set_step_seed): a recorded plan
+    then draws fresh masks on each replay once the caller updates ``t``.  None: host seeds only."""
     if t is not None and (t.dtype != torch.int64 or t.numel() != 1 or not t.is_cuda):
         raise ValueError("step seed must be a device int64 tensor with one element")
-    _STEP_SEED = t
+    current().step_seed = t
     _lib.lib().alignn_set_step_seed(None if t is None else t.data_ptr())
 
 
@@ -606,7 +706,7 @@ def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_w
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
     wsize = int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D))
     if reduce_stream is not None:
-        ws = torch.empty(max(wsize, 1), device=outp.device)   # its own buffer: read later on reduce_stream
+        ws = current().fresh("gate_ln_red", wsize, outp.device)   # its own buffer: read later on reduce_stream
         check(_lib.lib().alignn_gate_ln_bwd_partials(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), rp,
                                                      R.data_ptr(), R.stride(0), wbeta.data_ptr(), ln_w.data_ptr(),
                                                      ln_b.data_ptr(), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),

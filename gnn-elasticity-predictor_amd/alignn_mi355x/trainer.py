@@ -65,7 +65,17 @@ class FusedTrainer:
         self.step_count = 0
         self._graph = None
         self._seed_dev = None
+        # the engine's execution context (workspaces, side stream, device step seed): every launch of
+        # this trainer's step runs in it, and a recorded plan owns it (its buffers never move)
+        self.ctx = model._engine.ctx
         self.grad_hook = None  # called with the flat gradient between backward and clip (DP all_reduce)
+
+    def use_step_seed(self, t: Optional[torch.Tensor]) -> None:
+        """Device int64[1] step seed the dropout/jitter kernels of this trainer mix in (None: host
+        seeds only).  capture() installs its own; tests share one between two trainers."""
+        if t is not None and (t.dtype != torch.int64 or t.numel() != 1 or not t.is_cuda):
+            raise ValueError("step seed must be a device int64 tensor with one element")
+        self.ctx.step_seed = t
 
     def set_lr(self, lr: float, sigma_lr: Optional[float] = None) -> None:
         self.opt.param_groups[0]["lr"] = lr
@@ -76,6 +86,10 @@ class FusedTrainer:
                          sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward + loss + backward into the flat gradient buffer; returns the loss (device).
         sample_weights: per-graph KNN weights [B] (train.py:660-674), or None."""
+        with ops.using(self.ctx):
+            return self._forward_backward(batch, seed, training, sample_weights)
+
+    def _forward_backward(self, batch, seed: int, training: bool, sample_weights: Optional[torch.Tensor]):
         model, st = self.model, self.st
         bc = batch_cache(batch)
         x, gx = batch.x, batch.global_x
@@ -106,9 +120,11 @@ class FusedTrainer:
     def _clip_and_update(self) -> None:
         if self.optimizer == "hip":
             st = self.st
-            ops.grad_norm(st.grad, self.gnorm)
-            ops.adamw_step(st.flat, st.grad, self.exp_avg, self.exp_avg_sq, st.P.sigma_start, self.lr, self.sigma_lr,
-                           self.weight_decay, norm=self.gnorm, max_norm=self.max_norm, step=self.hip_step)
+            with ops.using(self.ctx):
+                ops.grad_norm(st.grad, self.gnorm)
+                ops.adamw_step(st.flat, st.grad, self.exp_avg, self.exp_avg_sq, st.P.sigma_start, self.lr,
+                               self.sigma_lr, self.weight_decay, norm=self.gnorm, max_norm=self.max_norm,
+                               step=self.hip_step)
             return
         torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
         self.opt.step()
@@ -119,7 +135,10 @@ class FusedTrainer:
     #   mode "plan" (default): two native launch plans (plan.hip) — every library launch and every
     #     cross-stream edge of the step, replayed from C++ onto the same two streams.  Recorded
     #     inside a torch graph capture, whose private memory pool keeps every buffer of the step at
-    #     its address; the captured graph's node census must match the plan (nothing foreign).
+    #     its address; the captured graph's node census must match the plan (nothing foreign), and
+    #     every device pointer the plan holds must lie in a buffer the trainer owns (its state, the
+    #     batch and its CSR cache, its engine's workspaces — sized by the warm-up steps and frozen
+    #     during the recording — or the capture's pool): alignn_plan_check_ptrs.
     #   mode "graph": ROCm HIP graphs of the same capture (measured slower on MI355X: 5.5 vs 5.2 ms
     #     eager, the two streams' branches lose concurrency).
     # ``grad_hook`` (e.g. the data-parallel all_reduce) runs eagerly between the two phases.
@@ -137,9 +156,11 @@ class FusedTrainer:
         self.release_capture()
         if self._seed_dev is None:
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)
-        ops.set_step_seed(self._seed_dev)
-        batch_cache(batch)
-        # warm-up (allocations, optimizer state) on a side stream, then restore the state
+        self.use_step_seed(self._seed_dev)
+        with ops.using(self.ctx):
+            batch_cache(batch)
+        # warm-up (allocations, optimizer state, every workspace at this batch's sizes) on a side
+        # stream, then restore the state
         snap = self._snapshot()
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -153,24 +174,44 @@ class FusedTrainer:
         keep = mode == "plan"
         g_fb, g_up = torch.cuda.CUDAGraph(keep_graph=keep), torch.cuda.CUDAGraph(keep_graph=keep)
         plans = []
-        for g, fn, pool in ((g_fb, lambda: self.forward_backward(batch, 0), None),
-                            (g_up, self._clip_and_update, "fb")):
-            with torch.cuda.graph(g, pool=(g_fb.pool() if pool else None)):
-                if keep:
-                    plans.append(_record_plan(fn))
-                else:
-                    fn()
-        torch.cuda.synchronize(dev)
-        self._restore(snap)
-        if keep:
-            try:
+        try:
+            with ops.recording():
+                for g, fn, pool in ((g_fb, lambda: self.forward_backward(batch, 0), None),
+                                    (g_up, self._clip_and_update, "fb")):
+                    with torch.cuda.graph(g, pool=(g_fb.pool() if pool else None)):
+                        if keep:
+                            plans.append(_record_plan(fn))
+                        else:
+                            fn()
+            torch.cuda.synchronize(dev)
+            self._restore(snap)
+            if keep:
+                ranges = self._held_ranges(batch, g_fb.pool())
                 for g, pl, what in ((g_fb, plans[0], "forward/backward"), (g_up, plans[1], "clip/AdamW")):
                     _check_census(g, pl, what)
-            except Exception:
-                for pl in plans:
-                    _lib.lib().alignn_plan_destroy(pl)
-                raise
+                    _check_ownership(pl, ranges, what)
+        except Exception:
+            for pl in plans:
+                _lib.lib().alignn_plan_destroy(pl)
+            raise
         self._graph = (g_fb, g_up, batch, plans if keep else None)
+
+    def _held_ranges(self, batch, pool_id):
+        """[lo, hi) device byte ranges this trainer holds for as long as a captured plan lives: its own
+        state, the model's buffers, the batch and its device caches, the engine's workspaces, and the
+        segments of the capture's private memory pool (kept by the captured graph)."""
+        ranges = []
+        for t in _cuda_tensors((self.st.flat, self.st.grad, getattr(self, "exp_avg", None),
+                                getattr(self, "exp_avg_sq", None), getattr(self, "hip_step", None),
+                                getattr(self, "gnorm", None), self.loss, self.log_means, self.log_stds,
+                                self._seed_dev, self.ctx.tensors(), batch, list(self.model.buffers()))):
+            s = t.untyped_storage()
+            ranges.append((s.data_ptr(), s.data_ptr() + s.nbytes()))
+        pool = tuple(pool_id)
+        for seg in torch.cuda.memory_snapshot():
+            if tuple(seg.get("segment_pool_id", ())) == pool:
+                ranges.append((seg["address"], seg["address"] + seg["total_size"]))
+        return ranges
 
     def release_capture(self) -> None:
         if self._graph is not None and self._graph[3]:
@@ -248,6 +289,46 @@ def plan_info(plan) -> dict:
     v = [ctypes.c_int64() for _ in range(4)]
     check(_lib.lib().alignn_plan_info(plan, *[ctypes.byref(x) for x in v]), "alignn_plan_info")
     return dict(zip(("launches", "edges", "streams", "arg_bytes"), (x.value for x in v)))
+
+
+def _cuda_tensors(root, depth: int = 6):
+    """Every device tensor reachable from ``root`` through containers and object attributes."""
+    out, seen = [], set()
+
+    def walk(o, d):
+        if o is None or id(o) in seen or d < 0:
+            return
+        seen.add(id(o))
+        if torch.is_tensor(o):
+            if o.is_cuda and o.numel():
+                out.append(o)
+            return
+        if isinstance(o, (list, tuple, set)):
+            for v in o:
+                walk(v, d - 1)
+        elif isinstance(o, dict):
+            for v in o.values():
+                walk(v, d - 1)
+        elif not isinstance(o, (int, float, str, bytes, bool, torch.nn.Module)) and not callable(o):
+            for v in getattr(o, "__dict__", {}).values():
+                walk(v, d - 1)
+            for k in getattr(type(o), "__slots__", ()):
+                walk(getattr(o, k, None), d - 1)
+
+    walk(root, depth)
+    return out
+
+
+def _check_ownership(plan, ranges, what: str) -> None:
+    """Every device pointer the recorded plan holds lies in a buffer the trainer holds (host check)."""
+    arr = (ctypes.c_uint64 * (2 * len(ranges)))(*[v for r in ranges for v in r])
+    bad, idx, n = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = _lib.lib().alignn_plan_check_ptrs(plan, arr, len(ranges), ctypes.byref(bad), ctypes.byref(idx),
+                                           ctypes.byref(n))
+    if rc != 0:
+        msg = _lib.lib().alignn_last_error()
+        raise RuntimeError(f"launch plan of the {what} phase references memory the trainer does not hold "
+                           f"(launch {idx.value}, 0x{bad.value:x}): {msg.decode() if msg else ''}")
 
 
 def _check_census(graph: torch.cuda.CUDAGraph, plan, what: str) -> None:

@@ -47,9 +47,18 @@ int hip_status(hipError_t e, const char* what);
 // kernel, grid, block, LDS bytes, stream and a copy of the argument bytes — so the plan can issue
 // the same step again from C++ (alignn_plan_replay) without any per-launch host work above HIP.
 // ---------------------------------------------------------------------------------------------
-extern bool g_recording;
+// Recording state is per host thread (a plan records the launches its own thread issues), so
+// independent callers on other threads neither see nor disturb it.
+extern thread_local bool g_recording;
 void record_launch(const void* func, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, void* const* args,
-                   const size_t* sizes, const size_t* aligns, int nargs);
+                   const size_t* sizes, const size_t* aligns, const unsigned char* kinds, int nargs);
+
+// Argument kinds kept with a recorded launch, for the plan's pointer-ownership check
+// (alignn_plan_check_ptrs): 1 = device pointer, 2 = struct (its 8-byte words are scanned), 0 = scalar.
+template <typename T>
+constexpr unsigned char arg_kind() {
+  return std::is_pointer<T>::value ? 1 : (std::is_class<T>::value ? 2 : 0);
+}
 
 template <typename... P, typename... A>
 inline void launch(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, A&&... a) {
@@ -60,7 +69,8 @@ inline void launch(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t shmem, 
   if (g_recording) {
     const size_t sizes[sizeof...(P) + 1] = {sizeof(std::decay_t<P>)..., 0};
     const size_t aligns[sizeof...(P) + 1] = {alignof(std::decay_t<P>)..., 1};
-    record_launch(reinterpret_cast<const void*>(kernel), grid, block, shmem, s, ptrs, sizes, aligns,
+    const unsigned char kinds[sizeof...(P) + 1] = {arg_kind<std::decay_t<P>>()..., 0};
+    record_launch(reinterpret_cast<const void*>(kernel), grid, block, shmem, s, ptrs, sizes, aligns, kinds,
                   (int)sizeof...(P));
   }
   // a failure is left in hipGetLastError for the caller's ALIGNN_LAUNCH_CHECK
@@ -105,8 +115,9 @@ __device__ __forceinline__ float dropout_mul(uint64_t seed, uint64_t idx, uint32
   return hash_u32(seed, idx) >= thresh ? inv_keep : 0.0f;
 }
 
-// Device-resident step seed registered by alignn_set_step_seed (NULL: host seeds only).
-extern const uint64_t* g_step_seed;
+// Device-resident step seed registered by alignn_set_step_seed (NULL: host seeds only).  Per host
+// thread: the registering caller's launches (and the plans they record) carry its pointer.
+extern thread_local const uint64_t* g_step_seed;
 
 __device__ __forceinline__ uint64_t mix_seed(uint64_t site, const uint64_t* sptr) {
   if (!sptr) return site;
@@ -120,6 +131,7 @@ struct DropParams {
   uint32_t thresh;   // p * 2^32
   float inv_keep;    // 1/(1-p)
   int active;
+  int pad_;              // explicit: kernel-argument structs have no undefined bytes (plan.hip)
   const uint64_t* sptr;  // step seed (mixed in once per thread: resolve_drop)
 };
 // Call once at kernel entry: folds the device step seed into d.seed.
@@ -132,6 +144,7 @@ inline DropParams make_drop(float p, uint64_t seed) {
   d.seed = seed;
   d.sptr = g_step_seed;
   d.active = p > 0.0f ? 1 : 0;
+  d.pad_ = 0;
   double t = (double)p * 4294967296.0;
   d.thresh = p > 0.0f ? (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t) : 0u;
   d.inv_keep = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;

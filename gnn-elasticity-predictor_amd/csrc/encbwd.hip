@@ -23,6 +23,8 @@
 // edge: 863 us at B = 32; profiles/r01/v13_sweep.log).  dW1/db1 partials: registers per thread,
 // one partial row per workgroup, a second kernel sums the workgroup partials in workgroup order
 // (deterministic: fixed grid, fixed orders).
+#include <cstring>
+
 #include "common.h"
 #include "vec.h"
 
@@ -222,6 +224,7 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
     return ALIGNN_E_WORKSPACE;
   }
   EncBwdParams p;
+  std::memset(&p, 0, sizeof p);  // defined padding bytes (plan.hip scans recorded struct words)
   p.n = a->n; p.T = a->T; p.D = a->D; p.H = a->H; p.L = a->L; p.kin = a->kin;
   p.off_dst = a->off_dst; p.x = a->x; p.ldx = a->ldx; p.w1 = a->w1; p.b1 = a->b1;
   for (int l = 0; l < EB_LMAX; ++l) {

@@ -23,6 +23,8 @@
 // LDS images follow global contiguity (no transposes while staging):
 //   operand contiguous along k   -> [row][BKT+4]
 //   operand contiguous along row -> [BKT][ROWS+4]
+#include <cstring>
+
 #include "common.h"
 
 // XCD-contiguous tile order (below): same-box A/B +1.5 % step (profiles/r01/v30_ab_gemm_xcd.log)
@@ -59,6 +61,7 @@ struct GemmParams {
   float* ws;
   int vecA, vecB;
   int reduce_batch;  // sum the batch into one output: K loop runs over (batch, k), K % BK == 0
+  int pad_;
   const int32_t* c_rows;  // optional scatter of C rows
 };
 
@@ -488,6 +491,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GemmParams p;
+  std::memset(&p, 0, sizeof p);  // defined padding bytes (plan.hip scans recorded struct words)
   p.M = a->M; p.N = a->N; p.K = a->K; p.batch = a->batch;
   p.A = a->A; p.sam = a->sam; p.sak = a->sak; p.sab = a->sab;
   p.B = a->B; p.sbk = a->sbk; p.sbn = a->sbn; p.sbb = a->sbb;

@@ -14,7 +14,9 @@
 // Stream slot 0 is the stream that was current at alignn_plan_begin; replay puts the caller's
 // stream there, every other slot keeps its recorded stream.  Buffers are referenced by address:
 // the caller keeps every tensor the step touched alive and in place (trainer.py records inside a
-// torch graph capture, whose private memory pool does that).
+// torch graph capture, whose private memory pool does that, and owns its workspaces), and proves
+// it once with alignn_plan_check_ptrs: every device pointer in every recorded argument must lie in
+// a range the caller declares it holds for the plan's lifetime.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -23,7 +25,7 @@
 
 namespace alignn {
 
-bool g_recording = false;
+thread_local bool g_recording = false;
 
 struct PlanEntry {
   const void* func;     // kernel (nullptr: stream-ordering edge or timestamp)
@@ -39,13 +41,15 @@ struct Plan {
   std::vector<PlanEntry> entries;
   std::vector<unsigned char> args;   // argument bytes (each at its type's alignment, max 16)
   std::vector<size_t> arg_off;
+  std::vector<size_t> arg_size;
+  std::vector<unsigned char> arg_kind;  // arg_kind<T>() of each argument (common.h)
   std::vector<hipStream_t> streams;  // recorded handles; [0] replaced by the replay stream
   std::vector<hipEvent_t> events;
   std::vector<hipEvent_t> stamps;    // timing events (roofline probes around chosen launches)
   int launches = 0;
 };
 
-static Plan* g_plan = nullptr;
+static thread_local Plan* g_plan = nullptr;
 
 }  // namespace alignn
 extern "C" int alignn_plan_destroy(void* plan);
@@ -59,7 +63,7 @@ static int slot_of(Plan* p, hipStream_t s) {
 }
 
 void record_launch(const void* func, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, void* const* args,
-                   const size_t* sizes, const size_t* aligns, int nargs) {
+                   const size_t* sizes, const size_t* aligns, const unsigned char* kinds, int nargs) {
   Plan* p = g_plan;
   if (!p) return;
   PlanEntry e{};
@@ -77,6 +81,8 @@ void record_launch(const void* func, dim3 grid, dim3 block, uint32_t shmem, hipS
     p->args.resize(off + sizes[i]);
     std::memcpy(p->args.data() + off, args[i], sizes[i]);
     p->arg_off.push_back(off);
+    p->arg_size.push_back(sizes[i]);
+    p->arg_kind.push_back(kinds[i]);
   }
   p->entries.push_back(e);
   p->launches++;
@@ -214,6 +220,67 @@ extern "C" int alignn_plan_destroy(void* plan) {
   for (auto& ev : p->stamps)
     if (ev) (void)hipEventDestroy(ev);
   delete p;
+  return ALIGNN_OK;
+}
+
+// Ownership check of a recorded plan.  ranges: n pairs [lo, hi) of device byte addresses the caller
+// holds for the plan's lifetime.  Every non-null pointer argument, and every 8-byte word of a
+// struct argument that the HIP runtime resolves to device memory, must fall in one of them;
+// otherwise the first offending value and its launch index are returned with ALIGNN_E_BAD_SHAPE.
+extern "C" int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, int64_t n, uint64_t* bad_value,
+                                      int64_t* bad_launch, int64_t* checked) {
+  const Plan* p = reinterpret_cast<const Plan*>(plan);
+  if (!p || n < 0 || (n > 0 && !ranges)) return ALIGNN_E_BAD_SHAPE;
+  std::vector<std::pair<uint64_t, uint64_t>> rs;
+  for (int64_t i = 0; i < n; ++i) rs.emplace_back(ranges[2 * i], ranges[2 * i + 1]);
+  auto held = [&](uint64_t v) {  // ranges may nest or overlap (views inside pool segments)
+    for (const auto& r : rs)
+      if (v >= r.first && v < r.second) return true;
+    return false;
+  };
+  auto device_word = [](uint64_t v) {
+    if (v < (1ull << 32) || v >= (1ull << 47)) return false;  // not a user-space device address
+    hipPointerAttribute_t at;
+    const hipError_t r = hipPointerGetAttributes(&at, reinterpret_cast<const void*>(v));
+    (void)hipGetLastError();  // an unknown address is an ordinary answer here, not a pending error
+    return r == hipSuccess && at.type == hipMemoryTypeDevice;
+  };
+  int64_t launch_idx = -1, nchecked = 0;
+  for (const PlanEntry& e : p->entries) {
+    if (!e.func) continue;
+    ++launch_idx;
+    for (size_t a = 0; a < e.nargs; ++a) {
+      const size_t j = e.arg0 + a;
+      const unsigned char* b = p->args.data() + p->arg_off[j];
+      if (p->arg_kind[j] == 1) {
+        uint64_t v;
+        std::memcpy(&v, b, sizeof v);
+        if (!v) continue;
+        ++nchecked;
+        if (!held(v)) {
+          if (bad_value) *bad_value = v;
+          if (bad_launch) *bad_launch = launch_idx;
+          set_error("plan_check_ptrs: launch %lld argument %zu points at 0x%llx, outside every held buffer",
+                    (long long)launch_idx, a, (unsigned long long)v);
+          return ALIGNN_E_BAD_SHAPE;
+        }
+      } else if (p->arg_kind[j] == 2) {
+        for (size_t o = 0; o + 8 <= p->arg_size[j]; o += 8) {
+          uint64_t v;
+          std::memcpy(&v, b + o, sizeof v);
+          if (!v || held(v)) { nchecked += v ? 1 : 0; continue; }
+          if (device_word(v)) {
+            if (bad_value) *bad_value = v;
+            if (bad_launch) *bad_launch = launch_idx;
+            set_error("plan_check_ptrs: launch %lld argument %zu (struct word %zu) points at 0x%llx, outside "
+                      "every held buffer", (long long)launch_idx, a, o / 8, (unsigned long long)v);
+            return ALIGNN_E_BAD_SHAPE;
+          }
+        }
+      }
+    }
+  }
+  if (checked) *checked = nchecked;
   return ALIGNN_OK;
 }
 

@@ -9,7 +9,7 @@
 namespace alignn {
 
 static thread_local char g_err[512] = "";
-const uint64_t* g_step_seed = nullptr;
+thread_local const uint64_t* g_step_seed = nullptr;
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -37,7 +37,7 @@ static int grid_for(int64_t work, int block = 256, int64_t cap = 8192) {
 // ---------------------------------------------------------------------------------------------
 struct GateFwdParams {
   int64_t n;
-  int D;
+  int D, pad_;
   const float* outp; const float* R; int64_t ldr;
   const float* wbeta;
   const float* X; int64_t ldx;
@@ -109,14 +109,14 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
 
 struct GateBwdParams {
   int64_t n;
-  int D;
+  int D, pad_;
   const float* dXn; int64_t lddx;
   const float* outp; const float* R; int64_t ldr;
   const float* wbeta; const float* lnw; const float* lnb;
   const float* beta; const float* mu; const float* rstd;
   float* dout; float* dR; int64_t lddr;
   float* part;  // [workgroups][5*D]: one merged partial row per workgroup
-  int nwaves;
+  int nwaves, pad2_;
   DropParams drop;
   const int32_t* orow;  // optional: o and dout rows through this map (-1: o = 0, dout not written)
 };
@@ -362,7 +362,7 @@ extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, 
     return ALIGNN_E_UNSUPPORTED;
   }
   if (n == 0) return ALIGNN_OK;
-  GateFwdParams p{n, D, outp, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd, make_drop(drop_p, seed),
+  GateFwdParams p{n, D, 0, outp, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd, make_drop(drop_p, seed),
                   outp_rows};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((n + 3) / 4));
@@ -407,8 +407,8 @@ extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dX
   }
   if (n == 0) return ALIGNN_OK;
   const int nwaves = (int)std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n);
-  GateBwdParams p{n, D, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
-                  nwaves, make_drop(drop_p, seed), outp_rows};
+  GateBwdParams p{n, D, 0, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
+                  nwaves, 0, make_drop(drop_p, seed), outp_rows};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
   switch (vpl) {

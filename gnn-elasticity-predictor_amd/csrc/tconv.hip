@@ -49,7 +49,7 @@ struct Sched {
 };
 
 struct EncParams {
-  const float* x; int64_t ldx; int kin;
+  const float* x; int64_t ldx; int kin; int pad_;
   const float* w1;  // [D, kin] (nn.Linear weight)
   const float* b1;  // [D]
 };
@@ -140,7 +140,7 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 // =============================================================================================
 struct FwdParams {
   int64_t n, m;
-  int D;
+  int D, pad_;
   const int32_t* off;
   const int32_t* src_at;
   const int32_t* feat_row;
@@ -388,7 +388,7 @@ __global__ TCONV_ATTR void tconv_fwd_kernel(FwdParams p, Sched sc, EncParams en)
 // =============================================================================================
 struct BwdDstParams {
   int64_t n, m;
-  int D;
+  int D, pad_;
   const int32_t* off;
   const int32_t* src_at;
   const int32_t* feat_row;
@@ -404,7 +404,7 @@ struct BwdDstParams {
   float* dq; int64_t lddq;
   float* Sz; float* sigz;
   float* dz_e; float* alpha_e;
-  float* dF; int64_t lddf; int acc_dF;
+  float* dF; int64_t lddf; int acc_dF, pad2_;
   DropParams drop;
 };
 
@@ -825,7 +825,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
       reduce_bcast<H>(c, lane);
     }
     EdgeSlot<VPL> ring[PF];
-    const EncParams no_enc{nullptr, 0, 0, nullptr, nullptr};
+    const EncParams no_enc{nullptr, 0, 0, 0, nullptr, nullptr};
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
@@ -1063,7 +1063,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
     EdgeSlot<VPL> ring[PF];
     float old[PF][VPL];
     int64_t rows_[PF];
-    const EncParams no_enc{nullptr, 0, 0, nullptr, nullptr};
+    const EncParams no_enc{nullptr, 0, 0, 0, nullptr, nullptr};
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
@@ -1269,7 +1269,7 @@ __global__ TCONV_ATTR void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
 // =============================================================================================
 struct BwdSrcParams {
   int64_t n, m;
-  int D;
+  int D, pad_;
   const int32_t* off_src;
   const int32_t* pos_src;
   const int32_t* dst_at;
@@ -1505,7 +1505,7 @@ static int check_dims(int D, int H) {
 
 // Validates the edge-feature source: exactly one of F (materialised rows) or enc (recomputed).
 static int edge_source(const float* F, const AlignnEdgeEncoder* enc, EncParams& en, int& km) {
-  en = EncParams{nullptr, 0, 0, nullptr, nullptr};
+  en = EncParams{nullptr, 0, 0, 0, nullptr, nullptr};
   km = 0;
   if (enc) {
     km = km_for(enc->kin);
@@ -1513,7 +1513,7 @@ static int edge_source(const float* F, const AlignnEdgeEncoder* enc, EncParams& 
       set_error("tconv: edge encoder needs 1 <= kin <= 16, x (ldx >= kin), w1 and b1 (kin=%d)", (int)enc->kin);
       return ALIGNN_E_BAD_SHAPE;
     }
-    en = EncParams{enc->x, enc->ldx, enc->kin, enc->w1, enc->b1};
+    en = EncParams{enc->x, enc->ldx, enc->kin, 0, enc->w1, enc->b1};
     return ALIGNN_OK;
   }
   if (!F) {
@@ -1538,7 +1538,7 @@ extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, cons
   EncParams en;
   int km;
   if ((rc = edge_source(F, enc, en, km))) return rc;
-  FwdParams p{n, m, D, off_dst, src_at, feat_row, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
+  FwdParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
               make_drop(drop_p, seed)};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
@@ -1591,8 +1591,8 @@ extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, 
     return ALIGNN_E_BAD_SHAPE;
   }
   const int flags = sched ? sched->flags : 0;
-  BwdDstParams p{n, m, D, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den,
-                 dq, lddq, Sz, sigz, dz_e, alpha_e, enc ? nullptr : dF, lddf, accumulate_dF,
+  BwdDstParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den,
+                 dq, lddq, Sz, sigz, dz_e, alpha_e, enc ? nullptr : dF, lddf, accumulate_dF, 0,
                  make_drop(drop_p, seed)};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
@@ -1628,7 +1628,7 @@ extern "C" int alignn_tconv_bwd_src(int64_t n, int64_t m, int32_t D, int32_t H, 
   int rc = check_dims(D, H);
   if (rc) return rc;
   if (n == 0) return ALIGNN_OK;
-  BwdSrcParams p{n, m, D, off_src, pos_src, dst_at, QKVR, ldq, dout, dz_e, alpha_e, dKV, lddkv};
+  BwdSrcParams p{n, m, D, 0, off_src, pos_src, dst_at, QKVR, ldq, dout, dz_e, alpha_e, dKV, lddkv};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
   ALIGNN_DISPATCH_VH(vpl, H, launch_bwd_src, p, s);

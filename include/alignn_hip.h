@@ -438,6 +438,14 @@ int alignn_plan_info(const void* plan, int64_t* launches, int64_t* waits, int64_
 int alignn_plan_destroy(void* plan);
 int alignn_plan_note_timestamp(void* stream);
 int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms);
+/* alignn_plan_check_ptrs(plan, ranges, n, &bad_value, &bad_launch, &checked): ownership proof of a
+ * recorded plan.  ranges = n pairs [lo, hi) of device byte addresses the caller holds for as long as
+ * the plan lives (its workspaces, parameters, batch buffers, the capture's memory pool).  Every
+ * non-null pointer argument and every struct-argument word that resolves to device memory must lie
+ * in one; otherwise ALIGNN_E_BAD_SHAPE with the offending value and launch index (trainer.capture
+ * refuses such a plan).  Recording state and the registered step seed are per host thread. */
+int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, int64_t n, uint64_t* bad_value,
+                           int64_t* bad_launch, int64_t* checked);
 int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);

@@ -28,7 +28,7 @@ def test_graph_replay_matches_eager_bitwise(mode, B):
     assert torch.equal(tr1.st.flat, tr2.st.flat)          # capture leaves the weights as they were
     for i, s in enumerate((11, 12, 13)):
         # eager reference with the same device step seed the replay uses
-        ops.set_step_seed(tr2._seed_dev)
+        tr1.use_step_seed(tr2._seed_dev)
         tr2._seed_dev.fill_(s)
         l1 = tr1.forward_backward(b1, 0).clone()
         tr1._clip_and_update()
@@ -90,3 +90,54 @@ def test_plan_needs_library_optimizer():
     tr = A.FusedTrainer(model, optimizer="torch")
     with pytest.raises(ValueError):
         tr.capture(mp_like_batch(2).to(DEV), mode="plan")
+
+
+def test_two_captured_trainers_interleave_bitwise():
+    """Two trainers (B = 4 and the bench's B = 32) hold captured plans at the same time; their
+    replays interleave, each matches an eager twin bit for bit (no shared workspace, stream or seed)."""
+    trs = []
+    for B in (4, 32):
+        _, te, be = _setup(B=B)
+        _, tp, bp = _setup(B=B)
+        tp.capture(bp)
+        te.use_step_seed(tp._seed_dev)
+        trs.append((te, be, tp, bp))
+    for s in (21, 22):
+        for te, be, tp, bp in trs:
+            tp._seed_dev.fill_(s)
+            le = te.forward_backward(be, 0).clone()
+            te._clip_and_update()
+            lp = tp.step(bp, seed=s).clone()
+            torch.cuda.synchronize()
+            assert torch.equal(le, lp)
+            assert torch.equal(te.st.flat, tp.st.flat)
+    for _, _, tp, _ in trs:
+        tp.release_capture()
+
+
+def test_plan_ownership_check():
+    """alignn_plan_check_ptrs: a recorded launch into a buffer outside the declared ranges is
+    reported with its address; declared, it passes."""
+    import ctypes
+    from alignn_mi355x import _lib, ops
+    from alignn_mi355x.trainer import _record_plan
+    lib = _lib.lib()
+    a = torch.empty(1000, device=DEV)
+    b = torch.empty(1000, device=DEV)
+    ctx = ops.ExecContext("t")
+    with ops.using(ctx), ops.recording():
+        plan = _record_plan(lambda: (ops.zero_(a), ops.copy_(b, a)))
+    try:
+        def check(tensors):
+            rs = [v for t in tensors for v in (t.data_ptr(), t.data_ptr() + 4 * t.numel())]
+            arr = (ctypes.c_uint64 * len(rs))(*rs)
+            bad, idx, n = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_int64()
+            rc = lib.alignn_plan_check_ptrs(plan, arr, len(tensors), ctypes.byref(bad), ctypes.byref(idx),
+                                            ctypes.byref(n))
+            return rc, bad.value, idx.value, n.value
+        assert check([a, b])[0] == 0 and check([a, b])[3] == 3
+        rc, bad, idx, _ = check([a])
+        assert rc != 0 and bad == b.data_ptr() and idx == 1
+    finally:
+        lib.alignn_plan_destroy(plan)
+    torch.cuda.synchronize()
