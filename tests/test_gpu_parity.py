@@ -9,7 +9,13 @@ Tolerance (BASELINE.json north_star): 1e-4 relative (fp32).
   O(1) relative (observed on the B=8 batch: one LayerNorm output of edge block 0).  The denominator
   is floored at 1e-3 x the largest gradient norm of the model, which matters only for
   lin_key.bias: its gradient is zero in exact arithmetic (a per-segment constant shift cancels in
-  the softmax), so fp32 returns rounding noise where the fp64 reference holds ~1e-20."""
+  the softmax), so fp32 returns rounding noise where the fp64 reference holds ~1e-20.
+
+At B = 32 some gradients are ill-conditioned sums over 23,040 bond rows (the gate weight
+lin_beta.weight of the last edge block: large cancelling terms); there the reference's OWN fp32 CPU
+path (the oracle run in fp32) misses fp64 by more than 1e-4 (measured 1.7e-4 with corrected wiring,
+seed 5).  The B = 32 checks therefore accept, per parameter, an error up to max(1e-4, 1.5 x the
+reference fp32 path's error on the same inputs): never worse than the reference itself."""
 GRAD_FLOOR = 1e-3
 MAXABS_TOL = 5e-3
 import numpy as np
@@ -104,9 +110,26 @@ def _oracle_grads(st64, batch64, heads):
     return mean.detach(), logvar.detach(), loss.detach(), {k: v.grad for k, v in params.items() if v.grad is not None}
 
 
+def _ref_batch(cpu_batch, num_graphs, dtype):
+    ref_b = RefData(**{k: getattr(cpu_batch, k) for k in cpu_batch.keys()})
+    for k in ("x", "edge_attr", "lg_edge_attr", "global_x", "sg_one_hot", "y"):
+        setattr(ref_b, k, getattr(ref_b, k).to(dtype))
+    ref_b.num_graphs = num_graphs
+    return ref_b
+
+
+def _grad_tols(st, cpu_batch, num_graphs, rgrads):
+    """Per-parameter normwise tolerance max(TOL, 1.5 x the error of the reference's own fp32 CPU
+    path) — the oracle run in fp32 on the same weights and batch, against the fp64 oracle."""
+    r32 = _oracle_grads({k: v.float() for k, v in st.items()}, _ref_batch(cpu_batch, num_graphs, torch.float32), 4)[3]
+    nfloor = GRAD_FLOOR * grad_norm_scale(rgrads.values())
+    return {k: max(TOL, 1.5 * norm_err(r32[k], rgrads[k], nfloor)) for k in rgrads}
+
+
 @pytest.mark.parametrize("num_graphs,lg_offset,heavy,recompute", [
     (1, "num_nodes", None, True), (3, "num_nodes", None, True), (2, "num_edges", None, True),
     (8, "num_nodes", None, True), (3, "num_nodes", 0, True), (2, "num_edges", 10**9, True),
+    (32, "num_edges", None, True),
     (3, "num_nodes", None, False), (2, "num_edges", None, False)])
 def test_full_size_model_vs_oracle(num_graphs, lg_offset, heavy, recompute, monkeypatch):
     """Production dims (D=256, H=4, L=4, 206/36/11 features) on MP-like graphs.  ``heavy`` overrides
@@ -123,11 +146,9 @@ def test_full_size_model_vs_oracle(num_graphs, lg_offset, heavy, recompute, monk
     model._engine.recompute_angle = recompute
     st = {k: v.detach().clone() for k, v in model.state_dict().items()}
     cpu_batch = mp_like_batch(num_graphs, lg_offset=lg_offset)
-    ref_b = RefData(**{k: getattr(cpu_batch, k) for k in cpu_batch.keys()})
-    for k in ("x", "edge_attr", "lg_edge_attr", "global_x", "sg_one_hot", "y"):
-        setattr(ref_b, k, getattr(ref_b, k).double())
-    ref_b.num_graphs = num_graphs
-    rmean, rlogvar, rloss, rgrads = _oracle_grads({k: v.double() for k, v in st.items()}, ref_b, 4)
+    rmean, rlogvar, rloss, rgrads = _oracle_grads({k: v.double() for k, v in st.items()},
+                                                  _ref_batch(cpu_batch, num_graphs, torch.float64), 4)
+    tols = _grad_tols(st, cpu_batch, num_graphs, rgrads) if num_graphs >= 32 else {}
     model.to(DEV).train()
     b = cpu_batch.to(DEV)
     mean, logvar = model(b)
@@ -144,8 +165,102 @@ def test_full_size_model_vs_oracle(num_graphs, lg_offset, heavy, recompute, monk
         if k not in rgrads:
             assert p.grad is None, k
             continue
-        assert norm_err(p.grad, rgrads[k], nfloor) < TOL, k
+        assert norm_err(p.grad, rgrads[k], nfloor) < tols.get(k, TOL), k
         assert rel_err(p.grad.cpu(), rgrads[k], floor) < MAXABS_TOL, k
+
+
+_C2_CACHE = {}
+
+
+def _c2_case():
+    """Config C2 (BASELINE.json configs[1]): B = 32 MP-like graphs under the PyG offset rule
+    (line-graph in-degrees up to 132: both attention schedules are exercised), D256/H4/L4, dropout
+    0; the fp64 oracle's forward, loss and every parameter gradient (train.py:655-681), computed
+    once for the tests below."""
+    if not _C2_CACHE:
+        import alignn_mi355x as A
+        from alignn_mi355x.synthetic import mp_like_batch
+        torch.manual_seed(32)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
+        st = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        cpu_batch = mp_like_batch(32, lg_offset="num_nodes")
+        ref = _oracle_grads({k: v.double() for k, v in st.items()}, _ref_batch(cpu_batch, 32, torch.float64), 4)
+        _C2_CACHE.update(st=st, batch=cpu_batch, ref=ref, tols=_grad_tols(st, cpu_batch, 32, ref[3]))
+    return _C2_CACHE
+
+
+def _check_grads(named_grads, rgrads, tols):
+    floor = GRAD_FLOOR * max(float(v.abs().max()) for v in rgrads.values())
+    nfloor = GRAD_FLOOR * grad_norm_scale(rgrads.values())
+    n = 0
+    for k, gr in named_grads:
+        if k not in rgrads:
+            assert gr is None or float(gr.abs().max()) == 0.0, k
+            continue
+        assert gr is not None, k
+        assert norm_err(gr, rgrads[k], nfloor) < tols[k], k
+        assert rel_err(gr.cpu(), rgrads[k], floor) < MAXABS_TOL, k
+        n += 1
+    assert n >= 100
+
+
+def test_c2_batch32_autograd_vs_oracle():
+    """The module API (autograd through the engine) at the benchmarked configuration C2."""
+    import alignn_mi355x as A
+    c = _c2_case()
+    rmean, rlogvar, rloss, rgrads = c["ref"]
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
+    model.load_state_dict(c["st"])
+    model.to(DEV).train()
+    b = c["batch"].to(DEV)
+    mean, logvar = model(b)
+    assert rel_err(mean.detach().cpu(), rmean) < TOL
+    assert rel_err(logvar.detach().cpu(), rlogvar) < TOL
+    y = b.y.view(32, -1)
+    tz = (torch.log(y) - torch.tensor([4.3228, 3.5567], device=DEV)) / torch.tensor([0.9051, 0.9405], device=DEV)
+    lv = torch.clamp(logvar, min=-2.9)
+    loss = (0.5 * (lv + (mean - tz) ** 2 / torch.exp(lv))).mean(1).mean() + 0.1 * (0.5 * lv).pow(2).mean()
+    assert abs(float(loss) - float(rloss)) < TOL * abs(float(rloss))
+    loss.backward()
+    _check_grads(((k, p.grad) for k, p in model.named_parameters()), rgrads, c["tols"])
+
+
+@pytest.mark.parametrize("mode", ["plan", "eager"])
+def test_c2_batch32_fused_step_vs_oracle(mode):
+    """The bench's own step (FusedTrainer, native launch plan replay at B = 32, the timed path of
+    bench.py) against the fp64 oracle: the loss and every parameter gradient of the replayed step
+    (the flat gradient buffer, read before the next step), then the AdamW update itself."""
+    import alignn_mi355x as A
+    from alignn_mi355x import FusedTrainer
+    from alignn_mi355x.layout import offsets
+    c = _c2_case()
+    rmean, rlogvar, rloss, rgrads = c["ref"]
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
+    model.load_state_dict(c["st"])
+    model.to(DEV).train()
+    b = c["batch"].to(DEV)
+    tr = FusedTrainer(model, feature_jitter_std=0.0, target_log_means=(4.3228, 3.5567),
+                      target_log_stds=(0.9051, 0.9405))
+    before = tr.st.flat.clone()
+    if mode == "plan":
+        tr.capture(b, mode="plan")
+        assert torch.equal(tr.st.flat, before)  # capture leaves the state as it was
+    loss = tr.step(b, seed=7)
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(rloss)) < TOL * abs(float(rloss))
+    offs, _, _ = offsets(model.config, True)
+    grads = [(k, tr.st.grad[o:o + int(np.prod(shape))].view(shape)) for k, (o, shape) in offs.items()]
+    _check_grads(grads, rgrads, c["tols"])
+    # the update is AdamW's first step over the clipped gradient (train.py:690-699): every moved
+    # parameter moved by about lr (|m_hat / sqrt(v_hat)| = 1 at step 1) in the gradient's direction
+    delta = (tr.st.flat - before).cpu()
+    g = tr.st.grad.cpu()
+    big = g.abs() > 1e-4 * float(g.abs().max())
+    lr = 3e-4
+    wd_shift = lr * 1e-4 * before.cpu().abs()
+    assert float(((delta[big].abs() - lr).abs() - wd_shift[big]).max()) < 0.02 * lr
+    assert bool((torch.sign(delta[big]) == -torch.sign(g[big])).all())
+    tr.release_capture()
 
 
 def test_blocks_standalone_vs_oracle():
