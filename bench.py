@@ -45,8 +45,10 @@ def parse():
     p.add_argument("--dropout", type=float, default=0.15)
     p.add_argument("--lg-offset", default="num_nodes", choices=["num_nodes", "num_edges"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--cpu-steps", type=int, default=5)
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the secondary lines of the default one-GPU run (corrected wiring, config C3)")
     p.add_argument("--dump-probes", default="", help="write the per-op probe summary (JSON) to this path")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM arithmetic: fp32 (BASELINE config 2, the default) or bf16 matrix-core inputs with "
@@ -83,6 +85,8 @@ def apply_settings(args, model):
             ops.GraphCSR.COMPACT_REGS = bool(int(v))
         elif k == "optimizer":
             kw["optimizer"] = v
+        elif k == "wave_items":
+            ops.GraphCSR.WAVE_ITEMS = bool(int(v))
         elif k == "sort_by_degree":
             ops.GraphCSR.SORT_BY_DEGREE = bool(int(v))
         elif k == "heavy_threshold":
@@ -94,25 +98,49 @@ def apply_settings(args, model):
     return kw
 
 
+def _cpu_threads() -> int:
+    """Host threads for the CPU baseline: the CPUs this process may use.  On the GPU box the job's
+    CPU share is set by OMP_NUM_THREADS (16 per GPU) while os.cpu_count() reports the whole machine;
+    more threads than the share would oversubscribe it."""
+    env = os.environ.get("ALIGNN_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(args, B):
-    """The oracle (PyTorch-CPU restatement, fp32) on a bounded sample of the same workload:
-    full fwd + NLL + bwd + clip + AdamW steps on the same synthetic graphs."""
+    """The oracle (PyTorch-CPU restatement of the reference's path, fp32) on a bounded sample of the
+    same workload: full fwd + NLL + bwd + clip + AdamW steps on the same synthetic graphs, protocol
+    of SURVEY §8d (all usable host threads, per-step median after warm-up)."""
     from oracle import model_ref
     from oracle.pyg_ref import RefData, collate
 
     from alignn_mi355x.synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS, mp_like_graph
     import alignn_mi355x as A
 
-    torch.manual_seed(0)
-    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads, 0.0), 2)
-    st = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    gs = [mp_like_graph(g) for g in range(B)]
-    b = collate([RefData(**{k: getattr(d, k) for k in d.keys()}) for d in gs], lg_offset=args.lg_offset)
-    threads = torch.get_num_threads()
-    model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)  # warm-up
-    t0 = time.perf_counter()
-    model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=args.cpu_steps)
-    dt = time.perf_counter() - t0
+    threads = _cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
+                                                          0.0), 2)
+        st = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        gs = [mp_like_graph(g) for g in range(B)]
+        b = collate([RefData(**{k: getattr(d, k) for k in d.keys()}) for d in gs], lg_offset=args.lg_offset)
+        model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)  # warm-up
+        times = []
+        for _ in range(args.cpu_steps):
+            t0 = time.perf_counter()
+            model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)
+            times.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    times.sort()
+    med = times[len(times) // 2]
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -121,9 +149,10 @@ def cpu_baseline(args, B):
                 break
     except OSError:
         pass
-    return {"value": round(B * args.cpu_steps / dt, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_steps} steps x {B} graphs (fp32 fwd+bwd+clip+AdamW, dropout 0) after 1 warm-up; "
-                      f"{cpu_model}"}
+    return {"value": round(B / med, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
+            "sample": f"median of {args.cpu_steps} steps x {B} graphs (fp32 fwd+NLL+bwd+clip+AdamW, dropout 0) after "
+                      f"1 warm-up, torch.set_num_threads({threads}) (the job's CPU share; os.cpu_count() = "
+                      f"{os.cpu_count()}); {cpu_model}"}
 
 
 def end_to_end(args, trainer, dev, rank, world):
@@ -180,36 +209,37 @@ def pmc_traffic(kernel_key):
     return None if rec is None else rec["traffic_bytes"]
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+def _roofline(summ, dominant, mfma_peak, probe_src):
+    s = summ[dominant]
+    avg_s = s["avg_ms"] / 1e3
+    if s["flops_per_launch"] > 0:
+        ach = s["flops_per_launch"] / avg_s / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 2), "peak": mfma_peak, "unit": "TFLOP/s",
+                "frac": round(ach / mfma_peak, 4), "traffic": None, "kernel": dominant,
+                "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
+                "flops_per_launch": s["flops_per_launch"], "timing": probe_src}
+    ach = s["bytes_per_launch"] / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dominant), "kernel": dominant,
+            "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
+            "bytes_per_launch": s["bytes_per_launch"], "timing": probe_src}
 
+
+def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roofline=True):
+    """Builds the model, trainer and a resident batch of B graphs, picks the dominant kernel (one
+    untimed eager probe step), captures the step, runs `warmup` steps and times exactly `steps`
+    (barrier + synchronize on both sides, max over ranks).  Returns the numbers and the trainer."""
     import alignn_mi355x as A
     from alignn_mi355x import profiling
     from alignn_mi355x.dp import grad_allreduce_hook, max_over_ranks, rank_graphs
     from alignn_mi355x.synthetic import mp_like_batch
 
-    B = args.batch
     torch.manual_seed(1234)  # identical initial weights on every rank
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                       args.dropout), 2).to(dev)
-    args.main_priority = 0
-    trainer = A.FusedTrainer(model, precision=args.precision, **apply_settings(args, model))
-    if args.main_priority:
-        # the step's critical-path stream at a higher HIP priority than the weight-gradient side
-        # stream (A/B option; priority -1 is the highest torch exposes)
-        hi = torch.cuda.Stream(device=dev, priority=-1)
-        hi.wait_stream(torch.cuda.current_stream(dev))
-        torch.cuda.set_stream(hi)
-    mfma_peak = BF16_MFMA_TFLOPS if args.precision == "bf16" else FP32_MFMA_TFLOPS
-    batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=args.lg_offset).to(dev)
+    trainer = A.FusedTrainer(model, precision=precision, **apply_settings(args, model))
+    mfma_peak = BF16_MFMA_TFLOPS if precision == "bf16" else FP32_MFMA_TFLOPS
+    batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=lg_offset).to(dev)
     if world > 1:
         trainer.grad_hook = grad_allreduce_hook(world)  # the DP exchange: one all_reduce of the flat gradient
 
@@ -217,9 +247,8 @@ def main():
         trainer.step(batch, seed=1000003 * rank + i)
 
     # pick the dominant kernel (untimed eager probe step with events around every launch)
-    dominant = None
-    step_work = None
-    if not args.no_roofline:
+    dominant, step_work = None, None
+    if roofline:
         step(0)
         torch.cuda.synchronize()
         profiling.enable(None)
@@ -232,16 +261,14 @@ def main():
         step_work = {"gemm_gflop": sum(v["flops_per_launch"] * v["count"] for v in summ.values()) / 1e9,
                      "tconv_gbyte": sum(v["bytes_per_launch"] * v["count"] for k, v in summ.items()
                                         if k.startswith("tconv")) / 1e9}
-        if args.dump_probes and rank == 0:
+        if args.dump_probes and rank == 0 and (B, lg_offset, precision) == (args.batch, args.lg_offset,
+                                                                             args.precision):
             with open(args.dump_probes, "w") as f:
                 json.dump(dict(sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"])), f, indent=1)
 
     # captured step: in a plan the dominant kernel's launches are bracketed by plan timestamps, so
     # every replay re-times them; the timed region's last replay is read back afterwards
-    if args.graph:
-        args.launch = "graph"
-    launch_mode = "eager"
-    probe_in_graph = False
+    launch_mode, probe_in_graph = "eager", False
     if args.launch != "eager":
         mode = args.launch
         # ROCm refuses external event nodes in a captured graph: graph mode probes eagerly after
@@ -253,7 +280,7 @@ def main():
         launch_mode = "native_plan" if mode == "plan" else "hip_graph"
         profiling.disable()
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         step(2 + i)
     torch.cuda.synchronize()
 
@@ -263,8 +290,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(2 + args.warmup + i)
+    for i in range(steps):
+        step(2 + warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -273,11 +300,10 @@ def main():
     if world > 1:
         dt = max_over_ranks(dt, dev)
     if probe_in_graph:
-        try:  # the event nodes hold the last replay's times
-            s_ = profiling.summary()[dominant]
-            probe_in_graph = s_["avg_ms"] > 0
+        try:  # the plan timestamps hold the last replay's times
+            probe_in_graph = profiling.summary()[dominant]["avg_ms"] > 0
         except Exception as e:  # noqa: BLE001
-            print(f"[bench] graph event timing unavailable ({e}); probing eagerly", file=sys.stderr)
+            print(f"[bench] plan probe timing unavailable ({e}); probing eagerly", file=sys.stderr)
             probe_in_graph = False
     if dominant is not None and launch_mode != "eager" and not probe_in_graph:
         # fallback: time the dominant kernel in two extra eager steps after the timed region
@@ -290,54 +316,100 @@ def main():
         torch.cuda.synchronize()
         profiling.disable()
         trainer._graph = saved
-
-    e2e = None
-    if args.e2e > 0:
-        e2e = end_to_end(args, trainer, dev, rank, world)
-
     probe_src = ("plan timestamps in the replayed step (last timed replay)" if (probe_in_graph and launch_mode == "native_plan") else
                  "hip events in the captured step (last timed replay)" if probe_in_graph else
                  "hip events around each launch, timed region" if launch_mode == "eager" else
                  "hip events, 2 eager steps after the timed region")
-    result = None
+    value = B * world * steps / dt
+    roof = _roofline(profiling.summary(), dominant, mfma_peak, probe_src) if dominant is not None else None
+    step_roof = None if step_work is None else {
+        # whole-step view: this formulation's GEMM flops and attention bytes per graph
+        # and the fraction of the MFMA / HBM peaks they imply at the measured rate
+        "gemm_gflop_per_graph": round(step_work["gemm_gflop"] / B, 4),
+        "mfma_frac": round(step_work["gemm_gflop"] / B * (value / world) / (mfma_peak * 1e3), 4),
+        "tconv_mbyte_per_graph": round(step_work["tconv_gbyte"] * 1e3 / B, 2),
+        "hbm_frac": round(step_work["tconv_gbyte"] / B * value / world / HBM_PEAK_GBS, 4)}
+    return {"value": value, "dt": dt, "ms_per_step": dt / steps * 1e3, "launch": launch_mode, "roofline": roof,
+            "step_roofline": step_roof, "trainer": trainer, "batch": batch}
+
+
+def _release(r):
+    tr = r.pop("trainer", None)
+    r.pop("batch", None)
+    if tr is not None:
+        tr.release_capture()
+    del tr
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def main():
+    args = parse()
+    if args.graph:
+        args.launch = "graph"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    args.main_priority = int(dict(x.split("=", 1) for x in args.set).get("main_priority", 0))
+    if args.main_priority:
+        # the step's critical-path stream at a higher HIP priority than the weight-gradient side
+        # stream (A/B option; priority -1 is the highest torch exposes)
+        hi = torch.cuda.Stream(device=dev, priority=-1)
+        hi.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(hi)
+
+    B = args.batch
+    r = measure(args, dev, rank, world, B, args.lg_offset, args.precision, args.steps, args.warmup,
+                roofline=not args.no_roofline)
+    e2e = None
+    if args.e2e > 0:
+        e2e = end_to_end(args, r["trainer"], dev, rank, world)
+    _release(r)
+
+    # secondary lines of the default run (one GPU): the same step with the corrected line-graph
+    # wiring (SURVEY §8d "also report num_edges": no compaction, every bond active) and config C3
+    # (B = 256, bf16 matrix-core inputs, its own dominant-kernel roofline).  Never `value`.
+    secondary = None
+    if world == 1 and not args.no_secondary:
+        secondary = {}
+        sec_steps, sec_warm = max(5, args.steps // 2), max(2, args.warmup // 2)
+        if args.lg_offset == "num_nodes":
+            w = measure(args, dev, rank, world, B, "num_edges", args.precision, sec_steps, sec_warm, roofline=True)
+            secondary["corrected_wiring"] = {
+                "config": f"B={B}, lg_offset=num_edges (every bond active: no line-graph compaction), {args.precision}",
+                "value": round(w["value"], 2), "unit": "graphs/s", "ms_per_step": round(w["ms_per_step"], 3),
+                "steps": sec_steps, "roofline": w["roofline"]}
+            _release(w)
+        if (B, args.precision) != (256, "bf16"):
+            c3 = measure(args, dev, rank, world, 256, args.lg_offset, "bf16", sec_steps, sec_warm, roofline=True)
+            secondary["c3_b256_bf16"] = {
+                "config": "BASELINE config 3: B=256 per GPU, bf16 matrix-core inputs (fp32 accumulation, fp32 "
+                          f"softmax/LayerNorm), lg_offset={args.lg_offset}",
+                "value": round(c3["value"], 2), "unit": "graphs/s", "ms_per_step": round(c3["ms_per_step"], 3),
+                "steps": sec_steps, "roofline": c3["roofline"], "step_roofline": c3["step_roofline"]}
+            _release(c3)
+
     if rank == 0:
-        value = B * world * args.steps / dt
-        roof = None
-        if dominant is not None:
-            s = profiling.summary()[dominant]
-            avg_s = s["avg_ms"] / 1e3
-            if s["flops_per_launch"] > 0:
-                ach = s["flops_per_launch"] / avg_s / 1e12
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": mfma_peak, "unit": "TFLOP/s",
-                        "frac": round(ach / mfma_peak, 4), "traffic": None, "kernel": dominant,
-                        "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
-                        "flops_per_launch": s["flops_per_launch"], "timing": probe_src}
-            else:
-                ach = s["bytes_per_launch"] / avg_s / 1e9
-                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dominant), "kernel": dominant,
-                        "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
-                        "bytes_per_launch": s["bytes_per_launch"], "timing": probe_src}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, B)
         result = {
-            "metric": METRIC, "value": round(value, 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16-gemm/f32", "data": "synthetic",
+            "metric": METRIC, "value": round(r["value"], 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(r["ms_per_step"], 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" if args.precision == "fp32" else "bf16-gemm/f32", "data": "synthetic",
             "config": {"workload": f"B={B} synthetic MP-like graphs per GPU (60 atoms/720 bonds/7920 triplets), "
                                    f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
-                       "dropout": args.dropout, "launch": launch_mode, "precision": args.precision,
+                       "dropout": args.dropout, "launch": r["launch"], "precision": args.precision,
                        **({"settings": args.set} if args.set else {})},
-            "roofline": roof, "cpu_baseline": cpu, "e2e": e2e,
-            # whole-step view: this formulation's GEMM flops and attention bytes per
-            # graph and the fraction of the fp32 MFMA / HBM peaks they imply at the measured rate
-            "step_roofline": None if step_work is None else {
-                "gemm_gflop_per_graph": round(step_work["gemm_gflop"] / B, 4),
-                "mfma_frac": round(step_work["gemm_gflop"] / B * (value / world) / (mfma_peak * 1e3), 4),
-                "tconv_mbyte_per_graph": round(step_work["tconv_gbyte"] * 1e3 / B, 2),
-                "hbm_frac": round(step_work["tconv_gbyte"] / B * value / world / HBM_PEAK_GBS, 4)},
+            "roofline": r["roofline"], "cpu_baseline": cpu, "e2e": e2e,
+            "step_roofline": r["step_roofline"], "secondary": secondary,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

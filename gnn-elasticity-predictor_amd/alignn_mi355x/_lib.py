@@ -48,6 +48,7 @@ class Schedule(ctypes.Structure):
 
 
 SCHED_COMPACT_REGS = 1
+SCHED_WAVE_ITEMS = 2
 
 
 class EdgeEncoder(ctypes.Structure):
@@ -83,6 +84,7 @@ _SIGNATURES = {
     "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_bwd_workspace": ([c_i32, c_i32, c_i32], c_i64),
+    "alignn_tconv_family": ([c_i32, c_i32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_tconv_bwd_dst": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                               c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                               c_i32, c_f32, c_u64, c_vp], c_i32),

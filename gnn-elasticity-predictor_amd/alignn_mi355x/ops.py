@@ -454,6 +454,9 @@ class GraphCSR:
     HEAVY_THRESHOLD = 256
     SORT_BY_DEGREE = False  # work items in descending in-degree order (A/B option; within noise, slower bwd_dst)
     COMPACT_REGS = True  # attention kernels with row-distributed softmax state (+1 %, bwd_dst 249 -> 231 us)
+    # every target a single-wave work item, longest in-edge list first (lgconv.hip, the D = 256
+    # materialised-F line-graph kernels; other calls keep the kernels above)
+    WAVE_ITEMS = True
 
     def __init__(self, edge_index: torch.Tensor, n: int):
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
@@ -493,7 +496,7 @@ class GraphCSR:
             light_mask = ~heavy_mask
             lit = idx[light_mask & (deg > 0)]
             hv = idx[heavy_mask]
-            if self.SORT_BY_DEGREE:
+            if self.SORT_BY_DEGREE or self.WAVE_ITEMS:
                 # longest segments first (their waves start in the first round of resident
                 # workgroups) and similar degrees in one workgroup (its 4 waves finish together);
                 # each node is still one wave's work, so results do not change
@@ -504,9 +507,19 @@ class GraphCSR:
             sc = _lib.Schedule()
             sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
             sc.heavy, sc.n_heavy = (heavy.data_ptr() if heavy.numel() else None), heavy.numel()
-            sc.flags = _lib.SCHED_COMPACT_REGS if self.COMPACT_REGS else 0
+            sc.flags = (_lib.SCHED_COMPACT_REGS if self.COMPACT_REGS else 0) | \
+                (_lib.SCHED_WAVE_ITEMS if self.WAVE_ITEMS else 0)
             self._sched = (sc, light, heavy)
         return self._sched[0]
+
+    def family(self, D: int, H: int, F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor] = None,
+               enc=None) -> int:
+        """Attention kernel family the library runs for this graph and operands (3: single-wave
+        items, 2: compact registers, 1: default); alignn_tconv_family."""
+        es = None if enc is None else enc.struct()
+        return int(_lib.lib().alignn_tconv_family(D, H, None if feat_row is None else feat_row.data_ptr(),
+                                                   None if es is None else ctypes.byref(es),
+                                                   None if F is None else F.data_ptr(), ctypes.byref(self.schedule())))
 
     def check_indices(self, what: str) -> None:
         """Host check of the device error flag (one sync).  PyG raises IndexError here."""

@@ -26,10 +26,13 @@ constexpr int SK_KMAX = 16;   // linear_smallk: K <= 16
 constexpr int SN_NMAX = 16;   // tn_smalln: N <= 16
 constexpr int SN_SLOTS = SN_NMAX + 1;
 
+// OutT = float, or uint16_t for bf16 output rows (RNE, v_cvt_pk_bf16_f32): the angle encoder's hidden
+// layer under config C3's autocast precision (train.py:632-636), read by the bf16 attention kernels.
+template <typename OutT>
 __global__ __launch_bounds__(256) void linear_smallk_kernel(const float* __restrict__ X, int64_t ldx, int64_t M,
                                                             int K, const float* __restrict__ W, int64_t ldw,
                                                             const float* __restrict__ bias, int64_t N, int relu,
-                                                            float* __restrict__ out, int64_t ldo) {
+                                                            OutT* __restrict__ out, int64_t ldo) {
   __shared__ float xs[SK_ROWS][SK_KMAX + 1];
   const int tid = threadIdx.x, rl = tid >> 6, cq = tid & 63;
   const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
@@ -60,7 +63,14 @@ __global__ __launch_bounds__(256) void linear_smallk_kernel(const float* __restr
         a[j] += b[j];
         if (relu) a[j] = fmaxf(a[j], 0.f);
       }
-      *reinterpret_cast<float4*>(out + (r0 + r) * ldo + c0) = make_float4(a[0], a[1], a[2], a[3]);
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<float4*>(out + (r0 + r) * ldo + c0) = make_float4(a[0], a[1], a[2], a[3]);
+      } else {
+        typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+        bf4 h;
+        h.x = (__bf16)a[0]; h.y = (__bf16)a[1]; h.z = (__bf16)a[2]; h.w = (__bf16)a[3];
+        *reinterpret_cast<bf4*>(out + (r0 + r) * ldo + c0) = h;
+      }
     }
   }
 }
@@ -202,8 +212,30 @@ extern "C" int alignn_linear_smallk_f32(const float* X, int64_t ldx, int64_t M, 
   if (M == 0 || N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned blocks = (unsigned)((M + SK_ROWS - 1) / SK_ROWS);
-  launch(linear_smallk_kernel, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, N,
+  launch(linear_smallk_kernel<float>, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, N,
                      (int)relu, out, ldo);
+  ALIGNN_LAUNCH_CHECK("linear_smallk_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_linear_smallk_bf16out(const float* X, int64_t ldx, int64_t M, int32_t K, const float* W,
+                                            int64_t ldw, const float* bias, int64_t N, int32_t relu, uint16_t* out,
+                                            int64_t ldo, void* stream) {
+  if (M < 0 || K < 0 || N < 0 || (M > 0 && (!X || !out)) || (N > 0 && K > 0 && !W)) {
+    set_error("linear_smallk_bf16out: bad arguments");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (K > SK_KMAX || N % 4 != 0 || ldo % 4 != 0 || (reinterpret_cast<uintptr_t>(out) & 7u) || ldx < K ||
+      ldw < K || ldo < N) {
+    set_error("linear_smallk_bf16out: needs K <= %d, N %% 4 == 0, 8-byte aligned output rows (K=%d N=%lld ldo=%lld)",
+              SK_KMAX, (int)K, (long long)N, (long long)ldo);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  if (M == 0 || N == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned blocks = (unsigned)((M + SK_ROWS - 1) / SK_ROWS);
+  launch(linear_smallk_kernel<uint16_t>, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, N,
+         (int)relu, out, ldo);
   ALIGNN_LAUNCH_CHECK("linear_smallk_kernel");
   return ALIGNN_OK;
 }

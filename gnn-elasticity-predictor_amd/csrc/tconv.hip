@@ -1523,6 +1523,20 @@ static int edge_source(const float* F, const AlignnEdgeEncoder* enc, EncParams& 
   return ALIGNN_OK;
 }
 
+// lgconv.hip: single-wave-item kernels (ALIGNN_SCHED_WAVE_ITEMS)
+bool lg3_supported(int D, int H, const int32_t* feat_row, const AlignnEdgeEncoder* enc, const float* F,
+                   const AlignnSchedule* sched);
+int lg3_fwd(int64_t n, int64_t m, int H, const int32_t* off, const int32_t* src_at, const AlignnSchedule* sched,
+            const float* QKV, int64_t ldq, const float* U, const float* wbar, const float* F, int64_t ldf,
+            float* aggV, float* S, float* sumA, float* mstat, float* den, const DropParams& drop, hipStream_t s,
+            const uint16_t* KV16 = nullptr, int64_t ldkv = 0, const uint16_t* F16 = nullptr);
+int lg3_bwd_dst(int64_t n, int64_t m, int H, const int32_t* off, const int32_t* src_at,
+                const AlignnSchedule* sched, const float* QKV, int64_t ldq, const float* U, const float* Vd,
+                const float* wbar, const float* F, int64_t ldf, const float* dout, const float* outp,
+                const float* mstat, const float* den, float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e,
+                float* alpha_e, const DropParams& drop, hipStream_t s, const uint16_t* KV16 = nullptr,
+                int64_t ldkv = 0, const uint16_t* F16 = nullptr);
+
 }  // namespace alignn
 
 using namespace alignn;
@@ -1538,15 +1552,25 @@ extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, cons
   EncParams en;
   int km;
   if ((rc = edge_source(F, enc, en, km))) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (lg3_supported(D, H, feat_row, enc, F, sched))
+    return lg3_fwd(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
+                   make_drop(drop_p, seed), s);
   FwdParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
               make_drop(drop_p, seed)};
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
   const Sched sc = make_sched(sched, n);
   const int flags = sched ? sched->flags : 0;
   ALIGNN_DISPATCH_VH(vpl, H, launch_fwd, p, sc, en, km, s, flags);
   ALIGNN_LAUNCH_CHECK("tconv_fwd_kernel");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_tconv_family(int32_t D, int32_t H, const int32_t* feat_row, const AlignnEdgeEncoder* enc,
+                                   const float* F, const AlignnSchedule* sched) {
+  if (check_dims(D, H)) return 0;
+  if (lg3_supported(D, H, feat_row, enc, F, sched)) return 3;
+  return (enc == nullptr && sched && (sched->flags & ALIGNN_SCHED_COMPACT_REGS)) ? 2 : 1;
 }
 
 extern "C" int64_t alignn_tconv_bwd_workspace(int32_t D, int32_t H, int32_t kin) {
@@ -1591,6 +1615,9 @@ extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, 
     return ALIGNN_E_BAD_SHAPE;
   }
   const int flags = sched ? sched->flags : 0;
+  if (dF == nullptr && lg3_supported(D, H, feat_row, enc, F, sched))
+    return lg3_bwd_dst(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den, dq,
+                       lddq, Sz, sigz, dz_e, alpha_e, make_drop(drop_p, seed), reinterpret_cast<hipStream_t>(stream));
   BwdDstParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den,
                  dq, lddq, Sz, sigz, dz_e, alpha_e, enc ? nullptr : dF, lddf, accumulate_dF, 0,
                  make_drop(drop_p, seed)};

@@ -99,6 +99,11 @@ int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
  * ---------------------------------------------------------------------------------------- */
 int alignn_linear_smallk_f32(const float* X, int64_t ldx, int64_t M, int32_t K, const float* W, int64_t ldw,
                              const float* bias, int64_t N, int32_t relu, float* out, int64_t ldo, void* stream);
+/* The same with bf16 output rows (RNE; out rows 8-byte aligned): the angle encoder's hidden layer in
+ * bf16 for the bf16-storage attention kernels (config C3). */
+int alignn_linear_smallk_bf16out(const float* X, int64_t ldx, int64_t M, int32_t K, const float* W, int64_t ldw,
+                                 const float* bias, int64_t N, int32_t relu, uint16_t* out, int64_t ldo,
+                                 void* stream);
 int64_t alignn_gemm_tn_smalln_workspace(int64_t K, int64_t M, int32_t N);
 int alignn_gemm_tn_smalln_f32(const float* A, int64_t lda, int64_t K, int64_t M, const float* X, int64_t ldx,
                               int32_t N, float* C, int64_t ldc, float* colsum, int32_t accumulate, float* workspace,
@@ -203,6 +208,12 @@ typedef struct AlignnSchedule {
   int32_t reserved;
 } AlignnSchedule;
 #define ALIGNN_SCHED_COMPACT_REGS 1
+/* ALIGNN_SCHED_WAVE_ITEMS: `light` is the list of ALL target nodes in launch order (longest
+ * in-edge list first), each processed by one single-wave workgroup (lgconv.hip); `heavy` must be
+ * empty.  Used for D = 256, H in {1,2,4,8}, materialised F (feat_row NULL), no encoder and, in the
+ * backward, no dF; other calls take the kernels above.  Arithmetic and outputs are those of the
+ * compact-register kernels (the same dropout masks); sums are formed in a different order. */
+#define ALIGNN_SCHED_WAVE_ITEMS 2
 
 /* Edge encoder (optional, replaces F): the edge features are the hidden layer of a
  * Linear->ReLU edge encoder, f_t = relu(W1 x[row(t)] + b1) — the angle encoder's first Linear
@@ -247,6 +258,34 @@ int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H,
                          float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
                          float* dF, int64_t lddf, int32_t accumulate_dF,
                          float drop_p, uint64_t seed, void* stream);
+
+/* bf16 storage variant of the line-graph attention (config C3, the reference's autocast precision:
+ * the Linear outputs K, V and the angle encoder's hidden layer are bf16, train.py:632-636): the
+ * gathered K|V rows (KV16 [n, ldkv], K at col 0, V at col D) and the streamed edge-feature rows
+ * (F16 [m, ldf], row of edge position t is t) are bf16; Q, U, Vd, dout, outp, the statistics and
+ * every output stay fp32, and all arithmetic is fp32 (bf16 -> fp32 is exact).  Same outputs as
+ * alignn_tconv_fwd / alignn_tconv_bwd_dst (dF == NULL).  Needs D = 256, H in {1, 2, 4} and an
+ * ALIGNN_SCHED_WAVE_ITEMS schedule listing every target (heavy list empty). */
+int alignn_lg_fwd_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
+                       const AlignnSchedule* sched, const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv,
+                       const float* U, const float* wbar, const uint16_t* F16, int64_t ldf, float* aggV, float* S,
+                       float* sumA, float* mstat, float* den, float drop_p, uint64_t seed, void* stream);
+int alignn_lg_bwd_dst_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                           const int32_t* src_at, const AlignnSchedule* sched, const float* Q, int64_t ldq,
+                           const uint16_t* KV16, int64_t ldkv, const float* U, const float* Vd, const float* wbar,
+                           const uint16_t* F16, int64_t ldf, const float* dout, const float* outp,
+                           const float* mstat, const float* den, float* dq, int64_t lddq, float* Sz, float* sigz,
+                           float* dz_e, float* alpha_e, float drop_p, uint64_t seed, void* stream);
+/* dst (bf16, RNE) = src (fp32) for a [rows, cols] block; cols and both leading dimensions multiples
+ * of 4, src rows 16-byte aligned. */
+int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, uint16_t* dst, int64_t ldd,
+                         void* stream);
+
+/* Which attention kernel family alignn_tconv_fwd / alignn_tconv_bwd_dst (with dF == NULL) run for
+ * these arguments: 3 = single-wave items (lgconv.hip), 2 = compact-register, 1 = default
+ * (tconv.hip), 0 = unsupported arguments.  A host query: no device work. */
+int alignn_tconv_family(int32_t D, int32_t H, const int32_t* feat_row, const AlignnEdgeEncoder* enc,
+                        const float* F, const AlignnSchedule* sched);
 
 /* Workspace (floats) alignn_tconv_bwd_dst needs for an edge encoder with kin inputs at full
  * parallelism on the current device; 0 without encoder, -1 for unsupported arguments. */

@@ -191,8 +191,9 @@ def _run_tconv(csr, m, t, D, H, drop, compact):
     ops = _ops()
     n = csr.n
     csr._sched = None
-    prev = ops.GraphCSR.COMPACT_REGS
+    prev = ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.WAVE_ITEMS
     ops.GraphCSR.COMPACT_REGS = compact
+    ops.GraphCSR.WAVE_ITEMS = False  # these tests pin the tconv.hip families (lgconv.hip: test_gpu_x_lg3.py)
     try:
         outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
         sumA, mstat, den = (torch.empty(n, H, device=DEV) for _ in range(3))
@@ -205,7 +206,7 @@ def _run_tconv(csr, m, t, D, H, drop, compact):
         ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], t["feat_row"], t["dout"], outp,
                           mstat, den, dq, Sz, sigz, dz, al, dF, 3, drop, 77)
     finally:
-        ops.GraphCSR.COMPACT_REGS = prev
+        ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.WAVE_ITEMS = prev
         csr._sched = None
     torch.cuda.synchronize()
     return dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz[:m], al=al[:m],

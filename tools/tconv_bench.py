@@ -38,7 +38,7 @@ def timeit(fn, reps):
     return sorted(ts)[1]
 
 
-def run_graph(name, g, n, m, D, H, F, enc, reps, out):
+def run_graph(name, g, n, m, D, H, F, enc, reps, out, nodf=False):
     dev = "cuda"
     # shapes the kernels assume (checked on the host before any launch)
     assert g.n == n and g.m == m, (g.n, n, g.m, m)
@@ -54,7 +54,7 @@ def run_graph(name, g, n, m, D, H, F, enc, reps, out):
     Sz, sigz = torch.empty(n, H, D, device=dev), torch.empty(n, H, device=dev)
     dz, al = torch.empty(max(m, 1), H, device=dev), torch.empty(max(m, 1), H, device=dev)
     dKV = torch.empty(n, 2 * D, device=dev)
-    dF = None if F is None else torch.zeros_like(F)
+    dF = None if (F is None or nodf) else torch.zeros_like(F)
     ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, None, aggV, S, sumA, mstat, den, 0.15, 1, enc=enc)
     t_f = timeit(lambda: ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, None, aggV, S, sumA, mstat, den, 0.15, 1,
                                        enc=enc), reps)
@@ -63,11 +63,13 @@ def run_graph(name, g, n, m, D, H, F, enc, reps, out):
         dw1, db1 = torch.zeros_like(enc.w1), torch.zeros_like(enc.b1)
         bwd_enc = ops.EdgeEncoder(enc.x, enc.w1, enc.b1, dw1, db1)
     t_b = timeit(lambda: ops.tconv_bwd_dst(g, D, H, QKVR, U, Vd, wbar, F, None, dout, aggV, mstat, den, dq, Sz,
-                                           sigz, dz, al, dF, 1, 0.15, 1, enc=bwd_enc), reps)
+                                           sigz, dz, al, dF, 0 if dF is None else 1, 0.15, 1, enc=bwd_enc),
+                 reps)
     t_s = timeit(lambda: ops.tconv_bwd_src(g, D, H, QKVR, dout, dz, al, dKV), reps)
-    res = {"fwd_us": t_f, "bwd_dst_us": t_b, "bwd_src_us": t_s, "n": n, "m": m}
+    fam = g.family(D, H, F, None, enc)
+    res = {"fwd_us": t_f, "bwd_dst_us": t_b, "bwd_src_us": t_s, "n": n, "m": m, "family": fam}
     out[name] = res
-    print(f"{name:28s} n={n:6d} m={m:7d}  fwd {t_f:8.1f} us  bwd_dst {t_b:8.1f} us  bwd_src {t_s:8.1f} us", flush=True)
+    print(f"{name:28s} fam={fam} n={n:6d} m={m:7d}  fwd {t_f:8.1f} us  bwd_dst {t_b:8.1f} us  bwd_src {t_s:8.1f} us", flush=True)
 
 
 def main():
@@ -92,6 +94,13 @@ def main():
         run_graph(f"line/{lg_offset}/enc", lg, nl, T, D, H, None, enc, a.reps, out)
         F = torch.relu(xa @ w1.t() + b1)
         run_graph(f"line/{lg_offset}/F", lg, nl, T, D, H, F, None, a.reps, out)
+        # the training step's configuration: materialised F, deferred encoder backward (no dF)
+        for wave_items in (False, True):
+            ops.GraphCSR.WAVE_ITEMS = wave_items
+            lg._sched = None
+            run_graph(f"line/{lg_offset}/F/nodF/wi{int(wave_items)}", lg, nl, T, D, H, F, None, a.reps, out,
+                      nodf=True)
+        lg._sched = None
         if lg_offset == "num_nodes":
             N = b.x.size(0)
             ag = ops.GraphCSR(b.edge_index, N)
