@@ -273,8 +273,15 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.sumA = torch.empty(na, H, device=dev)
     c.mstat = torch.empty(na, H, device=dev)
     c.den = torch.empty(na, H, device=dev)
-    ops.tconv_fwd(g, D, H, c.QKV, c.U, c.wbar, F, feat_row, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att,
-                  enc=enc)
+    c.KV16 = None
+    if F is not None and F.dtype == torch.bfloat16:
+        # bf16 storage (config C3): the attention gathers K|V from a bf16 copy and streams bf16 F rows
+        c.KV16 = ops.cast_bf16(c.QKV[:, D:3 * D])
+        ops.lg_fwd_bf16(g, D, H, c.QKV, c.KV16, c.U, c.wbar, F, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
+                        seed_att)
+    else:
+        ops.tconv_fwd(g, D, H, c.QKV, c.U, c.wbar, F, feat_row, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
+                      seed_att, enc=enc)
     if with_proj:
         ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp_a.view(na, H, C).transpose(0, 1),
                  beta=1.0, rowscale=c.sumA.t(), bias2=c.wbar.view(H, C))
@@ -353,8 +360,14 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     if c.enc is not None:
         enc = ops.EdgeEncoder(c.enc.x, c.enc.w1, c.enc.b1, enc_grads[0], enc_grads[1], accumulate=True)
         dF = None
-    ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
-                      dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
+    if c.KV16 is not None:
+        if dF is not None:
+            raise ValueError("bf16 edge-feature storage needs the deferred angle-encoder backward (no dF)")
+        ops.lg_bwd_dst_bf16(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, c.F, dout_a, c.outp_a, c.mstat, c.den,
+                            dQKV[:, :D], Sz, sigz, dz_e, al_e, c.p, c.seed_att)
+    else:
+        ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
+                          dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
     # dK/dV (source side) and the dQ products below are independent: with an aux stream the
     # source-side kernel runs beside them and the dX products wait for both
     aux = ops.aux_stream(dev) if (side is not None and overlap_src) else None
@@ -451,9 +464,12 @@ class AlignnEngine:
         # (measured +1.2 % graphs/s on MI355X, profiles/r01/v7_sweep.log)
         self.overlap_forward = True
         # GEMM arithmetic: "fp32" (the reference's CPU path; exact fp32 MFMA) or "bf16" (bf16 MFMA
-        # inputs, fp32 accumulation — the reference's CUDA autocast);
-        # attention, softmax, LayerNorm and all storage stay fp32 either way
+        # inputs, fp32 accumulation — the reference's CUDA autocast).  With
+        # "bf16" (and bf16_storage) the line-graph attention also streams its largest operands as the
+        # autocast Linear outputs they are — the angle hidden layer and the gathered K|V rows in bf16;
+        # softmax, accumulation, LayerNorm and every other tensor stay fp32
         self.precision = "fp32"
+        self.bf16_storage = True
         # the angle encoder's first Linear (11 inputs, T rows) and its weight/bias gradients as
         # streamed HBM-rate kernels (skinny.hip) instead of MFMA tiles (+3.2 %, v7_sweep.log)
         self.skinny_encoder = True
@@ -477,6 +493,16 @@ class AlignnEngine:
         self.enc_bwd_aux = False  # measured -0.6 % (v31_sweep_enc_bwd_aux_rejected.log)
         # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
         self.wbar_colsum = True
+
+    def _bf16_angle(self, bc, D: int) -> bool:
+        """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
+        deferred encoder backward, and a line graph in the bf16 kernels' domain (D = 256, H <= 4,
+        single-wave work items without heavy nodes)."""
+        if not (self.precision == "bf16" and self.bf16_storage and self.defer_angle_bwd and D == 256
+                and self.cfg.heads in (1, 2, 4) and bc.lg is not None and ops.GraphCSR.WAVE_ITEMS
+                and ops.enc_bwd_ok(D, self.cfg.heads, self.cfg.layers, bc.xa.size(1))):
+            return False
+        return bc.lg.schedule().n_heavy == 0
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -539,12 +565,23 @@ class AlignnEngine:
         if ctx.has_angle and self.recompute_angle and bc.xa.size(1) <= ops.ENC_MAX_KIN and T > 0:
             ctx.angle_enc = ops.EdgeEncoder(bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"))
         elif ctx.has_angle:
-            a = torch.empty(T, D, device=dev)
             W1, b1 = P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias")
-            if self.skinny_encoder and ops.linear_smallk_ok(bc.xa, W1, a):
-                ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
+            if self._bf16_angle(bc, D):
+                # config C3 (autocast): the hidden layer is a bf16 Linear output, stored as bf16 and read
+                # by the bf16-storage line-graph attention (its backward is the deferred enc_bwd)
+                a = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+                if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLK_MAX and D % 4 == 0:
+                    ops.linear_smallk_bf16(bc.xa, W1, b1, a, relu=True)
+                else:
+                    a32 = torch.empty(T, D, device=dev)
+                    ops.gemm(bc.xa, W1.t(), a32, bias=b1, relu=True)
+                    ops.cast_bf16(a32, a)
             else:
-                ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
+                a = torch.empty(T, D, device=dev)
+                if self.skinny_encoder and ops.linear_smallk_ok(bc.xa, W1, a):
+                    ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
+                else:
+                    ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
         else:
             a = ops.zeros(T, D, device=dev)
         ctx.h1a = ctx.a = a

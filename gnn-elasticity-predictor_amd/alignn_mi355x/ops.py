@@ -227,6 +227,7 @@ GEMM_TRACE: Optional[list] = None
 _GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
 GEMM_STAGE = 0        # ALIGNN_GEMM_BK32 (16) / ALIGNN_GEMM_BK64 (128): K stage depth of every planned GEMM
 GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
+GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
 
 
 @contextmanager
@@ -373,6 +374,23 @@ def linear_smallk(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor]
                                               W.stride(0), None if bias is None else bias.data_ptr(), W.size(0),
                                               int(bool(relu)), out.data_ptr(), out.stride(0), stream_ptr()),
           "alignn_linear_smallk_f32")
+    return out
+
+
+def linear_smallk_bf16(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor,
+                       relu: bool = False) -> torch.Tensor:
+    """out (bf16) = act(X W^T + bias), the bf16-output form of linear_smallk (same fma order)."""
+    if (out.dtype != torch.bfloat16 or not (X.dim() == 2 and X.stride(1) == 1 and W.dim() == 2 and W.stride(1) == 1
+                                            and out.stride(1) == 1 and W.size(1) == X.size(1) <= SMALLK_MAX
+                                            and out.size(1) == W.size(0) and out.size(0) == X.size(0)
+                                            and W.size(0) % 4 == 0 and out.stride(0) % 4 == 0
+                                            and out.data_ptr() % 8 == 0)):
+        raise ValueError(f"linear_smallk_bf16: unsupported shapes X{tuple(X.shape)} W{tuple(W.shape)} "
+                         f"out{tuple(out.shape)} {out.dtype}")
+    check(_lib.lib().alignn_linear_smallk_bf16out(X.data_ptr(), X.stride(0), X.size(0), X.size(1), W.data_ptr(),
+                                                  W.stride(0), None if bias is None else bias.data_ptr(), W.size(0),
+                                                  int(bool(relu)), out.data_ptr(), out.stride(0), stream_ptr()),
+          "alignn_linear_smallk_bf16out")
     return out
 
 
@@ -672,6 +690,70 @@ def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, d
                          sigz.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF),
                          0 if dF is None else dF.stride(0), int(accumulate_dF), float(drop_p),
                          int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_bwd_dst"))
+
+
+def _lg_bf16_bytes(n: int, m: int, D: int, H: int, kind: str) -> float:
+    """Compulsory HBM bytes of one bf16-storage launch: K|V and the edge-feature rows at 2 bytes,
+    everything else fp32 (as _tconv_bytes)."""
+    if kind == "fwd":   # Q (4) + K,V (2) + U + features (2) + CSR in; aggV + S + 3 stats out
+        return 4.0 * (n * D + n * H * D + 2 * m + n + n * D + n * H * D + 3 * n * H) + 2.0 * (2 * n * D + m * D)
+    # bwd_dst: Q,U,Vd,dout,outp,stats,CSR in (4) + K,V,features (2); dQ,Sz,sigz,dz,alpha out
+    return (4.0 * (n * D + 2 * n * H * D + 2 * n * D + 2 * n * H + 2 * m + n + n * D + n * H * D + n * H + 2 * m * H)
+            + 2.0 * (2 * n * D + m * D))
+
+
+def _check_lg_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, F16):
+    n, m = g.n, g.m
+    if QKV.size(0) < n or QKV.size(1) < 3 * D or QKV.stride(1) != 1:
+        raise ValueError(f"lg bf16: QKV {tuple(QKV.shape)} must cover [{n}, >= {3 * D}] row-major")
+    if KV16.dtype != torch.bfloat16 or KV16.size(0) < n or KV16.size(1) < 2 * D or KV16.stride(1) != 1:
+        raise ValueError(f"lg bf16: KV16 must be bf16 [{n}, >= {2 * D}] row-major")
+    if F16.dtype != torch.bfloat16 or F16.size(1) < D or F16.stride(1) != 1 or (m > 0 and F16.size(0) < m):
+        raise ValueError(f"lg bf16: F16 must be bf16 [{m}, >= {D}] row-major")
+
+
+def lg_fwd_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, wbar, F16, aggV, S, sumA, mstat, den, drop_p: float,
+                seed: int):
+    """alignn_lg_fwd_bf16: the line-graph attention forward with bf16 K|V and edge-feature rows."""
+    _check_lg_bf16(g, D, H, QKV, KV16, F16)
+    if U.numel() < g.n * H * D or S.numel() < g.n * H * D or aggV.numel() < g.n * D:
+        raise ValueError("lg_fwd_bf16: U and S must be [n, H, D], aggV [n, D]")
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m} bf16", 0.0, _lg_bf16_bytes(g.n, g.m, D, H, "fwd"),
+                     lambda: check(_lib.lib().alignn_lg_fwd_bf16(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
+                         QKV.data_ptr(), QKV.stride(0), KV16.data_ptr(), KV16.stride(0), U.data_ptr(), _p(wbar),
+                         F16.data_ptr(), F16.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(),
+                         mstat.data_ptr(), den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+                         "alignn_lg_fwd_bf16"))
+
+
+def lg_bwd_dst_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz,
+                    sigz, dz_e, alpha_e, drop_p: float, seed: int):
+    """alignn_lg_bwd_dst_bf16: the target-side attention backward with bf16 K|V and feature rows."""
+    _check_lg_bf16(g, D, H, QKV, KV16, F16)
+    if (U.numel() < g.n * H * D or Vd.numel() < g.n * H * D or Sz.numel() < g.n * H * D or dq.size(0) < g.n
+            or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H):
+        raise ValueError("lg_bwd_dst_bf16: U, Vd, Sz [n, H, D], dq [n, >= D], dz_e/alpha_e [m, H] required")
+    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m} bf16", 0.0, _lg_bf16_bytes(g.n, g.m, D, H, "bwd_dst"),
+                     lambda: check(_lib.lib().alignn_lg_bwd_dst_bf16(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
+                         QKV.data_ptr(), QKV.stride(0), KV16.data_ptr(), KV16.stride(0), U.data_ptr(), Vd.data_ptr(),
+                         _p(wbar), F16.data_ptr(), F16.stride(0), dout.data_ptr(), outp.data_ptr(), mstat.data_ptr(),
+                         den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
+                         dz_e.data_ptr(), alpha_e.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+                         "alignn_lg_bwd_dst_bf16"))
+
+
+def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out (bf16, round to nearest even) = src (fp32 [rows, cols], cols % 4 == 0)."""
+    if out is None:
+        out = torch.empty(src.shape, device=src.device, dtype=torch.bfloat16)
+    if (src.dim() != 2 or src.dtype != torch.float32 or src.stride(1) != 1 or out.dtype != torch.bfloat16
+            or out.stride(1) != 1 or tuple(out.shape) != tuple(src.shape)):
+        raise ValueError("cast_bf16: fp32 [rows, cols] row-major source and a bf16 output of the same shape")
+    check(_lib.lib().alignn_cast_bf16_f32(src.data_ptr(), src.stride(0), src.size(0), src.size(1), out.data_ptr(),
+                                          out.stride(0), stream_ptr()), "alignn_cast_bf16_f32")
+    return out
 
 
 def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):

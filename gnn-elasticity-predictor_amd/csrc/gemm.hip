@@ -189,6 +189,69 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, 
   return v;
 }
 
+// One LDS stage of MFMAs: BKT/16 slices of the wave's (BM/2) x (BN/2) subtile.
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF>
+__device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], const float* __restrict__ As,
+                                          const float* __restrict__ Bs, int wm, int wn, int h, int l32) {
+  constexpr int MI = BM / 64, NI = BN / 64;
+#pragma unroll
+  for (int sub = 0; sub < BKT / 16; ++sub) {
+    float fa[MI][8], fb[NI][8];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, BKT>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) read_frag<BN, B_KC, BKT>(Bs, wn * (BN / 2) + j * 32 + l32, h, sub, fb[j]);
+    if constexpr (BF) {
+      bf16x8 ha[MI], hb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) ha[i][s] = (__bf16)fa[i][s];
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) hb[j][s] = (__bf16)fb[j][s];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], hb[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+// Epilogue. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+template <int BM, int BN>
+__device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (&acc)[BM / 64][BN / 64], int64_t m0,
+                                           int64_t n0, int64_t b, int sidx, int wm, int wn, int h, int l32) {
+  constexpr int MI = BM / 64, NI = BN / 64;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int64_t col = n0 + wn * (BN / 2) + j * 32 + l32;
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        if (p.split_k > 1) {
+          p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
+        } else {
+          p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
+        }
+      }
+    }
+}
+
 template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF, bool RB>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
@@ -262,39 +325,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     const bool more = k0 + BKT < ke;
     if (more) load_stage(k0 + BKT);
     const float* As = smem + cur * (LA + LB);
-    const float* Bs = As + LA;
-#pragma unroll
-    for (int sub = 0; sub < BKT / 16; ++sub) {
-      float fa[MI][8], fb[NI][8];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, BKT>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) read_frag<BN, B_KC, BKT>(Bs, wn * (BN / 2) + j * 32 + l32, h, sub, fb[j]);
-      if constexpr (BF) {
-        bf16x8 ha[MI], hb[NI];
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int s = 0; s < 8; ++s) ha[i][s] = (__bf16)fa[i][s];
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int s = 0; s < 8; ++s) hb[j][s] = (__bf16)fb[j][s];
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], hb[j], acc[i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int s = 0; s < 8; ++s)
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-      }
-    }
+    mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, As, As + LA, wm, wn, h, l32);
     if (more) {
       float* nxt = smem + (cur ^ 1) * (LA + LB);
       la.store(nxt);
@@ -304,24 +335,93 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     cur ^= 1;
   }
 
-  // Epilogue. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
+}
+
+// Pipelined variant (ALIGNN_GEMM_PIPE): two register sets of global loads in flight, so a stage's
+// loads are covered by two stages of MFMAs instead of one (a 16-deep stage is 512 cycles of MFMA per
+// wave against a loaded global round trip of several thousand: the one-stage loop above is latency
+// bound).  Used when every stage of every workgroup is full and both operands take the vector fast
+// path (host check, gemm_pipe_ok), so the loop has no bounds logic.  Loads are unconditional, their
+// stage index clamped to the last (a load under a condition becomes a phi whose register copy waits
+// for it); the loop covers pairs of stages with one exit, the odd last stage's MFMAs under a
+// wave-uniform branch.  Same MFMA order and epilogue as gemm_f32_kernel: bitwise equal results.
+typedef float gf4 __attribute__((ext_vector_type(4)));
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF>
+__global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
+  constexpr int MI = BM / 64, NI = BN / 64;
+  constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
+  constexpr int FA = TileLoader<BM, A_KC, BKT>::F4, FB = TileLoader<BN, B_KC, BKT>::F4;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
+
+  const int64_t tiles_n = (p.N + BN - 1) / BN;
+#if ALIGNN_GEMM_XCD
+  const int64_t nlin = (int64_t)gridDim.x * gridDim.z;
+  const int64_t lin = (int64_t)blockIdx.z * gridDim.x + blockIdx.x;
+  const int64_t xq = nlin / 8, xr = nlin % 8, xcd = lin % 8;
+  const int64_t item = (ALIGNN_GEMM_XCD_SPLIT || p.split_k == 1) ? xcd * xq + min(xcd, xr) + lin / 8 : lin;
+  const int64_t tile = item % gridDim.x, zid = item / gridDim.x;
+#else
+  const int64_t tile = blockIdx.x, zid = blockIdx.z;
+#endif
+  const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int64_t b = zid / p.split_k;
+  const int sidx = zid % p.split_k;
+  const int64_t kb = (int64_t)sidx * p.kchunk;
+  const int64_t ke = min(p.K, kb + p.kchunk);
+  const int nst = (int)((ke - kb) / BKT);  // >= 1 full stages (host check)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+
+  floatx16 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int64_t col = n0 + wn * (BN / 2) + j * 32 + l32;
-      if (col >= p.N) continue;
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= p.M) continue;
-        if (p.split_k > 1) {
-          p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
-        } else {
-          p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
-        }
-      }
-    }
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  TileLoader<BM, A_KC, BKT> la;
+  TileLoader<BN, B_KC, BKT> lb;
+  la.setup_fast(p.A + b * p.sab, p.sam, p.sak, m0, p.M, kb);
+  lb.setup_fast(p.B + b * p.sbb, p.sbn, p.sbk, n0, p.N, kb);
+  gf4 pa[FA], pb[FB], qa[FA], qb[FB];
+  auto load = [&](gf4 (&ra)[FA], gf4 (&rb)[FB], int st) {
+    const int64_t koff = (int64_t)min(st, nst - 1) * BKT;
+#pragma unroll
+    for (int i = 0; i < FA; ++i) ra[i] = *reinterpret_cast<const gf4*>(la.base[i] + (A_KC ? koff : koff * p.sak));
+#pragma unroll
+    for (int i = 0; i < FB; ++i) rb[i] = *reinterpret_cast<const gf4*>(lb.base[i] + (B_KC ? koff : koff * p.sbk));
+    asm volatile("" ::: "memory");  // keep the loads here (not sunk to their first use)
+  };
+  auto store = [&](const gf4 (&ra)[FA], const gf4 (&rb)[FB], float* buf) {
+#pragma unroll
+    for (int i = 0; i < FA; ++i) la.r[i] = make_float4(ra[i].x, ra[i].y, ra[i].z, ra[i].w);
+#pragma unroll
+    for (int i = 0; i < FB; ++i) lb.r[i] = make_float4(rb[i].x, rb[i].y, rb[i].z, rb[i].w);
+    la.store(buf);
+    lb.store(buf + LA);
+  };
+  float* L0 = smem;
+  float* L1 = smem + (LA + LB);
+  load(pa, pb, 0);
+  store(pa, pb, L0);
+  load(pa, pb, 1);
+  load(qa, qb, 2);
+  __syncthreads();
+  const int npairs = (nst + 1) / 2;
+  for (int it = 0; it < npairs; ++it) {
+    const int s0 = 2 * it;
+    mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, L0, L0 + LA, wm, wn, h, l32);   // stage s0
+    store(pa, pb, L1);                                                          // stage s0 + 1
+    load(pa, pb, s0 + 3);
+    __syncthreads();
+    if (s0 + 1 < nst) mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, L1, L1 + LA, wm, wn, h, l32);
+    store(qa, qb, L0);                                                          // stage s0 + 2
+    load(qa, qb, s0 + 4);
+    __syncthreads();
+  }
+  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
@@ -346,6 +446,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
+#ifndef ALIGNN_GEMM_PIPE
+#define ALIGNN_GEMM_PIPE 1
+#endif
+template <int BM, int BN, bool A_KC, bool B_KC>
+static void launch_pipe(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
+  if (bf) {
+    if (bk >= 64) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 64, true>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
+    else launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
+  } else {
+    if (bk >= 64) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 64, false>), grid, dim3(256), 0, s, p);
+    else if (bk == 32) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
+    else launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
+  }
+}
+
 template <int BM, int BN, bool A_KC, bool B_KC, bool RB>
 static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
   if (bf) {
@@ -367,18 +483,37 @@ static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream
   }
 }
 
+// Every workgroup of the pipelined kernel must have only full stages and fast-path operands.
 template <int BM, int BN, bool A_KC, bool B_KC>
-static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
+static bool gemm_pipe_ok(const GemmParams& p, int bk) {
+  if (!ALIGNN_GEMM_PIPE || p.reduce_batch || !p.vecA || !p.vecB || bk > 64 || p.K <= 0) return false;
+  if (p.kchunk % bk != 0 || p.K % bk != 0) return false;   // every split chunk a whole number of stages
+  if (!A_KC && p.M % BM != 0) return false;                 // row-contiguous operands: interior tiles only
+  if (!B_KC && p.N % BN != 0) return false;
+  if (A_KC && p.sak != 1) return false;
+  if (B_KC && p.sbk != 1) return false;
+  return true;
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC>
+static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe, hipStream_t s) {
+  if constexpr (BM == 64 && BN == 64) {  // the automatic plan's tile (make_plan)
+    if (!nopipe && gemm_pipe_ok<BM, BN, A_KC, B_KC>(p, bk)) {
+      launch_pipe<BM, BN, A_KC, B_KC>(p, grid, bk, bf, s);
+      return;
+    }
+  }
   if (p.reduce_batch) launch_rb<BM, BN, A_KC, B_KC, true>(p, grid, bk, bf, s);
   else launch_rb<BM, BN, A_KC, B_KC, false>(p, grid, bk, bf, s);
 }
 
 template <int BM, int BN>
-static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, bool bf, hipStream_t s) {
-  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, bf, s);
-  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, bf, s);
-  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, bf, s);
-  else launch<BM, BN, false, false>(p, grid, bk, bf, s);
+static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, bool bf, bool nopipe,
+                            hipStream_t s) {
+  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, bf, nopipe, s);
+  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, bf, nopipe, s);
+  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, bf, nopipe, s);
+  else launch<BM, BN, false, false>(p, grid, bk, bf, nopipe, s);
 }
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -528,10 +663,11 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
   const bool bf = (a->tile & ALIGNN_GEMM_BF16) != 0;
-  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, bf, s);
-  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, bf, s);
-  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, bf, s);
-  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, s);
+  const bool np = (a->tile & ALIGNN_GEMM_NOPIPE) != 0;
+  if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, bf, np, s);
+  else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);
+  else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, bf, np, s);
+  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {
     int64_t total = nbatch_out * a->M * a->N;

@@ -77,6 +77,10 @@ typedef struct AlignnGemmArgs {
  * A and B are rounded to bf16 (round-to-nearest-even) as they enter the matrix cores
  * (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate); accumulation, epilogue and storage stay fp32. */
 #define ALIGNN_GEMM_BF16 64
+/* Force the one-stage-in-flight main loop (the pipelined loop — two register sets of loads in
+ * flight — is taken automatically when every stage is full and both operands are vectorisable; both
+ * give bitwise the same result).  For A/B tests. */
+#define ALIGNN_GEMM_NOPIPE 256
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 

@@ -108,3 +108,88 @@ def test_member_placement_and_seeds():
     assert dp.members_of_rank(5, 2, 0) == [0, 2, 4] and dp.members_of_rank(5, 2, 1) == [1, 3]
     with pytest.raises(ValueError):
         dp.members_of_rank(5, 2, 2)
+
+
+# ------------------------------------------------------------------------------------------------
+# FusedTrainer.grad_hook between the two replayed launch plans (trainer._replay), world size 2
+# ------------------------------------------------------------------------------------------------
+class _FakeLib:
+    """Stands in for libalignn_hip's plan replay: plan 1 = forward/backward (writes this rank's
+    gradient), plan 2 = clip + AdamW (the reference's two-group AdamW on CPU)."""
+
+    def __init__(self, trainer, grad, log):
+        self.tr, self.grad, self.log = trainer, grad, log
+
+    def alignn_plan_replay(self, plan, stream):
+        if plan == 1:
+            self.log.append("fb")
+            self.tr.st.grad.copy_(self.grad)
+        else:
+            self.log.append("update")
+            new = _step_flat(self.tr.st.flat, self.tr.st.grad, self.tr.st.P.sigma_start)
+            self.tr.st.flat.copy_(new)
+        return 0
+
+
+def _step_flat(flat, grad, s0):
+    p_base = torch.nn.Parameter(flat[:s0].clone())
+    p_sigma = torch.nn.Parameter(flat[s0:].clone())
+    p_base.grad, p_sigma.grad = grad[:s0].clone(), grad[s0:].clone()
+    opt = torch.optim.AdamW([{"params": [p_base], "lr": 3e-4}, {"params": [p_sigma], "lr": 3e-4}], lr=3e-4,
+                            weight_decay=1e-4)
+    torch.nn.utils.clip_grad_norm_([p_base, p_sigma], max_norm=5.0)
+    opt.step()
+    return torch.cat([p_base.detach(), p_sigma.detach()])
+
+
+def _trainer_worker(rank, world, port, out_dir):
+    import alignn_mi355x as A
+    from alignn_mi355x import _lib, ops, trainer as trainer_mod
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)  # identical initial weights on both ranks
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(6, 8, 7, 289, 2, 32, 1, 1, 0.0), 2)
+        tr = A.FusedTrainer(model, optimizer="torch")
+        n = tr.st.flat.numel()
+        grad = torch.randn(n, generator=torch.Generator().manual_seed(7 + rank)) * (2.0 + rank)
+        log = []
+        fake = _FakeLib(tr, grad, log)
+        _lib.lib = lambda: fake            # the replay goes through the stub library
+        ops.stream_ptr = lambda *a, **k: 0
+        trainer_mod.check = lambda rc, what: None
+        hook = dp.grad_allreduce_hook(world)
+
+        def logged_hook(g):
+            log.append("hook")
+            hook(g)
+
+        tr.grad_hook = logged_hook
+        tr._seed_dev = torch.zeros(1, dtype=torch.int64)
+        batch = object()
+        tr._graph = (None, None, batch, [1, 2])   # two captured plans, as capture(mode="plan") leaves them
+        before = tr.st.flat.clone()
+        tr.step(batch, seed=3)
+        torch.save({"log": log, "before": before, "after": tr.st.flat.clone(), "grad": tr.st.grad.clone(),
+                    "s0": tr.st.P.sigma_start, "steps": tr.step_count}, os.path.join(out_dir, f"t{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_fused_trainer_grad_hook_between_plan_phases_world2(tmp_path):
+    """The replayed step runs plan 1 (forward/backward), then the DP hook (one gloo all_reduce of the
+    flat gradient, mean over ranks), then plan 2 (clip + AdamW): afterwards both ranks hold the same
+    parameters, equal to one process stepping on the mean gradient (trainer.py _replay)."""
+    world = 2
+    mp.spawn(_trainer_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"t{i}.pt", weights_only=True) for i in range(world)]
+    for x in r:
+        assert x["log"] == ["fb", "hook", "update"], x["log"]
+        assert x["steps"] == 1
+    n = r[0]["before"].numel()
+    mean = sum(torch.randn(n, generator=torch.Generator().manual_seed(7 + i)) * (2.0 + i) for i in range(world)) / world
+    assert torch.allclose(r[0]["grad"], mean, atol=1e-6) and torch.equal(r[0]["grad"], r[1]["grad"])
+    want = _step_flat(r[0]["before"], mean, r[0]["s0"])
+    assert torch.equal(r[0]["after"], r[1]["after"])
+    assert torch.allclose(r[0]["after"], want, atol=1e-7)
