@@ -53,10 +53,11 @@ def parse():
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM arithmetic: fp32 (BASELINE config 2, the default) or bf16 matrix-core inputs with "
                         "fp32 accumulation (config 3's autocast precision; a secondary line, never the fp32 number)")
-    p.add_argument("--e2e", type=int, default=0, metavar="GRAPHS",
-                   help="also time the end-to-end loop over an HBM-resident dataset of this many graphs per rank: "
-                        "device collate of a random batch + CSR/compaction + step (SURVEY §8d's 'including collate' "
-                        "number; reported as a separate field, never as value)")
+    p.add_argument("--e2e", type=int, default=10000, metavar="GRAPHS",
+                   help="also time the end-to-end loop over an HBM-resident dataset of this many graphs per rank "
+                        "(config C5's ~10k graphs; 0 = off): device collate of a random batch + CSR/compaction + "
+                        "step, at the headline config and (one GPU) at config C5's B=256 bf16 (SURVEY §8d's "
+                        "'including collate' number; separate fields, never value)")
     p.add_argument("--launch", choices=["eager", "plan", "graph"], default="plan",
                    help="eager: Python issues every launch; plan: the step is recorded once as a native launch "
                         "plan and re-issued from C++ (plan.hip; the roofline probe is a pair of plan timestamps "
@@ -155,46 +156,72 @@ def cpu_baseline(args, B):
                       f"{os.cpu_count()}); {cpu_model}"}
 
 
-def end_to_end(args, trainer, dev, rank, world):
-    """Training loop over a dataset resident in HBM (store.GraphStore): per step a random batch is
-    collated on the device and its CSR lists / line-graph compaction are built, then the step runs."""
-    import numpy as np
+def build_store(args, dev, rank):
+    """This rank's shard of an HBM-resident dataset of args.e2e synthetic MP-like graphs
+    (store.GraphStore; config C5's ~10k-graph dataset split over the data-parallel ranks), built
+    once and shared by the end-to-end loops."""
     from alignn_mi355x.data import Data
-    from alignn_mi355x.dp import max_over_ranks
     from alignn_mi355x.store import GraphStore
     from alignn_mi355x.synthetic import mp_like_graph
 
     keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
-    first = rank * args.e2e
-    t_build = time.perf_counter()
-    graphs = [mp_like_graph(first + g) for g in range(args.e2e)]
-    store = GraphStore.from_data_list([Data(**{k: getattr(d, k) for k in keys}) for d in graphs], dev)
-    del graphs
-    t_build = time.perf_counter() - t_build
+    t0 = time.perf_counter()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    per = (args.e2e + world - 1) // world
+    first = rank * per
+    n = max(1, min(per, args.e2e - first))
+    store = GraphStore.from_data_list([Data(**{k: getattr(mp_like_graph(first + g), k) for k in keys})
+                                       for g in range(n)], dev)
+    torch.cuda.synchronize()
+    return store, time.perf_counter() - t0
+
+
+def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
+    """The reference's training loop (train.py:639-711) over a dataset resident in HBM: per step a
+    random batch is collated on the device and its CSR lists / line-graph compaction / schedules are
+    built on a loader stream (engine.prepare_batch) while the previous step runs; the step re-binds
+    the captured plan to it (FusedTrainer._rebind: copies into the captured batch's buffers) and
+    replays.  Timed like the headline: barrier + synchronize on both sides, max over ranks."""
+    import numpy as np
+    from alignn_mi355x.dp import max_over_ranks
+    from alignn_mi355x.engine import prepare_batch
+
     rng = np.random.default_rng(1234 + rank)
-    B = args.batch
+    loader = torch.cuda.Stream(device=dev)
 
-    def e2e_step(i):
-        batch = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset)
-        trainer.step(batch, seed=7919 * rank + i)
+    def make():
+        with torch.cuda.stream(loader):
+            b = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset)
+        prepare_batch(b, loader)
+        return b
 
+    r0, m0 = trainer.rebinds, trainer.rebind_misses
+    nxt = make()
     for i in range(args.warmup):
-        e2e_step(i)
+        cur = nxt
+        trainer.step(cur, seed=7919 * rank + i)
+        nxt = make()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        e2e_step(args.warmup + i)
+        cur = nxt
+        trainer.step(cur, seed=7919 * rank + args.warmup + i)
+        nxt = make()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
         dt = max_over_ranks(dt, dev)
-    return {"value": round(B * world * args.steps / dt, 2), "unit": "graphs/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "dataset_graphs_per_rank": args.e2e, "store_build_s": round(t_build, 1),
-            "includes": "device collate of a random batch + CSR/compaction + fwd/NLL/bwd/clip/AdamW"}
+    return {"value": round(B * world * args.steps / dt, 2), "unit": "graphs/s",
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "batch": B, "dataset_graphs": args.e2e,
+            "dataset_graphs_per_rank": store.num_graphs,
+            "store_build_s": round(t_build, 1), "replayed_steps": trainer.rebinds - r0,
+            "eager_steps": trainer.rebind_misses - m0,
+            "includes": "device collate of a random batch + CSR/compaction/schedules (loader stream) + "
+                        "fwd/NLL/bwd/clip/AdamW (captured plan re-bound to the batch)"}
 
 
 def pmc_traffic(kernel_key):
@@ -366,9 +393,10 @@ def main():
     B = args.batch
     r = measure(args, dev, rank, world, B, args.lg_offset, args.precision, args.steps, args.warmup,
                 roofline=not args.no_roofline)
-    e2e = None
+    e2e, store = None, None
     if args.e2e > 0:
-        e2e = end_to_end(args, r["trainer"], dev, rank, world)
+        store, t_build = build_store(args, dev, rank)
+        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
     _release(r)
 
     # secondary lines of the default run (one GPU): the same step with the corrected line-graph
@@ -392,7 +420,11 @@ def main():
                           f"softmax/LayerNorm), lg_offset={args.lg_offset}",
                 "value": round(c3["value"], 2), "unit": "graphs/s", "ms_per_step": round(c3["ms_per_step"], 3),
                 "steps": sec_steps, "roofline": c3["roofline"], "step_roofline": c3["step_roofline"]}
+            if store is not None:
+                # config C5 at N = 1: the B = 256 bf16 step over the ~10k-graph HBM dataset
+                secondary["c5_e2e_b256_bf16"] = end_to_end(args, store, t_build, c3["trainer"], 256, dev, rank, world)
             _release(c3)
+    store = None
 
     if rank == 0:
         cpu = None

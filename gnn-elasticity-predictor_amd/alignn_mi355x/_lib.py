@@ -152,6 +152,8 @@ _SIGNATURES = {
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                           c_vp, c_vp], c_i32),
+    "alignn_adamw_f32_dev": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
+                              c_vp, c_vp], c_i32),
 }
 
 EXPORTED = tuple(_SIGNATURES.keys())

@@ -134,10 +134,12 @@ class BatchCache:
             a = la.contiguous().float()
             ld = (a.size(1) + 3) // 4 * 4
             buf = torch.empty(self.T, ld, device=a.device)
+            self._xa_buf = buf
             self.xa = buf[:, :a.size(1)]
             ops.gather_rows(a, self.lg.perm_dst[: self.T], self.xa)
         else:
             self.xa = None
+            self._xa_buf = None
         if hasattr(batch, "batch") and batch.batch is not None:
             self.batch_vec = batch.batch.to(torch.int64).contiguous()
         else:
@@ -149,6 +151,44 @@ class BatchCache:
             cnt = torch.bincount(self.batch_vec, minlength=B)
             self.ptr = torch.cat([cnt.new_zeros(1), cnt.cumsum(0)])
         self.B = int(self.ptr.numel() - 1)
+
+    # -------------------------------------------------------------------------------------------
+    # Re-binding a captured step to a new batch (FusedTrainer._rebind): a launch plan holds the
+    # device addresses of its batch and of this cache, and the sizes every launch was recorded
+    # with.  A new batch whose cache has the same signature (every size a recorded launch depends
+    # on: node/edge/triplet counts, the compacted line graph's size, the schedules' list lengths and
+    # flags) can be copied into the captured batch's buffers and the plan replayed unchanged.
+    # -------------------------------------------------------------------------------------------
+    @staticmethod
+    def _graph_sig(g: ops.GraphCSR):
+        sc = g.schedule()
+        return (g.n, g.m, g.n_full, g.rows is not None, int(sc.n_light), int(sc.n_heavy), int(sc.flags))
+
+    def signature(self):
+        return (self.N, self.E, self.T, self.B, self.angle_dim,
+                None if self._xa_buf is None else tuple(self._xa_buf.shape),
+                self._graph_sig(self.ag), self._graph_sig(self.lg),
+                tuple(self.batch_vec.shape), tuple(self.ptr.shape))
+
+    @staticmethod
+    def _graph_tensors(g: ops.GraphCSR):
+        g.schedule()
+        _, light, heavy = g._sched
+        return [g.off_dst, g.perm_dst, g.src_at, g.dst_at, g.off_src, g.pos_src, g.err, light, heavy, g.rows, g.cmap]
+
+    def device_tensors(self):
+        """Every device buffer of this cache, in a fixed order (None where absent)."""
+        return self._graph_tensors(self.ag) + self._graph_tensors(self.lg) + [self._xa_buf, self.batch_vec, self.ptr]
+
+    def copy_into(self, dst: "BatchCache") -> None:
+        """dst's buffers <- this cache's contents (same signature; stream-ordered device copies)."""
+        for a, b in zip(self.device_tensors(), dst.device_tensors()):
+            if (a is None) != (b is None):
+                raise ValueError("batch caches of different structure")
+            if a is not None and a.numel():
+                if a.shape != b.shape or a.dtype != b.dtype:
+                    raise ValueError(f"batch cache buffer {tuple(a.shape)} {a.dtype} vs {tuple(b.shape)} {b.dtype}")
+                b.copy_(a)
 
     # A line-graph node (bond) with neither in- nor out-edges contributes nothing to the attention
     # (empty segment, never a source).  Under PyG's lg_edge_index offset rule (SURVEY §0.3) most
@@ -173,6 +213,26 @@ class BatchCache:
         gc.n_full = n
         gc.cmap = cmap.to(torch.int32)
         return gc
+
+
+def prepare_batch(batch, stream: Optional[torch.cuda.Stream] = None, validate: bool = True) -> BatchCache:
+    """Builds the batch's device cache (CSR lists, line-graph compaction, schedules) on ``stream``
+    (default: the current one) and records an event there that a step on another stream waits
+    for (FusedTrainer.step): a loader can prepare batch i + 1 on its own stream while step i runs."""
+    if stream is None:
+        bc = batch_cache(batch, validate)
+        bc.signature()  # builds the schedules too
+    else:
+        with torch.cuda.stream(stream):
+            bc = batch_cache(batch, validate)
+            bc.signature()
+    ev = torch.cuda.Event()
+    ev.record(stream if stream is not None else torch.cuda.current_stream())
+    try:
+        batch._alignn_ready = ev
+    except AttributeError:
+        pass
+    return bc
 
 
 def batch_cache(batch, validate: bool = True) -> BatchCache:

@@ -877,11 +877,23 @@ def grad_norm(g: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 
 def adamw_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, split: int, lr0: float,
                lr1: float, weight_decay: float, betas=(0.9, 0.999), eps: float = 1e-8,
-               norm: Optional[torch.Tensor] = None, max_norm: float = 5.0, step: torch.Tensor = None) -> None:
+               norm: Optional[torch.Tensor] = None, max_norm: float = 5.0, step: torch.Tensor = None,
+               lr_dev: Optional[torch.Tensor] = None) -> None:
+    """lr_dev: device float64 [2] = (lr0, lr1) read by the kernel when it runs (lr0/lr1 ignored), so a
+    recorded plan follows learning-rate changes (alignn_adamw_f32_dev)."""
     for t, n in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _require(t, n)
         if not t.is_contiguous() or t.numel() != p.numel():
             raise ValueError(f"adamw_step: {n} must be contiguous with {p.numel()} elements")
+    if lr_dev is not None:
+        _require(lr_dev, "lr_dev", torch.float64)
+        if lr_dev.numel() != 2 or not lr_dev.is_contiguous():
+            raise ValueError("adamw_step: lr_dev must be a contiguous float64 tensor of 2 elements")
+        check(_lib.lib().alignn_adamw_f32_dev(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                                              int(split), lr_dev.data_ptr(), float(weight_decay), float(betas[0]),
+                                              float(betas[1]), float(eps), _p(norm), float(max_norm), step.data_ptr(),
+                                              stream_ptr()), "alignn_adamw_f32_dev")
+        return
     check(_lib.lib().alignn_adamw_f32(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), int(split),
                                       float(lr0), float(lr1), float(weight_decay), float(betas[0]), float(betas[1]),
                                       float(eps), _p(norm), float(max_norm), step.data_ptr(), stream_ptr()),

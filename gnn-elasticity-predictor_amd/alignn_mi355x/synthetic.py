@@ -13,6 +13,7 @@
 """
 from __future__ import annotations
 
+import functools
 import itertools
 from typing import List, Optional
 
@@ -45,15 +46,27 @@ def _line_graph(src: np.ndarray, dst: np.ndarray, img: Optional[np.ndarray] = No
     return np.asarray(s_list, dtype=np.int64), np.asarray(d_list, dtype=np.int64)
 
 
+@functools.lru_cache(maxsize=8)
+def _circulant(n_atoms: int, half_degree: int):
+    """Bond list of the circulant graph i -> i±1..±half_degree and its line graph in bond indices.
+    An atom permutation relabels atoms only: bond b stays bond b, b1 -> b2 is a line-graph edge iff
+    dst[b1] == src[b2] and dst[b2] != src[b1] (a bijection preserves both), and the out-bond lists
+    keep their order, so every MP-like graph has this same line graph (computed once)."""
+    offs = list(range(1, half_degree + 1)) + [-d for d in range(1, half_degree + 1)]
+    base_src = np.repeat(np.arange(n_atoms), len(offs))
+    base_dst = (base_src + np.tile(np.asarray(offs), n_atoms)) % n_atoms
+    lsrc, ldst = _line_graph(base_src, base_dst)
+    for a in (base_src, base_dst, lsrc, ldst):
+        a.setflags(write=False)
+    return base_src, base_dst, lsrc, ldst
+
+
 def mp_like_graph(g: int, node_dim: int = 206, edge_dim: int = 36, angle_dim: int = 11,
                   n_atoms: int = 60, half_degree: int = 6, target_dim: int = 2) -> Data:
     gen = torch.Generator().manual_seed(1234 + g)
     perm = torch.randperm(n_atoms, generator=gen).numpy()
-    offs = list(range(1, half_degree + 1)) + [-d for d in range(1, half_degree + 1)]
-    base_src = np.repeat(np.arange(n_atoms), len(offs))
-    base_dst = (base_src + np.tile(np.asarray(offs), n_atoms)) % n_atoms
+    base_src, base_dst, lsrc, ldst = _circulant(n_atoms, half_degree)
     src, dst = perm[base_src], perm[base_dst]
-    lsrc, ldst = _line_graph(src, dst)
     E, T = len(src), len(lsrc)
     sg = torch.zeros(SPACE_GROUPS, 1)
     sg[int(torch.randint(0, SPACE_GROUPS, (1,), generator=gen)), 0] = 1.0

@@ -17,6 +17,11 @@ from torch import nn
 from . import _lib, ops, profiling
 from ._lib import check
 from .engine import MIN_LOGVAR_FLOOR, batch_cache, site_seed
+
+# batch fields a recorded step reads (train.py:547-573, :648-650); a re-bound batch is copied into
+# the captured batch's buffers field by field
+BATCH_FIELDS = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y",
+                "batch", "ptr")
 from .model import HeteroAlignnRegressor
 from .synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS
 
@@ -69,6 +74,12 @@ class FusedTrainer:
         # this trainer's step runs in it, and a recorded plan owns it (its buffers never move)
         self.ctx = model._engine.ctx
         self.grad_hook = None  # called with the flat gradient between backward and clip (DP all_reduce)
+        # re-binding (step() on a batch other than the captured one): copy it into the captured
+        # batch's buffers and replay when its signature matches (BatchCache.signature), else eager
+        self.rebind = True
+        self.rebinds = 0
+        self.rebind_misses = 0
+        self.lr_dev = None
 
     def use_step_seed(self, t: Optional[torch.Tensor]) -> None:
         """Device int64[1] step seed the dropout/jitter kernels of this trainer mix in (None: host
@@ -78,9 +89,15 @@ class FusedTrainer:
         self.ctx.step_seed = t
 
     def set_lr(self, lr: float, sigma_lr: Optional[float] = None) -> None:
+        """The reference's per-epoch learning rate (train.py:1641-1652; cosine schedule :1215-1232).
+        The HIP optimizer reads the rates from a device scalar pair, so captured plans follow."""
         self.opt.param_groups[0]["lr"] = lr
         self.opt.param_groups[1]["lr"] = lr if sigma_lr is None else sigma_lr
         self.lr, self.sigma_lr = lr, (lr if sigma_lr is None else sigma_lr)
+        if self.lr_dev is not None:
+            # stream-ordered: steps already queued keep the old rates, later ones get the new
+            self.lr_dev.copy_(torch.tensor([float(self.lr), float(self.sigma_lr)], dtype=torch.float64),
+                              non_blocking=False)
 
     def forward_backward(self, batch, seed: int, training: bool = True,
                          sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -108,8 +125,9 @@ class FusedTrainer:
     def step(self, batch, seed: Optional[int] = None, sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         if seed is None:
             seed = int(torch.randint(0, 2**62, (1,)).item())
-        if self._graph is not None and self._graph[2] is batch and sample_weights is None:
-            return self._replay(seed)
+        if self._graph is not None and sample_weights is None:
+            if self._graph[2] is batch or (self.rebind and self._rebind(batch)):
+                return self._replay(seed)
         loss = self.forward_backward(batch, seed, sample_weights=sample_weights)
         if self.grad_hook is not None:
             self.grad_hook(self.st.grad)
@@ -117,14 +135,51 @@ class FusedTrainer:
         self.step_count += 1
         return loss
 
+    def _rebind(self, batch) -> bool:
+        """Copies ``batch`` into the captured batch's buffers (fields and device cache) when every
+        size the recorded launches depend on matches; False (nothing copied) otherwise.  A batch
+        prepared on another stream (engine.prepare_batch) is waited for by event."""
+        slot = self._graph[2]
+        for k in BATCH_FIELDS:
+            a, b = getattr(batch, k, None), getattr(slot, k, None)
+            if (a is None) != (b is None):
+                self.rebind_misses += 1
+                return False
+            if a is not None and (a.shape != b.shape or a.dtype != b.dtype or a.device != b.device):
+                self.rebind_misses += 1
+                return False
+        main = torch.cuda.current_stream(self.st.flat.device)
+        ready = getattr(batch, "_alignn_ready", None)
+        if ready is not None:
+            main.wait_event(ready)
+        bc_new, bc_slot = batch_cache(batch), batch_cache(slot)
+        if bc_new.signature() != bc_slot.signature():
+            self.rebind_misses += 1
+            return False
+        for k in BATCH_FIELDS:
+            a = getattr(batch, k, None)
+            if a is not None and a.numel():
+                getattr(slot, k).copy_(a)
+        bc_new.copy_into(bc_slot)
+        if ready is not None:
+            # buffers made on the loader's stream and read here: not reusable before these copies ran
+            for t in [getattr(batch, k, None) for k in BATCH_FIELDS] + bc_new.device_tensors():
+                if t is not None and t.is_cuda:
+                    t.record_stream(main)
+        self.rebinds += 1
+        return True
+
     def _clip_and_update(self) -> None:
         if self.optimizer == "hip":
             st = self.st
+            if self.lr_dev is None:
+                self.lr_dev = torch.tensor([float(self.lr), float(self.sigma_lr)], dtype=torch.float64,
+                                           device=st.flat.device)
             with ops.using(self.ctx):
                 ops.grad_norm(st.grad, self.gnorm)
                 ops.adamw_step(st.flat, st.grad, self.exp_avg, self.exp_avg_sq, st.P.sigma_start, self.lr,
                                self.sigma_lr, self.weight_decay, norm=self.gnorm, max_norm=self.max_norm,
-                               step=self.hip_step)
+                               step=self.hip_step, lr_dev=self.lr_dev)
             return
         torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
         self.opt.step()
@@ -143,7 +198,9 @@ class FusedTrainer:
     #     eager, the two streams' branches lose concurrency).
     # ``grad_hook`` (e.g. the data-parallel all_reduce) runs eagerly between the two phases.
     # Randomness stays per step: the kernels read a device step seed (ops.set_step_seed) that
-    # step() updates before each replay.  The learning rate is baked in at capture.
+    # step() updates before each replay.  The learning rates are a device pair (set_lr).
+    # A new batch of the same signature is copied into the captured batch (``_rebind``), so the
+    # reference's loop over fresh batches (train.py:639-711) replays the plan every step.
     # --------------------------------------------------------------------------------------------
     def capture(self, batch, mode: str = "plan") -> None:
         """Capture the training step on ``batch`` (which must stay alive with unchanged shapes; its
@@ -203,7 +260,7 @@ class FusedTrainer:
         ranges = []
         for t in _cuda_tensors((self.st.flat, self.st.grad, getattr(self, "exp_avg", None),
                                 getattr(self, "exp_avg_sq", None), getattr(self, "hip_step", None),
-                                getattr(self, "gnorm", None), self.loss, self.log_means, self.log_stds,
+                                getattr(self, "gnorm", None), self.lr_dev, self.loss, self.log_means, self.log_stds,
                                 self._seed_dev, self.ctx.tensors(), batch, list(self.model.buffers()))):
             s = t.untyped_storage()
             ranges.append((s.data_ptr(), s.data_ptr() + s.nbytes()))

@@ -50,11 +50,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
                                                     float* __restrict__ v, int64_t n, int64_t split, double lr0,
                                                     double lr1, double wd, double b1, double b2, float eps,
                                                     const float* __restrict__ norm, float max_norm,
-                                                    const float* __restrict__ step) {
+                                                    const float* __restrict__ step, const double* __restrict__ lr_dev) {
   // The reference's CPU AdamW (torch _single_tensor_adam, decoupled decay) forms its scalars as
   // Python doubles and rounds each to fp32 once where a tensor op consumes it: 1 - lr*wd, 1 - b1
   // (lerp weight), 1 - b2 (addcmul value), lr / (1 - b1^t), sqrt(1 - b2^t).  Same here.
   const double t = (double)*step;
+  if (lr_dev) {  // device-resident learning rates (a recorded plan follows the schedule)
+    lr0 = lr_dev[0];
+    lr1 = lr_dev[1];
+  }
   const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2), fb2 = (float)b2;
   const float bc2s = (float)sqrt(1.0 - pow(b2, t));
   const double bc1 = 1.0 - pow(b1, t);
@@ -91,16 +95,29 @@ extern "C" int alignn_grad_norm_f32(const float* g, int64_t n, float* norm, floa
   return ALIGNN_OK;
 }
 
-extern "C" int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, double lr0,
-                                double lr1, double weight_decay, double beta1, double beta2, double eps,
-                                const float* norm, float max_norm, float* step, void* stream) {
+static int adamw(float* p, float* g, float* m, float* v, int64_t n, int64_t split, double lr0, double lr1,
+                 const double* lr_dev, double weight_decay, double beta1, double beta2, double eps, const float* norm,
+                 float max_norm, float* step, void* stream) {
   if (n < 0 || split < 0 || split > n || !step) return ALIGNN_E_BAD_SHAPE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   launch(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   if (n > 0)
     launch(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, split, lr0, lr1,
-                       weight_decay, beta1, beta2, (float)eps, norm, max_norm, step);
+                       weight_decay, beta1, beta2, (float)eps, norm, max_norm, step, lr_dev);
   ALIGNN_LAUNCH_CHECK("adamw_kernel");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, double lr0,
+                                double lr1, double weight_decay, double beta1, double beta2, double eps,
+                                const float* norm, float max_norm, float* step, void* stream) {
+  return adamw(p, g, m, v, n, split, lr0, lr1, nullptr, weight_decay, beta1, beta2, eps, norm, max_norm, step, stream);
+}
+
+extern "C" int alignn_adamw_f32_dev(float* p, float* g, float* m, float* v, int64_t n, int64_t split,
+                                    const double* lr, double weight_decay, double beta1, double beta2, double eps,
+                                    const float* norm, float max_norm, float* step, void* stream) {
+  if (!lr) return ALIGNN_E_BAD_SHAPE;
+  return adamw(p, g, m, v, n, split, 0.0, 0.0, lr, weight_decay, beta1, beta2, eps, norm, max_norm, step, stream);
 }

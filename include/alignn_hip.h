@@ -413,6 +413,13 @@ int alignn_grad_norm_f32(const float* g, int64_t n, float* norm, float* workspac
 int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t split, double lr0, double lr1,
                      double weight_decay, double beta1, double beta2, double eps, const float* norm, float max_norm,
                      float* step, void* stream);
+/* alignn_adamw_f32_dev: the same update with the two groups' learning rates read from device memory
+ * (lr: double[2] = {lr0, lr1}) when the kernel runs, so a recorded launch plan follows the
+ * reference's per-epoch schedule (set_lr before each epoch, train.py:1641-1652, cosine :1215-1232)
+ * without being re-recorded. */
+int alignn_adamw_f32_dev(float* p, float* g, float* m, float* v, int64_t n, int64_t split, const double* lr,
+                         double weight_decay, double beta1, double beta2, double eps, const float* norm,
+                         float max_norm, float* step, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Batch assembly from a dataset resident in HBM (replaces PyG Collater /

@@ -141,3 +141,86 @@ def test_plan_ownership_check():
     finally:
         lib.alignn_plan_destroy(plan)
     torch.cuda.synchronize()
+
+
+def _twin_step(te, tp, b, s):
+    """Eager step of ``te`` on ``b`` with the device step seed ``tp``'s replay uses."""
+    te.use_step_seed(tp._seed_dev)
+    tp._seed_dev.fill_(s)
+    le = te.forward_backward(b, 0).clone()
+    te._clip_and_update()
+    return le
+
+
+def test_rebind_new_batches_replay_bitwise():
+    """A captured plan re-bound to fresh batches of the same signature (FusedTrainer._rebind: copied
+    into the captured batch) equals the eager step on each of them bit for bit — including batches
+    collated on the device from an HBM store and prepared on a loader stream (engine.prepare_batch),
+    as the reference's loop over fresh batches (train.py:639-711) runs at plan speed."""
+    import numpy as np
+    from alignn_mi355x import ops
+    from alignn_mi355x.data import Data
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_batch, mp_like_graph
+    _, te, _ = _setup(B=8)
+    _, tp, bp = _setup(B=8)
+    tp.capture(bp)
+    keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+    store = GraphStore.from_data_list([Data(**{k: getattr(mp_like_graph(100 + g), k) for k in keys})
+                                       for g in range(24)], DEV)
+    loader = torch.cuda.Stream()
+    rng = np.random.default_rng(5)
+    batches = [mp_like_batch(8, first=40).to(DEV)]
+    for _ in range(3):
+        with torch.cuda.stream(loader):
+            b = store.collate(rng.choice(24, size=8, replace=False))
+        prepare_batch(b, loader)
+        batches.append(b)
+    for i, b in enumerate(batches):
+        s = 31 + i
+        lp = tp.step(b, seed=s).clone()
+        le = _twin_step(te, tp, b, s)
+        torch.cuda.synchronize()
+        assert torch.equal(le, lp), i
+        assert torch.equal(te.st.grad, tp.st.grad), i
+        assert torch.equal(te.st.flat, tp.st.flat), i
+    assert tp.rebinds == len(batches) and tp.rebind_misses == 0
+    # a batch of another signature runs eagerly (nothing copied) and is still the eager step
+    b3 = mp_like_batch(3, first=7).to(DEV)
+    tp._seed_dev.fill_(0)   # the eager path mixes the host seed with the device one, as the twin does
+    lp = tp.step(b3, seed=50).clone()
+    te.use_step_seed(tp._seed_dev)
+    le = te.forward_backward(b3, 50).clone()
+    te._clip_and_update()
+    torch.cuda.synchronize()
+    assert tp.rebind_misses == 1
+    assert torch.equal(le, lp) and torch.equal(te.st.flat, tp.st.flat)
+    tp.release_capture()
+    ops.set_step_seed(None)
+
+
+def test_set_lr_reaches_a_captured_plan():
+    """Learning rates are a device pair read by the AdamW kernel: set_lr after capture changes the
+    replayed update exactly as it changes the eager one (no re-capture; train.py:1641-1652)."""
+    from alignn_mi355x import ops
+    _, te, b1 = _setup()
+    _, tp, b2 = _setup()
+    tp.capture(b2)
+    for i, lr in enumerate((3e-4, 1e-3, 5e-5)):
+        te.set_lr(lr, lr / 3)
+        tp.set_lr(lr, lr / 3)
+        lp = tp.step(b2, seed=60 + i).clone()
+        le = _twin_step(te, tp, b1, 60 + i)
+        torch.cuda.synchronize()
+        assert torch.equal(le, lp) and torch.equal(te.st.flat, tp.st.flat), i
+    # and it matters: a different rate gives different parameters
+    flat = tp.st.flat.clone()
+    tp.set_lr(1e-2)
+    tp.step(b2, seed=70)
+    te.set_lr(1e-3)
+    _twin_step(te, tp, b1, 70)
+    torch.cuda.synchronize()
+    assert not torch.equal(te.st.flat, tp.st.flat) and not torch.equal(flat, tp.st.flat)
+    tp.release_capture()
+    ops.set_step_seed(None)

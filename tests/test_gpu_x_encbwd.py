@@ -2,7 +2,10 @@
 angle encoder's first Linear + ReLU, train.py:358-364, as reached from every EdgeUpdateBlock):
 kernel vs an fp64 restatement on random line graphs (ragged and empty segments, target changes
 inside a chunk, H*L = 1..16, kin 1..16), accumulate mode and determinism; then the engine with
-``defer_angle_bwd`` on vs off (only the W1/b1 gradients may differ, by summation order)."""
+``defer_angle_bwd`` on vs off: same loss bitwise, W1/b1 gradients equal up to summation order.  The
+other gradients agree to fp32 rounding, not bitwise: without deferral the line-graph ``bwd_dst``
+writes the [T, D] edge-feature gradient, which the single-wave-item kernels (lgconv.hip) do not, so
+that configuration takes the tconv.hip kernel family, whose dQ/Sz sums run in another order."""
 import pytest
 import torch
 
@@ -109,7 +112,13 @@ def test_engine_deferred_angle_backward(lg_offset):
     sl = [slice(o_w, o_w + w1.numel()), slice(o_b, o_b + b1.numel())]
     for s_ in sl:
         assert _rel(g1[s_], g0[s_]) < 1e-5
-    mask = torch.ones_like(g0, dtype=torch.bool)
-    for s_ in sl:
-        mask[s_] = False
-    assert torch.equal(g0[mask], g1[mask])
+    # per-parameter normwise agreement (different attention kernel families, see the module doc);
+    # the key-bias gradients are exactly 0 in exact arithmetic (softmax is shift-invariant), so they
+    # are held to a floor of 1e-6 of the whole gradient's norm
+    floor = 1e-6 * float(g0.double().norm())
+    for name, view in st.P.named.items():
+        o = view.storage_offset() - st.flat.storage_offset()
+        a, b = g1[o:o + view.numel()].double(), g0[o:o + view.numel()].double()
+        if o == o_w or o == o_b:
+            continue
+        assert float((a - b).norm()) / max(float(b.norm()), floor) < 1e-5, name

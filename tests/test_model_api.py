@@ -98,3 +98,16 @@ def test_tconv_host_shape_checks_reject_undersized_operands():
         ops._check_tconv(g, D, H, ok["QKVR"], None, None, None)                    # no edge features
     with pytest.raises(ValueError):
         ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None, None, edge_heads=(torch.zeros(40, 3),))
+
+
+def test_mp_like_line_graph_is_the_per_graph_construction():
+    """synthetic._circulant computes the line graph once: it equals the per-graph construction
+    (fetch.py:419-447 order) on the permuted bond list for any seed (SURVEY §8d generator)."""
+    import numpy as np
+    from alignn_mi355x import synthetic as S
+    for g in (0, 3, 1234):
+        d = mp_like_graph(g)
+        src, dst = d.edge_index.numpy()
+        ls, ld = S._line_graph(src, dst)
+        assert np.array_equal(ls, d.lg_edge_index[0].numpy()) and np.array_equal(ld, d.lg_edge_index[1].numpy())
+        assert d.lg_edge_index.size(1) == 7920 and d.edge_index.size(1) == 720

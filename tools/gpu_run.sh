@@ -13,14 +13,14 @@ for step in "$@"; do
     tests-all) cmd=(timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider) ;;
     smoke) cmd=(timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()") ;;
     bench) cmd=(timeout -k 10 600 python bench.py --steps 20 --warmup 5) ;;
-    bench-quick) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary) ;;
-    bench-bf16) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --precision bf16) ;;
-    bench-b256) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --batch 256 --precision bf16) ;;
-    bench-e2e) cmd=(timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 2048) ;;
-    probes) cmd=(timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-secondary --dump-probes gpurun_out/probes.json) ;;
-    rocprof) cmd=(timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary) ;;
-    pmc-fetch) cmd=(timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary --no-roofline) ;;
-    pmc-write) cmd=(timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary --no-roofline) ;;
+    bench-quick) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --e2e 0) ;;
+    bench-bf16) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --precision bf16 --e2e 0) ;;
+    bench-b256) cmd=(timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --batch 256 --precision bf16 --e2e 0) ;;
+    bench-e2e) cmd=(timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 10000) ;;
+    probes) cmd=(timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-secondary --dump-probes gpurun_out/probes.json --e2e 0) ;;
+    rocprof) cmd=(timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --e2e 0) ;;
+    pmc-fetch) cmd=(timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary --no-roofline --e2e 0) ;;
+    pmc-write) cmd=(timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary --no-roofline --e2e 0) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "=== $step: ${cmd[*]}" | tee -a gpurun_out/run.log
