@@ -94,6 +94,9 @@ def apply_settings(args, model):
             ops.GraphCSR.HEAVY_THRESHOLD = int(v)
         elif k == "main_priority":
             args.main_priority = int(v)
+        elif k == "splitk_combine":
+            ops.SPLITK_COMBINE = int(v) > 0
+            ops.SPLITK_COMBINE_MAX = int(v)
         else:
             raise ValueError(f"unknown --set key {k}")
     return kw

@@ -38,7 +38,7 @@ class GemmArgs(ctypes.Structure):
         ("relu", c_i32), ("split_k", c_i32),
         ("workspace", c_vp), ("workspace_elems", c_i64),
         ("reduce_batch", c_i32), ("tile", c_i32),
-        ("c_rows", c_vp),
+        ("c_rows", c_vp), ("counters", c_vp),
     ]
 
 
@@ -75,6 +75,7 @@ _SIGNATURES = {
     "alignn_set_step_seed": ([c_vp], None),
     "alignn_gemm_f32": ([ctypes.POINTER(GemmArgs), c_vp], c_i32),
     "alignn_gemm_workspace": ([ctypes.POINTER(GemmArgs)], c_i64),
+    "alignn_gemm_counters": ([ctypes.POINTER(GemmArgs)], c_i64),
     "alignn_colsum_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
     "alignn_wcolsum2_f32": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
                              c_vp], c_i32),

@@ -89,7 +89,7 @@ class ExecContext:
             return "aux"
         return "main"
 
-    def _take(self, k, n: int, device, dtype) -> torch.Tensor:
+    def _take(self, k, n: int, device, dtype, zeroed: bool = False) -> torch.Tensor:
         cur = self.buf.get(k)
         if cur is None or cur.numel() < n:
             if _RECORDING:
@@ -97,14 +97,16 @@ class ExecContext:
                     f"workspace {k[0]!r} ({self.name}) would grow to {n} elements while a launch plan is being "
                     f"recorded (earlier recorded launches hold the old buffer): run an uncaptured step of the same "
                     f"shapes first")
-            cur = torch.empty(max(n, 1), device=device, dtype=dtype)
+            cur = (torch.zeros if zeroed else torch.empty)(max(n, 1), device=device, dtype=dtype)
             self.buf[k] = cur
         return cur
 
-    def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
+    def get(self, key: str, n: int, device, dtype=torch.float32, zeroed: bool = False) -> torch.Tensor:
+        """zeroed: a buffer created (or grown) here starts as zeros — for state the kernels keep zero
+        between calls themselves (the split-K tile tickets)."""
         if _RECORDING and not self.owned:
             raise RuntimeError("launch-plan recording needs an engine-owned execution context (ops.using)")
-        return self._take((key, _dkey(device), dtype, self._role(device)), n, device, dtype)
+        return self._take((key, _dkey(device), dtype, self._role(device)), n, device, dtype, zeroed)
 
     def fresh(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
         if not self.owned:   # shared default context: a new allocation (eager use only)
@@ -171,8 +173,8 @@ def aux_stream(device) -> torch.cuda.Stream:
 class _WSProxy:
     """``WS.get`` = the current context's workspace (kept for the tools/ scripts)."""
 
-    def get(self, key: str, n: int, device, dtype=torch.float32) -> torch.Tensor:
-        return current().get(key, n, device, dtype)
+    def get(self, key: str, n: int, device, dtype=torch.float32, zeroed: bool = False) -> torch.Tensor:
+        return current().get(key, n, device, dtype, zeroed)
 
 
 WS = _WSProxy()
@@ -228,6 +230,14 @@ _GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
 GEMM_STAGE = 0        # ALIGNN_GEMM_BK32 (16) / ALIGNN_GEMM_BK64 (128): K stage depth of every planned GEMM
 GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
+# split-K partials combined inside the GEMM launch by each tile's last workgroup (AlignnGemmArgs.counters)
+# instead of a separate reduce launch: same bits, one launch fewer per split product (option, off).
+# Measured on the B = 32 step (profiles/r02/v9_ab_splitk_combine.log): every split product combined
+# in-launch 6,930 vs 8,655 graphs/s (the last workgroup reads split x 16 KB serially); only products of
+# <= 2 / <= 4 splits 8,320 / 8,205 vs 8,617 (the agent-scope release/acquire per tile costs more than
+# the reduce launch it saves).
+SPLITK_COMBINE = False
+SPLITK_COMBINE_MAX = 2
 
 
 @contextmanager
@@ -308,6 +318,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if need > 0:
         ws = WS.get("gemm", need, C.device)
         a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
+        split = need // max(1, (1 if a.reduce_batch else batch) * M * N)
+        if SPLITK_COMBINE and split <= SPLITK_COMBINE_MAX:
+            cn = int(_lib.lib().alignn_gemm_counters(ctypes.byref(a)))
+            if cn > 0:
+                a.counters = WS.get("gemm_tickets", cn, C.device, torch.int32, zeroed=True).data_ptr()
     if GEMM_TRACE is not None:   # tuning hook (tools/gemm_bench.py): record the call's operands
         GEMM_TRACE.append(dict(A=A, B=B, C=C, alpha=alpha, beta=beta, bias=bias, rowscale=rowscale, bias2=bias2,
                                relu=relu, mask=mask, reduce_batch=reduce_batch, c_rows=c_rows))

@@ -68,6 +68,11 @@ typedef struct AlignnGemmArgs {
                              + ALIGNN_GEMM_BK32 / BK16 / BK64 (stage depth), + ALIGNN_GEMM_BF16 */
   const int32_t* c_rows;  /* optional: logical row r of C is stored at row c_rows[r] (scatter; beta
                              reads the same row).  bias/rowscale/mask stay indexed by r. */
+  int32_t* counters;      /* optional, split-K only: alignn_gemm_counters(args) int32 tile tickets, all
+                             ZERO before the first call (every call leaves them zero again).  Given,
+                             the split partials are combined inside the GEMM launch by each tile's
+                             last-arriving workgroup (fixed summation order, the separate reduce's);
+                             NULL: a separate reduce launch.  Same result bits either way. */
 } AlignnGemmArgs;
 
 #define ALIGNN_GEMM_BK32 16
@@ -87,6 +92,9 @@ int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 /* Workspace floats alignn_gemm_f32 needs for these arguments (split_k = 0: the automatic plan on
  * the current device); 0 when no split is used, -1 for invalid shapes. */
 int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
+/* int32 tile tickets (AlignnGemmArgs.counters) the in-launch split-K combine needs: 0 when the plan
+ * does not split K. */
+int64_t alignn_gemm_counters(const AlignnGemmArgs* args);
 
 /* ----------------------------------------------------------------------------------------
  * Skinny products (skinny.hip), streamed at HBM rate: the angle encoder's first Linear over the
