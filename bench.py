@@ -63,6 +63,12 @@ def parse():
                         "plan and re-issued from C++ (plan.hip; the roofline probe is a pair of plan timestamps "
                         "in every replay); graph: ROCm HIP graphs of the same capture")
     p.add_argument("--graph", action="store_true", help="alias of --launch graph")
+    p.add_argument("--ensemble", type=int, default=0, metavar="MEMBERS",
+                   help="config C4: train an ensemble of this many members instead (member i on rank i %% world, "
+                        "seed +1007 i, fold i %% 5 — train.py:2052-2095 — no per-step communication; several "
+                        "members on one GPU run concurrently on their own streams), B = --batch graphs each; then "
+                        "one gather of every member's heads on an eval batch to rank 0 for the moment mix")
+    p.add_argument("--seed", type=int, default=42, help="base seed of the ensemble members (train.py --seed)")
     p.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
                    help="engine option (engine.<attr>=0/1), trainer optimizer (optimizer=hip) or GEMM stage "
                         "(gemm_stage=16|32|64); repeatable — for measuring opt-in paths")
@@ -363,6 +369,71 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
             "step_roofline": step_roof, "trainer": trainer, "batch": batch}
 
 
+def ensemble_bench(args, dev, rank, world):
+    """Config C4: ensemble training sharded member-per-rank.  The reference trains its
+    members one after the other (train.py:2052-2095); here every rank trains its members
+    (dp.members_of_rank) at the same time — each member a captured step on its own stream — with no
+    communication until the final gather of the members' heads for the moment mix.  Timed like the
+    headline (barrier + synchronize, max over ranks); value = members x B x steps / time."""
+    import alignn_mi355x as A
+    from alignn_mi355x import dp
+    from alignn_mi355x.ensemble import EnsemblePredictor, ShardedEnsemble
+    from alignn_mi355x.synthetic import mp_like_batch
+
+    M, B = args.ensemble, args.batch
+    mine = dp.members_of_rank(M, world, rank)
+    members = []
+    for i in mine:
+        torch.manual_seed(dp.member_seed(args.seed, i))          # train.py:2053 (weights per member)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
+                                                          args.dropout), 2).to(dev)
+        tr = A.FusedTrainer(model, precision=args.precision, **apply_settings(args, model))
+        # the member's own graphs (fold i % 5 of the dataset, train.py:2054): a disjoint synthetic slice
+        batch = mp_like_batch(B, first=100000 * (1 + dp.member_fold(i, 5)) + 1000 * i, lg_offset=args.lg_offset).to(dev)
+        tr.capture(batch)
+        stream = torch.cuda.Stream(device=dev)
+        members.append((i, model, tr, batch, stream))
+
+    def step(k):
+        for i, _, tr, batch, stream in members:
+            stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(stream):
+                tr.step(batch, seed=dp.member_seed(args.seed, i) * 1000003 + k)
+        for *_, stream in members:
+            torch.cuda.current_stream(dev).wait_stream(stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dt = dp.max_over_ranks(dt, dev)
+    # the members' eval pass: heads of every member on one batch, gathered to rank 0, moment mix
+    for _, model, tr, _, _ in members:
+        tr.release_capture()
+        model.eval()
+    eval_batch = mp_like_batch(B, first=900000, lg_offset=args.lg_offset).to(dev)
+    models = [m for _, m, *_ in members]
+    t1 = time.perf_counter()
+    if world > 1:
+        mixed = ShardedEnsemble(models, M, hidden=args.hidden).predict_batch(eval_batch)
+    else:
+        mixed = EnsemblePredictor(models).predict_batch(eval_batch)
+    torch.cuda.synchronize()
+    t_eval = time.perf_counter() - t1
+    ok = None if mixed is None else bool(torch.isfinite(mixed["mean_z"]).all() and torch.isfinite(mixed["std_z"]).all())
+    return {"value": M * B * args.steps / dt, "dt": dt, "ms_per_step": dt / args.steps * 1e3,
+            "members_per_rank": len(mine), "eval_ms": round(t_eval * 1e3, 2), "eval_finite": ok}
+
+
 def _release(r):
     tr = r.pop("trainer", None)
     r.pop("batch", None)
@@ -394,6 +465,25 @@ def main():
         torch.cuda.set_stream(hi)
 
     B = args.batch
+    if args.ensemble > 0:
+        r = ensemble_bench(args, dev, rank, world)
+        if rank == 0:
+            print(json.dumps({
+                "metric": METRIC, "value": round(r["value"], 2), "unit": "graphs/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["ms_per_step"], 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32" if args.precision == "fp32" else "bf16-gemm/f32", "data": "synthetic",
+                "config": {"workload": f"BASELINE config 4: {args.ensemble}-member ensemble training, B={B} synthetic "
+                                       f"MP-like graphs per member per step, full ALIGNN D={args.hidden} H={args.heads} "
+                                       f"L={args.layers}, fwd+NLL+bwd+clip+AdamW per member",
+                           "global_batch": B * args.ensemble, "parallelism": f"ensemble member-per-rank over {world}",
+                           "members_per_rank_0": r["members_per_rank"], "precision": args.precision,
+                           "lg_offset": args.lg_offset, "launch": "native_plan (one stream per member)"},
+                "ensemble_eval": {"gather_and_mix_ms": r["eval_ms"], "finite": r["eval_finite"]}}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     r = measure(args, dev, rank, world, B, args.lg_offset, args.precision, args.steps, args.warmup,
                 roofline=not args.no_roofline)
     e2e, store = None, None
