@@ -94,6 +94,8 @@ def apply_settings(args, model):
             kw["optimizer"] = v
         elif k == "wave_items":
             ops.GraphCSR.WAVE_ITEMS = bool(int(v))
+        elif k == "xcd_items":
+            ops.GraphCSR.XCD_ITEMS = bool(int(v))
         elif k == "sort_by_degree":
             ops.GraphCSR.SORT_BY_DEGREE = bool(int(v))
         elif k == "heavy_threshold":

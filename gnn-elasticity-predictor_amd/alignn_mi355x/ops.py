@@ -490,6 +490,14 @@ class GraphCSR:
     # every target a single-wave work item, longest in-edge list first (lgconv.hip, the D = 256
     # materialised-F line-graph kernels; other calls keep the kernels above)
     WAVE_ITEMS = True
+    # work items interleaved so that XCD x (workgroup i runs on XCD i % 8) walks the x-th contiguous
+    # eighth of the target ids, longest first within it: a target's sources lie near it (PyG's
+    # per-graph index windows), so each XCD's L2 holds the K/V rows its gathers need.  Measured
+    # (profiles/r02/v13_ab_xcd_items_rejected.log): line-graph bwd_dst fetch 588 -> 300 MB per launch
+    # (the K/V gathers hit L2), yet the kernels slow down (103 -> 128 us) and the step by 5 %: they
+    # are issue-bound (SQ counters, v12_pmc_sq_mix.json), not traffic-bound.  Off.
+    XCD_ITEMS = False
+    XCDS = 8
 
     def __init__(self, edge_index: torch.Tensor, n: int):
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
@@ -535,6 +543,18 @@ class GraphCSR:
                 # each node is still one wave's work, so results do not change
                 lit = lit[torch.sort(deg[lit.long()], descending=True, stable=True).indices]
                 hv = hv[torch.sort(deg[hv.long()], descending=True, stable=True).indices]
+            if self.XCD_ITEMS and self.WAVE_ITEMS and lit.numel() > self.XCDS:
+                # contiguous target ranges per XCD, LPT order inside each, interleaved i % XCDS
+                bounds = [self.n * x // self.XCDS for x in range(self.XCDS + 1)]
+                parts = []
+                for x in range(self.XCDS):
+                    sel = lit[(lit >= bounds[x]) & (lit < bounds[x + 1])]
+                    parts.append(sel[torch.sort(deg[sel.long()], descending=True, stable=True).indices].tolist())
+                order, j = [], 0
+                while any(j < len(q) for q in parts):
+                    order += [q[j] for q in parts if j < len(q)]
+                    j += 1
+                lit = torch.tensor(order, dtype=torch.int32)
             light = torch.cat([lit, idx[light_mask & (deg == 0)]]).to(self.off_dst.device)
             heavy = hv.to(self.off_dst.device)
             sc = _lib.Schedule()
