@@ -253,7 +253,7 @@ def _roofline(summ, dominant, mfma_peak, probe_src):
     if s["flops_per_launch"] > 0:
         ach = s["flops_per_launch"] / avg_s / 1e12
         return {"bound": "mfma", "achieved": round(ach, 2), "peak": mfma_peak, "unit": "TFLOP/s",
-                "frac": round(ach / mfma_peak, 4), "traffic": None, "kernel": dominant,
+                "frac": round(ach / mfma_peak, 4), "traffic": pmc_traffic(dominant), "kernel": dominant,
                 "avg_us": round(s["avg_ms"] * 1e3, 2), "launches": s["count"],
                 "flops_per_launch": s["flops_per_launch"], "timing": probe_src}
     ach = s["bytes_per_launch"] / avg_s / 1e9
