@@ -215,11 +215,16 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    host_step = host_make = 0.0
     t0 = time.perf_counter()
     for i in range(args.steps):
         cur = nxt
+        ta = time.perf_counter()
         trainer.step(cur, seed=7919 * rank + args.warmup + i)
+        tb = time.perf_counter()
         nxt = make()
+        host_step += tb - ta
+        host_make += time.perf_counter() - tb
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -230,6 +235,8 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
             "ms_per_step": round(dt / args.steps * 1e3, 3), "batch": B, "dataset_graphs": args.e2e,
             "dataset_graphs_per_rank": store.num_graphs,
             "store_build_s": round(t_build, 1), "replayed_steps": trainer.rebinds - r0,
+            "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
+                                 "collate_and_prepare": round(host_make / args.steps * 1e3, 3)},
             "eager_steps": trainer.rebind_misses - m0,
             "includes": "device collate of a random batch + CSR/compaction/schedules (loader stream) + "
                         "fwd/NLL/bwd/clip/AdamW (captured plan re-bound to the batch)"}

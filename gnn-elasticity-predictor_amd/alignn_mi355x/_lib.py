@@ -75,6 +75,7 @@ _SIGNATURES = {
     "alignn_set_step_seed": ([c_vp], None),
     "alignn_gemm_f32": ([ctypes.POINTER(GemmArgs), c_vp], c_i32),
     "alignn_gemm_workspace": ([ctypes.POINTER(GemmArgs)], c_i64),
+    "alignn_copy_many": ([c_i32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_gemm_counters": ([ctypes.POINTER(GemmArgs)], c_i64),
     "alignn_colsum_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
     "alignn_wcolsum2_f32": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,

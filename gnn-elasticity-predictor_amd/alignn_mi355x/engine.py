@@ -180,15 +180,21 @@ class BatchCache:
         """Every device buffer of this cache, in a fixed order (None where absent)."""
         return self._graph_tensors(self.ag) + self._graph_tensors(self.lg) + [self._xa_buf, self.batch_vec, self.ptr]
 
-    def copy_into(self, dst: "BatchCache") -> None:
-        """dst's buffers <- this cache's contents (same signature; stream-ordered device copies)."""
+    def copy_pairs(self, dst: "BatchCache"):
+        """(dst buffer, this cache's buffer) pairs for a copy into ``dst`` (same signature)."""
+        pairs = []
         for a, b in zip(self.device_tensors(), dst.device_tensors()):
             if (a is None) != (b is None):
                 raise ValueError("batch caches of different structure")
             if a is not None and a.numel():
                 if a.shape != b.shape or a.dtype != b.dtype:
                     raise ValueError(f"batch cache buffer {tuple(a.shape)} {a.dtype} vs {tuple(b.shape)} {b.dtype}")
-                b.copy_(a)
+                pairs.append((b, a))
+        return pairs
+
+    def copy_into(self, dst: "BatchCache") -> None:
+        """dst's buffers <- this cache's contents (same signature; stream-ordered device copies)."""
+        ops.copy_many(self.copy_pairs(dst))
 
     # A line-graph node (bond) with neither in- nor out-edges contributes nothing to the attention
     # (empty segment, never a source).  Under PyG's lg_edge_index offset rule (SURVEY §0.3) most

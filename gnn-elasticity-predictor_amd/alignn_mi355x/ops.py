@@ -210,6 +210,31 @@ def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
     return dst
 
 
+def copy_many(pairs) -> None:
+    """dst.copy_(src) for each (dst, src) pair of same-shape, same-dtype tensors, in one library
+    launch per 32 pairs (alignn_copy_many); pairs the kernel cannot take (non-contiguous, misaligned,
+    sizes not a multiple of 4 bytes) go through torch's copy."""
+    todo = []
+    for dst, src in pairs:
+        if dst.shape != src.shape or dst.dtype != src.dtype:
+            raise ValueError(f"copy_many: {tuple(src.shape)} {src.dtype} into {tuple(dst.shape)} {dst.dtype}")
+        nb = src.numel() * src.element_size()
+        if nb == 0:
+            continue
+        if (dst.is_contiguous() and src.is_contiguous() and nb % 4 == 0 and dst.data_ptr() % 16 == 0
+                and src.data_ptr() % 16 == 0 and dst.is_cuda and src.is_cuda):
+            todo.append((dst.data_ptr(), src.data_ptr(), nb))
+        else:
+            dst.copy_(src)
+    for i in range(0, len(todo), 32):
+        chunk = todo[i:i + 32]
+        n = len(chunk)
+        d = (ctypes.c_void_p * n)(*[c[0] for c in chunk])
+        s_ = (ctypes.c_void_p * n)(*[c[1] for c in chunk])
+        b = (ctypes.c_int64 * n)(*[c[2] for c in chunk])
+        check(_lib.lib().alignn_copy_many(n, s_, d, b, stream_ptr()), "alignn_copy_many")
+
+
 def clone(src: torch.Tensor) -> torch.Tensor:
     return copy_(torch.empty_like(src, memory_format=torch.contiguous_format), src.contiguous())
 

@@ -156,11 +156,9 @@ class FusedTrainer:
         if bc_new.signature() != bc_slot.signature():
             self.rebind_misses += 1
             return False
-        for k in BATCH_FIELDS:
-            a = getattr(batch, k, None)
-            if a is not None and a.numel():
-                getattr(slot, k).copy_(a)
-        bc_new.copy_into(bc_slot)
+        pairs = [(getattr(slot, k), getattr(batch, k)) for k in BATCH_FIELDS
+                 if getattr(batch, k, None) is not None and getattr(batch, k).numel()]
+        ops.copy_many(pairs + bc_new.copy_pairs(bc_slot))   # one launch for the batch and its cache
         if ready is not None:
             # buffers made on the loader's stream and read here: not reusable before these copies ran
             for t in [getattr(batch, k, None) for k in BATCH_FIELDS] + bc_new.device_tensors():

@@ -5,9 +5,40 @@
 // row ranges, and a batch is a set of segmented copies.  Index fields (edge_index, lg_edge_index:
 // two rows each) get the per-graph increment added — the caller passes PyG's increments, including
 // the lg_edge_index-by-num_nodes rule, so the batch is bit-identical to PyG's.
+#include <cstring>
+
 #include "common.h"
 
 namespace alignn {
+
+// Up to kCopyMany device-to-device copies in one launch (re-binding a captured step to a new batch:
+// the batch's fields and its device cache, FusedTrainer._rebind).  The list travels as a kernel
+// argument, so the launch needs no upload.  Workgroups stride over the concatenated 16-byte units.
+constexpr int kCopyMany = 32;
+struct CopyList {
+  const unsigned char* src[kCopyMany];
+  unsigned char* dst[kCopyMany];
+  int64_t units[kCopyMany + 1];  // exclusive prefix sums of 16-byte units per copy (last one may be partial)
+  int64_t bytes[kCopyMany];
+  int32_t n;
+  int32_t pad_;
+};
+
+__global__ __launch_bounds__(256) void copy_many_kernel(CopyList L) {
+  const int64_t total = L.units[L.n];
+  int c = 0;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < total; u += (int64_t)gridDim.x * blockDim.x) {
+    while (u >= L.units[c + 1]) ++c;  // units ascend along a thread's grid-stride walk
+    const int64_t o = (u - L.units[c]) * 16;
+    const int64_t left = L.bytes[c] - o;
+    if (left >= 16) {
+      *reinterpret_cast<uint4*>(L.dst[c] + o) = *reinterpret_cast<const uint4*>(L.src[c] + o);
+    } else {  // the copy's last, partial unit: 4-byte words
+      for (int64_t w = 0; w < left; w += 4)
+        *reinterpret_cast<uint32_t*>(L.dst[c] + o + w) = *reinterpret_cast<const uint32_t*>(L.src[c] + o + w);
+    }
+  }
+}
 
 // grid (chunks, G): graph g's segment [src_start[g], +count[g]) * width -> [dst_start[g], ...)
 __global__ void collate_rows_kernel(const float* __restrict__ src, int64_t width, const int64_t* __restrict__ src_start,
@@ -86,5 +117,31 @@ extern "C" int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, cons
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   launch(collate_batchvec_kernel, seg_grid(max_count, G), dim3(256), 0, s, dst_start, count, batch);
   ALIGNN_LAUNCH_CHECK("collate_batchvec_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_copy_many(int32_t n, const void* const* src, void* const* dst, const int64_t* bytes, void* stream) {
+  if (n < 0 || n > kCopyMany || (n > 0 && (!src || !dst || !bytes))) {
+    set_error("copy_many: 0..%d copies, host arrays of pointers and sizes", kCopyMany);
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  CopyList L;
+  memset(&L, 0, sizeof L);  // defined padding bytes (plan.hip scans recorded struct words)
+  L.n = n;
+  for (int i = 0; i < n; ++i) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src[i]), b = reinterpret_cast<uintptr_t>(dst[i]);
+    if (bytes[i] < 0 || bytes[i] % 4 || (bytes[i] && (!src[i] || !dst[i] || (a & 15) || (b & 15)))) {
+      set_error("copy_many: copy %d needs 16-byte aligned pointers and a multiple of 4 bytes", i);
+      return ALIGNN_E_BAD_SHAPE;
+    }
+    L.src[i] = static_cast<const unsigned char*>(src[i]);
+    L.dst[i] = static_cast<unsigned char*>(dst[i]);
+    L.bytes[i] = bytes[i];
+    L.units[i + 1] = L.units[i] + (bytes[i] + 15) / 16;
+  }
+  if (L.units[n] == 0) return ALIGNN_OK;
+  const int64_t blocks = std::min<int64_t>((L.units[n] + 255) / 256, 2048);
+  launch(copy_many_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), L);
+  ALIGNN_LAUNCH_CHECK("copy_many_kernel");
   return ALIGNN_OK;
 }

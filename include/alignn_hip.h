@@ -447,6 +447,10 @@ int alignn_collate_index_i64(int32_t G, const int64_t* src, int64_t src_ld, cons
                              int64_t* dst, int64_t dst_ld, void* stream);
 int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, const int64_t* count, int64_t max_count,
                             int64_t* batch, void* stream);
+/* Up to 32 device-to-device copies in one launch (src, dst: HOST arrays of device pointers, 16-byte
+ * aligned; bytes: host array, multiples of 4).  Re-binds a captured step to a new batch (the batch
+ * fields and its CSR / compaction / schedule cache copied into the captured buffers). */
+int alignn_copy_many(int32_t n, const void* const* src, void* const* dst, const int64_t* bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * KNN density weights over graph embeddings (compute_global_knn_weights,

@@ -51,3 +51,28 @@ def test_train_step_on_store_batch_equals_host_batch():
         grads.append(tr.st.grad.clone())
     torch.cuda.synchronize()
     assert torch.equal(grads[0], grads[1])
+
+
+def test_copy_many_one_launch_matches_torch_copies():
+    """alignn_copy_many (re-binding a captured step: batch fields + device cache in one launch):
+    mixed dtypes, sizes with a partial last 16-byte unit, more than 32 pairs (two launches), and
+    pairs the kernel does not take (non-contiguous) through torch's copy."""
+    import torch
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(3)
+    pairs, refs = [], []
+    for i in range(45):
+        n = int(torch.randint(1, 5000, (1,), generator=g))
+        dt = (torch.float32, torch.int32, torch.int64)[i % 3]
+        src = (torch.randn(n, generator=g) * 1000).to(dt).to("cuda")
+        dst = torch.zeros_like(src)
+        pairs.append((dst, src))
+        refs.append(src.clone())
+    big = torch.randn(300, 7, generator=g).to("cuda")
+    nc_dst = torch.zeros(7, 300, device="cuda").t()          # non-contiguous destination: torch fallback
+    pairs.append((nc_dst, big))
+    ops.copy_many(pairs)
+    torch.cuda.synchronize()
+    for (dst, _), ref in zip(pairs[:-1], refs):
+        assert torch.equal(dst, ref)
+    assert torch.equal(nc_dst, big)
