@@ -100,6 +100,8 @@ _SIGNATURES = {
                               c_i32, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_bwd_src": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                               c_i64, c_vp], c_i32),
+    "alignn_tconv_bwd_src_by": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                 c_i64, c_vp], c_i32),
     "alignn_gate_ln_fwd": ([c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
                             c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_gate_ln_bwd": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

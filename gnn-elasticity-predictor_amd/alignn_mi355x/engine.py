@@ -174,7 +174,8 @@ class BatchCache:
     def _graph_tensors(g: ops.GraphCSR):
         g.schedule()
         _, light, heavy = g._sched
-        return [g.off_dst, g.perm_dst, g.src_at, g.dst_at, g.off_src, g.pos_src, g.err, light, heavy, g.rows, g.cmap]
+        return [g.off_dst, g.perm_dst, g.src_at, g.dst_at, g.off_src, g.pos_src, g.err, light, heavy, g.rows, g.cmap,
+                g.dst_src()]
 
     def device_tensors(self):
         """Every device buffer of this cache, in a fixed order (None where absent)."""
@@ -227,11 +228,13 @@ def prepare_batch(batch, stream: Optional[torch.cuda.Stream] = None, validate: b
     for (FusedTrainer.step): a loader can prepare batch i + 1 on its own stream while step i runs."""
     if stream is None:
         bc = batch_cache(batch, validate)
-        bc.signature()  # builds the schedules too
+        bc.signature()       # builds the schedules too
+        bc.device_tensors()  # and the by-source target lists
     else:
         with torch.cuda.stream(stream):
             bc = batch_cache(batch, validate)
             bc.signature()
+            bc.device_tensors()
     ev = torch.cuda.Event()
     ev.record(stream if stream is not None else torch.cuda.current_stream())
     try:

@@ -503,7 +503,7 @@ class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
     __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
-                 "n_full", "cmap")
+                 "n_full", "cmap", "_dst_src")
 
     # in-degree above which a target node gets a 4-wave workgroup (LDS merge of the waves); below it
     # one wave walks the node's edges.  256: every node of the MP-like line graph (in-degree <= 132
@@ -540,6 +540,7 @@ class GraphCSR:
         self.pos_src = torch.empty(max(m, 1), **i32)
         self.err = torch.zeros(1, **i32)
         self._sched = None
+        self._dst_src = None
         self.rows = None     # compacted graph: int32 ids of its nodes in the full node set
         self.n_full = n
         self.cmap = None     # compacted graph: int32 [n_full] full row -> node id, -1 if inactive
@@ -548,6 +549,14 @@ class GraphCSR:
                                            self.src_at.data_ptr(), self.dst_at.data_ptr(), self.off_src.data_ptr(),
                                            self.pos_src.data_ptr(), ws.data_ptr(), self.err.data_ptr(),
                                            stream_ptr()), "alignn_graph_prep")
+
+    def dst_src(self) -> torch.Tensor:
+        """Targets in by-source order, dst_at[pos_src[i]] (int32 [m]; built once per graph)."""
+        if self._dst_src is None:
+            if _RECORDING:
+                raise RuntimeError("GraphCSR.dst_src built during a launch-plan recording: prepare the batch first")
+            self._dst_src = self.dst_at[self.pos_src.long()].contiguous() if self.m else self.dst_at[:0].clone()
+        return self._dst_src
 
     def schedule(self):
         """Light/heavy target-node lists for the attention kernels (host-built once per graph:
@@ -816,14 +825,26 @@ def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Te
     return out
 
 
+# source-side attention backward over the by-source target list (alignn_tconv_bwd_src_by)
+BWD_SRC_BY = True
+
+
 def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):
     if (QKVR.size(0) < g.n or dout.numel() < g.n * D or dKV.size(0) < g.n or dKV.size(1) < 2 * D
             or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H):
         raise ValueError("tconv_bwd_src: operands do not cover the graph's n nodes / m edges")
-    profiling.launch(f"tconv_bwd_src n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_src"), lambda: check(_lib.lib().alignn_tconv_bwd_src(g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(),
-                                          g.dst_at.data_ptr(), QKVR.data_ptr(), QKVR.stride(0), dout.data_ptr(),
-                                          dz_e.data_ptr(), alpha_e.data_ptr(), dKV.data_ptr(), dKV.stride(0),
-                                          stream_ptr()), "alignn_tconv_bwd_src"))
+    if BWD_SRC_BY and g.m > 0:
+        ds = g.dst_src()
+        fn = lambda: check(_lib.lib().alignn_tconv_bwd_src_by(  # noqa: E731
+            g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(), ds.data_ptr(), QKVR.data_ptr(),
+            QKVR.stride(0), dout.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), dKV.data_ptr(), dKV.stride(0),
+            stream_ptr()), "alignn_tconv_bwd_src_by")
+    else:
+        fn = lambda: check(_lib.lib().alignn_tconv_bwd_src(  # noqa: E731
+            g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(), g.dst_at.data_ptr(), QKVR.data_ptr(),
+            QKVR.stride(0), dout.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), dKV.data_ptr(), dKV.stride(0),
+            stream_ptr()), "alignn_tconv_bwd_src")
+    profiling.launch(f"tconv_bwd_src n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "bwd_src"), fn)
 
 
 # ------------------------------------------------------------------------------------------------

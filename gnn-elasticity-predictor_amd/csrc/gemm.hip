@@ -582,11 +582,10 @@ struct GemmPlan {
 // (tools/gemm_bench.py, profiles/r01/v11_gemm_sweep.log; all tiles x stage depths x splits):
 //  * tile 64x64 — it was the fastest tile for every one of the 52 shapes (these products are
 //    latency-bound at 1-20 us; more, smaller workgroups hide more of it);
-//  * split-K toward one workgroup per CU (tiles x split ~ CUs), each split >= 32 deep, when the
-//    product is long (K >= 512) or its grid tiny (< 32 tiles); short-K grids of >= 32 tiles do
-//    not split (the reduce costs more than it saves);
-//  * 64-deep stages (a quarter of the global round trips) when a split is >= 128 deep and the
-//    grid <= 2 x CUs; 16-deep otherwise (large grids keep more workgroups resident with them).
+//  * split-K toward one workgroup per CU (tiles x split ~ CUs) when the product is long (K >= 512)
+//    on fewer than 160 tiles, or its grid tiny (< 32 tiles); details at the rule below;
+//  * 64-deep stages (a quarter of the global round trips) when a split is >= 512 deep on at most
+//    one workgroup per CU; 16-deep otherwise (large grids keep more workgroups resident with them).
 // Explicit tile / stage bits (tuning) override the choice.
 static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int requested, int tile) {
   const int cus = device_cus();
@@ -601,16 +600,30 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   int split = requested;
   if (split <= 0) {
     split = 1;
-    if (Ktot >= 512 || tiles < 32) {
-#if ALIGNN_GEMM_SPLIT_FLOOR
-      // never past one wave of workgroups: 164 tiles stay unsplit (26.0 vs 30.3 us split in two)
-      const int64_t want = std::max<int64_t>(1, cus / std::max<int64_t>(tiles, 1));
-#else
-      const int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
+    // round-2 sweep of every product of the B = 32 step (profiles/r02/v15_gemm_sweep.json): a grid
+    // of >= 160 tiles is not split (M2580 N256 K768: 25.8 vs 29.9 us in two); long-K splits keep
+    // >= 240-deep chunks (M64 N256 K1920 b4: 8 splits, not 16) and go to two workgroups per CU when
+    // the chunks would be >= 1024 deep (M256 N256 K23040: 32 splits, 40 vs 51 us)
+#ifndef ALIGNN_GEMM_PLAN_V1
+#define ALIGNN_GEMM_PLAN_V1 0  // 1: round-1 rules (A/B builds)
 #endif
-      const int64_t maxs = std::max<int64_t>(1, Ktot / 32);
+#if ALIGNN_GEMM_PLAN_V1
+    if (Ktot >= 512 || tiles < 32) {
+      const int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
+      split = (int)std::min(want, std::max<int64_t>(1, Ktot / 32));
+    }
+#else
+    if ((Ktot >= 512 && tiles < 160) || tiles < 32) {
+#if ALIGNN_GEMM_SPLIT_FLOOR
+      int64_t want = std::max<int64_t>(1, cus / std::max<int64_t>(tiles, 1));
+#else
+      int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
+#endif
+      if (Ktot >= 512 && Ktot / want >= 1024) want *= 2;
+      const int64_t maxs = std::max<int64_t>(1, Ktot / (Ktot >= 512 ? 240 : 32));
       split = (int)std::min(want, maxs);
     }
+#endif
   }
   if (Ktot == 0) split = 1;
   int64_t kchunk = (Ktot + split - 1) / split;
@@ -623,7 +636,10 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   if (tile & ALIGNN_GEMM_BK64) pl.bk = 64;
   else if (tile & ALIGNN_GEMM_BK32) pl.bk = 32;
   else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;
-  else pl.bk = (kchunk >= 128 && tiles * split <= 2 * (int64_t)cus) ? 64 : 16;
+  // 64-deep stages only for long chunks on at most one workgroup per CU (short-K products and
+  // two-per-CU splits run faster 16-deep: M2580 N768 K256 18.3 vs 20.6 us, M1024 N256 K1920 23.3 vs 26.0)
+  else if (ALIGNN_GEMM_PLAN_V1) pl.bk = (kchunk >= 128 && tiles * split <= 2 * (int64_t)cus) ? 64 : 16;
+  else pl.bk = (kchunk >= 512 && tiles * split <= (int64_t)cus) ? 64 : 16;
 #if ALIGNN_GEMM_BK128
   // 128-deep stages (half the round trips of 64) for a long split on at most one workgroup per CU
   // (the 139 KB double-buffered stage allows one per CU); fp32 64x64 only

@@ -1278,6 +1278,7 @@ struct BwdSrcParams {
   const float* dz_e;
   const float* alpha_e;
   float* dKV; int64_t lddkv;
+  const int32_t* dst_src;  // optional: dst_at[pos_src[i]] in by-source order (one index level less)
 };
 
 #ifndef ALIGNN_SRC_PF
@@ -1327,6 +1328,67 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
           dv[k] = fmaf(al[j], gv[j][k], dv[k]);
         }
     }
+    vstore(p.dKV + s * p.lddkv + j0, dk);
+    vstore(p.dKV + s * p.lddkv + D + j0, dv);
+  }
+}
+
+// Same sums, in the same order, over a by-source target list (dst_src): each edge's target and its
+// position are two independent scalar loads instead of a dependent pair, the next group's indices are
+// loaded while this group's rows are in flight, and tail edges are clamped to the source's last
+// edge with their scalars zeroed (unconditional loads).  Bitwise equal to tconv_bwd_src_kernel.
+template <int VPL, int H>
+__global__ __launch_bounds__(256) void tconv_bwd_src2_kernel(BwdSrcParams p) {
+  constexpr int PF = SRC_PF;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
+  if (s >= p.n) return;
+  const int D = p.D, C = D / H;
+  const int j0 = lane * VPL;
+  const bool act = j0 < D;
+  const int hl = act ? j0 / C : 0;
+  float dk[VPL], dv[VPL];
+  vzero(dk);
+  vzero(dv);
+  const int32_t beg = uni(sld(p.off_src, s)), end = uni(sld(p.off_src, s + 1));
+  if (act && beg < end) {
+    const int32_t last = end - 1;
+    int32_t pos[2][PF], dd[2][PF];
+    auto indices = [&](int32_t (&po)[PF], int32_t (&d)[PF], int32_t ib) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int32_t i = min(ib + j, last);
+        po[j] = uni(sld(p.pos_src, i));
+        d[j] = uni(sld(p.dst_src, i));
+      }
+    };
+    indices(pos[0], dd[0], beg);
+    int cur = 0;
+    for (int32_t ib = beg; ib < end; ib += PF) {
+      float qv[PF][VPL], gv[PF][VPL], dz[PF], al[PF];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int64_t po = pos[cur][j], d = dd[cur][j];
+        dz[j] = p.dz_e[po * H + hl];
+        al[j] = p.alpha_e[po * H + hl];
+        vload(p.QKVR + d * p.ldq + j0, qv[j]);
+        vload(p.dout + d * D + j0, gv[j]);
+      }
+      if (ib + PF < end) indices(pos[cur ^ 1], dd[cur ^ 1], ib + PF);
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const bool valid = ib + j < end;  // wave-uniform
+        const float zj = valid ? dz[j] : 0.f, aj = valid ? al[j] : 0.f;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          dk[k] = fmaf(zj, valid ? qv[j][k] : 0.f, dk[k]);
+          dv[k] = fmaf(aj, valid ? gv[j][k] : 0.f, dv[k]);
+        }
+      }
+      cur ^= 1;
+    }
+  }
+  if (act) {
     vstore(p.dKV + s * p.lddkv + j0, dk);
     vstore(p.dKV + s * p.lddkv + D + j0, dv);
   }
@@ -1471,7 +1533,8 @@ static int64_t bwd_ws_elems(int km, int D) {
 
 template <int VPL, int H>
 static void launch_bwd_src(const BwdSrcParams& p, hipStream_t s) {
-  launch((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  if (p.dst_src) launch((tconv_bwd_src2_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  else launch((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
 }
 
 static Sched make_sched(const AlignnSchedule* sc, int64_t n) {
@@ -1655,10 +1718,29 @@ extern "C" int alignn_tconv_bwd_src(int64_t n, int64_t m, int32_t D, int32_t H, 
   int rc = check_dims(D, H);
   if (rc) return rc;
   if (n == 0) return ALIGNN_OK;
-  BwdSrcParams p{n, m, D, 0, off_src, pos_src, dst_at, QKVR, ldq, dout, dz_e, alpha_e, dKV, lddkv};
+  BwdSrcParams p{n, m, D, 0, off_src, pos_src, dst_at, QKVR, ldq, dout, dz_e, alpha_e, dKV, lddkv, nullptr};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int vpl = vpl_for(D);
   ALIGNN_DISPATCH_VH(vpl, H, launch_bwd_src, p, s);
   ALIGNN_LAUNCH_CHECK("tconv_bwd_src_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_tconv_bwd_src_by(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_src,
+                                       const int32_t* pos_src, const int32_t* dst_src, const float* QKVR,
+                                       int64_t ldq, const float* dout, const float* dz_e, const float* alpha_e,
+                                       float* dKV, int64_t lddkv, void* stream) {
+  int rc = check_dims(D, H);
+  if (rc) return rc;
+  if (!dst_src) {
+    set_error("tconv_bwd_src_by: dst_src (dst_at[pos_src[i]]) is required");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (n == 0) return ALIGNN_OK;
+  BwdSrcParams p{n, m, D, 0, off_src, pos_src, nullptr, QKVR, ldq, dout, dz_e, alpha_e, dKV, lddkv, dst_src};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int vpl = vpl_for(D);
+  ALIGNN_DISPATCH_VH(vpl, H, launch_bwd_src, p, s);
+  ALIGNN_LAUNCH_CHECK("tconv_bwd_src2_kernel");
   return ALIGNN_OK;
 }

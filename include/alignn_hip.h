@@ -310,6 +310,13 @@ int alignn_tconv_bwd_src(int64_t n, int64_t m, int32_t D, int32_t H,
                          const int32_t* off_src, const int32_t* pos_src, const int32_t* dst_at,
                          const float* QKVR, int64_t ldq, const float* dout,
                          const float* dz_e, const float* alpha_e, float* dKV, int64_t lddkv, void* stream);
+/* The same sums (bitwise) given dst_src[i] = dst_at[pos_src[i]], the targets in by-source order
+ * (built once per batch): a wave loads each edge's target and position independently and the next
+ * edge group's indices while the current group's rows are in flight. */
+int alignn_tconv_bwd_src_by(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_src,
+                            const int32_t* pos_src, const int32_t* dst_src, const float* QKVR, int64_t ldq,
+                            const float* dout, const float* dz_e, const float* alpha_e, float* dKV, int64_t lddkv,
+                            void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Gate + LayerNorm + ReLU + dropout + residual, fused row kernel.  Replaces TransformerConv's

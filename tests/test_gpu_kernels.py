@@ -212,3 +212,46 @@ def test_wcolsum2_matches_fp64(M, N, H):
     ops.wcolsum2(X1, W1, X2, W2, out, accumulate=True)
     torch.cuda.synchronize()
     assert torch.allclose(out, 2 * base, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,D,H", [(300, 256, 4), (57, 64, 1), (129, 128, 2)])
+def test_bwd_src_by_source_list_bitwise(n, D, H):
+    """alignn_tconv_bwd_src_by (targets in by-source order, next group's indices prefetched, clamped
+    tails) against alignn_tconv_bwd_src: the same sums in the same order, bit for bit; and against
+    an fp64 scatter of the per-edge terms.  Ragged out-degrees: 0, 1, 16, 17, up to 140."""
+    from alignn_mi355x import _lib, ops
+    g = torch.Generator(device="cpu").manual_seed(n + D)
+    outdeg = torch.randint(0, 141, (n,), generator=g)
+    outdeg[::7] = 0
+    outdeg[1], outdeg[2], outdeg[3] = 1, 16, 17
+    src = torch.repeat_interleave(torch.arange(n), outdeg)
+    dst = torch.randint(0, n, (src.numel(),), generator=g)
+    perm = torch.randperm(src.numel(), generator=g)
+    ei = torch.stack([src[perm], dst[perm]]).to(DEV)
+    csr = ops.GraphCSR(ei, n)
+    m = csr.m
+    QKVR = torch.randn(n, 4 * D, generator=g).to(DEV)
+    dout = torch.randn(n, D, generator=g).to(DEV)
+    dz = torch.randn(m, H, generator=g).to(DEV)
+    al = torch.randn(m, H, generator=g).to(DEV)
+    outs = []
+    for by in (False, True):
+        ops.BWD_SRC_BY = by
+        try:
+            dKV = torch.full((n, 2 * D), float("nan"), device=DEV)
+            ops.tconv_bwd_src(csr, D, H, QKVR, dout, dz, al, dKV)
+        finally:
+            ops.BWD_SRC_BY = True
+        outs.append(dKV)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    # fp64: edge position t (target-sorted) has source src_at[t], target dst_at[t]
+    s_t = csr.src_at[:m].long().cpu()
+    d_t = csr.dst_at[:m].long().cpu()
+    C = D // H
+    dzr = dz.double().cpu().repeat_interleave(C, 1)
+    alr = al.double().cpu().repeat_interleave(C, 1)
+    dK = torch.zeros(n, D, dtype=torch.float64).index_add_(0, s_t, dzr * QKVR.double().cpu()[d_t, :D])
+    dV = torch.zeros(n, D, dtype=torch.float64).index_add_(0, s_t, alr * dout.double().cpu()[d_t])
+    ref = torch.cat([dK, dV], 1)
+    assert float((outs[1].double().cpu() - ref).abs().max() / ref.abs().max()) < 1e-5
