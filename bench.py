@@ -94,6 +94,8 @@ def apply_settings(args, model):
             kw["optimizer"] = v
         elif k == "wave_items":
             ops.GraphCSR.WAVE_ITEMS = bool(int(v))
+        elif k == "bf16_stream":
+            ops.GEMM_EXTRA = 0 if int(v) else ops.GEMM_NOSTREAM
         elif k == "bwd_src_by":
             ops.BWD_SRC_BY = bool(int(v))
         elif k == "xcd_items":

@@ -77,6 +77,7 @@ _SIGNATURES = {
     "alignn_gemm_workspace": ([ctypes.POINTER(GemmArgs)], c_i64),
     "alignn_copy_many": ([c_i32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_gemm_counters": ([ctypes.POINTER(GemmArgs)], c_i64),
+    "alignn_gemm_path": ([ctypes.POINTER(GemmArgs)], c_i32),
     "alignn_colsum_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
     "alignn_wcolsum2_f32": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
                              c_vp], c_i32),

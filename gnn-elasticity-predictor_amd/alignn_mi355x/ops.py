@@ -255,6 +255,8 @@ _GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
 GEMM_STAGE = 0        # ALIGNN_GEMM_BK32 (16) / ALIGNN_GEMM_BK64 (128): K stage depth of every planned GEMM
 GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
+GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
+GEMM_EXTRA = 0        # flags ORed into every gemm() call (A/B switches, e.g. GEMM_NOSTREAM)
 # split-K partials combined inside the GEMM launch by each tile's last workgroup (AlignnGemmArgs.counters)
 # instead of a separate reduce launch: same bits, one launch fewer per split product (option, off).
 # Measured on the B = 32 step (profiles/r02/v9_ab_splitk_combine.log): every split product combined
@@ -293,7 +295,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
          bias: Optional[torch.Tensor] = None, rowscale: Optional[torch.Tensor] = None,
          bias2: Optional[torch.Tensor] = None, relu: bool = False, mask: Optional[torch.Tensor] = None,
          split_k: Optional[int] = None, reduce_batch: bool = False,
-         c_rows: Optional[torch.Tensor] = None, tile: int = 0) -> torch.Tensor:
+         c_rows: Optional[torch.Tensor] = None, tile: int = 0, path_only: bool = False):
     """C = act(alpha * A @ B + beta * C + bias + rowscale[:,None] * bias2) [* (mask > 0)].
 
     A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D);
@@ -336,7 +338,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if c_rows is not None:
         a.c_rows = c_rows.data_ptr()
     a.split_k = 0 if split_k is None else int(split_k)   # 0: the library plans tile shape and split-K
-    a.tile = int(tile) | _GEMM_FLAGS | (GEMM_STAGE if not (int(tile) & 0xF0) else 0)
+    a.tile = int(tile) | _GEMM_FLAGS | GEMM_EXTRA | (GEMM_STAGE if not (int(tile) & 0xF0) else 0)
+    if path_only:   # which kernel the library takes (0 tiled, 1 bf16 streaming); nothing runs
+        return int(_lib.lib().alignn_gemm_path(ctypes.byref(a)))
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
     if need < 0:
         raise ValueError("gemm: invalid shape")

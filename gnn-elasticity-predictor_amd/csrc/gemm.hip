@@ -662,6 +662,205 @@ static bool plan_args(const AlignnGemmArgs* a, GemmPlan& pl, int64_t& ktot, int6
   return true;
 }
 
+// -------------------------------------------------------------------------------------------
+// bf16 streaming GEMM (config C3's large-M products: C[M, N] = act(alpha A W + beta C + bias) with
+// K = 64/128/256, N a multiple of 256, M >= 4096 — every bond / node / line-graph row times a
+// weight).  With bf16 matrix cores these products are bound by HBM (fp32 A in, fp32 C out), which the
+// 64x64-tile kernel reaches only ~40 % of: it re-reads each A row band once per column tile and its
+// 16-deep stages leave the loads exposed.  Here one workgroup per CU keeps a 256-column slice of W
+// as bf16 in LDS ([n][K + 8]: the padding puts a ds_read_b128 lane group on distinct banks) for the
+// kernel's lifetime and streams 64-row bands of A: each wave owns 32 rows x 128 columns (four
+// accumulators), holds its rows' fp32 A values in VGPRs in MFMA operand order (two 16-byte loads per
+// 16-deep slice: k = 16 t + 8 h + j on lane half h), the next band's rows in flight during this
+// band's MFMAs (v_mfma_f32_32x32x16_bf16, inputs rounded to bf16 RNE as in the tiled BF path, fp32
+// accumulation), and writes each 32 x 32 accumulator through a wave-private LDS tile as 16-byte
+// row segments.  Loads and stores are unconditional (rows clamped / buffer descriptors), so the
+// compiler counts outstanding loads instead of draining the prefetch.
+// -------------------------------------------------------------------------------------------
+namespace bst {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int NB = 256;          // columns per slice
+constexpr int ROWS = 64;         // rows per band (2 wave rows x 32)
+constexpr int EPI_LD = 36;       // epilogue tile row stride (floats)
+
+template <int KT>
+__device__ __forceinline__ void load_band(gf4 (&a)[KT / 8], const float* __restrict__ Arow, int h) {
+#pragma unroll
+  for (int t = 0; t < KT / 16; ++t) {
+    a[2 * t] = *reinterpret_cast<const gf4*>(Arow + 16 * t + 8 * h);
+    a[2 * t + 1] = *reinterpret_cast<const gf4*>(Arow + 16 * t + 8 * h + 4);
+  }
+  asm volatile("" ::: "memory");  // a prefetch: issued here, not sunk to its first use
+}
+
+template <int KT>
+__device__ __forceinline__ void band_mma(floatx16 (&acc)[4], const gf4 (&a)[KT / 8], const __bf16* __restrict__ Bs,
+                                         int col0, int l32, int h) {
+  constexpr int KP = KT + 8;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const __bf16* Bl = Bs + (col0 + l32) * KP + 8 * h;
+#pragma unroll
+  for (int t = 0; t < KT / 16; ++t) {
+    bf16x8 ha;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ha[q] = (__bf16)a[2 * t][q];
+      ha[4 + q] = (__bf16)a[2 * t + 1][q];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(Bl + 32 * j * KP + 16 * t);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb, acc[j], 0, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n, 0x00020000);
+}
+
+// v = alpha acc + bias (column layout) -> LDS tile -> rows: (+ beta C), ReLU, 16-byte stores.  Rows
+// past M fall outside the store descriptor and are dropped; beta == 0 reads an empty descriptor.
+template <bool BETA, bool MASK>
+__device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], const float (&bias)[4],
+                                           float* __restrict__ Ls, __amdgpu_buffer_rsrc_t cst,
+                                           __amdgpu_buffer_rsrc_t cld, __amdgpu_buffer_rsrc_t cmk, int64_t row0,
+                                           int l32, int h, int lane) {
+  const int rr = lane >> 1, cc = (lane & 1) * 16;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ls[((r & 3) + 8 * (r >> 2) + 4 * h) * EPI_LD + l32] = p.alpha * acc[j][r] + bias[j];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gf4 v = *reinterpret_cast<const gf4*>(Ls + rr * EPI_LD + cc + 4 * i);
+      const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * 4);
+      if constexpr (BETA) v += p.beta * __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
+      const gf4 z = {0.f, 0.f, 0.f, 0.f};
+      v = p.relu ? __builtin_elementwise_max(v, z) : v;
+      if constexpr (MASK) {  // ReLU-backward mask: keep v where mask > 0 (the tiled epilogue's rule)
+        const int moff = (int)(((row0 + rr) * p.smk_m + 32 * j + cc + 4 * i) * 4);
+        const gf4 mk = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cmk, moff, 0, 0));
+        v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
+        v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cst, off, 0, 0);
+    }
+  }
+}
+
+// grid: G workgroups (<= one per CU), G a multiple of nslices = N / 256; workgroup g serves slice
+// g % nslices and bands q, q + Q, ... (q = g / nslices, Q = G / nslices).
+template <int KT, bool BETA, bool MASK>
+__global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, int nslices, int64_t nbands) {
+  constexpr int KP = KT + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NB * KP];
+  __shared__ __attribute__((aligned(16))) float Lepi[4 * 32 * EPI_LD];
+  const int g = blockIdx.x;
+  const int z = g % nslices, q = g / nslices, Q = gridDim.x / nslices;
+  const int64_t n0 = (int64_t)z * NB;
+  // W slice -> LDS as bf16 [n][k], once (RNE, as the tiled BF path rounds its operands)
+  if (p.sbk == 1) {  // W^T given (k contiguous): 16-byte loads along k
+    for (int i = threadIdx.x; i < NB * (KT / 4); i += 256) {
+      const int n = i / (KT / 4), k = (i % (KT / 4)) * 4;
+      const float* src = p.B + (n0 + n) * p.sbn + k;
+      const gf4 v = p.vecB ? *reinterpret_cast<const gf4*>(src) : gf4{src[0], src[1], src[2], src[3]};
+      __bf16* d = Bs + n * KP + k;
+      d[0] = (__bf16)v[0]; d[1] = (__bf16)v[1]; d[2] = (__bf16)v[2]; d[3] = (__bf16)v[3];
+    }
+  } else {  // W row-major (n contiguous): loads along n, transposed into the [n][k] image
+    for (int i = threadIdx.x; i < NB * (KT / 4); i += 256) {
+      const int k = i / (NB / 4), n = (i % (NB / 4)) * 4;
+      const float* src = p.B + (int64_t)k * p.sbk + (n0 + n) * p.sbn;
+      const gf4 v = (p.sbn == 1 && p.vecB) ? *reinterpret_cast<const gf4*>(src)
+                                            : gf4{src[0], src[p.sbn], src[2 * p.sbn], src[3 * p.sbn]};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Bs[(n + q) * KP + k] = (__bf16)v[q];
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int l32 = lane & 31, h = lane >> 5;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int col0 = wc * 128;
+  float bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = p.bias ? p.bias[n0 + col0 + 32 * j + l32] : 0.f;
+  const float* Cw = p.C + n0 + col0;
+  const int64_t cbytes = (p.M * p.scm - (n0 + col0)) * 4;
+  const __amdgpu_buffer_rsrc_t cst = rsrc(Cw, cbytes);
+  const __amdgpu_buffer_rsrc_t cld = rsrc(Cw, (BETA && p.beta != 0.f) ? cbytes : 0);
+  const __amdgpu_buffer_rsrc_t cmk = rsrc(MASK ? p.mask + n0 + col0 : Cw, MASK ? (p.M * p.smk_m - (n0 + col0)) * 4 : 0);
+  float* Ls = Lepi + wave * 32 * EPI_LD;
+  __syncthreads();
+  auto arow = [&](int64_t band) {
+    const int64_t row = min(band * ROWS + wr * 32 + l32, p.M - 1);
+    return p.A + row * p.sam;
+  };
+  gf4 a0[KT / 8], a1[KT / 8];
+  floatx16 acc[4];
+  int64_t band = q;
+  if (band >= nbands) return;
+  load_band<KT>(a0, arow(band), h);
+  while (true) {  // two bands per iteration: the register sets keep fixed names
+    const int64_t b1 = band + Q;
+    load_band<KT>(a1, arow(min(b1, nbands - 1)), h);
+    band_mma<KT>(acc, a0, Bs, col0, l32, h);
+    band_store<BETA, MASK>(p, acc, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane);
+    if (b1 >= nbands) break;
+    const int64_t b2 = b1 + Q;
+    load_band<KT>(a0, arow(min(b2, nbands - 1)), h);
+    band_mma<KT>(acc, a1, Bs, col0, l32, h);
+    band_store<BETA, MASK>(p, acc, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane);
+    if (b2 >= nbands) break;
+    band = b2;
+  }
+}
+
+}  // namespace bst
+
+// The streaming kernel's shapes (host check): bf16 arithmetic, K in {64, 128, 256}, N a multiple of
+// 256, M >= 4096, A k-contiguous 16-byte rows, no batch / split / batch reduction, epilogue alpha /
+// beta / bias / ReLU into a row-major C with 32-bit byte offsets.
+static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
+  if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOSTREAM) || (a->tile & 15) != 0) return false;
+  if (a->batch != 1 || a->reduce_batch || split != 1) return false;
+  if (a->K != 64 && a->K != 128 && a->K != 256) return false;
+  if (a->N % bst::NB != 0 || a->M < 4096) return false;
+  if (a->sak != 1 || a->sam % 4 || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
+  if (a->c_rows || a->rowscale || a->scn != 1 || a->scm < a->N) return false;
+  if (a->mask && (a->smk_n != 1 || a->smk_m < a->N || (reinterpret_cast<uintptr_t>(a->mask) & 15) || a->smk_m % 4))
+    return false;
+  if ((a->M + 64) * std::max(a->scm, a->mask ? a->smk_m : 0) * 4 >= ((int64_t)1 << 31)) return false;
+  if (a->scm % 4 || (reinterpret_cast<uintptr_t>(a->C) & 15)) return false;  // 16-byte row segments
+  return true;
+}
+
+template <int KT>
+static void bf16_stream_launch_k(const GemmParams& p, dim3 grid, int nslices, int64_t nbands, hipStream_t s) {
+  const bool beta = p.beta != 0.f, mask = p.mask != nullptr;
+  if (beta && mask) launch(bst::gemm_bf16_stream_kernel<KT, true, true>, grid, dim3(256), 0, s, p, nslices, nbands);
+  else if (beta) launch(bst::gemm_bf16_stream_kernel<KT, true, false>, grid, dim3(256), 0, s, p, nslices, nbands);
+  else if (mask) launch(bst::gemm_bf16_stream_kernel<KT, false, true>, grid, dim3(256), 0, s, p, nslices, nbands);
+  else launch(bst::gemm_bf16_stream_kernel<KT, false, false>, grid, dim3(256), 0, s, p, nslices, nbands);
+}
+
+static void bf16_stream_launch(const GemmParams& p, int cus, hipStream_t s) {
+  const int nslices = (int)(p.N / bst::NB);
+  const int64_t nbands = (p.M + bst::ROWS - 1) / bst::ROWS;
+  const int G = (int)(std::min<int64_t>(cus, nslices * nbands) / nslices * nslices);
+  const dim3 grid((unsigned)std::max(G, nslices));
+  if (p.K == 256) bf16_stream_launch_k<256>(p, grid, nslices, nbands, s);
+  else if (p.K == 128) bf16_stream_launch_k<128>(p, grid, nslices, nbands, s);
+  else bf16_stream_launch_k<64>(p, grid, nslices, nbands, s);
+}
+
 }  // namespace alignn
 
 using namespace alignn;
@@ -679,6 +878,13 @@ extern "C" int64_t alignn_gemm_counters(const AlignnGemmArgs* a) {
   if (!plan_args(a, pl, ktot, nb)) return -1;
   if (pl.split <= 1) return 0;
   return ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn) * nb;
+}
+
+extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
+  GemmPlan pl;
+  int64_t ktot, nb;
+  if (!plan_args(a, pl, ktot, nb)) return -1;
+  return bf16_stream_ok(a, pl.split) ? 1 : 0;
 }
 
 extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
@@ -727,6 +933,11 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
     set_error("gemm: split_k=%d needs %lld workspace floats", pl.split,
               (long long)pl.split * nbatch_out * a->M * a->N);
     return ALIGNN_E_WORKSPACE;
+  }
+  if (bf16_stream_ok(a, pl.split)) {
+    bf16_stream_launch(p, device_cus(), s);
+    ALIGNN_LAUNCH_CHECK("gemm_bf16_stream_kernel");
+    return ALIGNN_OK;
   }
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));

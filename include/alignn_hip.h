@@ -86,6 +86,9 @@ typedef struct AlignnGemmArgs {
  * flight — is taken automatically when every stage is full and both operands are vectorisable; both
  * give bitwise the same result).  For A/B tests. */
 #define ALIGNN_GEMM_NOPIPE 256
+/* bf16 only: never the streaming kernel (the large-M products K in {64, 128, 256}, N % 256 == 0,
+ * M >= 4096 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
+#define ALIGNN_GEMM_NOSTREAM 512
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
@@ -95,6 +98,10 @@ int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
 /* int32 tile tickets (AlignnGemmArgs.counters) the in-launch split-K combine needs: 0 when the plan
  * does not split K. */
 int64_t alignn_gemm_counters(const AlignnGemmArgs* args);
+
+/* Which kernel alignn_gemm_f32 takes (host query, no GPU work): 0 tiled, 1 the bf16 streaming
+ * kernel (ALIGNN_GEMM_NOSTREAM), -1 invalid arguments. */
+int alignn_gemm_path(const AlignnGemmArgs* args);
 
 /* ----------------------------------------------------------------------------------------
  * Skinny products (skinny.hip), streamed at HBM rate: the angle encoder's first Linear over the

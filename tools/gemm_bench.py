@@ -56,11 +56,15 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json")
     ap.add_argument("--quick", action="store_true", help="auto plan + torch.matmul (hipBLASLt/rocBLAS) only")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: the step's products with bf16 matrix-core inputs (config C3); the library "
+                         "reference is then torch.matmul on bf16 copies of the operands")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(dev)
-    tr = A.FusedTrainer(model)
+    tr = A.FusedTrainer(model, precision=a.precision)
+    bf = ops.GEMM_BF16 if a.precision == "bf16" else 0
     b = mp_like_batch(a.batch).to(dev)
     tr.forward_backward(b, 1)
     torch.cuda.synchronize()
@@ -82,7 +86,7 @@ def main():
         def run(tile=0, split=None, c=c):
             ops.gemm(c["A"], c["B"], c["C"], alpha=c["alpha"], beta=c["beta"], bias=c["bias"], rowscale=c["rowscale"],
                      bias2=c["bias2"], relu=c["relu"], mask=c["mask"], reduce_batch=c["reduce_batch"],
-                     c_rows=c["c_rows"], split_k=split, tile=tile)
+                     c_rows=c["c_rows"], split_k=split, tile=tile | bf)
 
         t_auto = timeit(lambda: run(), a.reps)
         # library reference: the same plain product through torch.matmul (no epilogue)
@@ -90,6 +94,8 @@ def main():
         if c["reduce_batch"]:
             Am = Am.transpose(0, 1).reshape(Am.shape[1], -1) if Am.dim() == 3 else Am
             Bm = Bm.reshape(-1, Bm.shape[-1]) if Bm.dim() == 3 else Bm
+        if bf:
+            Am, Bm = Am.bfloat16(), Bm.bfloat16()
         try:
             t_lib = timeit(lambda: torch.matmul(Am, Bm), a.reps)
         except Exception:  # noqa: BLE001
