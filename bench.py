@@ -85,7 +85,8 @@ def apply_settings(args, model):
             attr = k.split(".", 1)[1]
             if not hasattr(model._engine, attr):
                 raise ValueError(f"unknown engine option {attr}")
-            setattr(model._engine, attr, bool(int(v)))
+            cur = getattr(model._engine, attr)
+            setattr(model._engine, attr, int(v) if (isinstance(cur, int) and not isinstance(cur, bool)) else bool(int(v)))
         elif k == "gemm_stage":
             ops.GEMM_STAGE = {"16": 0, "32": 16, "64": 128}[v]
         elif k == "compact_regs":
