@@ -596,9 +596,24 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
     pl.bm = cand[shape - 1][0];
     pl.bn = cand[shape - 1][1];
   }
+  // bf16 long-K products (weight gradients over every row, M >= 128): 128 x 64 tiles, 32-deep
+  // stages, two workgroups per CU (B = 256 bf16 sweep, profiles/r02/v20_gemm_sweep_b256_bf16.json:
+  // M768 N256 K16020 38.7 vs 64.6 us, M256 N256 K184320 115 vs 129 us)
+#ifndef ALIGNN_GEMM_BF_LONG
+#define ALIGNN_GEMM_BF_LONG 1
+#endif
+  const bool bf_long = ALIGNN_GEMM_BF_LONG && (tile & ALIGNN_GEMM_BF16) && shape == 0 && !(tile & (ALIGNN_GEMM_BK16 | ALIGNN_GEMM_BK32 |
+                       ALIGNN_GEMM_BK64)) && Ktot >= 4096 && M >= 128 && requested <= 0;
+  if (bf_long) {
+    pl.bm = 128;
+    pl.bn = 64;
+  }
   const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn) * nb;
   int split = requested;
-  if (split <= 0) {
+  if (bf_long) {
+    split = (int)std::max<int64_t>(1, std::min<int64_t>((2 * cus + tiles / 2) / std::max<int64_t>(tiles, 1),
+                                                         Ktot / 256));
+  } else if (split <= 0) {
     split = 1;
     // round-2 sweep of every product of the B = 32 step (profiles/r02/v15_gemm_sweep.json): a grid
     // of >= 160 tiles is not split (M2580 N256 K768: 25.8 vs 29.9 us in two); long-K splits keep
@@ -633,7 +648,8 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   if (split < 1) split = 1;
   pl.split = split;
   pl.kchunk = kchunk;
-  if (tile & ALIGNN_GEMM_BK64) pl.bk = 64;
+  if (bf_long) pl.bk = 32;
+  else if (tile & ALIGNN_GEMM_BK64) pl.bk = 64;
   else if (tile & ALIGNN_GEMM_BK32) pl.bk = 32;
   else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;
   // 64-deep stages only for long chunks on at most one workgroup per CU (short-K products and
