@@ -121,11 +121,9 @@ class BatchCache:
         self.E = int(batch.edge_index.size(1))
         self.T = int(batch.lg_edge_index.size(1))
         self.ag = ops.GraphCSR(batch.edge_index, self.N)
-        self.lg = ops.GraphCSR(batch.lg_edge_index, self.E)
         if validate:
             self.ag.check_indices("edge_index")
-            self.lg.check_indices("lg_edge_index")
-        self.lg = self._compact(self.lg, batch.lg_edge_index, self.E)
+        self.lg = self._line_graph(batch.lg_edge_index, self.E, validate)
         la = batch.lg_edge_attr
         self.angle_dim = int(la.size(-1)) if la.dim() == 2 else 0
         if self.T > 0 and la.numel() > 0:
@@ -204,14 +202,31 @@ class BatchCache:
     COMPACT_FRACTION = 0.75
 
     @classmethod
-    def _compact(cls, g: ops.GraphCSR, edge_index: torch.Tensor, n: int) -> ops.GraphCSR:
-        if n == 0 or g.m == 0:
+    def _line_graph(cls, edge_index: torch.Tensor, n: int, validate: bool) -> ops.GraphCSR:
+        """CSR of the line graph, compacted when few bonds are active.  The active set is marked from
+        the edge endpoints directly (no CSR of all n bonds is built first): one CSR build per batch."""
+        if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
+            raise ValueError("edge_index must be int64 [2, m]")
+        m = edge_index.size(1)
+        if n == 0 or m == 0:
+            g = ops.GraphCSR(edge_index, n)
+            if validate:
+                g.check_indices("lg_edge_index")
             return g
-        deg = (g.off_dst[1:] - g.off_dst[:-1]) + (g.off_src[1:] - g.off_src[:-1])
-        active = deg > 0
+        if validate:
+            lo, hi = torch.stack([edge_index.min(), edge_index.max()]).tolist()
+            if lo < 0 or hi >= n:
+                raise IndexError(f"lg_edge_index: edge index out of range [0, {n})")
+        active = torch.zeros(n, dtype=torch.bool, device=edge_index.device)
+        active[edge_index[0]] = True
+        active[edge_index[1]] = True
+        return cls._compact(active, edge_index, n)
+
+    @classmethod
+    def _compact(cls, active: torch.Tensor, edge_index: torch.Tensor, n: int) -> ops.GraphCSR:
         na = int(active.sum().item())
         if na > cls.COMPACT_FRACTION * n:
-            return g
+            return ops.GraphCSR(edge_index, n)
         rows = torch.nonzero(active).flatten()
         cmap = torch.full((n,), -1, dtype=torch.int64, device=edge_index.device)
         cmap[rows] = torch.arange(na, dtype=torch.int64, device=edge_index.device)
