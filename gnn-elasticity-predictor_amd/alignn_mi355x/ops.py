@@ -520,12 +520,14 @@ class GraphCSR:
     # materialised-F line-graph kernels; other calls keep the kernels above)
     WAVE_ITEMS = True
     # work items interleaved so that XCD x (workgroup i runs on XCD i % 8) walks the x-th contiguous
-    # eighth of the target ids, longest first within it: a target's sources lie near it (PyG's
-    # per-graph index windows), so each XCD's L2 holds the K/V rows its gathers need.  Measured
-    # (profiles/r02/v13_ab_xcd_items_rejected.log): line-graph bwd_dst fetch 588 -> 300 MB per launch
-    # (the K/V gathers hit L2), yet the kernels slow down (103 -> 128 us) and the step by 5 %: they
-    # are issue-bound (SQ counters, v12_pmc_sq_mix.json), not traffic-bound.  Off.
-    XCD_ITEMS = False
+    # range of target ids, longest first within it: a target's sources lie near it (PyG's per-graph
+    # index windows), so each XCD's L2 holds the K/V rows its gathers need (line-graph bwd_dst fetch
+    # 588 -> 300 MB per launch).  With ranges of equal target COUNT the middle XCDs got 322 132-edge
+    # targets for 256 wave slots (two rounds: kernels 103 -> 128 us, step -5 %,
+    # profiles/r02/v13_ab_xcd_items_rejected.log); ranges of equal EDGE count give them 240: step
+    # +1.8 % at B = 32 (8,744-8,772 vs 8,602-8,611 graphs/s), neutral at B = 256 bf16
+    # (profiles/r02/v24_ab_xcd_items_edge_balanced.log).
+    XCD_ITEMS = True
     XCDS = 8
 
     def __init__(self, edge_index: torch.Tensor, n: int):
@@ -582,8 +584,13 @@ class GraphCSR:
                 lit = lit[torch.sort(deg[lit.long()], descending=True, stable=True).indices]
                 hv = hv[torch.sort(deg[hv.long()], descending=True, stable=True).indices]
             if self.XCD_ITEMS and self.WAVE_ITEMS and lit.numel() > self.XCDS:
-                # contiguous target ranges per XCD, LPT order inside each, interleaved i % XCDS
-                bounds = [self.n * x // self.XCDS for x in range(self.XCDS + 1)]
+                # contiguous target ranges per XCD holding equal numbers of EDGES (equal target
+                # counts put 322 132-edge targets on one XCD's 256 wave slots: two rounds), LPT
+                # order inside each, interleaved i % XCDS
+                cum = torch.cumsum(deg.to(torch.int64), 0)
+                tot = int(cum[-1]) if self.n else 0
+                bounds = [0] + [int(torch.searchsorted(cum, tot * x // self.XCDS, right=True)) for x in
+                                range(1, self.XCDS)] + [self.n]
                 parts = []
                 for x in range(self.XCDS):
                     sel = lit[(lit >= bounds[x]) & (lit < bounds[x + 1])]

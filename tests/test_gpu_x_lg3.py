@@ -34,12 +34,14 @@ def _case(H, degs, seed, with_wbar, D=256):
     return csr, m, t
 
 
-def _run(csr, m, t, D, H, drop, wave_items):
+def _run(csr, m, t, D, H, drop, wave_items, xcd_items=None):
     ops = _ops()
     n = csr.n
     csr._sched = None
-    prev = ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS
+    prev = ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.XCD_ITEMS
     ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS = wave_items, True
+    if xcd_items is not None:
+        ops.GraphCSR.XCD_ITEMS = xcd_items
     try:
         fam = csr.family(D, H, t["F"])
         outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
@@ -51,7 +53,7 @@ def _run(csr, m, t, D, H, drop, wave_items):
         ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], None, t["dout"], outp,
                           mstat, den, dq, Sz, sigz, dz, al, None, 0, drop, 77)
     finally:
-        ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS = prev
+        ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.XCD_ITEMS = prev
         csr._sched = None
     torch.cuda.synchronize()
     return fam, dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz[:m], al=al[:m])
@@ -79,6 +81,17 @@ def test_wave_items_match_compact_kernels(H, drop, degs):
             if k in ("dz", "al") and m == 0:
                 continue
             assert _rel(b[k], a[k]) < 1e-5, (k, H, drop, degs, seed)
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.15])
+def test_xcd_item_order_bitwise(drop):
+    """XCD-contiguous, edge-balanced work-item order (GraphCSR.XCD_ITEMS) only permutes which wave
+    runs which target: every output bitwise equal to the plain longest-first order."""
+    csr, m, t = _case(4, DEGREES["mp_mix"] * 3, 5, True)
+    _, a = _run(csr, m, t, 256, 4, drop, True, xcd_items=False)
+    _, b = _run(csr, m, t, 256, 4, drop, True, xcd_items=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
 
 
 def _pyg_reference(csr_cpu_ei, n, t, H, D=256):
