@@ -573,10 +573,18 @@ class AlignnEngine:
         self.gate_reduce_side = True  # +0.3 % (v34_sweep_gate_reduce_side.log)
         # projection chain rules on the main stream after the encoder MLP backward (see _backward)
         self.proj_main = False  # measured -0.3 % (with enc_bwd_aux -1.6 %; v35_sweep_proj_main_rejected.log)
-        # deferred angle-encoder backward on a third stream (see _backward)
-        self.enc_bwd_aux = False  # measured -0.6 % (v31_sweep_enc_bwd_aux_rejected.log)
+        # deferred angle-encoder backward on a third stream (see _backward): 1 always, 0 never, or
+        # from this many line-graph edges on.  B = 32 (253,440 triplets): -0.6 %
+        # (v31_sweep_enc_bwd_aux_rejected.log); B = 256 bf16 (2.03 M triplets, enc_bwd 1.06 ms, the
+        # step's last branch): +1.8 % (17,697-17,740 -> 18,027-18,051 graphs/s,
+        # profiles/r02/v30_ab_enc_bwd_aux_c3.log)
+        self.enc_bwd_aux = 1_000_000
         # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
         self.wbar_colsum = True
+        # the encoder MLPs' masked dX products (end of backward, beside the deferred angle-encoder
+        # backward on the side stream) on the tiled kernels: the bf16 streaming GEMM needs a whole
+        # CU's LDS, so it waited for enc_bwd to drain (C3: 1,212 us for a 150 us product)
+        self.mlp_bwd_stream = False
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
@@ -596,11 +604,11 @@ class AlignnEngine:
         ops.gemm(h1, W2.t(), out, bias=b2)
         return h1, out
 
-    def _mlp_bwd(self, dout, x, h1, W2, gW1, gb1, gW2, gb2):
+    def _mlp_bwd(self, dout, x, h1, W2, gW1, gb1, gW2, gb2, beside_side: bool = False):
         ops.gemm(dout.t(), h1, gW2)
         ops.colsum(dout, gb2)
         dh1 = torch.empty_like(h1)
-        ops.gemm(dout, W2, dh1, mask=h1)
+        ops.gemm(dout, W2, dh1, mask=h1, tile=ops.GEMM_NOSTREAM if beside_side and not self.mlp_bwd_stream else 0)
         ops.gemm(dh1.t(), x, gW1)
         ops.colsum(dh1, gb1)
 
@@ -808,7 +816,8 @@ class AlignnEngine:
         kept = [t for c in ctx.edge for t in (c.U, *c.edge_scalars)] if defer else []
         # the deferred angle-encoder backward (the longest branch of the tail) on a third stream,
         # started as soon as the last line block is done instead of behind the side stream's queue
-        aux = ops.aux_stream(dev) if (defer and side is not None and self.enc_bwd_aux) else None
+        use_aux = self.enc_bwd_aux == 1 or (self.enc_bwd_aux > 1 and T >= self.enc_bwd_aux)
+        aux = ops.aux_stream(dev) if (defer and side is not None and use_aux) else None
         if aux is not None:
             with _side_work(aux, kept):
                 ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
@@ -842,9 +851,11 @@ class AlignnEngine:
                     ops.colsum(da, G.enc("angle", 0, "bias"))
         if ctx.h1e is not None:
             self._mlp_bwd(de, ctx.edge_attr, ctx.h1e, P.enc("edge", 2, "weight"), G.enc("edge", 0, "weight"),
-                          G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))
+                          G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"),
+                          beside_side=side is not None)
         self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
-                      G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))
+                      G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"),
+                      beside_side=side is not None)
         if proj_main:
             # after the encoder MLPs: wait for the side stream's per-layer dM / dw̄, then the chain rules
             ops.stream_wait(torch.cuda.current_stream(dev), side)
