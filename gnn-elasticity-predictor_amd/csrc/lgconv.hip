@@ -42,6 +42,43 @@ __device__ __forceinline__ float dot4(const float (&a)[VPL], f4 b) {
   return fmaf(a[3], b.w, fmaf(a[2], b.z, fmaf(a[1], b.y, a[0] * b.x)));
 }
 
+// Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of fp32 FMAs per instruction, the
+// vector fp32 peak).  Every element goes through the same fmaf / multiply, in the same order, as
+// the scalar code (a per-head pair of dot4 chains; axpy over feature pairs), so results are bitwise
+// those of the scalar loops.  Node vectors of two heads h, h+1 sit interleaved in LDS so that one
+// 16-byte read gives (v_h[i], v_h+1[i], v_h[i+1], v_h+1[i+1]).
+#ifndef ALIGNN_LG3_PK
+#define ALIGNN_LG3_PK 1
+#endif
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void axpy_pk(float (&acc)[VPL], float a, f4 x) {
+  const f2 aa = {a, a};
+  f2 lo = {acc[0], acc[1]}, hi = {acc[2], acc[3]};
+  lo = __builtin_elementwise_fma(aa, f2{x.x, x.y}, lo);
+  hi = __builtin_elementwise_fma(aa, f2{x.z, x.w}, hi);
+  acc[0] = lo.x; acc[1] = lo.y; acc[2] = hi.x; acc[3] = hi.y;
+}
+__device__ __forceinline__ void scale_pk(float (&acc)[VPL], float a) {
+  const f2 aa = {a, a};
+  f2 lo = f2{acc[0], acc[1]} * aa, hi = f2{acc[2], acc[3]} * aa;
+  acc[0] = lo.x; acc[1] = lo.y; acc[2] = hi.x; acc[3] = hi.y;
+}
+// LDS slot of feature i (of this lane's four) of head h's node vector, paired layout (H even)
+__device__ __forceinline__ int pk_slot(int h, int i, int lane) {
+  return (((h >> 1) * 2 + (i >> 1)) * 64 + lane) * 4 + (i & 1) * 2 + (h & 1);
+}
+// (dot4(v_h, f) , dot4(v_h+1, f)) for the head pair whose interleaved vectors start at `pair`,
+// then fmaf(mk, qk, .) per head
+__device__ __forceinline__ f2 dot4_pair(const float* pair, int lane, f4 f, f2 mk, float qk) {
+  const f4 A = *reinterpret_cast<const f4*>(pair + lane * 4);
+  const f4 B = *reinterpret_cast<const f4*>(pair + (64 + lane) * 4);
+  f2 acc = f2{A.x, A.y} * f2{f.x, f.x};
+  acc = __builtin_elementwise_fma(f2{A.z, A.w}, f2{f.y, f.y}, acc);
+  acc = __builtin_elementwise_fma(f2{B.x, B.y}, f2{f.z, f.z}, acc);
+  acc = __builtin_elementwise_fma(f2{B.z, B.w}, f2{f.w, f.w}, acc);
+  return __builtin_elementwise_fma(mk, f2{qk, qk}, acc);
+}
+
 // bf16 storage (config C3, the reference's autocast: Linear outputs in bf16, train.py:632-636): the
 // gathered K/V rows and the streamed edge-feature rows are bf16 in HBM (four per lane = one 8-byte
 // load per row), widened to fp32 where a group is consumed; all arithmetic stays fp32.
@@ -177,6 +214,17 @@ __device__ __forceinline__ float own(const float (&e)[H], int hl) {
   return pick_r<H>(e, hl);
 }
 
+// Lane's own-head entry of per-head wave-uniform values, as sum_h e[h] * mk[h] (mk = the lane's
+// one-hot head mask): exact for finite e (one product is e[hl] * 1, the others 0) and branch-free —
+// own() over uniform values compiled to one exec-masked branch per head inside the edge loop.
+template <int H>
+__device__ __forceinline__ float sel_head(const float (&e)[H], const float (&mk)[H]) {
+  float r = e[0] * mk[0];
+#pragma unroll
+  for (int h = 1; h < H; ++h) r = fmaf(e[h], mk[h], r);
+  return r;
+}
+
 // Per-edge-head output rows [t, H] written by the first lanes of each 16-lane row.
 template <int H>
 __device__ __forceinline__ void store_edge_heads(float* __restrict__ out, int64_t t, int col, const float (&b)[H]) {
@@ -220,12 +268,24 @@ __device__ __forceinline__ void fwd_group(const Params& p, const Edge (&r)[G], c
     float ps[G * H], qk[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) qk[j] = dot4(q, r[j].k);
+    if constexpr (ALIGNN_LG3_PK && H % 2 == 0) {
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float u[VPL];
-      vload(uv + h * RS + j0, u);
+      for (int hp = 0; hp < H / 2; ++hp) {
 #pragma unroll
-      for (int j = 0; j < G; ++j) ps[j * H + h] = fmaf(mk[h], qk[j], dot4(u, r[j].f));
+        for (int j = 0; j < G; ++j) {
+          const f2 v = dot4_pair(uv + hp * 2 * RS, lane, r[j].f, f2{mk[2 * hp], mk[2 * hp + 1]}, qk[j]);
+          ps[j * H + 2 * hp] = v.x;
+          ps[j * H + 2 * hp + 1] = v.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float u[VPL];
+        vload(uv + h * RS + j0, u);
+#pragma unroll
+        for (int j = 0; j < G; ++j) ps[j * H + h] = fmaf(mk[h], qk[j], dot4(u, r[j].f));
+      }
     }
     reduce_rows<G * H>(ps, b);  // row j: b[h] = score partial of (edge tb + j, head h)
   }
@@ -249,12 +309,20 @@ __device__ __forceinline__ void fwd_group(const Params& p, const Edge (&r)[G], c
       m[h] = mn[h];
       s_row[h] *= corr[h];
       sa_row[h] *= corr[h];
+      if constexpr (ALIGNN_LG3_PK) {
+        scale_pk(accS[h], corr[h]);
+      } else {
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) accS[h][i] *= corr[h];
+        for (int i = 0; i < VPL; ++i) accS[h][i] *= corr[h];
+      }
     }
-    const float cl = own<H>(corr, hl);
+    const float cl = ALIGNN_LG3_PK ? sel_head<H>(corr, mk) : own<H>(corr, hl);
+    if constexpr (ALIGNN_LG3_PK) {
+      scale_pk(accV, cl);
+    } else {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) accV[i] *= cl;
+      for (int i = 0; i < VPL; ++i) accV[i] *= cl;
+    }
   }
   float ed[H];
 #pragma unroll
@@ -270,12 +338,20 @@ __device__ __forceinline__ void fwd_group(const Params& p, const Edge (&r)[G], c
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       e[h] = readlane_f(ed[h], 16 * j);
+      if constexpr (ALIGNN_LG3_PK) {
+        axpy_pk(accS[h], e[h], r[j].f);
+      } else {
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(e[h], r[j].f[i], accS[h][i]);
+        for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(e[h], r[j].f[i], accS[h][i]);
+      }
     }
-    const float el = own<H>(e, hl);
+    const float el = ALIGNN_LG3_PK ? sel_head<H>(e, mk) : own<H>(e, hl);
+    if constexpr (ALIGNN_LG3_PK) {
+      axpy_pk(accV, el, r[j].v);
+    } else {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, r[j].v[i], accV[i]);
+      for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, r[j].v[i], accV[i]);
+    }
   }
 }
 
@@ -313,7 +389,12 @@ void lg3_fwd_kernel(Params p) {
     for (int h = 0; h < H; ++h) {
       float t[VPL];
       vload(p.U + (d * H + h) * D + j0, t);
-      vstore(uv + h * RS + j0, t);
+      if constexpr (ALIGNN_LG3_PK && H % 2 == 0) {
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) uv[pk_slot(h, i, lane)] = t[i];
+      } else {
+        vstore(uv + h * RS + j0, t);
+      }
     }
 #pragma unroll
     for (int h = 0; h < H; ++h) c[h] = 0.f;
@@ -407,15 +488,31 @@ __device__ __forceinline__ void bwd_group(const Params& p, const Edge (&r)[G], c
       qk[j] = dot4(q, r[j].k);
       gv[j] = dot4(go, r[j].v);
     }
+    if constexpr (ALIGNN_LG3_PK && H % 2 == 0) {
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float u[VPL], vd[VPL];
-      vload(uv + h * RS + j0, u);
-      vload(uv + (H + h) * RS + j0, vd);
+      for (int hp = 0; hp < H / 2; ++hp) {
+        const f2 mk2 = {mk[2 * hp], mk[2 * hp + 1]};
 #pragma unroll
-      for (int j = 0; j < G; ++j) {
-        ps[j * H + h] = fmaf(mk[h], qk[j], dot4(u, r[j].f));
-        pd[j * H + h] = fmaf(mk[h], gv[j], dot4(vd, r[j].f));
+        for (int j = 0; j < G; ++j) {
+          const f2 a = dot4_pair(uv + hp * 2 * RS, lane, r[j].f, mk2, qk[j]);
+          const f2 b = dot4_pair(uv + (H + 2 * hp) * RS, lane, r[j].f, mk2, gv[j]);
+          ps[j * H + 2 * hp] = a.x;
+          ps[j * H + 2 * hp + 1] = a.y;
+          pd[j * H + 2 * hp] = b.x;
+          pd[j * H + 2 * hp + 1] = b.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float u[VPL], vd[VPL];
+        vload(uv + h * RS + j0, u);
+        vload(uv + (H + h) * RS + j0, vd);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          ps[j * H + h] = fmaf(mk[h], qk[j], dot4(u, r[j].f));
+          pd[j * H + h] = fmaf(mk[h], gv[j], dot4(vd, r[j].f));
+        }
       }
     }
     reduce_rows<G * H>(ps, bs);
@@ -450,12 +547,20 @@ __device__ __forceinline__ void bwd_group(const Params& p, const Edge (&r)[G], c
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       e[h] = readlane_f(bs[h], 16 * j);
+      if constexpr (ALIGNN_LG3_PK) {
+        axpy_pk(sz[h], e[h], r[j].f);
+      } else {
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(e[h], r[j].f[i], sz[h][i]);
+        for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(e[h], r[j].f[i], sz[h][i]);
+      }
     }
-    const float dzl = own<H>(e, hl);
+    const float dzl = ALIGNN_LG3_PK ? sel_head<H>(e, mk) : own<H>(e, hl);
+    if constexpr (ALIGNN_LG3_PK) {
+      axpy_pk(dqa, dzl, r[j].k);
+    } else {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, r[j].k[i], dqa[i]);
+      for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, r[j].k[i], dqa[i]);
+    }
   }
 }
 
@@ -495,11 +600,19 @@ void lg3_bwd_dst_kernel(Params p) {
       if (p.wbar) vload(p.wbar + j0, wb);
 #pragma unroll
       for (int h = 0; h < H; ++h) {
-        float t[VPL];
+        float t[VPL], w[VPL];
         vload(p.U + (d * H + h) * D + j0, t);
-        vstore(uv + h * RS + j0, t);
-        vload(p.Vd + (d * H + h) * D + j0, t);
-        vstore(uv + (H + h) * RS + j0, t);
+        vload(p.Vd + (d * H + h) * D + j0, w);
+        if constexpr (ALIGNN_LG3_PK && H % 2 == 0) {
+#pragma unroll
+          for (int i = 0; i < VPL; ++i) {
+            uv[pk_slot(h, i, lane)] = t[i];
+            uv[H * RS + pk_slot(h, i, lane)] = w[i];
+          }
+        } else {
+          vstore(uv + h * RS + j0, t);
+          vstore(uv + (H + h) * RS + j0, w);
+        }
       }
       const float pc = vdot(wb, q), pc2 = vdot(wb, go), pdl = vdot(go, op);
 #pragma unroll

@@ -84,7 +84,7 @@ def main():
         b = mp_like_batch(a.batch, lg_offset=lg_offset).to("cuda")
         E, T = b.edge_index.size(1), b.lg_edge_index.size(1)
         from alignn_mi355x.engine import BatchCache
-        lg = BatchCache._compact(ops.GraphCSR(b.lg_edge_index, E), b.lg_edge_index, E)
+        lg = BatchCache._line_graph(b.lg_edge_index, E, True)
         nl = lg.n  # line-graph nodes after compaction to the bonds with line-graph edges
         xa = torch.empty_like(b.lg_edge_attr)
         ops.gather_rows(b.lg_edge_attr, lg.perm_dst, xa)
