@@ -188,6 +188,21 @@ __device__ __forceinline__ float rows_max4(float x) {
   return fmaxf(f_bits(r[0]), f_bits(r[1]));
 }
 
+// Group maxima of four row-distributed per-head values (row j = edge j): the transpose-reduction
+// pattern (two value pairs per lane swap) instead of four separate row reductions, which each copy
+// their operand twice for the in-place swaps.  Head h's maximum over the four rows ends in row h;
+// returned as wave-uniform values.  Exact (max).
+__device__ __forceinline__ void group_max4(const float (&z)[4], float (&g)[4]) {
+  auto a = __builtin_amdgcn_permlane32_swap(u_bits(z[0]), u_bits(z[2]), false, false);
+  const float t0 = fmaxf(f_bits(a[0]), f_bits(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(u_bits(z[1]), u_bits(z[3]), false, false);
+  const float t1 = fmaxf(f_bits(b[0]), f_bits(b[1]));
+  auto c = __builtin_amdgcn_permlane16_swap(u_bits(t0), u_bits(t1), false, false);
+  const float u = fmaxf(f_bits(c[0]), f_bits(c[1]));
+#pragma unroll
+  for (int h = 0; h < 4; ++h) g[h] = readlane_f(u, 16 * h);
+}
+
 // Transpose-reduction (tconv.hip reduce_rows): value r*(N/4)+i ends in row r of b[i].
 template <int N>
 __device__ __forceinline__ void reduce_rows(const float (&v)[N], float (&b)[N / 4]) {
@@ -251,6 +266,32 @@ __device__ __forceinline__ void store_edge_heads(float* __restrict__ out, int64_
 template <int NR>
 struct Occ { static constexpr int wpe = NR == 1 ? ALIGNN_LG3_WPE1 : ALIGNN_LG3_WPE2; };
 
+// Four groups in flight (bf16 rows: a group's loads take half the registers of fp32, so four cost
+// what two do in fp32): fixed register names r0..r3, each refilled four groups ahead right after it
+// is consumed; an exit check after every group (the loads already issued are simply not waited
+// for), so a segment runs no fully masked groups beyond its last.  ra arrives holding group 0.
+#define ALIGNN_LG3_RING4_BODY(LOAD, GRP)                                                   \
+  do {                                                                                   \
+    R r1[G], r2[G], r3[G];                                                               \
+    LOAD(r1, beg + G);                                                                   \
+    LOAD(r2, beg + 2 * G);                                                               \
+    LOAD(r3, beg + 3 * G);                                                               \
+    for (int32_t tb = beg;; tb += 4 * G) {                                               \
+      GRP(ra, tb);                                                                       \
+      LOAD(ra, tb + 4 * G);                                                              \
+      if (tb + G >= end) break;                                                          \
+      GRP(r1, tb + G);                                                                   \
+      LOAD(r1, tb + 5 * G);                                                              \
+      if (tb + 2 * G >= end) break;                                                      \
+      GRP(r2, tb + 2 * G);                                                               \
+      LOAD(r2, tb + 6 * G);                                                              \
+      if (tb + 3 * G >= end) break;                                                      \
+      GRP(r3, tb + 3 * G);                                                               \
+      LOAD(r3, tb + 7 * G);                                                              \
+      if (tb + 4 * G >= end) break;                                                      \
+    }                                                                                    \
+  } while (0)
+
 // =============================================================================================
 // Forward: aggV = sum alpha' V_src, S[h] = sum alpha'_h f_t (normalised), sumA, mstat, den
 // =============================================================================================
@@ -295,11 +336,23 @@ __device__ __forceinline__ void fwd_group(const Params& p, const Edge (&r)[G], c
   float z[H];
   bool grow = false;
   float mn[H];
+  if constexpr (ALIGNN_LG3_PK && H == 4) {
+    float gm[4];
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    z[h] = rv ? (b[h] + c[h]) * scale : -INFINITY;
-    mn[h] = fmaxf(m[h], rows_max4(z[h]));
-    grow |= mn[h] != m[h];
+    for (int h = 0; h < H; ++h) z[h] = rv ? (b[h] + c[h]) * scale : -INFINITY;
+    group_max4(z, gm);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      mn[h] = fmaxf(m[h], gm[h]);
+      grow |= mn[h] != m[h];
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      z[h] = rv ? (b[h] + c[h]) * scale : -INFINITY;
+      mn[h] = fmaxf(m[h], rows_max4(z[h]));
+      grow |= mn[h] != m[h];
+    }
   }
   if (grow) {  // wave-uniform: rescale only when some running maximum moved
     float corr[H];
@@ -424,6 +477,9 @@ void lg3_fwd_kernel(Params p) {
         if (tb + G >= end) break;
         load_group<BF>(ra, p, tb + G, last, j0);
       }
+    } else if constexpr (NR == 4) {
+      auto ld = [&](R (&r)[G], int32_t t) { load_group<BF>(r, p, t, last, j0); };
+      ALIGNN_LG3_RING4_BODY(ld, grp);
     } else {
       // one exit: pairs of groups (an odd count ends with a fully masked group, exactly 0)
       R rb[G];
@@ -644,6 +700,9 @@ void lg3_bwd_dst_kernel(Params p) {
         if (tb + G >= end) break;
         load_group<BF>(ra, p, tb + G, last, j0);
       }
+    } else if constexpr (NR == 4) {
+      auto ld = [&](R (&r)[G], int32_t t) { load_group<BF>(r, p, t, last, j0); };
+      ALIGNN_LG3_RING4_BODY(ld, grp);
     } else {
       R rb[G];
       load_group<BF>(rb, p, beg + G, last, j0);
@@ -677,13 +736,19 @@ void lg3_bwd_dst_kernel(Params p) {
 #define ALIGNN_LG3_NR_BWD 2
 #endif
 
+// bf16 rows: groups in flight (4: the ring above; 2: as fp32)
+#ifndef ALIGNN_LG3_NR_BF
+#define ALIGNN_LG3_NR_BF 4
+#endif
 template <int H, bool DROP, bool BF>
 static void launch_fwd_h(const Params& p, hipStream_t s) {
-  launch((lg3_fwd_kernel<H, ALIGNN_LG3_NR_FWD, DROP, BF>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+  constexpr int NR = BF ? ALIGNN_LG3_NR_BF : ALIGNN_LG3_NR_FWD;
+  launch((lg3_fwd_kernel<H, NR, DROP, BF>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
 }
 template <int H, bool DROP, bool BF>
 static void launch_bwd_h(const Params& p, hipStream_t s) {
-  launch((lg3_bwd_dst_kernel<H, ALIGNN_LG3_NR_BWD, DROP, BF>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+  constexpr int NR = BF ? ALIGNN_LG3_NR_BF : ALIGNN_LG3_NR_BWD;
+  launch((lg3_bwd_dst_kernel<H, NR, DROP, BF>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
 }
 
 #define ALIGNN_LG3_DISPATCH_H(FN, H_, DROP_, BF_, ...)   \
