@@ -154,6 +154,7 @@ _SIGNATURES = {
     "alignn_plan_check_ptrs": ([c_vp, c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
     "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
+    "alignn_set_i64": ([c_vp, c_i64, c_vp], c_i32),
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                           c_vp, c_vp], c_i32),

@@ -281,7 +281,8 @@ class FusedTrainer:
             pass
 
     def _replay(self, seed: int) -> torch.Tensor:
-        self._seed_dev.fill_(int(seed) & (2**63 - 1))
+        check(_lib.lib().alignn_set_i64(self._seed_dev.data_ptr(), int(seed) & (2**63 - 1), ops.stream_ptr()),
+              "alignn_set_i64")
         g_fb, g_up, _, plans = self._graph
         if plans:
             check(_lib.lib().alignn_plan_replay(plans[0], ops.stream_ptr()), "alignn_plan_replay")

@@ -93,6 +93,12 @@ __global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ x, in
     x[i] = v;
 }
 
+// One int64 (the step seed a replayed plan's dropout/jitter kernels read), written by one lane
+// through a vector store.
+__global__ __launch_bounds__(64) void set_i64_kernel(int64_t* __restrict__ x, int64_t v) {
+  if (threadIdx.x == 0) x[0] = v;
+}
+
 __global__ __launch_bounds__(256) void copy_f32_kernel(float* __restrict__ dst, const float* __restrict__ src,
                                                        int64_t n) {
   const int64_t n4 = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) ? 0 : n / 4;
@@ -325,6 +331,13 @@ extern "C" int alignn_fill_f32(float* x, int64_t n, float value, void* stream) {
   if (n == 0) return ALIGNN_OK;
   launch(fill_f32_kernel, dim3(blocks_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, n, value);
   ALIGNN_LAUNCH_CHECK("fill_f32_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_set_i64(int64_t* x, int64_t value, void* stream) {
+  if (!x) return ALIGNN_E_BAD_SHAPE;
+  launch(set_i64_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), x, value);
+  ALIGNN_LAUNCH_CHECK("set_i64_kernel");
   return ALIGNN_OK;
 }
 

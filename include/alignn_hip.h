@@ -504,6 +504,8 @@ int alignn_knn_select_weights(const float* G, int64_t ldg, const float* r, int64
  *   that a plan recorded during that capture holds every kernel (other == 0).
  * alignn_fill_f32 / alignn_copy_f32: x[0:n] = value; dst[0:n] = src[0:n] (plan-recordable
  *   replacements for torch's zero_/copy_ inside the step).
+ * alignn_set_i64: x[0] = value on the stream — the per-step device seed written before a plan
+ *   replay (the reference draws fresh dropout masks every step, train.py:655).
  * ---------------------------------------------------------------------------------------- */
 int alignn_plan_begin(void* stream);
 int alignn_plan_note_wait(void* dst_stream, void* src_stream);
@@ -525,6 +527,7 @@ int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, int64_t n, 
 int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);
+int alignn_set_i64(int64_t* x, int64_t value, void* stream);
 
 #ifdef __cplusplus
 }

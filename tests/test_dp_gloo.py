@@ -120,6 +120,10 @@ class _FakeLib:
     def __init__(self, trainer, grad, log):
         self.tr, self.grad, self.log = trainer, grad, log
 
+    def alignn_set_i64(self, ptr, value, stream):  # the per-step device seed (no GPU here)
+        self.log.append("seed")
+        return 0
+
     def alignn_plan_replay(self, plan, stream):
         if plan == 1:
             self.log.append("fb")
@@ -185,7 +189,7 @@ def test_fused_trainer_grad_hook_between_plan_phases_world2(tmp_path):
     mp.spawn(_trainer_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     r = [torch.load(tmp_path / f"t{i}.pt", weights_only=True) for i in range(world)]
     for x in r:
-        assert x["log"] == ["fb", "hook", "update"], x["log"]
+        assert x["log"] == ["seed", "fb", "hook", "update"], x["log"]
         assert x["steps"] == 1
     n = r[0]["before"].numel()
     mean = sum(torch.randn(n, generator=torch.Generator().manual_seed(7 + i)) * (2.0 + i) for i in range(world)) / world
