@@ -34,7 +34,10 @@ constexpr int EB_HL = 16;       // max H * L
 constexpr int EB_CHUNK = 128;   // edges staged in LDS at a time
 // fixed grid (the partial-sum order does not depend on the device): 4 workgroups per CU of an
 // MI355X (22.5 KB LDS each), so segment-start loads of one hide behind the others' edge loops
-constexpr int EB_BLOCKS = 1024;
+#ifndef ALIGNN_EB_BLOCKS
+#define ALIGNN_EB_BLOCKS 1024
+#endif
+constexpr int EB_BLOCKS = ALIGNN_EB_BLOCKS;
 constexpr int EB_LMAX = ALIGNN_ENCBWD_MAX_LAYERS;
 
 struct EncBwdParams {
