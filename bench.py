@@ -500,16 +500,15 @@ def main():
         return
     r = measure(args, dev, rank, world, B, args.lg_offset, args.precision, args.steps, args.warmup,
                 roofline=not args.no_roofline)
-    e2e, store = None, None
-    if args.e2e > 0:
-        store, t_build = build_store(args, dev, rank)
-        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
-    _release(r)
 
     # secondary lines of the default run (one GPU): the same step with the corrected line-graph
     # wiring (SURVEY §8d "also report num_edges": no compaction, every bond active) and config C3
-    # (B = 256, bf16 matrix-core inputs, its own dominant-kernel roofline).  Never `value`.
-    secondary = None
+    # (B = 256, bf16 matrix-core inputs, its own dominant-kernel roofline).  Never `value`.  The
+    # pre-collated steps are all measured before the e2e dataset is built, each with at most one other
+    # captured trainer alive (the C3 step measured with the dataset resident and after the e2e loops
+    # read 8 % low: 16,900 vs 18,400-18,500 graphs/s; the corrected wiring with two other trainers
+    # alive 5,100 vs 5,580).
+    secondary, c3 = None, None
     if world == 1 and not args.no_secondary:
         secondary = {}
         sec_steps, sec_warm = max(5, args.steps // 2), max(2, args.warmup // 2)
@@ -527,10 +526,17 @@ def main():
                           f"softmax/LayerNorm), lg_offset={args.lg_offset}",
                 "value": round(c3["value"], 2), "unit": "graphs/s", "ms_per_step": round(c3["ms_per_step"], 3),
                 "steps": sec_steps, "roofline": c3["roofline"], "step_roofline": c3["step_roofline"]}
-            if store is not None:
-                # config C5 at N = 1: the B = 256 bf16 step over the ~10k-graph HBM dataset
-                secondary["c5_e2e_b256_bf16"] = end_to_end(args, store, t_build, c3["trainer"], 256, dev, rank, world)
-            _release(c3)
+
+    e2e, store = None, None
+    if args.e2e > 0:
+        store, t_build = build_store(args, dev, rank)
+        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
+        if c3 is not None:
+            # config C5 at N = 1: the B = 256 bf16 step over the ~10k-graph HBM dataset
+            secondary["c5_e2e_b256_bf16"] = end_to_end(args, store, t_build, c3["trainer"], 256, dev, rank, world)
+    _release(r)
+    if c3 is not None:
+        _release(c3)
     store = None
 
     if rank == 0:
