@@ -105,6 +105,8 @@ def apply_settings(args, model):
             ops.GraphCSR.SORT_BY_DEGREE = bool(int(v))
         elif k == "heavy_threshold":
             ops.GraphCSR.HEAVY_THRESHOLD = int(v)
+        elif k == "loader_priority":
+            args.loader_priority = int(v)
         elif k == "main_priority":
             args.main_priority = int(v)
         elif k == "splitk_combine":
@@ -203,7 +205,9 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
     from alignn_mi355x.engine import prepare_batch
 
     rng = np.random.default_rng(1234 + rank)
-    loader = torch.cuda.Stream(device=dev)
+    # high priority: the loader's small collate/CSR kernels (and the host syncs of batch preparation
+    # that wait for them) are dispatched ahead of the running step's queued kernels
+    loader = torch.cuda.Stream(device=dev, priority=getattr(args, "loader_priority", -1))
 
     def make():
         with torch.cuda.stream(loader):
