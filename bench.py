@@ -205,9 +205,14 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
     from alignn_mi355x.engine import prepare_batch
 
     rng = np.random.default_rng(1234 + rank)
-    # high priority: the loader's small collate/CSR kernels (and the host syncs of batch preparation
-    # that wait for them) are dispatched ahead of the running step's queued kernels
-    loader = torch.cuda.Stream(device=dev, priority=getattr(args, "loader_priority", -1))
+    # B >= 128: a high-priority loader stream, so the small collate/CSR kernels (and the host syncs of
+    # batch preparation that wait for them) are dispatched ahead of the running step's queued kernels
+    # (B = 256 bf16: 12,160-12,240 -> 16,110-16,150 graphs/s); at B = 32 the same costs 22-35 %
+    # (8,027-8,077 -> 5,226-6,286; profiles/r02/v43_ab_loader_priority_*.log)
+    prio = getattr(args, "loader_priority", None)
+    if prio is None:
+        prio = -1 if B >= 128 else 0
+    loader = torch.cuda.Stream(device=dev, priority=prio)
 
     def make():
         with torch.cuda.stream(loader):
