@@ -105,6 +105,9 @@ def apply_settings(args, model):
             ops.GraphCSR.SORT_BY_DEGREE = bool(int(v))
         elif k == "heavy_threshold":
             ops.GraphCSR.HEAVY_THRESHOLD = int(v)
+        elif k == "atom_xcd_chunk":
+            from alignn_mi355x import engine as _engine
+            _engine.BatchCache.ATOM_XCD_CHUNK = int(v)
         elif k == "loader_priority":
             args.loader_priority = int(v)
         elif k == "main_priority":

@@ -113,6 +113,10 @@ class FlatViews:
 class BatchCache:
     """CSR lists of the atom graph and the line graph, target-sorted angle inputs, ptr."""
 
+    # the atom graph's attention kernels take four targets per workgroup: XCD-contiguous item ranges
+    # interleaved in chunks of four (1: one item at a time, as for the line graph)
+    ATOM_XCD_CHUNK = 4
+
     def __init__(self, batch, validate: bool = True):
         x = batch.x
         if not x.is_cuda:
@@ -121,6 +125,7 @@ class BatchCache:
         self.E = int(batch.edge_index.size(1))
         self.T = int(batch.lg_edge_index.size(1))
         self.ag = ops.GraphCSR(batch.edge_index, self.N)
+        self.ag.xcd_chunk = self.ATOM_XCD_CHUNK
         if validate:
             self.ag.check_indices("edge_index")
         self.lg = self._line_graph(batch.lg_edge_index, self.E, validate)

@@ -507,7 +507,7 @@ class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
     __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
-                 "n_full", "cmap", "_dst_src")
+                 "n_full", "cmap", "_dst_src", "xcd_chunk")
 
     # in-degree above which a target node gets a 4-wave workgroup (LDS merge of the waves); below it
     # one wave walks the node's edges.  256: every node of the MP-like line graph (in-degree <= 132
@@ -547,6 +547,7 @@ class GraphCSR:
         self.err = torch.zeros(1, **i32)
         self._sched = None
         self._dst_src = None
+        self.xcd_chunk = 1   # work items per workgroup of the kernels that read this graph's list
         self.rows = None     # compacted graph: int32 ids of its nodes in the full node set
         self.n_full = n
         self.cmap = None     # compacted graph: int32 [n_full] full row -> node id, -1 if inactive
@@ -595,9 +596,13 @@ class GraphCSR:
                 for x in range(self.XCDS):
                     sel = lit[(lit >= bounds[x]) & (lit < bounds[x + 1])]
                     parts.append(sel[torch.sort(deg[sel.long()], descending=True, stable=True).indices].tolist())
+                # chunks of xcd_chunk items: kernels taking several items per workgroup (the atom
+                # graph's four-target workgroups) keep one workgroup's items in one range
+                c = max(1, int(self.xcd_chunk))
                 order, j = [], 0
-                while any(j < len(q) for q in parts):
-                    order += [q[j] for q in parts if j < len(q)]
+                while any(j * c < len(q) for q in parts):
+                    for q in parts:
+                        order += q[j * c:(j + 1) * c]
                     j += 1
                 lit = torch.tensor(order, dtype=torch.int32)
             light = torch.cat([lit, idx[light_mask & (deg == 0)]]).to(self.off_dst.device)
