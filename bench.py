@@ -35,7 +35,13 @@ BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no spars
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="GPUs (= ranks) of one node.  Without a torch.distributed launcher in the environment "
+                        "(no WORLD_SIZE) and N > 1, bench.py starts the N rank processes itself "
+                        "(torch.distributed.run, 127.0.0.1) before anything touches the GPU")
+    p.add_argument("--dry-run", action="store_true",
+                   help="no GPU: every rank runs only the data-parallel exchange (gloo all_reduce of a flat "
+                        "gradient of the model's size) — a CPU rehearsal of the rank plumbing")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=32, help="graphs per GPU (BASELINE config 2: 32)")
@@ -403,30 +409,22 @@ def ensemble_bench(args, dev, rank, world):
     headline (barrier + synchronize, max over ranks); value = members x B x steps / time."""
     import alignn_mi355x as A
     from alignn_mi355x import dp
-    from alignn_mi355x.ensemble import EnsemblePredictor, ShardedEnsemble
-    from alignn_mi355x.synthetic import mp_like_batch
+    from alignn_mi355x.ensemble import EnsemblePredictor, EnsembleTrainer, ShardedEnsemble
+    from alignn_mi355x.synthetic import ensemble_member_batch, mp_like_batch
 
     M, B = args.ensemble, args.batch
-    mine = dp.members_of_rank(M, world, rank)
-    members = []
-    for i in mine:
-        torch.manual_seed(dp.member_seed(args.seed, i))          # train.py:2053 (weights per member)
+
+    def build():
         model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                           args.dropout), 2).to(dev)
-        tr = A.FusedTrainer(model, precision=args.precision, **apply_settings(args, model))
-        # the member's own graphs (fold i % 5 of the dataset, train.py:2054): a disjoint synthetic slice
-        batch = mp_like_batch(B, first=100000 * (1 + dp.member_fold(i, 5)) + 1000 * i, lg_offset=args.lg_offset).to(dev)
-        tr.capture(batch)
-        stream = torch.cuda.Stream(device=dev)
-        members.append((i, model, tr, batch, stream))
+        apply_settings(args, model)
+        return model
 
-    def step(k):
-        for i, _, tr, batch, stream in members:
-            stream.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(stream):
-                tr.step(batch, seed=dp.member_seed(args.seed, i) * 1000003 + k)
-        for *_, stream in members:
-            torch.cuda.current_stream(dev).wait_stream(stream)
+    # the member's own graphs (fold i % 5 of the dataset, train.py:2054): a disjoint synthetic slice
+    ens = EnsembleTrainer(M, build, lambda i, fold: ensemble_member_batch(B, i, fold, args.lg_offset).to(dev),
+                          world=world, rank=rank, seed=args.seed, precision=args.precision)
+    mine = ens.ids
+    step = ens.step
 
     for k in range(args.warmup):
         step(k)
@@ -443,11 +441,11 @@ def ensemble_bench(args, dev, rank, world):
     if world > 1:
         dt = dp.max_over_ranks(dt, dev)
     # the members' eval pass: heads of every member on one batch, gathered to rank 0, moment mix
-    for _, model, tr, _, _ in members:
-        tr.release_capture()
+    ens.release()
+    models = ens.models()
+    for model in models:
         model.eval()
     eval_batch = mp_like_batch(B, first=900000, lg_offset=args.lg_offset).to(dev)
-    models = [m for _, m, *_ in members]
     t1 = time.perf_counter()
     if world > 1:
         mixed = ShardedEnsemble(models, M, hidden=args.hidden).predict_batch(eval_batch)
@@ -470,13 +468,79 @@ def _release(r):
     torch.cuda.empty_cache()
 
 
+def launch_ranks(args) -> int:
+    """``--gpus N`` run without a launcher: start N ranks with torch.distributed.run on this node
+    (rendezvous on 127.0.0.1, a free port), each running this script with the same arguments, and
+    return their exit status (non-zero if any rank failed or fewer than N could start).  Nothing
+    here initialises the GPU (device_count does not on this image), so no process that touched it
+    ever starts another."""
+    import socket
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"[bench] --gpus {n}: only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only (RCCL across processes)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, _cpu_threads() // n)))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank, world):
+    """CPU rehearsal of the data-parallel step's exchange: every rank all_reduces (gloo) a flat
+    gradient of the model's size each step; timed like the real bench (barrier both sides, max over
+    ranks) and reported with the world size the ranks agreed on."""
+    from alignn_mi355x.dp import grad_allreduce_hook, max_over_ranks
+    from alignn_mi355x.layout import AlignnConfig, offsets
+    _, total, _ = offsets(AlignnConfig(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads, 0.0), True)
+    grad = torch.full((total,), float(rank + 1))
+    hook = grad_allreduce_hook(world)
+    for _ in range(args.warmup):
+        hook(grad)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        grad.fill_(float(rank + 1))
+        hook(grad)
+    dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, torch.device("cpu"))
+    ok = bool(torch.all(grad == (world + 1) / 2.0))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(args.batch * world * args.steps / dt, 2),
+                          "unit": "graphs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                          "data": "dry run: no GPU, gloo all_reduce of the flat gradient only",
+                          "config": {"workload": "DP exchange rehearsal", "global_batch": args.batch * world,
+                                     "parallelism": f"dp{world}", "grad_elems": total, "allreduce_ok": ok}}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.graph:
         args.launch = "graph"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+            return dry_run(args, rank, world)
+        raise SystemExit("[bench] --dry-run rehearses the multi-rank exchange: use --gpus N with N > 1")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

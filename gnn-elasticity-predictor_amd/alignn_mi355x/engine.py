@@ -256,15 +256,22 @@ def prepare_batch(batch, stream: Optional[torch.cuda.Stream] = None, validate: b
             bc.signature()
             bc.device_tensors()
     ev = torch.cuda.Event()
-    ev.record(stream if stream is not None else torch.cuda.current_stream())
+    s = stream if stream is not None else torch.cuda.current_stream()
+    ev.record(s)
     try:
         batch._alignn_ready = ev
+        batch._alignn_adopted = {s.cuda_stream}
     except AttributeError:
         pass
     return bc
 
 
 def batch_cache(batch, validate: bool = True) -> BatchCache:
+    """The batch's device cache (built on first use).  A batch prepared on another stream
+    (:func:`prepare_batch`) is adopted by the current stream first: it waits for the preparation's
+    event, and every buffer of the batch and its cache is marked as used here, so the caching
+    allocator cannot hand them out again before this stream's reads ran — on every path that reads
+    the batch (replay, re-binding, eager steps, the module API)."""
     bc = getattr(batch, "_alignn_cache", None)
     if bc is None:
         bc = BatchCache(batch, validate)
@@ -272,7 +279,32 @@ def batch_cache(batch, validate: bool = True) -> BatchCache:
             batch._alignn_cache = bc
         except AttributeError:
             pass
+    else:
+        adopt(batch, bc)
     return bc
+
+
+def adopt(batch, bc: Optional[BatchCache] = None) -> None:
+    """Current stream waits for ``batch``'s preparation event and records its use of the batch's
+    buffers (once per stream; no-op for batches prepared on the current stream or never prepared,
+    and inside a graph capture, whose stream is ordered after the eager stream that adopted it)."""
+    ev = getattr(batch, "_alignn_ready", None)
+    if ev is None or torch.cuda.is_current_stream_capturing():
+        return
+    bc = bc if bc is not None else getattr(batch, "_alignn_cache", None)
+    dev = batch.x.device
+    s = torch.cuda.current_stream(dev)
+    seen = batch.__dict__.setdefault("_alignn_adopted", set())
+    if s.cuda_stream in seen:
+        return
+    seen.add(s.cuda_stream)
+    s.wait_event(ev)
+    tensors = [v for v in vars(batch).values() if torch.is_tensor(v)]
+    if bc is not None:
+        tensors += bc.device_tensors()
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(s)
 
 
 def site_seed(seed: int, site: int) -> int:

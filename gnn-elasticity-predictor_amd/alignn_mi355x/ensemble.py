@@ -213,6 +213,69 @@ class ShardedEnsemble:
         return torch.cat(out)
 
 
+class EnsembleTrainer:
+    """Ensemble training sharded member-per-rank.
+
+    The reference trains its members one after the other on one device (train.py:2052-2095):
+    member i is seeded ``seed + 1007 i`` (train.py:2053, before the model is built) and trains against
+    fold ``i % num_folds`` (:2054).  Here member i lives on rank ``i % world`` (dp.members_of_rank);
+    a rank's members each get their own :class:`FusedTrainer` (own execution context, workspaces and
+    device step seed), captured as a native launch plan on its own batch, and :meth:`step` issues
+    every local member's step at once, one HIP stream per member, so their latency-bound attention
+    kernels share the CUs.  Members never communicate while training.
+
+    ``build_model()`` is called right after ``torch.manual_seed(member_seed(seed, i))`` and must return
+    the member's model on the device; ``batch_for(i, fold)`` returns member i's (resident) batch."""
+
+    def __init__(self, num_members: int, build_model, batch_for, world: int = 1, rank: int = 0, seed: int = 42,
+                 num_folds: int = 5, precision: Optional[str] = None, capture: bool = True, concurrent: bool = True,
+                 trainer_kw: Optional[Dict] = None, members: Optional[Sequence[int]] = None):
+        from . import dp
+        from .trainer import FusedTrainer
+        self.num_members, self.seed = int(num_members), int(seed)
+        self.ids = list(members) if members is not None else dp.members_of_rank(num_members, world, rank)
+        self.members = []
+        for i in self.ids:
+            torch.manual_seed(dp.member_seed(seed, i))
+            model = build_model()
+            tr = FusedTrainer(model, precision=precision, **(trainer_kw or {}))
+            batch = batch_for(i, dp.member_fold(i, num_folds))
+            if capture:
+                tr.capture(batch)
+            self.members.append((i, model, tr, batch))
+        dev = self.members[0][1]._ensure_flat().flat.device if self.members else None
+        self.streams = [torch.cuda.Stream(device=dev) if concurrent else None for _ in self.members]
+
+    def step_seed(self, i: int, k: int) -> int:
+        """Host seed of member i's k-th step (a function of the member, not of its placement)."""
+        from . import dp
+        return dp.member_seed(self.seed, i) * 1000003 + int(k)
+
+    def step(self, k: int) -> None:
+        """Step k of every local member (concurrently: one stream each, joined at the end)."""
+        if not self.members:
+            return
+        dev = self.members[0][3].x.device
+        main = torch.cuda.current_stream(dev)
+        for (i, _, tr, batch), s in zip(self.members, self.streams):
+            if s is None:
+                tr.step(batch, seed=self.step_seed(i, k))
+                continue
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                tr.step(batch, seed=self.step_seed(i, k))
+        for s in self.streams:
+            if s is not None:
+                main.wait_stream(s)
+
+    def models(self) -> List:
+        return [m for _, m, _, _ in self.members]
+
+    def release(self) -> None:
+        for _, _, tr, _ in self.members:
+            tr.release_capture()
+
+
 # ------------------------------------------------------------------------------------------------
 # Calibration on the collected predictions (host, as in the reference)
 # ------------------------------------------------------------------------------------------------

@@ -44,12 +44,16 @@ class ExecContext:
     """What the launches of one engine (model) share: per-purpose scratch buffers, the side / aux
     streams for work off the critical path, and the device step seed its dropout kernels read.
 
-    Buffers are keyed by (purpose, device, dtype, stream role) — role "main" (whatever stream is
-    current), "side" or "aux" (this context's own streams) — so kernels on different streams never
-    share one, and a buffer is reused only in its stream's order.  A buffer grows on demand while
-    nothing is being recorded; during a launch-plan recording (:func:`recording`) growth is refused,
-    because earlier recorded launches hold the old buffer's address.  The trainer sizes them with
-    uncaptured warm-up steps of the same shapes first and owns them for as long as its plans live.
+    Buffers are keyed by (purpose, device, dtype, stream role).  In an engine-owned context the role
+    is "main" (whatever stream is current: a plan is recorded on a capture stream and replayed on
+    another), "side" or "aux" (this context's own streams); in the shared default context it is the
+    stream itself.  Kernels on different streams therefore never share one, and a buffer is reused
+    only in its stream's order.  A buffer grows on demand while nothing is being recorded; during a
+    launch-plan recording (:func:`recording`) growth is refused, because earlier recorded launches
+    hold the old buffer's address.  While a recorded plan is alive (:meth:`freeze`) a buffer is never
+    replaced either: an eager launch that needs more than a plan's buffer gets a separate one, so
+    the plan's addresses stay valid.  The trainer sizes them with uncaptured warm-up steps of the same
+    shapes first and owns them for as long as its plans live.
 
     ``fresh(purpose, ...)`` hands out a distinct buffer per call within one backward pass (reset by
     :meth:`new_pass`): for data written on one stream and read later on another (the gate/LayerNorm
@@ -63,6 +67,23 @@ class ExecContext:
         self._side = {}
         self._aux = {}
         self.step_seed: Optional[torch.Tensor] = None
+        self.frozen = 0       # live plans / graphs holding this context's buffers
+        self._eager = {}      # buffers of eager launches that outgrew a frozen buffer
+
+    def freeze(self) -> None:
+        """A recorded plan now holds this context's buffers: none may be replaced while it lives."""
+        self.frozen += 1
+
+    def thaw(self) -> None:
+        """A plan holding the buffers was released; with none left, eager overflow buffers become
+        the regular ones."""
+        self.frozen = max(0, self.frozen - 1)
+        if self.frozen == 0:
+            for k, t in self._eager.items():
+                cur = self.buf.get(k)
+                if cur is None or cur.numel() < t.numel():
+                    self.buf[k] = t
+            self._eager.clear()
 
     def side(self, device) -> torch.cuda.Stream:
         """A second stream per device for work off the critical path (weight gradients)."""
@@ -78,10 +99,12 @@ class ExecContext:
             self._aux[key] = torch.cuda.Stream(device=device)
         return self._aux[key]
 
-    def _role(self, device) -> str:
+    def _role(self, device):
         if torch.device(device).type != "cuda":
             return "main"
         cur = torch.cuda.current_stream(device).cuda_stream
+        if not self.owned:
+            return ("stream", cur)   # shared context: one buffer per stream (loader and main never share)
         key = _dkey(device)
         if key in self._side and self._side[key].cuda_stream == cur:
             return "side"
@@ -91,14 +114,23 @@ class ExecContext:
 
     def _take(self, k, n: int, device, dtype, zeroed: bool = False) -> torch.Tensor:
         cur = self.buf.get(k)
-        if cur is None or cur.numel() < n:
-            if _RECORDING:
-                raise RuntimeError(
-                    f"workspace {k[0]!r} ({self.name}) would grow to {n} elements while a launch plan is being "
-                    f"recorded (earlier recorded launches hold the old buffer): run an uncaptured step of the same "
-                    f"shapes first")
-            cur = (torch.zeros if zeroed else torch.empty)(max(n, 1), device=device, dtype=dtype)
-            self.buf[k] = cur
+        if cur is not None and cur.numel() >= n:
+            return cur
+        if _RECORDING:
+            raise RuntimeError(
+                f"workspace {k[0]!r} ({self.name}) would grow to {n} elements while a launch plan is being "
+                f"recorded (earlier recorded launches hold the old buffer): run an uncaptured step of the same "
+                f"shapes first")
+        alloc = torch.zeros if zeroed else torch.empty
+        if self.frozen:
+            # a live plan holds buf[k]'s address: this (eager) launch gets a buffer of its own
+            e = self._eager.get(k)
+            if e is None or e.numel() < n:
+                e = alloc(max(n, 1), device=device, dtype=dtype)
+                self._eager[k] = e
+            return e
+        cur = alloc(max(n, 1), device=device, dtype=dtype)
+        self.buf[k] = cur
         return cur
 
     def get(self, key: str, n: int, device, dtype=torch.float32, zeroed: bool = False) -> torch.Tensor:

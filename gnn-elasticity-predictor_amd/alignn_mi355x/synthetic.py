@@ -119,6 +119,12 @@ def mp_like_batch(num_graphs: int, first: int = 0, lg_offset: str = "num_nodes",
                                 lg_offset=lg_offset)
 
 
+def ensemble_member_batch(num_graphs: int, member: int, fold: int, lg_offset: str = "num_nodes") -> Batch:
+    """Member ``member``'s synthetic training batch: graphs of its fold (train.py:2054) — a slice
+    disjoint from every other member's and from the headline batches."""
+    return mp_like_batch(num_graphs, first=100000 * (1 + int(fold)) + 1000 * int(member), lg_offset=lg_offset)
+
+
 # LogTransformer statistics of the shipped ensemble (artifacts/ensemble/scaler_state.pt, SURVEY §2 #20)
 TARGET_LOG_MEANS = (4.3228, 3.5567)
 TARGET_LOG_STDS = (0.9051, 0.9405)

@@ -16,7 +16,7 @@ from torch import nn
 
 from . import _lib, ops, profiling
 from ._lib import check
-from .engine import MIN_LOGVAR_FLOOR, batch_cache, site_seed
+from .engine import MIN_LOGVAR_FLOOR, adopt, batch_cache, site_seed
 
 # batch fields a recorded step reads (train.py:547-573, :648-650); a re-bound batch is copied into
 # the captured batch's buffers field by field
@@ -103,6 +103,7 @@ class FusedTrainer:
                          sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward + loss + backward into the flat gradient buffer; returns the loss (device).
         sample_weights: per-graph KNN weights [B] (train.py:660-674), or None."""
+        adopt(batch)
         with ops.using(self.ctx):
             return self._forward_backward(batch, seed, training, sample_weights)
 
@@ -125,6 +126,7 @@ class FusedTrainer:
     def step(self, batch, seed: Optional[int] = None, sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         if seed is None:
             seed = int(torch.randint(0, 2**62, (1,)).item())
+        adopt(batch)   # a loader-prepared batch: wait for it and mark its buffers as used here (any path)
         if self._graph is not None and sample_weights is None:
             if self._graph[2] is batch or (self.rebind and self._rebind(batch)):
                 return self._replay(seed)
@@ -138,7 +140,7 @@ class FusedTrainer:
     def _rebind(self, batch) -> bool:
         """Copies ``batch`` into the captured batch's buffers (fields and device cache) when every
         size the recorded launches depend on matches; False (nothing copied) otherwise.  A batch
-        prepared on another stream (engine.prepare_batch) is waited for by event."""
+        prepared on another stream (engine.prepare_batch) was adopted by step() (engine.adopt)."""
         slot = self._graph[2]
         for k in BATCH_FIELDS:
             a, b = getattr(batch, k, None), getattr(slot, k, None)
@@ -148,22 +150,14 @@ class FusedTrainer:
             if a is not None and (a.shape != b.shape or a.dtype != b.dtype or a.device != b.device):
                 self.rebind_misses += 1
                 return False
-        main = torch.cuda.current_stream(self.st.flat.device)
-        ready = getattr(batch, "_alignn_ready", None)
-        if ready is not None:
-            main.wait_event(ready)
-        bc_new, bc_slot = batch_cache(batch), batch_cache(slot)
-        if bc_new.signature() != bc_slot.signature():
-            self.rebind_misses += 1
-            return False
-        pairs = [(getattr(slot, k), getattr(batch, k)) for k in BATCH_FIELDS
-                 if getattr(batch, k, None) is not None and getattr(batch, k).numel()]
-        ops.copy_many(pairs + bc_new.copy_pairs(bc_slot))   # one launch for the batch and its cache
-        if ready is not None:
-            # buffers made on the loader's stream and read here: not reusable before these copies ran
-            for t in [getattr(batch, k, None) for k in BATCH_FIELDS] + bc_new.device_tensors():
-                if t is not None and t.is_cuda:
-                    t.record_stream(main)
+        with ops.using(self.ctx):   # a cache built here uses the engine's workspaces, not the shared ones
+            bc_new, bc_slot = batch_cache(batch), batch_cache(slot)
+            if bc_new.signature() != bc_slot.signature():
+                self.rebind_misses += 1
+                return False
+            pairs = [(getattr(slot, k), getattr(batch, k)) for k in BATCH_FIELDS
+                     if getattr(batch, k, None) is not None and getattr(batch, k).numel()]
+            ops.copy_many(pairs + bc_new.copy_pairs(bc_slot))   # one launch for the batch and its cache
         self.rebinds += 1
         return True
 
@@ -250,6 +244,7 @@ class FusedTrainer:
                 _lib.lib().alignn_plan_destroy(pl)
             raise
         self._graph = (g_fb, g_up, batch, plans if keep else None)
+        self.ctx.freeze()   # the plans hold the workspaces' addresses: eager steps may not replace them
 
     def _held_ranges(self, batch, pool_id):
         """[lo, hi) device byte ranges this trainer holds for as long as a captured plan lives: its own
@@ -269,9 +264,11 @@ class FusedTrainer:
         return ranges
 
     def release_capture(self) -> None:
-        if self._graph is not None and self._graph[3]:
-            for pl in self._graph[3]:
-                _lib.lib().alignn_plan_destroy(pl)
+        if self._graph is not None:
+            if self._graph[3]:
+                for pl in self._graph[3]:
+                    _lib.lib().alignn_plan_destroy(pl)
+            self.ctx.thaw()
         self._graph = None
 
     def __del__(self):

@@ -64,3 +64,30 @@ def test_using_is_nested_and_thread_local():
         assert ops.current() is c1
     assert seen["t"] is not c1 and seen["t"] is not c2
     assert not ops.current().owned
+
+
+def test_frozen_context_never_replaces_a_plan_buffer():
+    """While a plan holds the buffers (freeze), an eager launch that needs more gets a separate
+    buffer; the plan's buffer keeps its address, and after thaw the larger one takes over."""
+    from alignn_mi355x import ops
+    ctx = ops.ExecContext("t")
+    a = ctx.get("gemm", 100, "cpu")
+    ctx.freeze()
+    big = ctx.get("gemm", 500, "cpu")
+    assert big.data_ptr() != a.data_ptr() and big.numel() >= 500
+    assert ctx.buf[next(k for k in ctx.buf if k[0] == "gemm")].data_ptr() == a.data_ptr()
+    assert ctx.get("gemm", 50, "cpu").data_ptr() == a.data_ptr()      # fits: the plan's buffer
+    assert ctx.get("gemm", 400, "cpu").data_ptr() == big.data_ptr()   # the eager overflow is reused
+    assert a.data_ptr() in {t.data_ptr() for t in ctx.tensors()}
+    ctx.thaw()
+    assert ctx.get("gemm", 500, "cpu").data_ptr() == big.data_ptr()
+
+
+def test_default_context_keys_buffers_by_stream():
+    """The shared default context keys its buffers by the stream itself (a loader stream and the
+    main stream never share a scratch buffer); an engine context keys the current stream as 'main'."""
+    from alignn_mi355x import ops
+    d = ops.ExecContext("default", owned=False)
+    assert d._role("cpu") == "main"
+    e = ops.ExecContext("engine")
+    assert e._role("cpu") == "main"

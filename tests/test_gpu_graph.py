@@ -224,3 +224,74 @@ def test_set_lr_reaches_a_captured_plan():
     assert not torch.equal(te.st.flat, tp.st.flat) and not torch.equal(flat, tp.st.flat)
     tp.release_capture()
     ops.set_step_seed(None)
+
+
+def test_larger_miss_then_rebind_hit_bitwise():
+    """A re-bind miss on a LARGER batch runs eagerly in the captured trainer's context; its bigger
+    workspaces must not replace the ones the plan holds (ExecContext.freeze), so the next replay and
+    re-bound hit still equal the eager twin bit for bit."""
+    from alignn_mi355x import ops
+    from alignn_mi355x.synthetic import mp_like_batch
+    _, te, _ = _setup(B=8)
+    _, tp, bp = _setup(B=8)
+    tp.capture(bp)
+    big = mp_like_batch(20, first=300).to(DEV)
+    hit = mp_like_batch(8, first=500).to(DEV)
+    for i, b in enumerate((big, hit, bp, big, hit)):
+        s = 80 + i
+        if b is big:
+            tp._seed_dev.fill_(0)
+            lp = tp.step(b, seed=s).clone()
+            te.use_step_seed(tp._seed_dev)
+            le = te.forward_backward(b, s).clone()
+            te._clip_and_update()
+        else:
+            lp = tp.step(b, seed=s).clone()
+            le = _twin_step(te, tp, b, s)
+        torch.cuda.synchronize()
+        assert torch.equal(le, lp), i
+        assert torch.equal(te.st.grad, tp.st.grad), i
+        assert torch.equal(te.st.flat, tp.st.flat), i
+    assert tp.rebind_misses == 2 and tp.rebinds >= 2
+    tp.release_capture()
+    ops.set_step_seed(None)
+
+
+@pytest.mark.parametrize("path", ["sample_weights", "no_capture"])
+def test_loader_prepared_batch_on_eager_paths(path):
+    """A batch collated and prepared on a loader stream is waited for and kept alive on every path
+    that reads it (engine.adopt): the KNN-weighted eager step of a captured trainer and a trainer with
+    no capture equal the same step on the same batch prepared on the main stream."""
+    import numpy as np
+    from alignn_mi355x import ops
+    from alignn_mi355x.data import Data
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_batch, mp_like_graph
+    keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+    store = GraphStore.from_data_list([Data(**{k: getattr(mp_like_graph(200 + g), k) for k in keys})
+                                       for g in range(16)], DEV)
+    idx = np.random.default_rng(3).choice(16, size=8, replace=False)
+    loader = torch.cuda.Stream()
+    _, t1, _ = _setup(B=8)
+    _, t2, b2 = _setup(B=8)
+    if path == "sample_weights":
+        t2.capture(b2)
+    w = torch.linspace(0.5, 1.5, 8, device=DEV) if path == "sample_weights" else None
+    for i in range(2):
+        with torch.cuda.stream(loader):
+            bl = store.collate(idx)
+            torch.cuda._sleep(2_000_000)    # the loader is still busy when the step is queued
+        prepare_batch(bl, loader)
+        bm = store.collate(idx)
+        prepare_batch(bm)
+        t1.use_step_seed(None)
+        t2.use_step_seed(None)
+        ops.set_step_seed(None)
+        l1 = t1.step(bm, seed=90 + i, sample_weights=w).clone()
+        l2 = t2.step(bl, seed=90 + i, sample_weights=w).clone()
+        del bl
+        torch.cuda.synchronize()
+        assert torch.equal(l1, l2), i
+        assert torch.equal(t1.st.flat, t2.st.flat), i
+    t2.release_capture()

@@ -1,0 +1,202 @@
+"""BASELINE configs C3, C4 and C5 on the HIP path (reference step train.py:628-699,
+members train.py:2052-2095).
+
+* C3 — B = 256 per GPU, bf16 matrix-core inputs (the reference's CUDA autocast, train.py:628-636):
+  the captured plan replays the eager step bit for bit; the bf16 step tracks the fp32 step (stated
+  bf16 tolerance: loss within 2e-2 relative, cosine of the flat gradient > 0.999 — the fp32 step
+  itself is pinned to the fp64 oracle by test_gpu_parity.py); the bf16-storage line-graph attention
+  over the full C3 line graph (m = 2,027,520 triplets) equals the fp32 kernels bit for bit on
+  bf16-representable inputs.
+* C4 — the ensemble launcher (ensemble.EnsembleTrainer: member i seeded seed + 1007 i, fold i % 5,
+  every member's captured step on its own stream): each of 5 members trained concurrently equals
+  the same member trained alone, bit for bit.
+* C5 at N = 1 — B = 256 batches collated on the device from an HBM store and prepared on a loader
+  stream, re-bound into the captured bf16 plan, equal the eager step bit for bit.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+_CPU = {}
+
+
+def _cpu_batch(B, first=0):
+    from alignn_mi355x.synthetic import mp_like_batch
+    key = (B, first)
+    if key not in _CPU:
+        _CPU[key] = mp_like_batch(B, first=first)
+    return _CPU[key]
+
+
+def _dev(b):
+    from alignn_mi355x.data import Batch
+    out = Batch()
+    for k in b.keys():
+        v = getattr(b, k)
+        setattr(out, k, v.to(DEV) if torch.is_tensor(v) else v)
+    return out
+
+
+def _trainer(precision, dropout=0.15, seed=0):
+    import alignn_mi355x as A
+    torch.manual_seed(seed)
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, dropout), 2).to(DEV)
+    return A.FusedTrainer(model, precision=precision)
+
+
+def _twin(te, tp, b, s):
+    te.use_step_seed(tp._seed_dev)
+    tp._seed_dev.fill_(s)
+    le = te.forward_backward(b, 0).clone()
+    te._clip_and_update()
+    return le
+
+
+def test_c3_plan_replay_bitwise_vs_eager_b256_bf16():
+    from alignn_mi355x import ops
+    te, tp = _trainer("bf16"), _trainer("bf16")
+    be, bp = _dev(_cpu_batch(256)), _dev(_cpu_batch(256))
+    tp.capture(bp)
+    from alignn_mi355x.engine import batch_cache
+    assert tp.model._engine._bf16_angle(batch_cache(bp), 256)   # the bf16-storage attention is the path taken
+    assert torch.equal(te.st.flat, tp.st.flat)
+    for i, s in enumerate((5, 6)):
+        lp = tp.step(bp, seed=s).clone()
+        le = _twin(te, tp, be, s)
+        torch.cuda.synchronize()
+        assert torch.isfinite(lp).all()
+        assert torch.equal(le, lp), i
+        assert torch.equal(te.st.grad, tp.st.grad), i
+        assert torch.equal(te.st.flat, tp.st.flat), i
+    tp.release_capture()
+    ops.set_step_seed(None)
+
+
+def test_c3_bf16_step_tracks_fp32_b256():
+    res = {}
+    b = _dev(_cpu_batch(256))
+    for prec in ("fp32", "bf16"):
+        tr = _trainer(prec, dropout=0.0)
+        loss = tr.forward_backward(b, 5, training=False).clone()
+        torch.cuda.synchronize()
+        res[prec] = (loss, tr.st.grad.clone())
+        del tr
+    (l32, g32), (l16, g16) = res["fp32"], res["bf16"]
+    assert torch.isfinite(l16).all() and torch.isfinite(g16).all()
+    assert abs(float(l16) - float(l32)) <= 2e-2 * abs(float(l32)), (float(l16), float(l32))
+    cos = float((g16.double() @ g32.double()) / (g16.double().norm() * g32.double().norm()))
+    assert cos > 0.999, cos
+    assert not torch.equal(g16, g32)
+
+
+def test_c3_bf16_attention_full_line_graph_bitwise_vs_fp32_on_rounded_inputs():
+    """The C3 line graph itself (B = 256 under the PyG offset rule: 16,020 active bonds, 2,027,520
+    triplets): alignn_lg_fwd_bf16 / alignn_lg_bwd_dst_bf16 against the fp32 single-wave-item kernels
+    on K|V and F rows that are bf16-representable, dropout on."""
+    from alignn_mi355x import ops
+    from alignn_mi355x.engine import batch_cache
+    bc = batch_cache(_dev(_cpu_batch(256)))
+    g = bc.lg
+    n, m, D, H = g.n, g.m, 256, 4
+    assert m == 2_027_520 and g.rows is not None
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    r = lambda *s: torch.randn(*s, device=DEV, generator=gen) * 0.5  # noqa: E731
+    QKV = r(n, 3 * D)
+    QKV[:, D:] = QKV[:, D:].bfloat16().float()
+    U, Vd, dout, wbar = r(n, H, D), r(n, H, D), r(n, D), r(D)
+    F16 = r(m, D).bfloat16()
+    F = F16.float()
+    KV16 = ops.cast_bf16(QKV[:, D:])
+    assert g.family(D, H, F) == 3
+    outs = {}
+    for mode in ("fp32", "bf16"):
+        outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
+        sumA, mstat, den, sigz = (torch.empty(n, H, device=DEV) for _ in range(4))
+        dq, Sz = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
+        dz, al = torch.empty(m, H, device=DEV), torch.empty(m, H, device=DEV)
+        if mode == "fp32":
+            ops.tconv_fwd(g, D, H, QKV, U, wbar, F, None, outp, S, sumA, mstat, den, 0.15, 9)
+            ops.tconv_bwd_dst(g, D, H, QKV, U, Vd, wbar, F, None, dout, outp, mstat, den, dq, Sz, sigz, dz, al, None,
+                              0, 0.15, 9)
+        else:
+            ops.lg_fwd_bf16(g, D, H, QKV, KV16, U, wbar, F16, outp, S, sumA, mstat, den, 0.15, 9)
+            ops.lg_bwd_dst_bf16(g, D, H, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz, sigz, dz, al,
+                                0.15, 9)
+        torch.cuda.synchronize()
+        outs[mode] = dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz, al=al)
+    for k in outs["fp32"]:
+        assert torch.isfinite(outs["fp32"][k]).all(), k
+        assert torch.equal(outs["bf16"][k], outs["fp32"][k]), k
+
+
+@pytest.mark.parametrize("precision,B", [("fp32", 4), ("bf16", 256)])
+def test_c4_concurrent_members_bitwise_vs_solo(precision, B):
+    """5 members on one GPU, each a captured plan on its own stream, trained concurrently; every
+    member equals the same member (seed 42 + 1007 i, fold i % 5) trained alone on the main stream."""
+    import alignn_mi355x as A
+    from alignn_mi355x import ops
+    from alignn_mi355x.ensemble import EnsembleTrainer
+    from alignn_mi355x.synthetic import ensemble_member_batch
+
+    def build():
+        return A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(DEV)
+
+    batches = {}
+
+    def batch_for(i, fold):
+        if i not in batches:
+            batches[i] = ensemble_member_batch(B, i, fold)
+        return _dev(batches[i])
+
+    ens = EnsembleTrainer(5, build, batch_for, seed=42, precision=precision)
+    assert ens.ids == [0, 1, 2, 3, 4] and all(s is not None for s in ens.streams)
+    for k in range(3):
+        ens.step(k)
+    torch.cuda.synchronize()
+    together = [tr.st.flat.clone() for _, _, tr, _ in ens.members]
+    ens.release()
+    del ens
+    for i in range(5):
+        solo = EnsembleTrainer(5, build, batch_for, seed=42, precision=precision, members=[i], concurrent=False)
+        for k in range(3):
+            solo.step(k)
+        torch.cuda.synchronize()
+        assert torch.equal(solo.members[0][2].st.flat, together[i]), i
+        if i:
+            assert not torch.equal(together[i], together[0])   # members really differ (seed, fold)
+        solo.release()
+        del solo
+    ops.set_step_seed(None)
+
+
+def test_c5_store_batches_b256_rebound_bitwise_vs_eager():
+    """C5's loop at N = 1: random B = 256 batches collated on the device from an HBM store of
+    MP-like graphs, prepared on a loader stream, re-bound into the captured bf16 plan (no eager
+    steps) — each step equal to the eager step on the same batch, bit for bit."""
+    import numpy as np
+    from alignn_mi355x import ops
+    from alignn_mi355x.data import Data
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_graph
+    te, tp = _trainer("bf16"), _trainer("bf16")
+    tp.capture(_dev(_cpu_batch(256)))
+    keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+    store = GraphStore.from_data_list([Data(**{k: getattr(mp_like_graph(5000 + g), k) for k in keys})
+                                       for g in range(320)], DEV)
+    loader = torch.cuda.Stream()
+    rng = np.random.default_rng(17)
+    for i in range(2):
+        with torch.cuda.stream(loader):
+            b = store.collate(rng.choice(320, size=256, replace=False))
+        prepare_batch(b, loader)
+        s = 40 + i
+        lp = tp.step(b, seed=s).clone()
+        le = _twin(te, tp, b, s)
+        torch.cuda.synchronize()
+        assert torch.equal(le, lp), i
+        assert torch.equal(te.st.flat, tp.st.flat), i
+    assert tp.rebinds == 2 and tp.rebind_misses == 0
+    tp.release_capture()
+    ops.set_step_seed(None)
