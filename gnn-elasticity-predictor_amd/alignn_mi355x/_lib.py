@@ -129,6 +129,11 @@ _SIGNATURES = {
     "alignn_collate_rows_f32": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "alignn_collate_index_i64": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp], c_i32),
     "alignn_collate_batchvec": ([c_i32, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
+    "alignn_collate_rows_std_f32": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32,
+                                     c_vp], c_i32),
+    "alignn_segment_finite_f32": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
+    "alignn_feature_stats_workspace": ([c_i32, c_i64], c_i64),
+    "alignn_feature_stats_f64": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_col_center_sq_f32": ([c_vp, c_i64, c_i32, c_vp, c_vp, c_vp], c_i32),
     "alignn_standardize_f32": ([c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_row_sqnorm_f32": ([c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),

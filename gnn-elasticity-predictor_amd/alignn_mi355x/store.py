@@ -14,6 +14,16 @@ with ``index`` in the key are concatenated along the last dim and shifted by the
 SURVEY §0.3); ``lg_offset='num_edges'`` gives the corrected wiring.  Other tensors are concatenated
 along dim 0.
 
+The reference's per-sample transform (``PtGraphDataset``, ``scripts/train.py:49-216``) is part of the
+store: graphs holding a NaN or an infinity in any float field are dropped when the store is built
+(``_is_valid``, train.py:174-182; checked on the device, one launch per field), dataset indices count
+the kept graphs only (train.py:64-87), the node features are cut to the scalar block without
+mat2vec, padded or truncated to ``force_node_dim`` (train.py:103-117, :137-154), and once
+:meth:`GraphStore.set_feature_standardization` has statistics the node scalars, mat2vec block and
+global scalars are z-scored (train.py:184-216).  The transform runs inside the collate copy
+(``alignn_collate_rows_std_f32``), so it costs no extra pass; :meth:`GraphStore.feature_stats`
+computes the statistics over a training selection like train.py:1324-1380 (fp64 sums on the device).
+
 On disk: a directory of ``<field>.npy`` arrays plus ``meta.json`` (no pickles; loaded with
 ``numpy.load(mmap_mode='r')``), written by :meth:`GraphStore.save`.
 """
@@ -80,16 +90,161 @@ class CollatePlan:
         return out
 
 
+# PtGraphDataset's float fields checked by _is_valid (train.py:176)
+VALIDATED_FIELDS = ("x", "edge_attr", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+BASE_SCALAR_DIM = 6   # train.py:102
+
+
 class GraphStore:
     def __init__(self, arrays: Dict[str, torch.Tensor], counts: Dict[str, np.ndarray], meta: Dict,
-                 extras: Optional[Dict[str, List]] = None):
+                 extras: Optional[Dict[str, List]] = None, *, drop_invalid: bool = True, use_mat2vec: bool = True,
+                 force_node_dim: Optional[int] = None):
         self.arrays = arrays          # field -> device tensor ([total, width] float32 or [2, total] int64)
-        self.counts = counts          # field -> int64 [num_graphs] rows per graph
+        self.counts = counts          # field -> int64 [stored graphs] rows per graph
         self.meta = meta              # field -> {"kind": "rows"|"index", "shape": trailing shape}
         self.starts = {f: _excl_cumsum(c) for f, c in counts.items()}
         self.extras = extras or {}    # non-tensor per-graph attributes (e.g. material ids)
-        self.num_graphs = len(next(iter(counts.values())))
+        self.num_stored = len(next(iter(counts.values())))
         self._staging = None
+        # dataset index -> stored graph (graphs with NaN / inf dropped, as PtGraphDataset's file list)
+        self.ids = self._valid_ids() if drop_invalid else np.arange(self.num_stored, dtype=np.int64)
+        self.num_graphs = len(self.ids)
+        if self.num_graphs == 0:
+            raise ValueError("Dataset is empty after filtering for targets.")
+        self._configure_nodes(use_mat2vec, force_node_dim)
+        self._x_stats = None   # device (mean, std) over node_dim columns, identity where a block has none
+        self._g_stats = None   # device (mean, std) over the global scalars
+
+    # -------------------------------------------------------------------------------- transform
+    def _configure_nodes(self, use_mat2vec: bool, force_node_dim: Optional[int]) -> None:
+        """PtGraphDataset.__init__'s node-dimension rules (train.py:95-117)."""
+        w = int(self.meta["x"].get("width", 1))
+        self.raw_node_dim = w
+        self.scalar_dim = min(BASE_SCALAR_DIM, w)
+        raw_m2v = max(0, w - self.scalar_dim)
+        self.use_mat2vec = bool(use_mat2vec)
+        self.mat2vec_dim = raw_m2v if self.use_mat2vec else 0
+        if force_node_dim is not None:
+            force_node_dim = int(force_node_dim)
+            if force_node_dim < self.scalar_dim:
+                raise ValueError(f"Forced node dimension {force_node_dim} is smaller than scalar dimension "
+                                 f"{self.scalar_dim}.")
+            self.mat2vec_dim = max(force_node_dim - self.scalar_dim, 0)
+            self.use_mat2vec = self.mat2vec_dim > 0
+        self.node_dim = self.scalar_dim + self.mat2vec_dim
+        # columns taken from a stored row (train.py:139-153): the scalar block alone without mat2vec,
+        # then pad with zeros or truncate to node_dim
+        sel = self.scalar_dim if (not self.use_mat2vec and raw_m2v > 0) else w
+        self._x_copy_w = min(sel, self.node_dim)
+        g = self.meta.get("global_x")
+        self.global_scalar_dim = 0 if g is None else int(self.counts["global_x"][self.ids[0]]) * int(g.get("width", 1))
+
+    def set_feature_standardization(self, scalar_mean=None, scalar_std=None, embed_mean=None, embed_std=None,
+                                    global_mean=None, global_std=None) -> None:
+        """PtGraphDataset.set_feature_standardization (train.py:184-198): z-score statistics applied by
+        every later collate (None: that block is left as is)."""
+        dev = next(iter(self.arrays.values())).device
+
+        def vec(t, n, what):
+            t = torch.as_tensor(t, dtype=torch.float32).reshape(-1)
+            if t.numel() != n:
+                raise ValueError(f"{what}: {t.numel()} statistics for {n} features")
+            return t
+
+        mean = torch.zeros(self.node_dim)
+        std = torch.ones(self.node_dim)
+        have = False
+        if self.scalar_dim > 0 and scalar_mean is not None and scalar_std is not None:
+            mean[:self.scalar_dim] = vec(scalar_mean, self.scalar_dim, "scalar_mean")
+            std[:self.scalar_dim] = vec(scalar_std, self.scalar_dim, "scalar_std")
+            have = True
+        if self.mat2vec_dim > 0 and embed_mean is not None and embed_std is not None:
+            mean[self.scalar_dim:] = vec(embed_mean, self.mat2vec_dim, "embed_mean")
+            std[self.scalar_dim:] = vec(embed_std, self.mat2vec_dim, "embed_std")
+            have = True
+        # (v - 0) / 1 == v exactly, so a block without statistics passes through unchanged
+        self._x_stats = (mean.to(dev), std.to(dev)) if have else None
+        if self.global_scalar_dim > 0 and global_mean is not None and global_std is not None:
+            self._g_stats = (vec(global_mean, self.global_scalar_dim, "global_mean").to(dev),
+                             vec(global_std, self.global_scalar_dim, "global_std").to(dev))
+        else:
+            self._g_stats = None
+
+    def feature_stats(self, train_idx, eps: float = 1e-12) -> Dict[str, Optional[torch.Tensor]]:
+        """The reference's standardization statistics over the training graphs (train.py:1324-1380),
+        from the features as a dataset item yields them before standardization: per-graph fp64 sums
+        on the device accumulated in ``train_idx`` order, then mean, clamped variance and std in fp64,
+        returned as fp32 host tensors (keys as the reference's scaler_state)."""
+        idx = np.asarray(train_idx, dtype=np.int64).reshape(-1)
+        gids = self.ids[idx]
+        out: Dict[str, Optional[torch.Tensor]] = {k: None for k in ("scalar_mean", "scalar_std", "embed_mean",
+                                                                     "embed_std", "global_mean", "global_std")}
+        if len(gids) == 0:
+            return out
+        total_nodes = int(self.counts["x"][gids].sum())
+
+        def sums(field, K, by_row):
+            a = self.arrays[field]
+            w = int(self.meta[field].get("width", 1))
+            dev = a.device
+            st = torch.from_numpy(np.stack([self.starts[field][gids], self.counts[field][gids]])).to(dev)
+            lib = _lib.lib()
+            ws = torch.empty(max(1, int(lib.alignn_feature_stats_workspace(len(gids), K))), dtype=torch.float64,
+                             device=dev)
+            sm = torch.empty(max(K, 1), dtype=torch.float64, device=dev)
+            sq = torch.empty(max(K, 1), dtype=torch.float64, device=dev)
+            _lib.check(lib.alignn_feature_stats_f64(len(gids), a.data_ptr(), w, st[0].data_ptr(), st[1].data_ptr(),
+                                                    K, int(by_row), sm.data_ptr(), sq.data_ptr(), ws.data_ptr(),
+                                                    ws.numel(), stream_ptr()), "alignn_feature_stats_f64")
+            return sm[:K].cpu().numpy(), sq[:K].cpu().numpy()
+
+        if total_nodes > 0:
+            s_all = np.zeros(self.node_dim)
+            q_all = np.zeros(self.node_dim)
+            if self._x_copy_w > 0:
+                s_all[:self._x_copy_w], q_all[:self._x_copy_w] = sums("x", self._x_copy_w, False)
+            for name, lo, hi in (("scalar", 0, self.scalar_dim), ("embed", self.scalar_dim, self.node_dim)):
+                if hi <= lo:
+                    continue
+                mean = s_all[lo:hi] / total_nodes
+                var = np.maximum(q_all[lo:hi] / total_nodes - mean ** 2, eps)
+                out[f"{name}_mean"] = torch.from_numpy(mean.astype(np.float32))
+                out[f"{name}_std"] = torch.from_numpy(np.sqrt(var).astype(np.float32))
+        if self.global_scalar_dim > 0:
+            s, q = sums("global_x", self.global_scalar_dim, True)
+            mean = s / len(gids)
+            var = np.maximum(q / len(gids) - mean ** 2, eps)
+            out["global_mean"] = torch.from_numpy(mean.astype(np.float32))
+            out["global_std"] = torch.from_numpy(np.sqrt(var).astype(np.float32))
+        return out
+
+    def _valid_ids(self) -> np.ndarray:
+        """Stored graphs without NaN / inf in any checked float field (device check, one launch per field)."""
+        dev = next(iter(self.arrays.values())).device
+        G = self.num_stored
+        if dev.type != "cuda":   # a host-side store (save / load round trips): the same rule in numpy
+            ok = np.ones(G, dtype=bool)
+            for f in VALIDATED_FIELDS:
+                if f in self.arrays and self.meta[f]["kind"] == "rows" and self.arrays[f].numel():
+                    w = int(self.meta[f].get("width", 1))
+                    fin = np.isfinite(self.arrays[f].numpy().reshape(-1, w)).all(axis=1)
+                    bad = np.add.reduceat(~fin, self.starts[f]) if len(fin) else np.zeros(G, dtype=int)
+                    ok &= (bad == 0) | (self.counts[f] == 0)
+            return np.nonzero(ok)[0].astype(np.int64)
+        ok = torch.ones(max(G, 1), dtype=torch.int32, device=dev)
+        lib = _lib.lib()
+        for f in VALIDATED_FIELDS:
+            if f not in self.arrays or self.meta[f]["kind"] != "rows":
+                continue
+            a = self.arrays[f]
+            w = int(self.meta[f].get("width", 1))
+            if a.dtype != torch.float32 or a.numel() == 0:
+                continue
+            st = torch.from_numpy(np.stack([self.starts[f], self.counts[f]])).to(dev)
+            _lib.check(lib.alignn_segment_finite_f32(G, a.data_ptr(), w, st[0].data_ptr(), st[1].data_ptr(),
+                                                     int(self.counts[f].max()) if G else 0, ok.data_ptr(),
+                                                     stream_ptr()), "alignn_segment_finite_f32")
+        return np.nonzero(ok[:G].cpu().numpy())[0].astype(np.int64)
 
     # -------------------------------------------------------------------------------- building
     @classmethod
@@ -112,6 +267,9 @@ class GraphStore:
                 counts[key] = np.asarray([v.size(1) for v in vals], dtype=np.int64)
                 meta[key] = {"kind": "index", "shape": []}
             else:
+                if key in ("global_x", "sg_one_hot"):
+                    # a column per graph (train.py:164-169): fetch.to_pyg_data stores [1, 59] / [1, 230]
+                    vals = [v.reshape(-1, 1) for v in vals]
                 vals = [v.reshape(1) if v.dim() == 0 else v for v in vals]
                 shape = list(vals[0].shape[1:])
                 width = int(np.prod(shape)) if shape else 1
@@ -123,10 +281,14 @@ class GraphStore:
         return arrays, counts, meta, extras
 
     @classmethod
-    def from_data_list(cls, data_list: Sequence[Data], device) -> "GraphStore":
+    def from_data_list(cls, data_list: Sequence[Data], device, require_target: bool = True, **kw) -> "GraphStore":
+        """kw: drop_invalid, use_mat2vec, force_node_dim (PtGraphDataset's options, train.py:50-57).
+        require_target: graphs without ``y`` are skipped (train.py:74-75)."""
+        if require_target:
+            data_list = [d for d in data_list if getattr(d, "y", None) is not None]
         arrays, counts, meta, extras = cls.host_arrays(data_list)
         dev = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in arrays.items()}
-        return cls(dev, counts, meta, extras)
+        return cls(dev, counts, meta, extras, **kw)
 
     def save(self, path: str) -> None:
         os.makedirs(path, exist_ok=True)
@@ -137,7 +299,7 @@ class GraphStore:
             json.dump({"fields": self.meta, "extras": {k: [str(x) for x in v] for k, v in self.extras.items()}}, f)
 
     @classmethod
-    def load(cls, path: str, device) -> "GraphStore":
+    def load(cls, path: str, device, **kw) -> "GraphStore":
         with open(os.path.join(path, "meta.json")) as f:
             m = json.load(f)
         arrays, counts = {}, {}
@@ -145,16 +307,19 @@ class GraphStore:
             a = np.load(os.path.join(path, f"{k}.npy"), mmap_mode="r")      # no pickles
             arrays[k] = torch.from_numpy(np.ascontiguousarray(a)).to(device)
             counts[k] = np.load(os.path.join(path, f"{k}.counts.npy"))
-        return cls(arrays, counts, m["fields"], m.get("extras", {}))
+        return cls(arrays, counts, m["fields"], m.get("extras", {}), **kw)
 
     # -------------------------------------------------------------------------------- batches
     def plan(self, indices, lg_offset: str = "num_nodes") -> CollatePlan:
+        """indices: dataset indices (over the kept graphs)."""
         idx = np.asarray(indices, dtype=np.int64).reshape(-1)
         if idx.size == 0:
             raise ValueError("cannot collate an empty list")
         if idx.min() < 0 or idx.max() >= self.num_graphs:
             raise IndexError("graph index out of range")
-        return CollatePlan(self.meta, self.counts, self.starts, idx, lg_offset)
+        pl = CollatePlan(self.meta, self.counts, self.starts, self.ids[idx], lg_offset)
+        pl.sample_index = idx
+        return pl
 
     def collate(self, indices, lg_offset: str = "num_nodes") -> Batch:
         """Batch of the given graphs, assembled on the device (same tensors as
@@ -169,7 +334,7 @@ class GraphStore:
             host += [ent["src"], ent["dst"], ent["count"]]
             if "add" in ent:
                 host.append(ent["add"])
-        host += [pl.node_dst, pl.nodes, pl.ptr]
+        host += [pl.node_dst, pl.nodes, pl.ptr, pl.sample_index]
         flat = np.concatenate(host).astype(np.int64)
         staged = torch.from_numpy(flat)
         if dev.type == "cuda":
@@ -197,19 +362,31 @@ class GraphStore:
                                                         out.size(1), s), "alignn_collate_index_i64")
             else:
                 w = int(m.get("width", 1))
-                out = torch.empty(ent["total"], w, dtype=torch.float32, device=dev)
-                _lib.check(lib.alignn_collate_rows_f32(G, a.data_ptr(), w, src.data_ptr(), dst.data_ptr(),
-                                                       cnt.data_ptr(), ent["max"], out.data_ptr(), s),
-                           "alignn_collate_rows_f32")
-                shape = m["shape"]
+                ow, copy_w, stats, by_row = w, w, None, 0
+                if f == "x":
+                    ow, copy_w, stats = self.node_dim, self._x_copy_w, self._x_stats
+                elif f == "global_x":
+                    stats, by_row = self._g_stats, 1
+                out = torch.empty(ent["total"], ow, dtype=torch.float32, device=dev)
+                if (ow, copy_w, stats) == (w, w, None):
+                    _lib.check(lib.alignn_collate_rows_f32(G, a.data_ptr(), w, src.data_ptr(), dst.data_ptr(),
+                                                           cnt.data_ptr(), ent["max"], out.data_ptr(), s),
+                               "alignn_collate_rows_f32")
+                else:   # PtGraphDataset.__getitem__'s select / pad / truncate / z-score, fused
+                    _lib.check(lib.alignn_collate_rows_std_f32(
+                        G, a.data_ptr(), w, src.data_ptr(), dst.data_ptr(), cnt.data_ptr(), ent["max"],
+                        out.data_ptr(), ow, copy_w, None if stats is None else stats[0].data_ptr(),
+                        None if stats is None else stats[1].data_ptr(), by_row, s), "alignn_collate_rows_std_f32")
+                shape = m["shape"] if ow == w else [ow]
                 out = out.view(ent["total"], *shape) if shape else out.view(ent["total"])
             setattr(b, f, out)
-        node_dst, nodes, ptr = views[vi], views[vi + 1], views[vi + 2]
+        node_dst, nodes, ptr, sample_index = views[vi], views[vi + 1], views[vi + 2], views[vi + 3]
         batch = torch.empty(int(pl.nodes.sum()), dtype=torch.int64, device=dev)
         _lib.check(lib.alignn_collate_batchvec(G, node_dst.data_ptr(), nodes.data_ptr(), int(pl.nodes.max()),
                                                batch.data_ptr(), s), "alignn_collate_batchvec")
         b.batch = batch
         b.ptr = ptr.clone()
+        b.sample_index = sample_index.clone()   # train.py:171 (dataset indices of the batch's graphs)
         b.num_graphs = G
         for k, vals in self.extras.items():
             setattr(b, k, [vals[i] for i in pl.idx])

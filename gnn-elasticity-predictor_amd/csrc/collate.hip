@@ -75,6 +75,86 @@ __global__ void collate_batchvec_kernel(const int64_t* __restrict__ dst_start, c
     batch[dst_start[g] + i] = g;
 }
 
+// Rows with PtGraphDataset.__getitem__'s per-sample transform fused into the copy
+// (train.py:137-154 node-dim select / pad / truncate, :200-216 z-scoring): a destination row is the
+// source row's first copy_w values, zero-padded to dst_w; with statistics, every value becomes
+// (v - mean[k]) / std[k] (fp32, correctly rounded as the reference's tensor ops), k = the column
+// (by_row = 0: node features) or the element's index inside the graph's segment (by_row = 1:
+// global_x, one value per row, standardized per position).
+__global__ void collate_rows_std_kernel(const float* __restrict__ src, int64_t src_w,
+                                        const int64_t* __restrict__ src_start, const int64_t* __restrict__ dst_start,
+                                        const int64_t* __restrict__ count, float* __restrict__ dst, int64_t dst_w,
+                                        int64_t copy_w, const float* __restrict__ mean, const float* __restrict__ stdv,
+                                        int by_row) {
+  const int g = blockIdx.y;
+  const int64_t n = count[g] * dst_w;
+  const float* s = src + src_start[g] * src_w;
+  float* d = dst + dst_start[g] * dst_w;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / dst_w, c = i - r * dst_w;
+    float v = c < copy_w ? s[r * src_w + c] : 0.f;
+    if (mean) {
+      const int64_t k = by_row ? i : c;
+      v = (v - mean[k]) / stdv[k];
+    }
+    d[i] = v;
+  }
+}
+
+// ok[g] = 0 when graph g's segment of a float field holds a NaN or an infinity (PtGraphDataset._is_valid,
+// train.py:174-182).  ok is preset to 1 by the caller; fields are checked one launch each.
+__global__ void segment_finite_kernel(const float* __restrict__ src, int64_t width, const int64_t* __restrict__ start,
+                                      const int64_t* __restrict__ count, int32_t* __restrict__ ok) {
+  const int g = blockIdx.y;
+  const int64_t n = count[g] * width;
+  const float* s = src + start[g] * width;
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(s[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) ok[g] = 0;
+}
+
+// Per-graph fp64 sums for the feature statistics (train.py:1337-1352): for graph j of the selection,
+// part[j][k] = sum over its rows of v and of v^2 (by_row = 0: k = column, rows summed in order;
+// by_row = 1: k = the element's index in the segment, one value each).  Block (j, column chunk).
+__global__ void seg_stats_f64_kernel(const float* __restrict__ src, int64_t width, const int64_t* __restrict__ start,
+                                     const int64_t* __restrict__ count, int64_t K, int by_row,
+                                     double* __restrict__ psum, double* __restrict__ psq) {
+  const int64_t j = blockIdx.y;
+  const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const float* s = src + start[j] * width;
+  double a = 0.0, q = 0.0;
+  if (by_row) {
+    if (k < count[j] * width) {
+      a = (double)s[k];
+      q = a * a;
+    }
+  } else {
+    for (int64_t r = 0; r < count[j]; ++r) {
+      const double v = (double)s[r * width + k];
+      a += v;
+      q += v * v;
+    }
+  }
+  psum[j * K + k] = a;
+  psq[j * K + k] = q;
+}
+
+// sum[k] = sum_j part[j][k] in selection order (the reference's running per-graph accumulation)
+__global__ void stats_reduce_f64_kernel(const double* __restrict__ psum, const double* __restrict__ psq, int64_t J,
+                                        int64_t K, double* __restrict__ sum, double* __restrict__ sq) {
+  const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double a = 0.0, q = 0.0;
+  for (int64_t j = 0; j < J; ++j) {
+    a += psum[j * K + k];
+    q += psq[j * K + k];
+  }
+  sum[k] = a;
+  sq[k] = q;
+}
+
 static dim3 seg_grid(int64_t max_count_elems, int G) {
   int64_t chunks = (max_count_elems + 1023) / 1024;
   if (chunks < 1) chunks = 1;
@@ -143,5 +223,59 @@ extern "C" int alignn_copy_many(int32_t n, const void* const* src, void* const* 
   const int64_t blocks = std::min<int64_t>((L.units[n] + 255) / 256, 2048);
   launch(copy_many_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), L);
   ALIGNN_LAUNCH_CHECK("copy_many_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_collate_rows_std_f32(int32_t G, const float* src, int64_t src_width, const int64_t* src_start,
+                                           const int64_t* dst_start, const int64_t* count, int64_t max_count,
+                                           float* dst, int64_t dst_width, int64_t copy_width, const float* mean,
+                                           const float* stdv, int32_t by_row, void* stream) {
+  if (G < 0 || src_width < 0 || dst_width < 0 || max_count < 0 || copy_width < 0 || copy_width > src_width ||
+      copy_width > dst_width || (!mean) != (!stdv)) {
+    set_error("collate_rows_std: 0 <= copy_width <= min(src_width, dst_width); mean and std both or neither");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (G == 0 || dst_width == 0 || max_count == 0) return ALIGNN_OK;
+  launch(collate_rows_std_kernel, seg_grid(max_count * dst_width, G), dim3(256), 0,
+         reinterpret_cast<hipStream_t>(stream), src, src_width, src_start, dst_start, count, dst, dst_width,
+         copy_width, mean, stdv, (int)by_row);
+  ALIGNN_LAUNCH_CHECK("collate_rows_std_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_segment_finite_f32(int32_t G, const float* src, int64_t width, const int64_t* start,
+                                         const int64_t* count, int64_t max_count, int32_t* ok, void* stream) {
+  if (G < 0 || width < 0 || max_count < 0) return ALIGNN_E_BAD_SHAPE;
+  if (G == 0 || width == 0 || max_count == 0) return ALIGNN_OK;
+  launch(segment_finite_kernel, seg_grid(max_count * width, G), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+         src, width, start, count, ok);
+  ALIGNN_LAUNCH_CHECK("segment_finite_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int64_t alignn_feature_stats_workspace(int32_t J, int64_t K) {
+  if (J < 0 || K < 0) return -1;
+  return 2 * (int64_t)J * K;
+}
+
+extern "C" int alignn_feature_stats_f64(int32_t J, const float* src, int64_t width, const int64_t* start,
+                                        const int64_t* count, int64_t K, int32_t by_row, double* sum, double* sq,
+                                        double* workspace, int64_t workspace_elems, void* stream) {
+  if (J < 0 || width <= 0 || K < 0 || (!by_row && K > width) || workspace_elems < 2 * (int64_t)J * K) {
+    set_error("feature_stats: K <= width (columns) and a workspace of 2 J K doubles");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (K == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  double* psum = workspace;
+  double* psq = workspace + (int64_t)J * K;
+  if (J > 0) {
+    launch(seg_stats_f64_kernel, dim3((unsigned)((K + 255) / 256), (unsigned)J), dim3(256), 0, s, src, width, start,
+           count, K, (int)by_row, psum, psq);
+    ALIGNN_LAUNCH_CHECK("seg_stats_f64_kernel");
+  }
+  launch(stats_reduce_f64_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, psum, psq, (int64_t)J, K, sum,
+         sq);
+  ALIGNN_LAUNCH_CHECK("stats_reduce_f64_kernel");
   return ALIGNN_OK;
 }

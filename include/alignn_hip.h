@@ -461,6 +461,28 @@ int alignn_collate_index_i64(int32_t G, const int64_t* src, int64_t src_ld, cons
                              int64_t* dst, int64_t dst_ld, void* stream);
 int alignn_collate_batchvec(int32_t G, const int64_t* dst_start, const int64_t* count, int64_t max_count,
                             int64_t* batch, void* stream);
+/* The dataset's per-sample transform fused into the row copy (PtGraphDataset.__getitem__,
+ * train.py:137-154 and :200-216): a destination row of dst_width values takes the source row's first
+ * copy_width values and zeros after them (use_mat2vec / force_node_dim: select, pad, truncate); with
+ * mean/std (device fp32, both or neither) each value v becomes (v - mean[k]) / std[k], k = the column
+ * (by_row = 0, node features: scalar | mat2vec statistics) or the element's index inside the graph's
+ * segment (by_row = 1, global_x: one statistic per global scalar). */
+int alignn_collate_rows_std_f32(int32_t G, const float* src, int64_t src_width, const int64_t* src_start,
+                                const int64_t* dst_start, const int64_t* count, int64_t max_count, float* dst,
+                                int64_t dst_width, int64_t copy_width, const float* mean, const float* stdv,
+                                int32_t by_row, void* stream);
+/* ok[g] = 0 when graph g's segment holds a NaN or an infinity (PtGraphDataset._is_valid,
+ * train.py:174-182; ok preset to 1 by the caller, one launch per float field). */
+int alignn_segment_finite_f32(int32_t G, const float* src, int64_t width, const int64_t* start,
+                              const int64_t* count, int64_t max_count, int32_t* ok, void* stream);
+/* Feature statistics over a selection of J graphs (train.py:1324-1380): fp64 sum and sum of squares
+ * per statistic k < K — a column summed over the graph's rows (by_row = 0) or the element at index
+ * k of the graph's segment (by_row = 1) — per graph first, then accumulated in selection order.
+ * workspace: alignn_feature_stats_workspace(J, K) doubles. */
+int64_t alignn_feature_stats_workspace(int32_t J, int64_t K);
+int alignn_feature_stats_f64(int32_t J, const float* src, int64_t width, const int64_t* start, const int64_t* count,
+                             int64_t K, int32_t by_row, double* sum, double* sq, double* workspace,
+                             int64_t workspace_elems, void* stream);
 /* Up to 32 device-to-device copies in one launch (src, dst: HOST arrays of device pointers, 16-byte
  * aligned; bytes: host array, multiples of 4).  Re-binds a captured step to a new batch (the batch
  * fields and its CSR / compaction / schedule cache copied into the captured buffers). */

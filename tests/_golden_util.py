@@ -55,3 +55,34 @@ def norm_err(a, b, floor=0.0):
 
 def grad_norm_scale(grads):
     return max(float(torch.as_tensor(v, dtype=torch.float64).norm()) for v in grads)
+
+
+def dataset_graphs(z):
+    """The raw on-disk graphs of tests/golden/dataset.npz as dicts of CPU tensors (fetch.to_pyg_data
+    layout: global_x [1, 59], sg_one_hot [1, 230]; y None for the graph without a target)."""
+    n, e, t = (np.asarray(z[f"raw/{k}"]) for k in ("n", "e", "t"))
+    cut = lambda a, c, ax=0: np.split(np.asarray(a), np.cumsum(c)[:-1], axis=ax)  # noqa: E731
+    G = len(n)
+    parts = {
+        "x": cut(z["raw/x"], n), "edge_attr": cut(z["raw/edge_attr"], e), "lg_edge_attr": cut(z["raw/lg_edge_attr"], t),
+        "edge_index": cut(z["raw/edge_index"], e, 1), "lg_edge_index": cut(z["raw/lg_edge_index"], t, 1),
+        "global_x": [r[None] for r in np.asarray(z["raw/global_x"])],
+        "sg_one_hot": [r[None] for r in np.asarray(z["raw/sg_one_hot"])], "y": list(np.asarray(z["raw/y"])),
+    }
+    out = []
+    for g in range(G):
+        d = {k: torch.from_numpy(np.ascontiguousarray(v[g])) for k, v in parts.items()}
+        if not bool(z["raw/has_y"][g]):
+            d["y"] = None
+        out.append(d)
+    return out
+
+
+DATASET_MODES = {"setup": {}, "shipped": {}, "no_m2v": {"use_mat2vec": False}, "force100": {"force_node_dim": 100},
+                 "force220": {"force_node_dim": 220}}
+
+
+def dataset_stats(z, mode):
+    keys = ("scalar_mean", "scalar_std", "embed_mean", "embed_std", "global_mean", "global_std")
+    return {k: (torch.from_numpy(np.asarray(z[f"{mode}/stats/{k}"])) if f"{mode}/stats/{k}" in z else None)
+            for k in keys}
