@@ -203,7 +203,7 @@ def build_store(args, dev, rank):
     return store, time.perf_counter() - t0
 
 
-def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
+def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None):
     """The reference's training loop (train.py:639-711) over a dataset resident in HBM: per step a
     random batch is collated on the device and its CSR lists / line-graph compaction / schedules are
     built on a loader stream (engine.prepare_batch) while the previous step runs; the step re-binds
@@ -225,7 +225,8 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
 
     def make():
         with torch.cuda.stream(loader):
-            b = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset)
+            b = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset,
+                              capacity=capacity)
         prepare_batch(b, loader)
         return b
 
@@ -261,8 +262,60 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world):
             "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
                                  "collate_and_prepare": round(host_make / args.steps * 1e3, 3)},
             "eager_steps": trainer.rebind_misses - m0,
+            "signature": ("every batch padded to one capacity (store.BatchCapacity)" if capacity is not None else
+                          "fixed: every synthetic graph has 60 atoms, so every batch has the captured signature "
+                          "(best case; see e2e_variable for variable-size graphs)"),
             "includes": "device collate of a random batch + CSR/compaction/schedules (loader stream) + "
                         "fwd/NLL/bwd/clip/AdamW (captured plan re-bound to the batch)"}
+
+
+def build_variable_store(args, dev, rank):
+    """This rank's shard of a dataset of variable-size MP-like graphs (8-60 atoms, 2-6 neighbour
+    shells: synthetic.variable_mp_like_graph), built once."""
+    from alignn_mi355x.data import Data
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import variable_mp_like_graph
+
+    keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+    t0 = time.perf_counter()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    per = (args.e2e + world - 1) // world
+    first = rank * per
+    n = max(1, min(per, args.e2e - first))
+    store = GraphStore.from_data_list([Data(**{k: getattr(variable_mp_like_graph(first + g), k) for k in keys})
+                                       for g in range(n)], dev)
+    torch.cuda.synchronize()
+    return store, time.perf_counter() - t0
+
+
+def end_to_end_variable(args, dev, rank, world, B):
+    """The reference's loop over real-crystal-like data: graphs of variable size, every batch padded to
+    one capacity by a ghost graph (store.BatchCapacity) so that the plan captured once is re-bound to
+    every batch.  value = real graphs per second."""
+    import alignn_mi355x as A
+    import numpy as np
+    from alignn_mi355x.dp import grad_allreduce_hook
+    store, t_build = build_variable_store(args, dev, rank)
+    cap = store.capacity(B, args.lg_offset)
+    torch.manual_seed(1234)
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
+                                                      args.dropout), 2).to(dev)
+    trainer = A.FusedTrainer(model, precision=args.precision)
+    if world > 1:
+        trainer.grad_hook = grad_allreduce_hook(world)
+    rng = np.random.default_rng(99)
+    first = next(i for i in (rng.choice(store.num_graphs, size=B, replace=False) for _ in range(1000))
+                 if store.fits(i, cap, args.lg_offset) is not None)
+    trainer.capture(store.collate(first, lg_offset=args.lg_offset, capacity=cap))
+    sizes = [store.batch_sizes(np.random.default_rng(s).choice(store.num_graphs, size=B, replace=False),
+                               args.lg_offset)["nodes"] for s in range(64)]
+    r = end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=cap)
+    r["capacity"] = {"graphs": cap.graphs, "nodes": cap.nodes, "edges": cap.edges, "triplets": cap.triplets,
+                     "active_bonds": cap.active}
+    r["mean_real_atoms_per_batch"] = round(float(np.mean(sizes)), 1)
+    r["real_atom_fraction_of_capacity"] = round(float(np.mean(sizes)) / cap.nodes, 3)
+    trainer.release_capture()
+    return r
 
 
 def pmc_traffic(kernel_key):
@@ -614,6 +667,11 @@ def main():
     if c3 is not None:
         _release(c3)
     store = None
+    e2e_var = None
+    if args.e2e > 0:
+        e2e_var = end_to_end_variable(args, dev, rank, world, B)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
 
     if rank == 0:
         cpu = None
@@ -629,7 +687,7 @@ def main():
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
                        "dropout": args.dropout, "launch": r["launch"], "precision": args.precision,
                        **({"settings": args.set} if args.set else {})},
-            "roofline": r["roofline"], "cpu_baseline": cpu, "e2e": e2e,
+            "roofline": r["roofline"], "cpu_baseline": cpu, "e2e": e2e, "e2e_variable": e2e_var,
             "step_roofline": r["step_roofline"], "secondary": secondary,
         }
         print(json.dumps(result), flush=True)

@@ -131,6 +131,7 @@ _SIGNATURES = {
     "alignn_collate_batchvec": ([c_i32, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "alignn_collate_rows_std_f32": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32,
                                      c_vp], c_i32),
+    "alignn_ghost_edges_i64": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
     "alignn_segment_finite_f32": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "alignn_feature_stats_workspace": ([c_i32, c_i64], c_i64),
     "alignn_feature_stats_f64": ([c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
@@ -158,6 +159,8 @@ _SIGNATURES = {
     "alignn_plan_elapsed_ms": ([c_vp, c_i32, c_i32, c_vp], c_i32),
     "alignn_plan_check_ptrs": ([c_vp, c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
     "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
+    "alignn_stream_create": ([c_i32, ctypes.POINTER(c_vp)], c_i32),
+    "alignn_stream_destroy": ([c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
     "alignn_set_i64": ([c_vp, c_i64, c_vp], c_i32),
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),

@@ -128,7 +128,11 @@ class BatchCache:
         self.ag.xcd_chunk = self.ATOM_XCD_CHUNK
         if validate:
             self.ag.check_indices("edge_index")
-        self.lg = self._line_graph(batch.lg_edge_index, self.E, validate)
+        # a batch padded to a store.BatchCapacity: the ghost graph fills the compacted line graph up
+        # to the capacity's size (and the loss covers the real graphs only, trainer)
+        self.pad = getattr(batch, "_alignn_pad", None)
+        self.real_graphs = getattr(batch, "num_real_graphs", None)
+        self.lg = self._line_graph(batch.lg_edge_index, self.E, validate, self.pad)
         la = batch.lg_edge_attr
         self.angle_dim = int(la.size(-1)) if la.dim() == 2 else 0
         if self.T > 0 and la.numel() > 0:
@@ -168,7 +172,7 @@ class BatchCache:
         return (g.n, g.m, g.n_full, g.rows is not None, int(sc.n_light), int(sc.n_heavy), int(sc.flags))
 
     def signature(self):
-        return (self.N, self.E, self.T, self.B, self.angle_dim,
+        return (self.N, self.E, self.T, self.B, self.real_graphs, self.angle_dim,
                 None if self._xa_buf is None else tuple(self._xa_buf.shape),
                 self._graph_sig(self.ag), self._graph_sig(self.lg),
                 tuple(self.batch_vec.shape), tuple(self.ptr.shape))
@@ -207,9 +211,12 @@ class BatchCache:
     COMPACT_FRACTION = 0.75
 
     @classmethod
-    def _line_graph(cls, edge_index: torch.Tensor, n: int, validate: bool) -> ops.GraphCSR:
+    def _line_graph(cls, edge_index: torch.Tensor, n: int, validate: bool, pad=None) -> ops.GraphCSR:
         """CSR of the line graph, compacted when few bonds are active.  The active set is marked from
-        the edge endpoints directly (no CSR of all n bonds is built first): one CSR build per batch."""
+        the edge endpoints directly (no CSR of all n bonds is built first): one CSR build per batch.
+        pad (a padded batch): compaction as its capacity says; with a compacted capacity, ghost bonds
+        past the first pad['kg'] (those the ghost triplets use) join the active set until it has
+        pad['active'] members — device arithmetic, no host round trip."""
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError("edge_index must be int64 [2, m]")
         m = edge_index.size(1)
@@ -222,15 +229,22 @@ class BatchCache:
             lo, hi = torch.stack([edge_index.min(), edge_index.max()]).tolist()
             if lo < 0 or hi >= n:
                 raise IndexError(f"lg_edge_index: edge index out of range [0, {n})")
+        if pad is not None and pad["active"] is None:
+            return ops.GraphCSR(edge_index, n)
         active = torch.zeros(n, dtype=torch.bool, device=edge_index.device)
         active[edge_index[0]] = True
         active[edge_index[1]] = True
-        return cls._compact(active, edge_index, n)
+        if pad is not None:
+            first = pad["edges"] + pad["kg"]
+            need = pad["active"] - active.sum()
+            j = torch.arange(n, device=edge_index.device) - first
+            active |= (j >= 0) & (j < need)
+        return cls._compact(active, edge_index, n, force=pad is not None)
 
     @classmethod
-    def _compact(cls, active: torch.Tensor, edge_index: torch.Tensor, n: int) -> ops.GraphCSR:
+    def _compact(cls, active: torch.Tensor, edge_index: torch.Tensor, n: int, force: bool = False) -> ops.GraphCSR:
         na = int(active.sum().item())
-        if na > cls.COMPACT_FRACTION * n:
+        if na > cls.COMPACT_FRACTION * n and not force:
             return ops.GraphCSR(edge_index, n)
         rows = torch.nonzero(active).flatten()
         cmap = torch.full((n,), -1, dtype=torch.int64, device=edge_index.device)

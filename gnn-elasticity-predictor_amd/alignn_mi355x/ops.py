@@ -8,6 +8,7 @@ import threading
 from contextlib import contextmanager
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib, profiling
@@ -40,6 +41,9 @@ def _dkey(device) -> str:
     return str(d)
 
 
+_FREE_STREAMS: dict = {}   # device -> library streams no live context holds
+
+
 class ExecContext:
     """What the launches of one engine (model) share: per-purpose scratch buffers, the side / aux
     streams for work off the critical path, and the device step seed its dropout kernels read.
@@ -67,6 +71,7 @@ class ExecContext:
         self._side = {}
         self._aux = {}
         self.step_seed: Optional[torch.Tensor] = None
+        self._owned_streams = []
         self.frozen = 0       # live plans / graphs holding this context's buffers
         self._eager = {}      # buffers of eager launches that outgrew a frozen buffer
 
@@ -85,19 +90,43 @@ class ExecContext:
                     self.buf[k] = t
             self._eager.clear()
 
+    def _own_stream(self, device) -> torch.cuda.Stream:
+        """A stream created by the library (alignn_stream_create), not taken from torch's pool: pooled
+        streams repeat after 32 and could coincide with a capture or caller stream, which this context
+        would then mistake for its side / aux stream.  Held by one live context at a time; a released
+        one is reused, never destroyed (tensors recorded on it may outlive the context)."""
+        key = _dkey(device)
+        free = _FREE_STREAMS.setdefault(key, [])
+        if free:
+            h = free.pop()
+        else:
+            hv = ctypes.c_void_p()
+            check(_lib.lib().alignn_stream_create(0, ctypes.byref(hv)), "alignn_stream_create")
+            h = hv.value
+        self._owned_streams.append((key, h))
+        return torch.cuda.ExternalStream(h, device=torch.device(key))
+
     def side(self, device) -> torch.cuda.Stream:
         """A second stream per device for work off the critical path (weight gradients)."""
         key = _dkey(device)
         if key not in self._side:
-            self._side[key] = torch.cuda.Stream(device=device)
+            self._side[key] = self._own_stream(device)
         return self._side[key]
 
     def aux(self, device) -> torch.cuda.Stream:
         """A third stream per device for short branches beside the critical path."""
         key = _dkey(device)
         if key not in self._aux:
-            self._aux[key] = torch.cuda.Stream(device=device)
+            self._aux[key] = self._own_stream(device)
         return self._aux[key]
+
+    def __del__(self):
+        try:
+            for key, h in self._owned_streams:
+                _FREE_STREAMS.setdefault(key, []).append(h)
+            self._owned_streams = []
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
     def _role(self, device):
         if torch.device(device).type != "cuda":
@@ -599,46 +628,14 @@ class GraphCSR:
 
     def schedule(self):
         """Light/heavy target-node lists for the attention kernels (host-built once per graph:
-        one small device->host copy of the offsets)."""
+        one small device->host copy of the offsets, numpy ordering, one upload)."""
         if self._sched is None:
-            off = self.off_dst.cpu()
-            deg = off[1:] - off[:-1]
-            heavy_mask = deg > self.HEAVY_THRESHOLD
-            idx = torch.arange(self.n, dtype=torch.int32)
-            # light list: nodes with in-edges first, in-degree-0 nodes last (the kernels skip
-            # per-workgroup setup for items that start with an empty node)
-            light_mask = ~heavy_mask
-            lit = idx[light_mask & (deg > 0)]
-            hv = idx[heavy_mask]
-            if self.SORT_BY_DEGREE or self.WAVE_ITEMS:
-                # longest segments first (their waves start in the first round of resident
-                # workgroups) and similar degrees in one workgroup (its 4 waves finish together);
-                # each node is still one wave's work, so results do not change
-                lit = lit[torch.sort(deg[lit.long()], descending=True, stable=True).indices]
-                hv = hv[torch.sort(deg[hv.long()], descending=True, stable=True).indices]
-            if self.XCD_ITEMS and self.WAVE_ITEMS and lit.numel() > self.XCDS:
-                # contiguous target ranges per XCD holding equal numbers of EDGES (equal target
-                # counts put 322 132-edge targets on one XCD's 256 wave slots: two rounds), LPT
-                # order inside each, interleaved i % XCDS
-                cum = torch.cumsum(deg.to(torch.int64), 0)
-                tot = int(cum[-1]) if self.n else 0
-                bounds = [0] + [int(torch.searchsorted(cum, tot * x // self.XCDS, right=True)) for x in
-                                range(1, self.XCDS)] + [self.n]
-                parts = []
-                for x in range(self.XCDS):
-                    sel = lit[(lit >= bounds[x]) & (lit < bounds[x + 1])]
-                    parts.append(sel[torch.sort(deg[sel.long()], descending=True, stable=True).indices].tolist())
-                # chunks of xcd_chunk items: kernels taking several items per workgroup (the atom
-                # graph's four-target workgroups) keep one workgroup's items in one range
-                c = max(1, int(self.xcd_chunk))
-                order, j = [], 0
-                while any(j * c < len(q) for q in parts):
-                    for q in parts:
-                        order += q[j * c:(j + 1) * c]
-                    j += 1
-                lit = torch.tensor(order, dtype=torch.int32)
-            light = torch.cat([lit, idx[light_mask & (deg == 0)]]).to(self.off_dst.device)
-            heavy = hv.to(self.off_dst.device)
+            off = self.off_dst.cpu().numpy().astype(np.int64)
+            deg = off[1:] - off[:-1] if self.n else np.zeros(0, np.int64)
+            light, heavy = schedule_lists(deg, self.HEAVY_THRESHOLD, self.SORT_BY_DEGREE or self.WAVE_ITEMS,
+                                          self.XCD_ITEMS and self.WAVE_ITEMS, self.XCDS, self.xcd_chunk)
+            both = torch.from_numpy(np.concatenate([light, heavy]).astype(np.int32)).to(self.off_dst.device)
+            light, heavy = both[:len(light)], both[len(light):]
             sc = _lib.Schedule()
             sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
             sc.heavy, sc.n_heavy = (heavy.data_ptr() if heavy.numel() else None), heavy.numel()
@@ -660,6 +657,42 @@ class GraphCSR:
         """Host check of the device error flag (one sync).  PyG raises IndexError here."""
         if int(self.err.item()) != 0:
             raise IndexError(f"{what}: edge index out of range [0, {self.n})")
+
+
+def schedule_lists(deg: np.ndarray, heavy_threshold: int, by_degree: bool, xcd_ranges: bool, xcds: int = 8,
+                   chunk: int = 1):
+    """(light, heavy) work lists of target ids for the attention kernels, from the in-degrees.
+
+    light: targets with in-degree 1..heavy_threshold, then the in-degree-0 ones (the kernels skip
+    per-workgroup setup for items that start with an empty node); heavy: in-degree above it.
+    by_degree: longest segments first (their waves start in the first round of resident workgroups;
+    each node is still one wave's work, so results do not change).  xcd_ranges: the light targets
+    with in-edges split into ``xcds`` contiguous id ranges holding equal numbers of EDGES (a target's
+    sources lie near it, so XCD x, which runs workgroups i % xcds == x, keeps the K/V rows of its
+    range in its own L2; equal target counts put 322 132-edge targets on one XCD's 256 wave slots),
+    longest first within each range, and interleaved range by range in chunks of ``chunk`` items
+    (kernels taking several items per workgroup keep one workgroup's items in one range)."""
+    n = len(deg)
+    idx = np.arange(n, dtype=np.int64)
+    light_m = deg <= heavy_threshold
+    lit = idx[light_m & (deg > 0)]
+    hv = idx[~light_m]
+    if by_degree:
+        lit = lit[np.argsort(-deg[lit], kind="stable")]
+        hv = hv[np.argsort(-deg[hv], kind="stable")]
+    if xcd_ranges and len(lit) > xcds:
+        cum = np.cumsum(deg)
+        tot = int(cum[-1]) if n else 0
+        bounds = np.asarray([0] + [int(np.searchsorted(cum, tot * x // xcds, side="right")) for x in range(1, xcds)]
+                            + [n])
+        xr = np.searchsorted(bounds, lit, side="right") - 1          # range of each target
+        perm = np.argsort(xr, kind="stable")                           # by range, keeping the lit order
+        start = np.searchsorted(xr[perm], np.arange(xcds))
+        rank = np.empty(len(lit), np.int64)
+        rank[perm] = np.arange(len(lit)) - start[xr[perm]]             # position within its range
+        c = max(1, int(chunk))
+        lit = lit[np.lexsort((rank % c, xr, rank // c))]               # chunk j of range 0, 1, ..., then j + 1
+    return np.concatenate([lit, idx[light_m & (deg == 0)]]), hv
 
 
 def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

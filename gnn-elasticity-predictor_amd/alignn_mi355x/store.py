@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import json
 import os
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -90,6 +91,55 @@ class CollatePlan:
         return out
 
 
+# ------------------------------------------------------------------------------------------------
+# Fixed-capacity batches: a captured training plan (trainer.FusedTrainer) holds every size its
+# launches were recorded with, so batches of real, variable-size crystals would each need a new plan.
+# Instead a batch is padded to a capacity with one inert "ghost" graph: ghost atoms, ghost bonds in a
+# ring over the ghost atoms, ghost triplets in a ring over a few ghost bonds (in-degrees below the
+# attention kernels' heavy threshold), zero features; under the PyG offset rule the compacted line
+# graph is filled up to the capacity with further ghost bonds (engine.BatchCache).  The ghost graph
+# is disconnected from the real ones and its heads get no loss gradient, so every real output and
+# gradient is the unpadded batch's (up to the summation order of reductions over rows); every padded
+# batch has the capacity's sizes, i.e. one plan signature.
+# ------------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class BatchCapacity:
+    graphs: int                    # real graphs per batch (the ghost graph is one more)
+    nodes: int                     # atoms, ghost atoms included
+    edges: int                     # bonds
+    triplets: int                  # line-graph edges
+    active: Optional[int] = None   # compacted line-graph nodes (PyG offset rule); None: no compaction
+    max_in_degree: int = 200       # of a ghost node (below GraphCSR.HEAVY_THRESHOLD = 256)
+
+
+def ghost_plan(cap: BatchCapacity, B: int, N: int, E: int, T: int) -> Optional[Dict[str, int]]:
+    """Ghost sizes padding a batch of B graphs with N atoms / E bonds / T triplets to ``cap``, or None
+    when it does not fit: ga ghost atoms (>= 1), ge ghost bonds (ring over the ghost atoms), gt ghost
+    triplets (ring over the first kg ghost bonds)."""
+    if B != cap.graphs:
+        return None
+    ga, ge, gt = cap.nodes - N, cap.edges - E, cap.triplets - T
+    if ga < 1 or ge < 0 or gt < 0:
+        return None
+    d = cap.max_in_degree
+    if ge and -(-ge // ga) > d:
+        return None
+    kg = 0
+    if gt:
+        if ge == 0:
+            return None
+        kg = min(ge, max(1, -(-gt // d)))
+        if -(-gt // kg) > d:
+            return None
+    return {"ga": ga, "ge": ge, "gt": gt, "kg": kg, "N": N, "E": E, "T": T}
+
+
+def ghost_edges_host(count: int, base: int, mod: int) -> np.ndarray:
+    """Host restatement of alignn_ghost_edges_i64 (tests): [2, count] ring edges."""
+    j = np.arange(count, dtype=np.int64)
+    return np.stack([base + (j + 1) % max(mod, 1), base + j % max(mod, 1)]) if count else np.zeros((2, 0), np.int64)
+
+
 # PtGraphDataset's float fields checked by _is_valid (train.py:176)
 VALIDATED_FIELDS = ("x", "edge_attr", "lg_edge_attr", "global_x", "sg_one_hot", "y")
 BASE_SCALAR_DIM = 6   # train.py:102
@@ -114,6 +164,82 @@ class GraphStore:
         self._configure_nodes(use_mat2vec, force_node_dim)
         self._x_stats = None   # device (mean, std) over node_dim columns, identity where a block has none
         self._g_stats = None   # device (mean, std) over the global scalars
+
+    # -------------------------------------------------------------------------------- capacity
+    def field_kind(self, f: str) -> str:
+        """'node' / 'edge' / 'triplet' (rows per graph = its atoms / bonds / line-graph edges) or
+        'graph' (the same number of rows for every graph: global_x, sg_one_hot, y)."""
+        named = {"x": "node", "edge_index": "edge", "edge_attr": "edge", "lg_edge_index": "triplet",
+                 "lg_edge_attr": "triplet"}
+        if f in named:
+            return named[f]
+        c = self.counts[f]
+        if len(c) and np.all(c == c[0]):
+            return "graph"
+        for kind, ref in (("node", "x"), ("edge", "edge_index"), ("triplet", "lg_edge_index")):
+            if ref in self.counts and np.array_equal(c, self.counts[ref]):
+                return kind
+        raise ValueError(f"field {f!r}: rows per graph follow neither atoms, bonds, triplets nor a constant")
+
+    def _lg_spans(self) -> np.ndarray:
+        """Per stored graph: [lo, hi] of its local line-graph endpoint ids (the bonds it touches lie
+        inside), once, on the device."""
+        if getattr(self, "_spans", None) is None:
+            a = self.arrays["lg_edge_index"]
+            cnt = torch.from_numpy(self.counts["lg_edge_index"]).to(a.device)
+            lo = torch.segment_reduce(a.min(0).values.double(), "min", lengths=cnt, unsafe=True)
+            hi = torch.segment_reduce(a.max(0).values.double(), "max", lengths=cnt, unsafe=True)
+            self._spans = torch.stack([lo, hi], 1).cpu().numpy().astype(np.int64)
+        return self._spans
+
+    def batch_sizes(self, indices, lg_offset: str = "num_nodes") -> Dict[str, int]:
+        """Host sizes of a batch: atoms, bonds, triplets, and an upper bound of the line graph's active
+        bonds (union of each graph's touched-bond span shifted by its PyG increment)."""
+        gids = self.ids[np.asarray(indices, dtype=np.int64)]
+        n, e, t = (self.counts[f][gids].astype(np.int64) for f in ("x", "edge_index", "lg_edge_index"))
+        inc = _excl_cumsum(n if lg_offset == "num_nodes" else e)
+        sp = self._lg_spans()[gids]
+        has = t > 0
+        lo, hi = (inc + sp[:, 0])[has], (inc + sp[:, 1])[has]
+        order = np.argsort(lo, kind="stable")
+        active, end = 0, -1
+        for a, b in zip(lo[order], hi[order]):
+            if b <= end:
+                continue
+            active += b - max(a, end + 1) + 1
+            end = b
+        return {"nodes": int(n.sum()), "edges": int(e.sum()), "triplets": int(t.sum()), "active": int(active)}
+
+    def fits(self, indices, capacity: BatchCapacity, lg_offset: str = "num_nodes") -> Optional[Dict[str, int]]:
+        """The ghost plan padding this batch to ``capacity``, or None when it does not fit (then the
+        batch runs uncaptured).  With a compacted capacity the ghost bonds must be able to fill the
+        line graph up to ``capacity.active``: real active bonds + kg <= active <= real active bonds +
+        ghost bonds (real active bonds: the span bound of batch_sizes, exact when every bond has
+        line-graph edges; if the true count is lower the batch's signature misses and it runs eagerly)."""
+        sz = self.batch_sizes(indices, lg_offset)
+        gp = ghost_plan(capacity, len(np.asarray(indices).reshape(-1)), sz["nodes"], sz["edges"], sz["triplets"])
+        if gp is None or capacity.active is None:
+            return gp
+        if sz["active"] + gp["kg"] > capacity.active or capacity.active - sz["active"] > gp["ge"]:
+            return None
+        return gp
+
+    def capacity(self, graphs: int, lg_offset: str = "num_nodes", samples: int = 512, margin: float = 0.02,
+                 seed: int = 0, compact_fraction: float = 0.75) -> BatchCapacity:
+        """A capacity that random batches of ``graphs`` dataset graphs fit (the largest of ``samples``
+        random batches plus ``margin``, plus ghost room); rare larger batches run uncaptured."""
+        rng = np.random.default_rng(seed)
+        sz = [self.batch_sizes(rng.choice(self.num_graphs, size=graphs, replace=graphs > self.num_graphs), lg_offset)
+              for _ in range(samples)]
+        col = {k: np.asarray([z[k] for z in sz], dtype=np.int64) for k in sz[0]}
+        grow = lambda v, extra: int(np.ceil(v * (1.0 + margin))) + extra  # noqa: E731
+        nodes, edges, trip = grow(col["nodes"].max(), 4), grow(col["edges"].max(), 16), grow(col["triplets"].max(), 16)
+        # the compacted line graph must hold each batch's active bonds plus the ghost bonds its ghost
+        # triplets use (more for smaller batches: more ghost triplets)
+        d = BatchCapacity.max_in_degree
+        act = grow(int((col["active"] + -(-(trip - col["triplets"]) // d)).max()), 8)
+        active = act if act <= compact_fraction * edges else None
+        return BatchCapacity(graphs, nodes, edges, trip, active)
 
     # -------------------------------------------------------------------------------- transform
     def _configure_nodes(self, use_mat2vec: bool, force_node_dim: Optional[int]) -> None:
@@ -321,12 +447,21 @@ class GraphStore:
         pl.sample_index = idx
         return pl
 
-    def collate(self, indices, lg_offset: str = "num_nodes") -> Batch:
+    def collate(self, indices, lg_offset: str = "num_nodes", capacity: Optional[BatchCapacity] = None) -> Batch:
         """Batch of the given graphs, assembled on the device (same tensors as
-        ``Batch.from_data_list([graphs...], lg_offset)``)."""
+        ``Batch.from_data_list([graphs...], lg_offset)``).  With a ``capacity`` the batch is padded
+        to it by one ghost graph (``num_real_graphs`` = the real graph count); a batch that does not
+        fit is returned unpadded."""
         pl = self.plan(indices, lg_offset)
         G = len(pl.idx)
         dev = next(iter(self.arrays.values())).device
+        gh = None
+        if capacity is not None and "lg_edge_index" in pl.fields:
+            gh = self.fits(indices, capacity, lg_offset)
+        if gh is not None:   # the ghost graph's atoms in the batch vector and ptr
+            pl.node_dst = np.append(pl.node_dst, gh["N"])
+            pl.nodes = np.append(pl.nodes, gh["ga"])
+            pl.ptr = np.append(pl.ptr, capacity.nodes)
         # one upload of every per-graph int64 offset array
         order = list(pl.fields.items())
         host = []
@@ -353,13 +488,22 @@ class GraphStore:
             vi += 3
             m = self.meta[f]
             a = self.arrays[f]
+            rows = ent["total"]
+            if gh is not None:
+                kind = self.field_kind(f)
+                rows = {"node": capacity.nodes, "edge": capacity.edges, "triplet": capacity.triplets,
+                        "graph": ent["total"] + (ent["total"] // G if G else 0)}[kind]
             if m["kind"] == "index":
                 add = views[vi]
                 vi += 1
-                out = torch.empty(2, ent["total"], dtype=torch.int64, device=dev)
+                out = torch.empty(2, rows, dtype=torch.int64, device=dev)
                 _lib.check(lib.alignn_collate_index_i64(G, a.data_ptr(), a.size(1), src.data_ptr(), dst.data_ptr(),
                                                         cnt.data_ptr(), add.data_ptr(), ent["max"], out.data_ptr(),
                                                         out.size(1), s), "alignn_collate_index_i64")
+                if gh is not None:   # ghost bonds: ring over the ghost atoms; ghost triplets: over kg ghost bonds
+                    base, mod = (gh["N"], gh["ga"]) if kind == "edge" else (gh["E"], gh["kg"])
+                    _lib.check(lib.alignn_ghost_edges_i64(out.data_ptr(), out.size(1), ent["total"],
+                                                          rows - ent["total"], base, mod, s), "alignn_ghost_edges_i64")
             else:
                 w = int(m.get("width", 1))
                 ow, copy_w, stats, by_row = w, w, None, 0
@@ -367,7 +511,10 @@ class GraphStore:
                     ow, copy_w, stats = self.node_dim, self._x_copy_w, self._x_stats
                 elif f == "global_x":
                     stats, by_row = self._g_stats, 1
-                out = torch.empty(ent["total"], ow, dtype=torch.float32, device=dev)
+                out = torch.empty(rows, ow, dtype=torch.float32, device=dev)
+                if rows > ent["total"]:   # ghost rows: zero features, target 1 (positive for the log transform)
+                    _lib.check(lib.alignn_fill_f32(out[ent["total"]:].data_ptr(), (rows - ent["total"]) * ow,
+                                                   1.0 if f == "y" else 0.0, s), "alignn_fill_f32")
                 if (ow, copy_w, stats) == (w, w, None):
                     _lib.check(lib.alignn_collate_rows_f32(G, a.data_ptr(), w, src.data_ptr(), dst.data_ptr(),
                                                            cnt.data_ptr(), ent["max"], out.data_ptr(), s),
@@ -378,16 +525,21 @@ class GraphStore:
                         out.data_ptr(), ow, copy_w, None if stats is None else stats[0].data_ptr(),
                         None if stats is None else stats[1].data_ptr(), by_row, s), "alignn_collate_rows_std_f32")
                 shape = m["shape"] if ow == w else [ow]
-                out = out.view(ent["total"], *shape) if shape else out.view(ent["total"])
+                out = out.view(rows, *shape) if shape else out.view(rows)
             setattr(b, f, out)
         node_dst, nodes, ptr, sample_index = views[vi], views[vi + 1], views[vi + 2], views[vi + 3]
         batch = torch.empty(int(pl.nodes.sum()), dtype=torch.int64, device=dev)
-        _lib.check(lib.alignn_collate_batchvec(G, node_dst.data_ptr(), nodes.data_ptr(), int(pl.nodes.max()),
-                                               batch.data_ptr(), s), "alignn_collate_batchvec")
+        _lib.check(lib.alignn_collate_batchvec(len(pl.nodes), node_dst.data_ptr(), nodes.data_ptr(),
+                                               int(pl.nodes.max()), batch.data_ptr(), s), "alignn_collate_batchvec")
         b.batch = batch
         b.ptr = ptr.clone()
         b.sample_index = sample_index.clone()   # train.py:171 (dataset indices of the batch's graphs)
         b.num_graphs = G
+        if gh is not None:
+            b.num_graphs = G + 1
+            b.num_real_graphs = G
+            # read by engine.BatchCache: ghost bonds after the first kg fill the compacted line graph
+            b._alignn_pad = {"edges": gh["E"], "kg": gh["kg"], "active": capacity.active}
         for k, vals in self.extras.items():
             setattr(b, k, [vals[i] for i in pl.idx])
         b._staging = (staged, offs)  # keep the pinned source alive until the copy has run

@@ -82,6 +82,16 @@ def mp_like_graph(g: int, node_dim: int = 206, edge_dim: int = 36, angle_dim: in
     )
 
 
+def variable_mp_like_graph(g: int, min_atoms: int = 8, max_atoms: int = 60, **kw) -> Data:
+    """An MP-like graph of seeded size: n_atoms uniform in [min_atoms, max_atoms], neighbour shells
+    half_degree uniform in [2, min(6, (n_atoms - 1) // 2)] (E = 2 half_degree n_atoms bonds,
+    T = E (2 half_degree - 1) triplets) — real crystals' spread of sizes for the variable-size loop."""
+    r = np.random.default_rng(777 + g)
+    n = int(r.integers(min_atoms, max_atoms + 1))
+    hd = int(r.integers(2, min(6, (n - 1) // 2) + 1))
+    return mp_like_graph(g, n_atoms=n, half_degree=hd, **kw)
+
+
 def si2_smoke_graph(g: int, cutoff: float = 5.0, a: float = 3.5, node_dim: int = 6, edge_dim: int = 8,
                     angle_dim: int = 7, target_dim: int = 2) -> Data:
     frac = np.array([[0.0, 0.0, 0.0], [0.25, 0.25, 0.25]])

@@ -118,8 +118,14 @@ class FusedTrainer:
             ops.add_noise(gx, self.jitter, site_seed(seed, (1 << 20) + 1))
         out, ctx = model._engine.forward(st.P, batch, bc, training, seed, x, gx, "hetero")
         dout = torch.empty_like(out)
-        ops.hetero_nll(out, batch.y.contiguous().float(), self.log_means, self.log_stds, self.floor, self.l2,
-                       self.loss, dout, weights=sample_weights)
+        # a batch padded to a capacity (store.BatchCapacity): the loss is the real graphs' mean and the
+        # ghost graph's heads get a zero gradient
+        nr = out.size(0) if bc.real_graphs is None else bc.real_graphs
+        y = batch.y.contiguous().float()
+        ops.hetero_nll(out[:nr], y[:nr * (out.size(1) // 2)], self.log_means, self.log_stds, self.floor, self.l2,
+                       self.loss, dout[:nr], weights=sample_weights)
+        if nr < out.size(0):
+            ops.zero_(dout[nr:])
         model._engine.backward(st.P, st.G, ctx, dout)
         return self.loss
 

@@ -155,6 +155,17 @@ __global__ void stats_reduce_f64_kernel(const double* __restrict__ psum, const d
   sq[k] = q;
 }
 
+// The inert "ghost" graph that pads a batch to a fixed capacity (store.BatchCapacity): ghost edge j
+// (j < count) of a two-row int64 index field runs base + (j + 1) % mod -> base + j % mod, i.e. a ring
+// over `mod` ghost nodes (in-degree ceil(count / mod)).
+__global__ void ghost_edges_kernel(int64_t* __restrict__ dst, int64_t ld, int64_t start, int64_t count, int64_t base,
+                                   int64_t mod) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < count; j += (int64_t)gridDim.x * blockDim.x) {
+    dst[start + j] = base + (j + 1) % mod;
+    dst[ld + start + j] = base + j % mod;
+  }
+}
+
 static dim3 seg_grid(int64_t max_count_elems, int G) {
   int64_t chunks = (max_count_elems + 1023) / 1024;
   if (chunks < 1) chunks = 1;
@@ -277,5 +288,19 @@ extern "C" int alignn_feature_stats_f64(int32_t J, const float* src, int64_t wid
   launch(stats_reduce_f64_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, psum, psq, (int64_t)J, K, sum,
          sq);
   ALIGNN_LAUNCH_CHECK("stats_reduce_f64_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_ghost_edges_i64(int64_t* dst, int64_t ld, int64_t start, int64_t count, int64_t base,
+                                      int64_t mod, void* stream) {
+  if (count < 0 || start < 0 || base < 0 || (count > 0 && mod <= 0)) {
+    set_error("ghost_edges: count >= 0, start >= 0, base >= 0 and mod > 0");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (count == 0) return ALIGNN_OK;
+  const int64_t blocks = std::min<int64_t>((count + 255) / 256, 1024);
+  launch(ghost_edges_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dst, ld,
+         start, count, base, mod);
+  ALIGNN_LAUNCH_CHECK("ghost_edges_kernel");
   return ALIGNN_OK;
 }

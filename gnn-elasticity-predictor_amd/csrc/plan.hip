@@ -349,3 +349,30 @@ extern "C" int alignn_copy_f32(float* dst, const float* src, int64_t n, void* st
   ALIGNN_LAUNCH_CHECK("copy_f32_kernel");
   return ALIGNN_OK;
 }
+
+// A HIP stream of the library's own (non-blocking, given priority): an execution context's side / aux
+// streams must be distinct from every stream torch hands out from its pool, since the context tells
+// its stream roles apart by handle.
+extern "C" int alignn_stream_create(int32_t priority, void** out) {
+  if (!out) return ALIGNN_E_BAD_SHAPE;
+  hipStream_t s = nullptr;
+  hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, (int)priority);
+  if (e != hipSuccess) {
+    set_error("hipStreamCreateWithPriority: %s", hipGetErrorString(e));
+    return ALIGNN_E_HIP;
+  }
+  *out = reinterpret_cast<void*>(s);
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_stream_destroy(void* stream) {
+  if (!stream) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipStreamDestroy(s);
+  if (e != hipSuccess) {
+    set_error("hipStreamDestroy: %s", hipGetErrorString(e));
+    return ALIGNN_E_HIP;
+  }
+  return ALIGNN_OK;
+}

@@ -89,6 +89,9 @@ typedef struct AlignnGemmArgs {
 /* bf16 only: never the streaming kernel (the large-M products K in {64, 128, 256}, N % 256 == 0,
  * M >= 4096 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
 #define ALIGNN_GEMM_NOSTREAM 512
+/* 64x64 tiles shared by two groups of four waves, each multiplying half of every 32-deep stage
+ * (twice the waves per tile for small grids; the groups' partial sums added in group order). */
+#define ALIGNN_GEMM_KW2 1024
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
@@ -483,6 +486,11 @@ int64_t alignn_feature_stats_workspace(int32_t J, int64_t K);
 int alignn_feature_stats_f64(int32_t J, const float* src, int64_t width, const int64_t* start, const int64_t* count,
                              int64_t K, int32_t by_row, double* sum, double* sq, double* workspace,
                              int64_t workspace_elems, void* stream);
+/* Ghost edges of the inert graph that pads a batch to a fixed capacity (a captured plan replays any
+ * batch that fits; alignn_mi355x.store.BatchCapacity): for j < count, dst[start + j] =
+ * base + (j + 1) % mod (source row) and dst[ld + start + j] = base + j % mod (target row). */
+int alignn_ghost_edges_i64(int64_t* dst, int64_t ld, int64_t start, int64_t count, int64_t base, int64_t mod,
+                           void* stream);
 /* Up to 32 device-to-device copies in one launch (src, dst: HOST arrays of device pointers, 16-byte
  * aligned; bytes: host array, multiples of 4).  Re-binds a captured step to a new batch (the batch
  * fields and its CSR / compaction / schedule cache copied into the captured buffers). */
@@ -547,6 +555,11 @@ int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms);
 int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, int64_t n, uint64_t* bad_value,
                            int64_t* bad_launch, int64_t* checked);
 int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other);
+/* A non-blocking HIP stream of the library's own at `priority` (an execution context's side / aux
+ * streams: never one of torch's pooled streams, which may coincide with a capture or loader stream);
+ * destroy synchronises it first. */
+int alignn_stream_create(int32_t priority, void** out);
+int alignn_stream_destroy(void* stream);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);
 int alignn_set_i64(int64_t* x, int64_t value, void* stream);

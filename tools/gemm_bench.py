@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json")
     ap.add_argument("--quick", action="store_true", help="auto plan + torch.matmul (hipBLASLt/rocBLAS) only")
+    ap.add_argument("--flag", type=int, default=0,
+                    help="also time the auto plan with these tile flag bits ORed in (e.g. 1024: ALIGNN_GEMM_KW2) "
+                         "and report its result's max difference from the auto plan's")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="bf16: the step's products with bf16 matrix-core inputs (config C3); the library "
                          "reference is then torch.matmul on bf16 copies of the operands")
@@ -100,6 +103,18 @@ def main():
             t_lib = timeit(lambda: torch.matmul(Am, Bm), a.reps)
         except Exception:  # noqa: BLE001
             t_lib = float("nan")
+        extra = ""
+        if a.flag:
+            c["C"].copy_(C_save)
+            run()
+            ref = c["C"].clone()
+            c["C"].copy_(C_save)
+            run(a.flag)
+            diff = float((c["C"] - ref).abs().max() / ref.abs().max().clamp(min=1e-30))
+            t_flag = timeit(lambda: run(a.flag), a.reps)
+            extra = f"  flag{a.flag} {t_flag:7.1f}us (diff {diff:.1e})"
+            tot_flag = globals().setdefault("_tot_flag", [0.0])
+            tot_flag[0] += t_flag * len(cs)
         trials = {}
         for tile in ([] if a.quick else sorted(TILES)):
             if tile < 16 or tile == 20:
@@ -129,8 +144,9 @@ def main():
         res.append(row)
         print(f"M{M:6d} N{N:5d} K{K:6d} b{bt} x{n:2d} A{key[1]} B{key[3]}: auto {t_auto:7.1f}us "
               f"({row['auto_tflops']:5.1f} TF)  best {TILES[best[0]]}/s{best[1]} {trials[best]:7.1f}us "
-              f"({row['best_tflops']:5.1f} TF)  torch.matmul {t_lib:7.1f}us ({fl / t_lib / 1e6:5.1f} TF)", flush=True)
-    print(f"step gemm total: auto {tot_auto:.0f} us, best {tot_best:.0f} us, torch.matmul {tot_lib:.0f} us")
+              f"({row['best_tflops']:5.1f} TF)  torch.matmul {t_lib:7.1f}us ({fl / t_lib / 1e6:5.1f} TF){extra}", flush=True)
+    print(f"step gemm total: auto {tot_auto:.0f} us, best {tot_best:.0f} us, torch.matmul {tot_lib:.0f} us"
+          + (f", flag {a.flag}: {globals()['_tot_flag'][0]:.0f} us" if a.flag else ""))
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)

@@ -20,12 +20,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=15)
+    ap.add_argument("--by-kernel", action="store_true", help="per-queue time by kernel (name, grid) in the step")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Queue_Id"]),
-                         r["Kernel_Name"]))
+                         r["Kernel_Name"] + (f" grid={int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) * int(r['Grid_Size_Z'])}" if a.by_kernel else "")))
     rows.sort()
     ends = [e for s, e, q, n in rows if "adamw_kernel" in n]
     if len(ends) < 3:
@@ -61,6 +62,17 @@ def main():
           ", ".join(f"{b}: {t/1e3:.0f}" for b, t in sorted(hist.items())))
     for g, p, n in gaps[:a.top]:
         print(f"  gap {g/1e3:7.1f} us  after {short(p)}  before {short(n)}")
+    if a.by_kernel:
+        for q in sorted(per_q):
+            agg = {}
+            for s_, e_, q_, n in ks:
+                if q_ == q:
+                    k = short(n) + " " + n.split(" grid=")[-1]
+                    c, t = agg.get(k, (0, 0))
+                    agg[k] = (c + 1, t + e_ - s_)
+            print(f"queue {q} by kernel:")
+            for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top * 2]:
+                print(f"  {t/1e3:8.1f} us  n={c:3d}  {k}")
 
 
 if __name__ == "__main__":
