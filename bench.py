@@ -39,6 +39,11 @@ def parse():
                    help="GPUs (= ranks) of one node.  Without a torch.distributed launcher in the environment "
                         "(no WORLD_SIZE) and N > 1, bench.py starts the N rank processes itself "
                         "(torch.distributed.run, 127.0.0.1) before anything touches the GPU")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend of a multi-rank run (nccl = RCCL over xGMI; gloo only to rehearse "
+                        "the multi-rank path where RCCL cannot run, e.g. several ranks on one GPU)")
+    p.add_argument("--share-device", action="store_true",
+                   help="every rank on cuda:0 (with --dist-backend gloo: a multi-rank rehearsal on a one-GPU box)")
     p.add_argument("--dry-run", action="store_true",
                    help="no GPU: every rank runs only the data-parallel exchange (gloo all_reduce of a flat "
                         "gradient of the model's size) — a CPU rehearsal of the rank plumbing")
@@ -530,7 +535,7 @@ def launch_ranks(args) -> int:
     import socket
     import subprocess
     n = args.gpus
-    if not args.dry_run:
+    if not args.dry_run and not args.share_device:
         have = torch.cuda.device_count()
         if have < n:
             print(f"[bench] --gpus {n}: only {have} GPU(s) visible", file=sys.stderr)
@@ -594,9 +599,14 @@ def main():
             dist.init_process_group("gloo")
             return dry_run(args, rank, world)
         raise SystemExit("[bench] --dry-run rehearses the multi-rank exchange: use --gpus N with N > 1")
+    if args.share_device:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     args.main_priority = int(dict(x.split("=", 1) for x in args.set).get("main_priority", 0))
@@ -686,6 +696,8 @@ def main():
                                    f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
                        "dropout": args.dropout, "launch": r["launch"], "precision": args.precision,
+                       **({"dist_backend": args.dist_backend + (" (all ranks on cuda:0: rehearsal)" if args.share_device
+                                                                 else "")} if world > 1 else {}),
                        **({"settings": args.set} if args.set else {})},
             "roofline": r["roofline"], "cpu_baseline": cpu, "e2e": e2e, "e2e_variable": e2e_var,
             "step_roofline": r["step_roofline"], "secondary": secondary,

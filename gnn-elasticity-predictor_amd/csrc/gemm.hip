@@ -179,12 +179,15 @@ __device__ __forceinline__ int64_t c_row(const GemmParams& p, int64_t row) {
   return p.c_rows ? (int64_t)p.c_rows[row] : row;
 }
 
+// Epilogue arithmetic, in one explicit order shared by every GEMM path (the bf16 streaming kernel's
+// band_store too): v = alpha acc; v = fma(beta, C, v); v = v + bias; v = fma(rowscale, bias2, v).
+// Written with explicit roundings so that no path's compiler contraction changes the bits.
 __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, int64_t row, int64_t col, float acc) {
-  float v = p.alpha * acc;
+  float v = __fmul_rn(p.alpha, acc);
   float* Cb = p.C + b * p.scb;
-  if (p.beta != 0.f) v += p.beta * Cb[c_row(p, row) * p.scm + col * p.scn];
-  if (p.bias) v += p.bias[b * p.sbias_b + col];
-  if (p.rowscale) v += p.rowscale[b * p.srs_b + row * p.srs_m] * p.bias2[b * p.sb2_b + col];
+  if (p.beta != 0.f) v = fmaf(p.beta, Cb[c_row(p, row) * p.scm + col * p.scn], v);
+  if (p.bias) v = __fadd_rn(v, p.bias[b * p.sbias_b + col]);
+  if (p.rowscale) v = fmaf(p.rowscale[b * p.srs_b + row * p.srs_m], p.bias2[b * p.sb2_b + col], v);
   if (p.relu) v = fmaxf(v, 0.f);
   if (p.mask) v = p.mask[row * p.smk_m + col * p.smk_n] > 0.f ? v : 0.f;
   return v;
@@ -481,115 +484,6 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
   if (p.split_k > 1 && p.cnt) splitk_combine<BM, BN>(p, b * gridDim.x + tile, m0, n0, b, smem);
 }
 
-// Wave-group K-split (ALIGNN_GEMM_KW2): KW groups of four waves share one 64x64 tile; a stage is
-// BKT x KW deep and group g multiplies its BKT-deep slice of it, so a tile's MFMA work is spread over
-// 4 KW waves — for grids too small to give every SIMD several waves (the mid-size projections of the
-// step: M 1,920-2,580 x N 64-1,024 x K 256-1,024 run one or two waves per SIMD at 4 waves per tile).
-// Loads as in gemm_pipe_kernel (two register sets in flight, full stages, fast-path operands); at the
-// end groups 1.. hand their accumulators to group 0 through LDS, which adds them in group order
-// (fixed: one fp32 rounding per group) and runs the common epilogue.
-template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int KW, bool BF>
-__global__ __launch_bounds__(256 * KW) void gemm_kw_kernel(GemmParams p) {
-  constexpr int MI = BM / 64, NI = BN / 64;
-  constexpr int NT = 256 * KW, SD = BKT * KW;
-  constexpr int LA = lds_floats<BM, A_KC, SD>(), LB = lds_floats<BN, B_KC, SD>();
-  constexpr int RED = (KW - 1) * 4 * MI * NI * 16 * 64;   // hand-off floats of groups 1..KW-1
-  constexpr int SM = 2 * (LA + LB) > RED ? 2 * (LA + LB) : RED;
-  __shared__ __attribute__((aligned(16))) float smem[SM];
-  using TLA = TileLoader<BM, A_KC, SD, NT>;
-  using TLB = TileLoader<BN, B_KC, SD, NT>;
-  constexpr int FA = TLA::F4, FB = TLB::F4;
-
-  const int64_t tiles_n = (p.N + BN - 1) / BN;
-  const int64_t nlin = (int64_t)gridDim.x * gridDim.z;
-  const int64_t lin = (int64_t)blockIdx.z * gridDim.x + blockIdx.x;
-  const int64_t xq = nlin / 8, xr = nlin % 8, xcd = lin % 8;
-  const int64_t item = xcd * xq + min(xcd, xr) + lin / 8;
-  const int64_t tile = item % gridDim.x, zid = item / gridDim.x;
-  const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-  const int64_t b = zid / p.split_k;
-  const int sidx = zid % p.split_k;
-  const int64_t kb = (int64_t)sidx * p.kchunk;
-  const int64_t ke = min(p.K, kb + p.kchunk);
-  const int nst = (int)((ke - kb) / SD);  // >= 1 full stages (host check)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = wave >> 2, wq = wave & 3;
-  const int wm = wq >> 1, wn = wq & 1, h = lane >> 5, l32 = lane & 31;
-  const int sub0 = grp * (BKT / 16);
-
-  floatx16 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  TLA la;
-  TLB lb;
-  la.setup_fast(p.A + b * p.sab, p.sam, p.sak, m0, p.M, kb);
-  lb.setup_fast(p.B + b * p.sbb, p.sbn, p.sbk, n0, p.N, kb);
-  gf4 pa[FA], pb[FB], qa[FA], qb[FB];
-  auto load = [&](gf4 (&ra)[FA], gf4 (&rb)[FB], int st) {
-    const int64_t koff = (int64_t)min(st, nst - 1) * SD;
-#pragma unroll
-    for (int i = 0; i < FA; ++i) ra[i] = *reinterpret_cast<const gf4*>(la.base[i] + (A_KC ? koff : koff * p.sak));
-#pragma unroll
-    for (int i = 0; i < FB; ++i) rb[i] = *reinterpret_cast<const gf4*>(lb.base[i] + (B_KC ? koff : koff * p.sbk));
-    asm volatile("" ::: "memory");
-  };
-  auto store = [&](const gf4 (&ra)[FA], const gf4 (&rb)[FB], float* buf) {
-#pragma unroll
-    for (int i = 0; i < FA; ++i) la.r[i] = make_float4(ra[i].x, ra[i].y, ra[i].z, ra[i].w);
-#pragma unroll
-    for (int i = 0; i < FB; ++i) lb.r[i] = make_float4(rb[i].x, rb[i].y, rb[i].z, rb[i].w);
-    la.store(buf);
-    lb.store(buf + LA);
-  };
-  float* L0 = smem;
-  float* L1 = smem + (LA + LB);
-  load(pa, pb, 0);
-  store(pa, pb, L0);
-  load(pa, pb, 1);
-  load(qa, qb, 2);
-  __syncthreads();
-  const int npairs = (nst + 1) / 2;
-  for (int it = 0; it < npairs; ++it) {
-    const int s0 = 2 * it;
-    mma_stage<BM, BN, A_KC, B_KC, BKT, BF, SD>(acc, L0, L0 + LA, wm, wn, h, l32, sub0);
-    store(pa, pb, L1);
-    load(pa, pb, s0 + 3);
-    __syncthreads();
-    if (s0 + 1 < nst) mma_stage<BM, BN, A_KC, B_KC, BKT, BF, SD>(acc, L1, L1 + LA, wm, wn, h, l32, sub0);
-    store(qa, qb, L0);
-    load(qa, qb, s0 + 4);
-    __syncthreads();
-  }
-  // groups 1..KW-1 -> LDS (lane-major: conflict-free), group 0 adds them in group order
-  if (grp > 0) {
-    float* dst = smem + ((grp - 1) * 4 + wq) * (MI * NI * 16 * 64);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[((i * NI + j) * 16 + r) * 64 + lane] = acc[i][j][r];
-  }
-  __syncthreads();
-  if (grp > 0) return;
-#pragma unroll
-  for (int g = 1; g < KW; ++g) {
-    const float* src = smem + ((g - 1) * 4 + wq) * (MI * NI * 16 * 64);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * NI + j) * 16 + r) * 64 + lane];
-  }
-  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
-}
-
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   const int64_t total = (p.reduce_batch ? 1 : p.batch) * p.M * p.N;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -650,33 +544,8 @@ static bool gemm_pipe_ok(const GemmParams& p, int bk) {
   return true;
 }
 
-// The wave-group K-split kernel's shapes (host check): 64x64 tiles, every split chunk whole 32-deep
-// stages, fast-path operands (as gemm_pipe_ok), no batch reduction.
-template <bool A_KC, bool B_KC>
-static bool gemm_kw_ok(const GemmParams& p) {
-  constexpr int SD = 32;
-  if (p.reduce_batch || !p.vecA || !p.vecB || p.K <= 0 || p.K % SD || p.kchunk % SD) return false;
-  if (!A_KC && p.M % 64 != 0) return false;
-  if (!B_KC && p.N % 64 != 0) return false;
-  if (A_KC && p.sak != 1) return false;
-  if (B_KC && p.sbk != 1) return false;
-  return true;
-}
-
-template <bool A_KC, bool B_KC>
-static void launch_kw(const GemmParams& p, dim3 grid, bool bf, hipStream_t s) {
-  if (bf) launch((gemm_kw_kernel<64, 64, A_KC, B_KC, 16, 2, true>), grid, dim3(512), 0, s, p);
-  else launch((gemm_kw_kernel<64, 64, A_KC, B_KC, 16, 2, false>), grid, dim3(512), 0, s, p);
-}
-
 template <int BM, int BN, bool A_KC, bool B_KC>
-static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe, hipStream_t s, bool kw = false) {
-  if constexpr (BM == 64 && BN == 64) {
-    if (kw && !nopipe && gemm_kw_ok<A_KC, B_KC>(p)) {
-      launch_kw<A_KC, B_KC>(p, grid, bf, s);
-      return;
-    }
-  }
+static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe, hipStream_t s) {
 #ifndef ALIGNN_GEMM_PIPE_TILES
 #define ALIGNN_GEMM_PIPE_TILES 1  // 0: the pipelined loop for 64x64 tiles only (round-2 behaviour)
 #endif
@@ -690,11 +559,11 @@ static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe,
 
 template <int BM, int BN>
 static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, bool bf, bool nopipe,
-                            hipStream_t s, bool kw = false) {
-  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, bf, nopipe, s, kw);
-  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, bf, nopipe, s, kw);
-  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, bf, nopipe, s, kw);
-  else launch<BM, BN, false, false>(p, grid, bk, bf, nopipe, s, kw);
+                            hipStream_t s) {
+  if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, bf, nopipe, s);
+  else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, bf, nopipe, s);
+  else if (!akc && bkc) launch<BM, BN, false, true>(p, grid, bk, bf, nopipe, s);
+  else launch<BM, BN, false, false>(p, grid, bk, bf, nopipe, s);
 }
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -714,7 +583,6 @@ static int device_cus() {
 struct GemmPlan {
   int bm, bn, split, bk;
   int64_t kchunk;
-  bool kw;   // wave-group K-split kernel (gemm_kw_kernel)
 };
 
 // Automatic plan, fitted to a sweep of every product of the training step on MI355X
@@ -729,7 +597,7 @@ struct GemmPlan {
 static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int requested, int tile) {
   const int cus = device_cus();
   static const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
-  GemmPlan pl{64, 64, 1, 16, 0, false};
+  GemmPlan pl{64, 64, 1, 16, 0};
   const int shape = tile & 15;  // bits 16/32/128: stage depth, bit 64: bf16 compute
   if (shape >= 1 && shape <= 4) {
     pl.bm = cand[shape - 1][0];
@@ -795,19 +663,6 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   // two-per-CU splits run faster 16-deep: M2580 N768 K256 18.3 vs 20.6 us, M1024 N256 K1920 23.3 vs 26.0)
   else if (ALIGNN_GEMM_PLAN_V1) pl.bk = (kchunk >= 128 && tiles * split <= 2 * (int64_t)cus) ? 64 : 16;
   else pl.bk = (kchunk >= 512 && tiles * split <= (int64_t)cus) ? 64 : 16;
-  // wave-group K-split: forced by ALIGNN_GEMM_KW2, or automatically (ALIGNN_GEMM_KW_AUTO) for 64x64
-  // grids of fewer than KW_TILES workgroups whose split chunks are at least 64 deep
-#ifndef ALIGNN_GEMM_KW_AUTO
-#define ALIGNN_GEMM_KW_AUTO 0
-#endif
-#ifndef ALIGNN_GEMM_KW_TILES
-#define ALIGNN_GEMM_KW_TILES 768
-#endif
-  if (tile & ALIGNN_GEMM_KW2) pl.kw = true;
-  else if (ALIGNN_GEMM_KW_AUTO && shape == 0 && !bf_long && pl.bm == 64 && pl.bn == 64 &&
-           !(tile & (ALIGNN_GEMM_BK64 | ALIGNN_GEMM_BK32 | ALIGNN_GEMM_BK16)) && kchunk >= 64 &&
-           tiles * split < ALIGNN_GEMM_KW_TILES)
-    pl.kw = true;
 #if ALIGNN_GEMM_BK128
   // 128-deep stages (half the round trips of 64) for a long split on at most one workgroup per CU
   // (the 139 KB double-buffered stage allows one per CU); fp32 64x64 only
@@ -894,10 +749,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n, 0x00020000);
 }
 
-// v = alpha acc + bias (column layout) -> LDS tile -> rows: (+ beta C), ReLU, 16-byte stores.  Rows
-// past M fall outside the store descriptor and are dropped; beta == 0 reads an empty descriptor.
+// alpha acc (column layout) -> LDS tile -> rows: fma(beta, C, .), + bias, ReLU, mask, 16-byte stores
+// (epilogue_value's order).  Rows past M fall outside the store descriptor and are dropped; beta == 0
+// reads an empty descriptor.
 template <bool BETA, bool MASK>
-__device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], const float (&bias)[4],
+__device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], const float* __restrict__ bptr,
                                            float* __restrict__ Ls, __amdgpu_buffer_rsrc_t cst,
                                            __amdgpu_buffer_rsrc_t cld, __amdgpu_buffer_rsrc_t cmk, int64_t row0,
                                            int l32, int h, int lane) {
@@ -905,12 +761,20 @@ __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Ls[((r & 3) + 8 * (r >> 2) + 4 * h) * EPI_LD + l32] = p.alpha * acc[j][r] + bias[j];
+    for (int r = 0; r < 16; ++r) Ls[((r & 3) + 8 * (r >> 2) + 4 * h) * EPI_LD + l32] = __fmul_rn(p.alpha, acc[j][r]);
+    const int bc = 32 * j + cc;   // this lane's 16 output columns start here (bias from LDS-free registers below)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       gf4 v = *reinterpret_cast<const gf4*>(Ls + rr * EPI_LD + cc + 4 * i);
       const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * 4);
-      if constexpr (BETA) v += p.beta * __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
+      if constexpr (BETA) {   // the tiled epilogue's order: fma(beta, C, alpha acc), then + bias
+        const gf4 c = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
+        v = gf4{fmaf(p.beta, c.x, v.x), fmaf(p.beta, c.y, v.y), fmaf(p.beta, c.z, v.z), fmaf(p.beta, c.w, v.w)};
+      }
+      if (bptr) {
+        const gf4 bb = *reinterpret_cast<const gf4*>(bptr + bc + 4 * i);
+        v = gf4{__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z), __fadd_rn(v.w, bb.w)};
+      }
       const gf4 z = {0.f, 0.f, 0.f, 0.f};
       v = p.relu ? __builtin_elementwise_max(v, z) : v;
       if constexpr (MASK) {  // ReLU-backward mask: keep v where mask > 0 (the tiled epilogue's rule)
@@ -957,9 +821,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
   const int l32 = lane & 31, h = lane >> 5;
   const int wr = wave >> 1, wc = wave & 1;
   const int col0 = wc * 128;
-  float bias[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bias[j] = p.bias ? p.bias[n0 + col0 + 32 * j + l32] : 0.f;
+  const float* bias = p.bias ? p.bias + n0 + col0 : nullptr;   // this wave's 128 columns
   const float* Cw = p.C + n0 + col0;
   const int64_t cbytes = (p.M * p.scm - (n0 + col0)) * 4;
   const __amdgpu_buffer_rsrc_t cst = rsrc(Cw, cbytes);
@@ -1114,7 +976,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, bf, np, s);
   else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);
   else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, bf, np, s);
-  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, np, s, pl.kw);
+  else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1 && !p.cnt) {
     int64_t total = nbatch_out * a->M * a->N;

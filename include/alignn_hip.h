@@ -89,9 +89,6 @@ typedef struct AlignnGemmArgs {
 /* bf16 only: never the streaming kernel (the large-M products K in {64, 128, 256}, N % 256 == 0,
  * M >= 4096 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
 #define ALIGNN_GEMM_NOSTREAM 512
-/* 64x64 tiles shared by two groups of four waves, each multiplying half of every 32-deep stage
- * (twice the waves per tile for small grids; the groups' partial sums added in group order). */
-#define ALIGNN_GEMM_KW2 1024
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 

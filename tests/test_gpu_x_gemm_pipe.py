@@ -50,3 +50,4 @@ def test_pipelined_gemm_bitwise_vs_one_stage(M, N, K, batch, layout, bf):
     if not bf:
         ref = torch.relu(A.double() @ B.double() + C0.double() + bias.double()[:, None, :])
         assert _rel(outs[0], ref) < 5e-6
+
