@@ -5,9 +5,10 @@ B synthetic MP-like graphs (60 atoms / 720 bonds / 7,920 triplets each, SURVEY Â
 L=4, dropout 0.15, feature jitter 0.1: forward, hetero NLL, backward, clip_grad_norm_(5), AdamW.
 Inputs are collated and resident in HBM before the timed region (CSR built once per batch).
 
-Multi-GPU: one process per GPU (torch.distributed.run); each rank trains on its own batch of B
-graphs (weak scaling) and the gradients are averaged with ONE all_reduce over the flat gradient
-buffer (13.2 MB fp32) per step â€” the data-parallel exchange of SURVEY Â§8e.
+Multi-GPU: one process per GPU (torch.distributed.run, started by bench.py itself for --gpus N);
+each rank trains on its own batch of B graphs (weak scaling) and the gradients are averaged over the
+flat gradient buffer (13.2 MB fp32) per step in two buckets, the first (the conv blocks, 10.4 MB)
+all_reduced while the backward's tail runs â€” the data-parallel exchange of SURVEY Â§8e.
 
 Prints one JSON line (rank 0).  Also reports the dominant kernel's roofline (HIP events around
 its launches inside the timed region) and the oracle's CPU throughput on a bounded sample.
@@ -299,7 +300,8 @@ def end_to_end_variable(args, dev, rank, world, B):
     every batch.  value = real graphs per second."""
     import alignn_mi355x as A
     import numpy as np
-    from alignn_mi355x.dp import grad_allreduce_hook
+    from alignn_mi355x.dp import GradBuckets
+    from alignn_mi355x.layout import bucket_split
     store, t_build = build_variable_store(args, dev, rank)
     cap = store.capacity(B, args.lg_offset)
     torch.manual_seed(1234)
@@ -307,7 +309,7 @@ def end_to_end_variable(args, dev, rank, world, B):
                                                       args.dropout), 2).to(dev)
     trainer = A.FusedTrainer(model, precision=args.precision)
     if world > 1:
-        trainer.grad_hook = grad_allreduce_hook(world)
+        trainer.grad_buckets = GradBuckets(trainer.st.grad, bucket_split(model.config, True), world)
     rng = np.random.default_rng(99)
     first = next(i for i in (rng.choice(store.num_graphs, size=B, replace=False) for _ in range(1000))
                  if store.fits(i, cap, args.lg_offset) is not None)
@@ -357,7 +359,8 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
     (barrier + synchronize on both sides, max over ranks).  Returns the numbers and the trainer."""
     import alignn_mi355x as A
     from alignn_mi355x import profiling
-    from alignn_mi355x.dp import grad_allreduce_hook, max_over_ranks, rank_graphs
+    from alignn_mi355x.dp import GradBuckets, max_over_ranks, rank_graphs
+    from alignn_mi355x.layout import bucket_split
     from alignn_mi355x.synthetic import mp_like_batch
 
     torch.manual_seed(1234)  # identical initial weights on every rank
@@ -367,7 +370,8 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
     mfma_peak = BF16_MFMA_TFLOPS if precision == "bf16" else FP32_MFMA_TFLOPS
     batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=lg_offset).to(dev)
     if world > 1:
-        trainer.grad_hook = grad_allreduce_hook(world)  # the DP exchange: one all_reduce of the flat gradient
+        # the DP exchange: the flat gradient's mean in two buckets, the first beside the backward's tail
+        trainer.grad_buckets = GradBuckets(trainer.st.grad, bucket_split(model.config, True), world)
 
     def step(i):
         trainer.step(batch, seed=1000003 * rank + i)
@@ -696,6 +700,9 @@ def main():
                                    f"full ALIGNN D={args.hidden} H={args.heads} L={args.layers}, fwd+NLL+bwd+clip+AdamW",
                        "global_batch": B * world, "parallelism": f"dp{world}", "lg_offset": args.lg_offset,
                        "dropout": args.dropout, "launch": r["launch"], "precision": args.precision,
+                       **({"dp_exchange": "flat gradient mean in two buckets (conv blocks' parameters reduced "
+                                          "beside the backward's tail, then the rest), RCCL all_reduce"}
+                          if world > 1 else {}),
                        **({"dist_backend": args.dist_backend + (" (all ranks on cuda:0: rehearsal)" if args.share_device
                                                                  else "")} if world > 1 else {}),
                        **({"settings": args.set} if args.set else {})},

@@ -1,7 +1,8 @@
 """Data parallelism for the training step: one process per GPU, each rank trains on
-its own batch of graphs (weak scaling), and the ranks exchange ONE all_reduce of the flat gradient
-buffer per step (RCCL over xGMI on MI355X; the 13.2 MB fp32 buffer is a single bucket) before the
-reference's clip_grad_norm_(5.0) + AdamW, which then run identically on every rank.
+its own batch of graphs (weak scaling), and the ranks exchange the flat gradient buffer per step
+(RCCL over xGMI on MI355X, 13.2 MB fp32: one all_reduce, or two buckets with the first overlapped with
+the backward's tail, GradBuckets) before the reference's clip_grad_norm_(5.0) + AdamW, which then run
+identically on every rank.
 
 The reference trains on one device (scripts/train.py:607-723); with the PyG lg_edge_index offset
 rule a rank's batch is collated on its own, so DP parity means: every rank's
@@ -30,6 +31,44 @@ def grad_allreduce_hook(world: Optional[int] = None, group=None) -> Callable[[to
         grad.mul_(inv)
 
     return hook
+
+
+class GradBuckets:
+    """The data-parallel gradient mean in two buckets, the first overlapped with the backward's tail.
+
+    The flat layout (layout.flat_entries) puts the conv blocks' own parameters first: their
+    gradients are final once the per-layer backward is done (engine.backward_layers; written on the
+    main stream and the engine's side stream).  :meth:`start` — called between the per-layer backward
+    and the tail — all_reduces that bucket (10.4 MB of the 13.2 MB at the reference's size) on the
+    communication stream after both, while the tail (edge-projection chain rules, deferred angle-encoder
+    backward, encoder MLPs) runs; :meth:`finish` — after the tail, every stream joined — reduces the
+    rest, waits for both and scales by 1/world.  Sum then scale, as grad_allreduce_hook."""
+
+    def __init__(self, grad: torch.Tensor, split: int, world: Optional[int] = None, group=None):
+        if not 0 < split < grad.numel():
+            raise ValueError(f"bucket split {split} outside the gradient (1..{grad.numel() - 1})")
+        self.grad, self.group = grad, group
+        self.first, self.rest = grad[:split], grad[split:]
+        self.inv = 1.0 / (dist.get_world_size(group) if world is None else world)
+        self.work = None
+
+    def start(self, side: Optional[torch.cuda.Stream] = None) -> None:
+        if self.grad.is_cuda:
+            main = torch.cuda.current_stream(self.grad.device)
+            s = side if side is not None else main
+            if s is not main:
+                s.wait_stream(main)
+            with torch.cuda.stream(s):
+                self.work = dist.all_reduce(self.first, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            self.work = dist.all_reduce(self.first, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def finish(self) -> None:
+        dist.all_reduce(self.rest, op=dist.ReduceOp.SUM, group=self.group)
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        self.grad.mul_(self.inv)
 
 
 def rank_graphs(per_rank: int, rank: int) -> range:

@@ -668,11 +668,27 @@ class AlignnEngine:
         with ops.using(self.ctx), ops.gemm_precision(self.precision):
             return self._forward(P, batch, bc, training, seed, x, global_x, mode)
 
-    def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
-        """Writes d(loss)/d(param) for every parameter into G (see _backward)."""
+    def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor, between=None) -> None:
+        """Writes d(loss)/d(param) for every parameter into G: the per-layer backward, then
+        ``between()`` (if given), then the tail.  When ``between`` runs, the gradients of the conv
+        blocks' own parameters (flat [0, layout.bucket_split)) are final on the main and side streams
+        — the first data-parallel bucket (dp.GradBuckets) can be reduced while the tail runs."""
+        t = self.backward_layers(P, G, ctx, dout)
+        if between is not None:
+            between()
+        self.backward_tail(t)
+
+    def backward_layers(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor):
+        """Heads, readout and the L x (node block, edge block) backward; returns the tail's state."""
         with ops.using(self.ctx), ops.gemm_precision(self.precision):
             self.ctx.new_pass()
-            self._backward(P, G, ctx, dout)
+            return self._backward_layers(P, G, ctx, dout)
+
+    def backward_tail(self, t) -> None:
+        """The edge-projection chain rules, the deferred angle-encoder backward and the encoder MLPs'
+        backward, then the join of every stream into the current one."""
+        with ops.using(self.ctx), ops.gemm_precision(self.precision):
+            self._backward_tail(t)
 
     def _forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
                  x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
@@ -780,9 +796,9 @@ class AlignnEngine:
         ops.gemm(ctx.shared, P.Wout.t(), out, bias=P.bout)
         return out, ctx
 
-    def _backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor) -> None:
+    def _backward_layers(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor):
         """Writes d(loss)/d(param) for every parameter into G (overwrites; head grads are zero in
-        'embed' mode).  ``dout`` is the gradient of the forward's output."""
+        'embed' mode) together with _backward_tail.  ``dout`` is the gradient of the forward's output."""
         cfg = self.cfg
         D, L = cfg.hidden, cfg.layers
         Tt = cfg.target_dim
@@ -860,6 +876,27 @@ class AlignnEngine:
                                    overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
                                    overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
                 da_written = True
+        t = _Ctx()
+        t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj
+        t.da_written, t.enc_grads = da_written, enc_grads
+        if E > 0 and L > 0:
+            t.dM_all, t.dwbar_all = dM_all, dwbar_all
+        if line_proj:
+            t.dMl_all, t.dwl_all = dMl_all, dwl_all
+        return t
+
+    def _backward_tail(self, t) -> None:
+        cfg = self.cfg
+        L = cfg.layers
+        P, G, ctx, bc, dh, de, da, defer, side, line_proj = (t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side,
+                                                             t.line_proj)
+        da_written = t.da_written
+        N, E, T = bc.N, bc.E, bc.T
+        dev = dh.device
+        if E > 0 and L > 0:
+            dM_all, dwbar_all = t.dM_all, t.dwbar_all
+        if line_proj:
+            dMl_all, dwl_all = t.dMl_all, t.dwl_all
         if self.debug is not None:
             self.debug["de0"] = de.clone()
         # projection chain rules and the angle encoder's first layer: side stream (after the

@@ -47,6 +47,7 @@ def _linear(prefix: str, fin: int, fout: int, bias: bool = True) -> List[Tuple[s
 
 
 def conv_entries(prefix: str, D: int, H: int, edge_dim: int) -> List[Tuple[str, Tuple[int, ...]]]:
+    """A TransformerConv's parameters except lin_edge (kept with the tail group, flat_entries)."""
     HC = D  # heads * out_channels with out_channels = D // H
     c = prefix + "conv."
     return [
@@ -58,29 +59,38 @@ def conv_entries(prefix: str, D: int, H: int, edge_dim: int) -> List[Tuple[str, 
         (c + "lin_key.bias", (HC,)),
         (c + "lin_value.bias", (HC,)),
         (c + "lin_skip.bias", (HC,)),
-        (c + "lin_edge.weight", (HC, edge_dim)),
         (c + "lin_beta.weight", (1, 3 * HC)),
     ]
 
 
 def flat_entries(cfg: AlignnConfig, hetero: bool = True) -> List[Tuple[str, Tuple[int, ...]]]:
     """``hetero``: HeteroAlignnRegressor (mean/logvar heads; output_heads excluded) or the base
-    AlignnRegressor (output_heads, train.py:373/:400)."""
+    AlignnRegressor (output_heads, train.py:373/:400).
+
+    Order = the order in which the backward completes the gradients (two data-parallel buckets,
+    dp.GradBuckets): first every conv block's own projections, gate and LayerNorm (written by the
+    per-layer backward, engine._backward_layers), then what the backward's tail writes — the encoders,
+    the edge projections folded into the convs (lin_edge, edge_proj: their chain rules run after the
+    layers), the readout and the heads (logvar heads last: the second optimizer group)."""
     D = cfg.hidden
     e: List[Tuple[str, Tuple[int, ...]]] = []
-    e += _linear("base.node_encoder.0.", cfg.node_dim, D) + _linear("base.node_encoder.2.", D, D)
-    e += _linear("base.edge_encoder.0.", cfg.edge_dim, D) + _linear("base.edge_encoder.2.", D, D)
-    if cfg.angle_dim > 0:
-        e += _linear("base.angle_encoder.0.", cfg.angle_dim, D) + _linear("base.angle_encoder.2.", D, D)
     for l in range(cfg.layers):
         p = f"base.edge_blocks.{l}."
         e += conv_entries(p, D, cfg.heads, D)
         e += [(p + "norm.weight", (D,)), (p + "norm.bias", (D,))]
     for l in range(cfg.layers):
         p = f"base.node_blocks.{l}."
-        e += _linear(p + "edge_proj.", D, D)
         e += conv_entries(p, D, cfg.heads, D)
         e += [(p + "norm.weight", (D,)), (p + "norm.bias", (D,))]
+    e += _linear("base.node_encoder.0.", cfg.node_dim, D) + _linear("base.node_encoder.2.", D, D)
+    e += _linear("base.edge_encoder.0.", cfg.edge_dim, D) + _linear("base.edge_encoder.2.", D, D)
+    if cfg.angle_dim > 0:
+        e += _linear("base.angle_encoder.0.", cfg.angle_dim, D) + _linear("base.angle_encoder.2.", D, D)
+    # per-layer blocks at a constant stride (FlatViews._stack)
+    e += [(f"base.edge_blocks.{l}.conv.lin_edge.weight", (D, D)) for l in range(cfg.layers)]
+    e += [(f"base.node_blocks.{l}.conv.lin_edge.weight", (D, D)) for l in range(cfg.layers)]
+    e += [(f"base.node_blocks.{l}.edge_proj.weight", (D, D)) for l in range(cfg.layers)]
+    e += [(f"base.node_blocks.{l}.edge_proj.bias", (D,)) for l in range(cfg.layers)]
     e += _linear("base.feat_proj.0.", D + cfg.global_dim, D)
     if not hetero:
         e = [(k[len("base."):], s) for k, s in e]
@@ -98,6 +108,13 @@ def flat_entries(cfg: AlignnConfig, hetero: bool = True) -> List[Tuple[str, Tupl
     for t in range(cfg.target_dim):
         e += [(f"logvar_heads.{t}.bias", (1,))]
     return e
+
+
+def bucket_split(cfg: AlignnConfig, hetero: bool = True) -> int:
+    """Flat offset where the tail group starts: [0, split) holds the conv blocks' own parameters,
+    whose gradients are final once the per-layer backward is done (dp.GradBuckets)."""
+    offs, total, _ = offsets(cfg, hetero)
+    return offs[("base." if hetero else "") + "node_encoder.0.weight"][0]
 
 
 def offsets(cfg: AlignnConfig, hetero: bool = True) -> Tuple[Dict[str, Tuple[int, Tuple[int, ...]]], int, int]:

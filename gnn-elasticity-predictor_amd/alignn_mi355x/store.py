@@ -202,13 +202,11 @@ class GraphStore:
         has = t > 0
         lo, hi = (inc + sp[:, 0])[has], (inc + sp[:, 1])[has]
         order = np.argsort(lo, kind="stable")
-        active, end = 0, -1
-        for a, b in zip(lo[order], hi[order]):
-            if b <= end:
-                continue
-            active += b - max(a, end + 1) + 1
-            end = b
-        return {"nodes": int(n.sum()), "edges": int(e.sum()), "triplets": int(t.sum()), "active": int(active)}
+        lo, hi = lo[order], hi[order]
+        # union length of the spans: each adds what lies beyond the furthest end before it
+        prev = np.concatenate([[-1], np.maximum.accumulate(hi)[:-1]]) if len(hi) else hi
+        active = int(np.maximum(0, hi - np.maximum(lo, prev + 1) + 1).sum()) if len(hi) else 0
+        return {"nodes": int(n.sum()), "edges": int(e.sum()), "triplets": int(t.sum()), "active": active}
 
     def fits(self, indices, capacity: BatchCapacity, lg_offset: str = "num_nodes") -> Optional[Dict[str, int]]:
         """The ghost plan padding this batch to ``capacity``, or None when it does not fit (then the

@@ -74,6 +74,9 @@ class FusedTrainer:
         # this trainer's step runs in it, and a recorded plan owns it (its buffers never move)
         self.ctx = model._engine.ctx
         self.grad_hook = None  # called with the flat gradient between backward and clip (DP all_reduce)
+        # data-parallel gradient mean in two buckets (dp.GradBuckets): the first reduced while the
+        # backward's tail runs; takes the place of grad_hook when set
+        self.grad_buckets = None
         # re-binding (step() on a batch other than the captured one): copy it into the captured
         # batch's buffers and replay when its signature matches (BatchCache.signature), else eager
         self.rebind = True
@@ -102,10 +105,25 @@ class FusedTrainer:
     def forward_backward(self, batch, seed: int, training: bool = True,
                          sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward + loss + backward into the flat gradient buffer; returns the loss (device).
-        sample_weights: per-graph KNN weights [B] (train.py:660-674), or None."""
+        sample_weights: per-graph KNN weights [B] (train.py:660-674), or None.  With grad_buckets the
+        first bucket's reduction is started between the per-layer backward and the tail (it is
+        finished by step())."""
+        t = self._fb_layers(batch, seed, training, sample_weights)
+        if self.grad_buckets is not None:
+            self.grad_buckets.start(self.ctx.side(self.st.flat.device))
+        self._fb_tail(t)
+        return self.loss
+
+    def _fb_layers(self, batch, seed: int, training: bool = True, sample_weights: Optional[torch.Tensor] = None):
+        """Forward, loss and the per-layer backward (the first phase of a captured step)."""
         adopt(batch)
         with ops.using(self.ctx):
             return self._forward_backward(batch, seed, training, sample_weights)
+
+    def _fb_tail(self, t) -> None:
+        """The backward's tail (the second phase)."""
+        with ops.using(self.ctx):
+            self.model._engine.backward_tail(t)
 
     def _forward_backward(self, batch, seed: int, training: bool, sample_weights: Optional[torch.Tensor]):
         model, st = self.model, self.st
@@ -126,8 +144,7 @@ class FusedTrainer:
                        self.loss, dout[:nr], weights=sample_weights)
         if nr < out.size(0):
             ops.zero_(dout[nr:])
-        model._engine.backward(st.P, st.G, ctx, dout)
-        return self.loss
+        return model._engine.backward_layers(st.P, st.G, ctx, dout)
 
     def step(self, batch, seed: Optional[int] = None, sample_weights: Optional[torch.Tensor] = None) -> torch.Tensor:
         if seed is None:
@@ -137,7 +154,9 @@ class FusedTrainer:
             if self._graph[2] is batch or (self.rebind and self._rebind(batch)):
                 return self._replay(seed)
         loss = self.forward_backward(batch, seed, sample_weights=sample_weights)
-        if self.grad_hook is not None:
+        if self.grad_buckets is not None:
+            self.grad_buckets.finish()
+        elif self.grad_hook is not None:
             self.grad_hook(self.st.grad)
         self._clip_and_update()
         self.step_count += 1
@@ -221,35 +240,44 @@ class FusedTrainer:
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):
-                self.forward_backward(batch, 0)
+                self._fb_tail(self._fb_layers(batch, 0))   # (no gradient exchange in the warm-up)
                 self._clip_and_update()
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         profiling.clear()  # roofline probes (bench.py): keep only the launches captured below
         keep = mode == "plan"
-        g_fb, g_up = torch.cuda.CUDAGraph(keep_graph=keep), torch.cuda.CUDAGraph(keep_graph=keep)
+        # phases: forward/backward | clip/AdamW; with grad_buckets the backward splits at the end of
+        # the per-layer part, where the first bucket's all_reduce is issued between the two phases
+        state = {}
+        if self.grad_buckets is None:
+            phases = [("forward/backward", lambda: self._fb_tail(self._fb_layers(batch, 0)))]
+        else:
+            phases = [("forward/backward layers", lambda: state.__setitem__("t", self._fb_layers(batch, 0))),
+                      ("backward tail", lambda: self._fb_tail(state["t"]))]
+        phases.append(("clip/AdamW", self._clip_and_update))
+        graphs = [torch.cuda.CUDAGraph(keep_graph=keep) for _ in phases]
         plans = []
         try:
             with ops.recording():
-                for g, fn, pool in ((g_fb, lambda: self.forward_backward(batch, 0), None),
-                                    (g_up, self._clip_and_update, "fb")):
-                    with torch.cuda.graph(g, pool=(g_fb.pool() if pool else None)):
+                for i, (g, (_, fn)) in enumerate(zip(graphs, phases)):
+                    with torch.cuda.graph(g, pool=(graphs[0].pool() if i else None)):
                         if keep:
                             plans.append(_record_plan(fn))
                         else:
                             fn()
+            state.clear()
             torch.cuda.synchronize(dev)
             self._restore(snap)
             if keep:
-                ranges = self._held_ranges(batch, g_fb.pool())
-                for g, pl, what in ((g_fb, plans[0], "forward/backward"), (g_up, plans[1], "clip/AdamW")):
+                ranges = self._held_ranges(batch, graphs[0].pool())
+                for g, pl, (what, _) in zip(graphs, plans, phases):
                     _check_census(g, pl, what)
                     _check_ownership(pl, ranges, what)
         except Exception:
             for pl in plans:
                 _lib.lib().alignn_plan_destroy(pl)
             raise
-        self._graph = (g_fb, g_up, batch, plans if keep else None)
+        self._graph = (graphs[0], graphs[-1], batch, plans if keep else None, graphs)
         self.ctx.freeze()   # the plans hold the workspaces' addresses: eager steps may not replace them
 
     def _held_ranges(self, batch, pool_id):
@@ -286,17 +314,24 @@ class FusedTrainer:
     def _replay(self, seed: int) -> torch.Tensor:
         check(_lib.lib().alignn_set_i64(self._seed_dev.data_ptr(), int(seed) & (2**63 - 1), ops.stream_ptr()),
               "alignn_set_i64")
-        g_fb, g_up, _, plans = self._graph
-        if plans:
-            check(_lib.lib().alignn_plan_replay(plans[0], ops.stream_ptr()), "alignn_plan_replay")
-        else:
-            g_fb.replay()
-        if self.grad_hook is not None:
+        plans = self._graph[3]
+        graphs = self._graph[4] if len(self._graph) > 4 else [self._graph[0], self._graph[1]]
+        n = len(plans) if plans else len(graphs)
+
+        def run(i):
+            if plans:
+                check(_lib.lib().alignn_plan_replay(plans[i], ops.stream_ptr()), "alignn_plan_replay")
+            else:
+                graphs[i].replay()
+
+        run(0)
+        if n == 3:   # bucketed: first bucket beside the backward's tail, the rest after it
+            self.grad_buckets.start(self.ctx.side(self.st.flat.device))
+            run(1)
+            self.grad_buckets.finish()
+        elif self.grad_hook is not None:
             self.grad_hook(self.st.grad)
-        if plans:
-            check(_lib.lib().alignn_plan_replay(plans[1], ops.stream_ptr()), "alignn_plan_replay")
-        else:
-            g_up.replay()
+        run(n - 1)
         self.step_count += 1
         return self.loss
 

@@ -197,3 +197,95 @@ def test_fused_trainer_grad_hook_between_plan_phases_world2(tmp_path):
     want = _step_flat(r[0]["before"], mean, r[0]["s0"])
     assert torch.equal(r[0]["after"], r[1]["after"])
     assert torch.allclose(r[0]["after"], want, atol=1e-7)
+
+
+# ------------------------------------------------------------------------------------------------
+# Bucketed gradient exchange (dp.GradBuckets) between three replayed plans, world size 2
+# ------------------------------------------------------------------------------------------------
+class _FakeLib3(_FakeLib):
+    """Plan 1 = forward + per-layer backward (writes the first bucket's gradient), plan 2 = the
+    backward's tail (writes the rest), plan 3 = clip + AdamW."""
+
+    def __init__(self, trainer, grad, log, split):
+        super().__init__(trainer, grad, log)
+        self.split = split
+
+    def alignn_plan_replay(self, plan, stream):
+        g = self.tr.st.grad
+        if plan == 1:
+            self.log.append("layers")
+            g[:self.split].copy_(self.grad[:self.split])
+            g[self.split:].fill_(float("nan"))     # not final yet: the tail writes it
+        elif plan == 2:
+            self.log.append("tail")
+            g[self.split:].copy_(self.grad[self.split:])
+        else:
+            return super().alignn_plan_replay(2, stream)
+        return 0
+
+
+def _bucket_worker(rank, world, port, out_dir):
+    import alignn_mi355x as A
+    from alignn_mi355x import _lib, ops, trainer as trainer_mod
+    from alignn_mi355x.layout import bucket_split
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(6, 8, 7, 289, 2, 32, 1, 1, 0.0), 2)
+        tr = A.FusedTrainer(model, optimizer="torch")
+        split = bucket_split(model.config, True)
+        n = tr.st.flat.numel()
+        grad = torch.randn(n, generator=torch.Generator().manual_seed(11 + rank)) * (1.0 + rank)
+        log = []
+        fake = _FakeLib3(tr, grad, log, split)
+        _lib.lib = lambda: fake
+        ops.stream_ptr = lambda *a, **k: 0
+        trainer_mod.check = lambda rc, what: None
+        buckets = dp.GradBuckets(tr.st.grad, split, world)
+        orig_start, orig_finish = buckets.start, buckets.finish
+        buckets.start = lambda side=None: (log.append("start"), orig_start(None))[1]
+        buckets.finish = lambda: (log.append("finish"), orig_finish())[1]
+        tr.grad_buckets = buckets
+        tr._seed_dev = torch.zeros(1, dtype=torch.int64)
+        tr.ctx.side = lambda dev: None
+        batch = object()
+        tr._graph = (None, None, batch, [1, 2, 3])
+        before = tr.st.flat.clone()
+        tr.step(batch, seed=3)
+        torch.save({"log": log, "before": before, "after": tr.st.flat.clone(), "grad": tr.st.grad.clone(),
+                    "s0": tr.st.P.sigma_start, "split": split, "n": n}, os.path.join(out_dir, f"b{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_bucketed_gradient_exchange_world2(tmp_path):
+    """Three replayed phases: per-layer backward, first bucket's all_reduce started, backward tail,
+    second bucket reduced and both scaled, clip + AdamW — the same parameters on both ranks as one
+    process stepping on the mean gradient; the flat layout puts the conv blocks first."""
+    world = 2
+    mp.spawn(_bucket_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"b{i}.pt", weights_only=True) for i in range(world)]
+    for x in r:
+        assert x["log"] == ["seed", "layers", "start", "tail", "finish", "update"], x["log"]
+        assert 0 < x["split"] < x["n"]
+    n = r[0]["n"]
+    mean = sum(torch.randn(n, generator=torch.Generator().manual_seed(11 + i)) * (1.0 + i) for i in range(world)) / world
+    assert torch.allclose(r[0]["grad"], mean, atol=1e-6) and torch.equal(r[0]["grad"], r[1]["grad"])
+    assert torch.equal(r[0]["after"], r[1]["after"])
+    assert torch.allclose(r[0]["after"], _step_flat(r[0]["before"], mean, r[0]["s0"]), atol=1e-7)
+
+
+def test_layout_conv_blocks_first():
+    """The first bucket is exactly the conv blocks' own parameters (no lin_edge / edge_proj, no
+    encoder, readout or head), the second everything else."""
+    from alignn_mi355x.layout import AlignnConfig, bucket_split, offsets
+    cfg = AlignnConfig(206, 36, 11, 289, 2, 256, 4, 4)
+    offs, total, s0 = offsets(cfg, True)
+    split = bucket_split(cfg, True)
+    first = {k for k, (o, _) in offs.items() if o < split}
+    assert first and all((".edge_blocks." in k or ".node_blocks." in k) for k in first)
+    assert not any("lin_edge" in k or "edge_proj" in k for k in first)
+    assert all(o >= split for k, (o, _) in offs.items() if k not in first)
+    assert s0 > split and total == 3307270 - 514

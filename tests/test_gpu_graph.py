@@ -295,3 +295,42 @@ def test_loader_prepared_batch_on_eager_paths(path):
         assert torch.equal(l1, l2), i
         assert torch.equal(t1.st.flat, t2.st.flat), i
     t2.release_capture()
+
+
+def test_bucketed_dp_plan_replay_bitwise():
+    """The data-parallel step with the bucketed gradient exchange (dp.GradBuckets: three captured
+    phases, the first bucket's all_reduce issued between the per-layer backward and the tail) equals
+    the plain eager step bit for bit (one rank: the reductions are identities)."""
+    import socket
+    import torch.distributed as dist
+    from alignn_mi355x import dp, ops
+    from alignn_mi355x.layout import bucket_split
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        _, te, b1 = _setup(B=8)
+        _, tp, b2 = _setup(B=8)
+        tp.grad_buckets = dp.GradBuckets(tp.st.grad, bucket_split(tp.model.config, True), 1)
+        tp.capture(b2)
+        assert len(tp._graph[3]) == 3
+        for i, s in enumerate((41, 42, 43)):
+            lp = tp.step(b2, seed=s).clone()
+            le = _twin_step(te, tp, b1, s)
+            torch.cuda.synchronize()
+            assert torch.equal(le, lp), i
+            assert torch.equal(te.st.grad, tp.st.grad), i
+            assert torch.equal(te.st.flat, tp.st.flat), i
+        tp.release_capture()
+        # the eager bucketed step too
+        tp.use_step_seed(None)
+        te.use_step_seed(None)
+        ops.set_step_seed(None)
+        lp = tp.step(b2, seed=50).clone()
+        le = te.step(b1, seed=50).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(le, lp) and torch.equal(te.st.flat, tp.st.flat)
+    finally:
+        dist.destroy_process_group()
+        ops.set_step_seed(None)
