@@ -70,6 +70,9 @@ def parse():
                         "(config C5's ~10k graphs; 0 = off): device collate of a random batch + CSR/compaction + "
                         "step, at the headline config and (one GPU) at config C5's B=256 bf16 (SURVEY §8d's "
                         "'including collate' number; separate fields, never value)")
+    p.add_argument("--e2e-sync", action="store_true",
+                   help="e2e: prepare each next batch on this thread between the steps instead of on the "
+                        "prefetch thread (for comparison)")
     p.add_argument("--launch", choices=["eager", "plan", "graph"], default="plan",
                    help="eager: Python issues every launch; plan: the step is recorded once as a native launch "
                         "plan and re-issued from C++ (plan.hip; the roofline probe is a pair of plan timestamps "
@@ -82,14 +85,15 @@ def parse():
                         "one gather of every member's heads on an eval batch to rank 0 for the moment mix")
     p.add_argument("--seed", type=int, default=42, help="base seed of the ensemble members (train.py --seed)")
     p.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
-                   help="engine option (engine.<attr>=0/1), trainer optimizer (optimizer=hip) or GEMM stage "
-                        "(gemm_stage=16|32|64); repeatable — for measuring opt-in paths")
+                   help="engine option of this run's model (engine.<attr>=0/1|N), trainer optimizer (optimizer=hip) "
+                        "or stream priorities (loader_priority / main_priority); repeatable — for measuring "
+                        "opt-in paths")
     return p.parse_args()
 
 
 def apply_settings(args, model):
-    """--set KEY=VAL: opt-in engine paths for A/B measurement; returns the trainer kwargs."""
-    from alignn_mi355x import ops
+    """--set KEY=VAL: per-model engine options (engine.<attr>, instance state of this model's engine —
+    nothing process-global is changed) and run options; returns the trainer kwargs."""
     kw = {}
     for item in args.set:
         k, v = item.split("=", 1)
@@ -99,34 +103,12 @@ def apply_settings(args, model):
                 raise ValueError(f"unknown engine option {attr}")
             cur = getattr(model._engine, attr)
             setattr(model._engine, attr, int(v) if (isinstance(cur, int) and not isinstance(cur, bool)) else bool(int(v)))
-        elif k == "gemm_stage":
-            ops.GEMM_STAGE = {"16": 0, "32": 16, "64": 128}[v]
-        elif k == "compact_regs":
-            ops.GraphCSR.COMPACT_REGS = bool(int(v))
         elif k == "optimizer":
             kw["optimizer"] = v
-        elif k == "wave_items":
-            ops.GraphCSR.WAVE_ITEMS = bool(int(v))
-        elif k == "bf16_stream":
-            ops.GEMM_EXTRA = 0 if int(v) else ops.GEMM_NOSTREAM
-        elif k == "bwd_src_by":
-            ops.BWD_SRC_BY = bool(int(v))
-        elif k == "xcd_items":
-            ops.GraphCSR.XCD_ITEMS = bool(int(v))
-        elif k == "sort_by_degree":
-            ops.GraphCSR.SORT_BY_DEGREE = bool(int(v))
-        elif k == "heavy_threshold":
-            ops.GraphCSR.HEAVY_THRESHOLD = int(v)
-        elif k == "atom_xcd_chunk":
-            from alignn_mi355x import engine as _engine
-            _engine.BatchCache.ATOM_XCD_CHUNK = int(v)
         elif k == "loader_priority":
             args.loader_priority = int(v)
         elif k == "main_priority":
             args.main_priority = int(v)
-        elif k == "splitk_combine":
-            ops.SPLITK_COMBINE = int(v) > 0
-            ops.SPLITK_COMBINE_MAX = int(v)
         else:
             raise ValueError(f"unknown --set key {k}")
     return kw
@@ -218,6 +200,7 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     import numpy as np
     from alignn_mi355x.dp import max_over_ranks
     from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.prefetch import BatchPrefetcher
 
     rng = np.random.default_rng(1234 + rank)
     # B >= 128: a high-priority loader stream, so the small collate/CSR kernels (and the host syncs of
@@ -227,14 +210,27 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     prio = getattr(args, "loader_priority", None)
     if prio is None:
         prio = -1 if B >= 128 else 0
-    loader = torch.cuda.Stream(device=dev, priority=prio)
+    draw = lambda: rng.choice(store.num_graphs, size=B, replace=False)  # noqa: E731
+    total = 1 + args.warmup + args.steps
+    if args.e2e_sync:   # the loader's host work between the steps, on this thread
+        loader = torch.cuda.Stream(device=dev, priority=prio)
 
-    def make():
-        with torch.cuda.stream(loader):
-            b = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset,
-                              capacity=capacity)
-        prepare_batch(b, loader)
-        return b
+        def make():
+            with torch.cuda.stream(loader):
+                b = store.collate(draw(), lg_offset=args.lg_offset, capacity=capacity)
+            prepare_batch(b, loader)
+            return b
+        pf = None
+    else:               # a host thread prepares the next batches while this one re-binds and replays
+        drawn = [0]
+
+        def nxt_idx():
+            if drawn[0] >= total:
+                return None
+            drawn[0] += 1
+            return draw()
+        pf = BatchPrefetcher(store, nxt_idx, depth=2, lg_offset=args.lg_offset, capacity=capacity, priority=prio)
+        make = pf.get
 
     r0, m0 = trainer.rebinds, trainer.rebind_misses
     nxt = make()
@@ -261,18 +257,24 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     dt = time.perf_counter() - t0
     if world > 1:
         dt = max_over_ranks(dt, dev)
-    return {"value": round(B * world * args.steps / dt, 2), "unit": "graphs/s",
-            "ms_per_step": round(dt / args.steps * 1e3, 3), "batch": B, "dataset_graphs": args.e2e,
-            "dataset_graphs_per_rank": store.num_graphs,
-            "store_build_s": round(t_build, 1), "replayed_steps": trainer.rebinds - r0,
-            "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
-                                 "collate_and_prepare": round(host_make / args.steps * 1e3, 3)},
-            "eager_steps": trainer.rebind_misses - m0,
-            "signature": ("every batch padded to one capacity (store.BatchCapacity)" if capacity is not None else
-                          "fixed: every synthetic graph has 60 atoms, so every batch has the captured signature "
-                          "(best case; see e2e_variable for variable-size graphs)"),
-            "includes": "device collate of a random batch + CSR/compaction/schedules (loader stream) + "
-                        "fwd/NLL/bwd/clip/AdamW (captured plan re-bound to the batch)"}
+    out = {"value": round(B * world * args.steps / dt, 2), "unit": "graphs/s",
+           "ms_per_step": round(dt / args.steps * 1e3, 3), "batch": B, "dataset_graphs": args.e2e,
+           "dataset_graphs_per_rank": store.num_graphs,
+           "store_build_s": round(t_build, 1), "replayed_steps": trainer.rebinds - r0,
+           "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
+                                ("collate_and_prepare" if args.e2e_sync else "wait_for_prefetched_batch"):
+                                    round(host_make / args.steps * 1e3, 3)},
+           "loader": ("synchronous (this thread)" if args.e2e_sync else
+                      "host thread, 2 batches ahead (prefetch.BatchPrefetcher)"),
+           "eager_steps": trainer.rebind_misses - m0,
+           "signature": ("every batch padded to one capacity (store.BatchCapacity)" if capacity is not None else
+                         "fixed: every synthetic graph has 60 atoms, so every batch has the captured signature "
+                         "(best case; see e2e_variable for variable-size graphs)"),
+           "includes": "device collate of a random batch + CSR/compaction/schedules (loader stream) + "
+                       "fwd/NLL/bwd/clip/AdamW (captured plan re-bound to the batch)"}
+    if pf is not None:
+        pf.close()
+    return out
 
 
 def build_variable_store(args, dev, rank):

@@ -38,7 +38,7 @@ class GemmArgs(ctypes.Structure):
         ("relu", c_i32), ("split_k", c_i32),
         ("workspace", c_vp), ("workspace_elems", c_i64),
         ("reduce_batch", c_i32), ("tile", c_i32),
-        ("c_rows", c_vp), ("counters", c_vp),
+        ("c_rows", c_vp),
     ]
 
 
@@ -47,14 +47,7 @@ class Schedule(ctypes.Structure):
                 ("flags", c_i32), ("reserved", c_i32)]
 
 
-SCHED_COMPACT_REGS = 1
 SCHED_WAVE_ITEMS = 2
-
-
-class EdgeEncoder(ctypes.Structure):
-    _fields_ = [("x", c_vp), ("ldx", c_i64), ("kin", c_i32), ("accumulate", c_i32),
-                ("w1", c_vp), ("b1", c_vp), ("dw1", c_vp), ("db1", c_vp),
-                ("workspace", c_vp), ("workspace_elems", c_i64)]
 
 
 ENCBWD_MAX_LAYERS = 8
@@ -76,7 +69,6 @@ _SIGNATURES = {
     "alignn_gemm_f32": ([ctypes.POINTER(GemmArgs), c_vp], c_i32),
     "alignn_gemm_workspace": ([ctypes.POINTER(GemmArgs)], c_i64),
     "alignn_copy_many": ([c_i32, c_vp, c_vp, c_vp, c_vp], c_i32),
-    "alignn_gemm_counters": ([ctypes.POINTER(GemmArgs)], c_i64),
     "alignn_gemm_path": ([ctypes.POINTER(GemmArgs)], c_i32),
     "alignn_colsum_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
     "alignn_wcolsum2_f32": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
@@ -85,9 +77,8 @@ _SIGNATURES = {
     "alignn_gather_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "alignn_scatter_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp], c_i32),
     "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
-                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
-    "alignn_tconv_bwd_workspace": ([c_i32, c_i32, c_i32], c_i64),
-    "alignn_tconv_family": ([c_i32, c_i32, c_vp, c_vp, c_vp, c_vp], c_i32),
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_tconv_family": ([c_i32, c_i32, c_vp, c_vp, c_vp], c_i32),
     "alignn_lg_fwd_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_lg_bwd_dst_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
@@ -97,7 +88,7 @@ _SIGNATURES = {
     "alignn_linear_smallk_bf16out": ([c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp],
                                      c_i32),
     "alignn_tconv_bwd_dst": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
-                              c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                              c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                               c_i32, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_bwd_src": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                               c_i64, c_vp], c_i32),

@@ -369,10 +369,8 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
 
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
-                  seed_blk: int, enc: Optional[ops.EdgeEncoder] = None, side: Optional[torch.cuda.Stream] = None,
-                  compact_gate: bool = False):
+                  seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
-    enc: edge features recomputed in-kernel from raw inputs (then F is None).
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
     (no zero-filled [n, D] copy; the backward writes the compacted dout directly).
 
@@ -384,7 +382,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     C = D // H
     dev = X.device
     c = _Ctx()
-    c.X, c.F, c.feat_row, c.enc = X, F, feat_row, enc
+    c.X, c.F, c.feat_row = X, F, feat_row
     c.M, c.wbar = M, wbar
     c.rows = rows = g.rows
     with_proj = wbar is not None
@@ -416,7 +414,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
                         seed_att)
     else:
         ops.tconv_fwd(g, D, H, c.QKV, c.U, c.wbar, F, feat_row, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
-                      seed_att, enc=enc)
+                      seed_att)
     if with_proj:
         ops.gemm(c.S.transpose(0, 1), c.M.view(H, C, D).transpose(1, 2), c.outp_a.view(na, H, C).transpose(0, 1),
                  beta=1.0, rowscale=c.sumA.t(), bias2=c.wbar.view(H, C))
@@ -445,24 +443,17 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
 
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
-                   dwbar: Optional[torch.Tensor] = None, enc_grads=None,
-                   side: Optional[torch.cuda.Stream] = None, keep_edge_scalars: bool = False,
-                   overlap_src: bool = False, wbar_colsum: bool = True, overlap_skip: bool = False,
-                   gate_reduce_side: bool = False) -> None:
+                   dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
+                   keep_edge_scalars: bool = False, gate_reduce_side: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
     (c.wbar set) the gradients of M and w̄ are written to dM / dwbar for :func:`proj_grads`.
-    With an in-kernel edge encoder (c.enc), enc_grads = (dW1, db1) receive its gradients (+=).
     side: a second stream for the weight-gradient products (dM, dw̄, dW, db), which nothing
     downstream in the backward reads; they overlap the next block's latency-bound attention.  The
     caller joins the side stream before reading those gradients.
     keep_edge_scalars: leave (Vd, dz_e, alpha_e) on ``c.edge_scalars`` for the deferred angle-encoder
     backward (ops.enc_bwd; then dF is None).
-    overlap_src: with a side stream, run the source-side attention backward on a third stream beside
-    the dQ products.
-    overlap_skip: on a compacted graph with a side stream, the skip projection's dX product (all n rows)
-    runs on a third stream beside the attention backward; dX accumulates in the same order.
     gate_reduce_side: the gate/LayerNorm parameter-gradient reduction on the side stream."""
     n, D = c.X.shape
     H = c.H
@@ -481,20 +472,12 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
                     gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None)
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
-    skip = ops.aux_stream(dev) if (side is not None and overlap_skip and rows is not None) else None
-    if skip is not None:
-        with _side_work(skip, (dR, dX)):
-            ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                # residual + skip projection
     Vd = torch.empty(na, H, D, device=dev)
     ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
     Sz = torch.empty(na, H, D, device=dev)
     sigz = torch.empty(na, H, device=dev)
     dz_e = torch.empty(max(m, 1), H, device=dev)
     al_e = torch.empty(max(m, 1), H, device=dev)
-    enc = None
-    if c.enc is not None:
-        enc = ops.EdgeEncoder(c.enc.x, c.enc.w1, c.enc.b1, enc_grads[0], enc_grads[1], accumulate=True)
-        dF = None
     if c.KV16 is not None:
         if dF is not None:
             raise ValueError("bf16 edge-feature storage needs the deferred angle-encoder backward (no dF)")
@@ -502,12 +485,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                             dQKV[:, :D], Sz, sigz, dz_e, al_e, c.p, c.seed_att)
     else:
         ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
-                          dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att, enc=enc)
-    # dK/dV (source side) and the dQ products below are independent: with an aux stream the
-    # source-side kernel runs beside them and the dX products wait for both
-    aux = ops.aux_stream(dev) if (side is not None and overlap_src) else None
-    with _side_work(aux, (c.QKV, dout_a, dz_e, al_e, dQKVR if rows is None else dQKV)):
-        ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
+                          dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att)
+    ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
     if keep_edge_scalars:
         c.edge_scalars = (Vd, dz_e, al_e)
     Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
@@ -519,26 +498,18 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0, rowscale=sigz.t(), bias2=c.wbar.view(H, C))
     else:
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0)
-    if aux is not None:
-        ops.stream_wait(torch.cuda.current_stream(dev), aux)
     if rows is None:
         ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
     else:
-        if skip is None:
-            ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                # residual + skip projection
-        else:
-            ops.stream_wait(torch.cuda.current_stream(dev), skip)
+        ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                    # residual + skip projection
         ops.gemm(dQKV, cv.Wqkvr[:3 * D], dX, beta=1.0, c_rows=rows)     # + Q/K/V projections (active rows)
     # weight gradients: off the critical path
     with _side_work(side, (c.QKV, dout_a, Sz, sigz, c.S, c.sumA, dQKV, dR, c.X, c.Xa)):
         if c.with_proj:
             ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
             ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
-            if wbar_colsum:   # dw̄_h = Σ Q_h σz_h + dout_h ΣA_h in one weighted column-sum kernel
-                ops.wcolsum2(c.QKV[:, :D], sigz, dout_a, c.sumA, dwbar)
-            else:
-                ops.gemm(Qh, sigz.t().unsqueeze(-1), dwbar.view(H, C, 1))
-                ops.gemm(Oh, c.sumA.t().unsqueeze(-1), dwbar.view(H, C, 1), beta=1.0)
+            # dw̄_h = Σ Q_h σz_h + dout_h ΣA_h in one weighted column-sum kernel
+            ops.wcolsum2(c.QKV[:, :D], sigz, dout_a, c.sumA, dwbar)
         else:
             ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
             ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
@@ -590,9 +561,6 @@ class AlignnEngine:
         # workspaces, side/aux streams and device step seed of this engine's launches (ops.ExecContext)
         self.ctx = ops.ExecContext("engine")
         self.debug = None  # dict -> backward stores intermediate gradients (diagnostics only)
-        # recompute the angle hidden layer inside the line convs (kin <= 16) instead of materialising
-        # it: measured slower than streaming the materialised rows so far (occupancy-bound), so off
-        self.recompute_angle = False
         # weight-gradient products on a second stream, overlapping the next block's attention
         self.overlap = True
         # forward: the line blocks' skip projection on the second stream beside the attention
@@ -615,34 +583,21 @@ class AlignnEngine:
         # line convs leave per-edge scalars instead of read-modify-writing a [T, D] gradient per layer
         # (+4.0 % graphs/s on MI355X once enc_bwd was column-parallel, profiles/r01/v13_sweep.log)
         self.defer_angle_bwd = True
-        # backward: source-side attention kernel on a third stream beside the dQ products (measured
-        # -1.1 %: the cross-queue sync costs more than the overlap saves, v23_sweep_overlap_src.log)
-        self.overlap_src = False
-        # line blocks: the skip projection's dX product beside the attention backward (third stream)
-        self.overlap_skip = False
         # gate/LayerNorm parameter-gradient reduction on the side stream (off the critical path)
         self.gate_reduce_side = True  # +0.3 % (v34_sweep_gate_reduce_side.log)
-        # projection chain rules on the main stream after the encoder MLP backward (see _backward)
-        self.proj_main = False  # measured -0.3 % (with enc_bwd_aux -1.6 %; v35_sweep_proj_main_rejected.log)
         # deferred angle-encoder backward on a third stream (see _backward): 1 always, 0 never, or
         # from this many line-graph edges on.  B = 32 (253,440 triplets): -0.6 %
         # (v31_sweep_enc_bwd_aux_rejected.log); B = 256 bf16 (2.03 M triplets, enc_bwd 1.06 ms, the
         # step's last branch): +1.8 % (17,697-17,740 -> 18,027-18,051 graphs/s,
         # profiles/r02/v30_ab_enc_bwd_aux_c3.log)
         self.enc_bwd_aux = 1_000_000
-        # the w-bar gradient as one weighted column-sum kernel instead of two N=1 GEMMs + reduces
-        self.wbar_colsum = True
-        # the encoder MLPs' masked dX products (end of backward, beside the deferred angle-encoder
-        # backward on the side stream) on the tiled kernels: the bf16 streaming GEMM needs a whole
-        # CU's LDS, so it waited for enc_bwd to drain (C3: 1,212 us for a 150 us product)
-        self.mlp_bwd_stream = False
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
         deferred encoder backward, and a line graph in the bf16 kernels' domain (D = 256, H <= 4,
         single-wave work items without heavy nodes)."""
         if not (self.precision == "bf16" and self.bf16_storage and self.defer_angle_bwd and D == 256
-                and self.cfg.heads in (1, 2, 4) and bc.lg is not None and ops.GraphCSR.WAVE_ITEMS
+                and self.cfg.heads in (1, 2, 4) and bc.lg is not None and bc.lg.policy.wave_items
                 and ops.enc_bwd_ok(D, self.cfg.heads, self.cfg.layers, bc.xa.size(1))):
             return False
         return bc.lg.schedule().n_heavy == 0
@@ -659,7 +614,10 @@ class AlignnEngine:
         ops.gemm(dout.t(), h1, gW2)
         ops.colsum(dout, gb2)
         dh1 = torch.empty_like(h1)
-        ops.gemm(dout, W2, dh1, mask=h1, tile=ops.GEMM_NOSTREAM if beside_side and not self.mlp_bwd_stream else 0)
+        # beside the deferred angle-encoder backward (side stream) the masked dX product takes the
+        # tiled kernels: the bf16 streaming GEMM needs a whole CU's LDS, so it waited for enc_bwd to
+        # drain (C3: 1,212 us for a 150 us product)
+        ops.gemm(dout, W2, dh1, mask=h1, tile=ops.GEMM_NOSTREAM if beside_side else 0)
         ops.gemm(dh1.t(), x, gW1)
         ops.colsum(dh1, gb1)
 
@@ -717,13 +675,8 @@ class AlignnEngine:
         # w̄_l = W_edge,l b2 — exact algebra, so the [T, D] x [D, D] GEMM and its two
         # backward GEMMs never run.
         ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
-        # With few raw angle inputs (kin <= 16) even the hidden layer is not materialised: the line
-        # convs recompute relu(W1 x_t + b1) per edge in-kernel (ops.EdgeEncoder).
-        ctx.angle_enc = None
         a = None
-        if ctx.has_angle and self.recompute_angle and bc.xa.size(1) <= ops.ENC_MAX_KIN and T > 0:
-            ctx.angle_enc = ops.EdgeEncoder(bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"))
-        elif ctx.has_angle:
+        if ctx.has_angle:
             W1, b1 = P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias")
             if self._bf16_angle(bc, D):
                 # config C3 (autocast): the hidden layer is a bf16 Linear output, stored as bf16 and read
@@ -756,8 +709,7 @@ class AlignnEngine:
             if T > 0 and E > 0:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
-                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), enc=ctx.angle_enc,
-                                     side=side, compact_gate=self.compact_gate)
+                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate)
             else:
                 c = None
             ctx.edge.append(c)
@@ -838,10 +790,9 @@ class AlignnEngine:
         dh = torch.empty(N, D, device=dev)
         ops.readout_pool_bwd(dfeats, bc.ptr, bc.batch_vec, dh, False, p_drop, site_seed(seed, 4 * L))
         de = ops.zeros(E, D, device=dev)
-        defer = (self.defer_angle_bwd and ctx.has_angle and ctx.angle_enc is None and T > 0 and E > 0 and L > 0
+        defer = (self.defer_angle_bwd and ctx.has_angle and T > 0 and E > 0 and L > 0
                  and ops.enc_bwd_ok(D, cfg.heads, L, bc.xa.size(1)))
-        da = torch.empty(T, D, device=dev) if (T > 0 and ctx.angle_enc is None and not defer) else None
-        enc_grads = (G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias")) if ctx.angle_enc is not None else None
+        da = torch.empty(T, D, device=dev) if (T > 0 and not defer) else None
         da_written = False
         if E > 0 and L > 0:
             dM_all = torch.empty(L, D, D, device=dev)
@@ -857,8 +808,7 @@ class AlignnEngine:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
-                               overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
+                               gate_reduce_side=self.gate_reduce_side)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -867,18 +817,15 @@ class AlignnEngine:
                 # the last (l = 0) applies the ReLU mask in place
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
                 if line_proj:
-                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l],
-                                   enc_grads=enc_grads, side=side, keep_edge_scalars=defer,
-                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
-                                   overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
+                    block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
+                                   keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
-                                   overlap_src=self.overlap_src, wbar_colsum=self.wbar_colsum,
-                                   overlap_skip=self.overlap_skip, gate_reduce_side=self.gate_reduce_side)
+                                   gate_reduce_side=self.gate_reduce_side)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj
-        t.da_written, t.enc_grads = da_written, enc_grads
+        t.da_written = da_written
         if E > 0 and L > 0:
             t.dM_all, t.dwbar_all = dM_all, dwbar_all
         if line_proj:
@@ -912,25 +859,19 @@ class AlignnEngine:
                             [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                             [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
                             G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
-        proj_main = self.proj_main and side is not None
-
-        def projections():
+        with _side_work(side, (da, *kept)):
             if E > 0 and L > 0:
                 proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
             if line_proj:
                 proj_grads_shared(P.edge_We, P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias"), dMl_all,
                                   dwl_all, G.edge_We, G.enc("angle", 2, "weight"), G.enc("angle", 2, "bias"))
-
-        with _side_work(side, (da, *kept)):
-            if not proj_main:
-                projections()
             if defer:
                 if aux is None:
                     ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
                                 [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                                 [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
                                 G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"))
-            elif ctx.has_angle and da_written and ctx.angle_enc is None:
+            elif ctx.has_angle and da_written:
                 # da is the masked hidden-layer gradient
                 if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLN_MAX:
                     ops.gemm_tn_smalln(da, bc.xa, G.enc("angle", 0, "weight"), colsum=G.enc("angle", 0, "bias"))
@@ -944,10 +885,6 @@ class AlignnEngine:
         self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
                       G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"),
                       beside_side=side is not None)
-        if proj_main:
-            # after the encoder MLPs: wait for the side stream's per-layer dM / dw̄, then the chain rules
-            ops.stream_wait(torch.cuda.current_stream(dev), side)
-            projections()
         if side is not None:
             ops.stream_wait(torch.cuda.current_stream(dev), side)  # join: every gradient is written
         if aux is not None:

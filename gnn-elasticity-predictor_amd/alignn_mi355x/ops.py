@@ -6,6 +6,7 @@ import ctypes
 import math
 import threading
 from contextlib import contextmanager
+from dataclasses import dataclass
 from typing import Optional
 
 import numpy as np
@@ -313,19 +314,9 @@ def _as3(t: torch.Tensor):
 
 GEMM_TRACE: Optional[list] = None
 _GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
-GEMM_STAGE = 0        # ALIGNN_GEMM_BK32 (16) / ALIGNN_GEMM_BK64 (128): K stage depth of every planned GEMM
 GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
 GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
-GEMM_EXTRA = 0        # flags ORed into every gemm() call (A/B switches, e.g. GEMM_NOSTREAM)
-# split-K partials combined inside the GEMM launch by each tile's last workgroup (AlignnGemmArgs.counters)
-# instead of a separate reduce launch: same bits, one launch fewer per split product (option, off).
-# Measured on the B = 32 step (profiles/r02/v9_ab_splitk_combine.log): every split product combined
-# in-launch 6,930 vs 8,655 graphs/s (the last workgroup reads split x 16 KB serially); only products of
-# <= 2 / <= 4 splits 8,320 / 8,205 vs 8,617 (the agent-scope release/acquire per tile costs more than
-# the reduce launch it saves).
-SPLITK_COMBINE = False
-SPLITK_COMBINE_MAX = 2
 
 
 @contextmanager
@@ -399,7 +390,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if c_rows is not None:
         a.c_rows = c_rows.data_ptr()
     a.split_k = 0 if split_k is None else int(split_k)   # 0: the library plans tile shape and split-K
-    a.tile = int(tile) | _GEMM_FLAGS | GEMM_EXTRA | (GEMM_STAGE if not (int(tile) & 0xF0) else 0)
+    a.tile = int(tile) | _GEMM_FLAGS
     if path_only:   # which kernel the library takes (0 tiled, 1 bf16 streaming); nothing runs
         return int(_lib.lib().alignn_gemm_path(ctypes.byref(a)))
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
@@ -408,11 +399,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if need > 0:
         ws = WS.get("gemm", need, C.device)
         a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
-        split = need // max(1, (1 if a.reduce_batch else batch) * M * N)
-        if SPLITK_COMBINE and split <= SPLITK_COMBINE_MAX:
-            cn = int(_lib.lib().alignn_gemm_counters(ctypes.byref(a)))
-            if cn > 0:
-                a.counters = WS.get("gemm_tickets", cn, C.device, torch.int32, zeroed=True).data_ptr()
     if GEMM_TRACE is not None:   # tuning hook (tools/gemm_bench.py): record the call's operands
         GEMM_TRACE.append(dict(A=A, B=B, C=C, alpha=alpha, beta=beta, bias=bias, rowscale=rowscale, bias2=bias2,
                                relu=relu, mask=mask, reduce_batch=reduce_batch, c_rows=c_rows))
@@ -568,30 +554,13 @@ class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
     __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
-                 "n_full", "cmap", "_dst_src", "xcd_chunk")
+                 "n_full", "cmap", "_dst_src", "xcd_chunk", "policy")
 
     # in-degree above which a target node gets a 4-wave workgroup (LDS merge of the waves); below it
     # one wave walks the node's edges.  256: every node of the MP-like line graph (in-degree <= 132
     # under the PyG offset rule) takes the 1-wave path — measured +6.2 % step at B = 32, +8.7 % at
     # B = 256 bf16 vs 32 (line bwd_dst 194 -> 159 us; profiles/r01/v27_sweep_heavy_threshold.log)
-    HEAVY_THRESHOLD = 256
-    SORT_BY_DEGREE = False  # work items in descending in-degree order (A/B option; within noise, slower bwd_dst)
-    COMPACT_REGS = True  # attention kernels with row-distributed softmax state (+1 %, bwd_dst 249 -> 231 us)
-    # every target a single-wave work item, longest in-edge list first (lgconv.hip, the D = 256
-    # materialised-F line-graph kernels; other calls keep the kernels above)
-    WAVE_ITEMS = True
-    # work items interleaved so that XCD x (workgroup i runs on XCD i % 8) walks the x-th contiguous
-    # range of target ids, longest first within it: a target's sources lie near it (PyG's per-graph
-    # index windows), so each XCD's L2 holds the K/V rows its gathers need (line-graph bwd_dst fetch
-    # 588 -> 300 MB per launch).  With ranges of equal target COUNT the middle XCDs got 322 132-edge
-    # targets for 256 wave slots (two rounds: kernels 103 -> 128 us, step -5 %,
-    # profiles/r02/v13_ab_xcd_items_rejected.log); ranges of equal EDGE count give them 240: step
-    # +1.8 % at B = 32 (8,744-8,772 vs 8,602-8,611 graphs/s), neutral at B = 256 bf16
-    # (profiles/r02/v24_ab_xcd_items_edge_balanced.log).
-    XCD_ITEMS = True
-    XCDS = 8
-
-    def __init__(self, edge_index: torch.Tensor, n: int):
+    def __init__(self, edge_index: torch.Tensor, n: int, policy: Optional["SchedulePolicy"] = None):
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError("edge_index must be int64 [2, m]")
         ei = edge_index.contiguous()
@@ -608,6 +577,7 @@ class GraphCSR:
         self.err = torch.zeros(1, **i32)
         self._sched = None
         self._dst_src = None
+        self.policy = DEFAULT_SCHEDULE if policy is None else policy
         self.xcd_chunk = 1   # work items per workgroup of the kernels that read this graph's list
         self.rows = None     # compacted graph: int32 ids of its nodes in the full node set
         self.n_full = n
@@ -632,31 +602,53 @@ class GraphCSR:
         if self._sched is None:
             off = self.off_dst.cpu().numpy().astype(np.int64)
             deg = off[1:] - off[:-1] if self.n else np.zeros(0, np.int64)
-            light, heavy = schedule_lists(deg, self.HEAVY_THRESHOLD, self.SORT_BY_DEGREE or self.WAVE_ITEMS,
-                                          self.XCD_ITEMS and self.WAVE_ITEMS, self.XCDS, self.xcd_chunk)
+            po = self.policy
+            light, heavy = schedule_lists(deg, po.heavy_threshold, po.wave_items, po.xcd_items and po.wave_items,
+                                          po.xcds, self.xcd_chunk)
             both = torch.from_numpy(np.concatenate([light, heavy]).astype(np.int32)).to(self.off_dst.device)
             light, heavy = both[:len(light)], both[len(light):]
             sc = _lib.Schedule()
             sc.light, sc.n_light = (light.data_ptr() if light.numel() else None), light.numel()
             sc.heavy, sc.n_heavy = (heavy.data_ptr() if heavy.numel() else None), heavy.numel()
-            sc.flags = (_lib.SCHED_COMPACT_REGS if self.COMPACT_REGS else 0) | \
-                (_lib.SCHED_WAVE_ITEMS if self.WAVE_ITEMS else 0)
+            sc.flags = _lib.SCHED_WAVE_ITEMS if po.wave_items else 0
             self._sched = (sc, light, heavy)
         return self._sched[0]
 
-    def family(self, D: int, H: int, F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor] = None,
-               enc=None) -> int:
+    def family(self, D: int, H: int, F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor] = None) -> int:
         """Attention kernel family the library runs for this graph and operands (3: single-wave
-        items, 2: compact registers, 1: default); alignn_tconv_family."""
-        es = None if enc is None else enc.struct()
+        items, lgconv.hip; 2: light/heavy workgroups, tconv.hip); alignn_tconv_family."""
         return int(_lib.lib().alignn_tconv_family(D, H, None if feat_row is None else feat_row.data_ptr(),
-                                                   None if es is None else ctypes.byref(es),
                                                    None if F is None else F.data_ptr(), ctypes.byref(self.schedule())))
 
     def check_indices(self, what: str) -> None:
         """Host check of the device error flag (one sync).  PyG raises IndexError here."""
         if int(self.err.item()) != 0:
             raise IndexError(f"{what}: edge index out of range [0, {self.n})")
+
+
+@dataclass(frozen=True)
+class SchedulePolicy:
+    """How GraphCSR.schedule() lays out the attention kernels' work items — fixed per graph at
+    construction (an immutable value: two trainers in one process never share mutable switches).
+
+    heavy_threshold: in-degree above which a target node gets a 4-wave workgroup (LDS merge of the
+    waves); below it one wave walks the node's edges.  256: every node of the MP-like line graph
+    (in-degree <= 132 under the PyG offset rule) takes the 1-wave path — measured +6.2 % step at
+    B = 32, +8.7 % at B = 256 bf16 vs 32 (profiles/r01/v27_sweep_heavy_threshold.log).
+    wave_items: every target a single-wave work item, longest in-edge list first (lgconv.hip, the
+    D = 256 line-graph kernels; other calls keep tconv.hip's light/heavy kernels).
+    xcd_items: work items interleaved so that XCD x (workgroup i runs on XCD i % 8) walks the x-th
+    contiguous range of target ids, ranges of equal EDGE count, longest first within each: a
+    target's sources lie near it (PyG's per-graph index windows), so each XCD's L2 holds the K/V
+    rows its gathers need (line-graph bwd_dst fetch 588 -> 300 MB per launch; step +1.8 % at B = 32,
+    profiles/r02/v24_ab_xcd_items_edge_balanced.log)."""
+    heavy_threshold: int = 256
+    wave_items: bool = True
+    xcd_items: bool = True
+    xcds: int = 8
+
+
+DEFAULT_SCHEDULE = SchedulePolicy()
 
 
 def schedule_lists(deg: np.ndarray, heavy_threshold: int, by_degree: bool, xcd_ranges: bool, xcds: int = 8,
@@ -718,77 +710,31 @@ def scatter_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, accumu
     return out
 
 
-def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, kin: int = 0, dF_rw: int = 1) -> float:
-    """Compulsory HBM bytes of one launch (every operand touched once, ideal caching).  kin > 0:
-    edge features recomputed from kin raw inputs per edge (no [m, D] feature / gradient rows).
+def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, dF_rw: int = 1) -> float:
+    """Compulsory HBM bytes of one launch (every operand touched once, ideal caching).
     dF_rw: [m, D] edge-feature gradient rows moved by bwd_dst (0 none, 1 written, 2 read + written)."""
     f = 4.0
-    feat = m * kin if kin else m * D
+    feat = m * D
     if kind == "fwd":   # Q,K,V + U + edge features + CSR in; aggV + S + 3 stats out
         return f * (3 * n * D + n * H * D + feat + 2 * m + n + n * D + n * H * D + 3 * n * H)
     if kind == "bwd_dst":  # Q,K,V,U,Vd,dout,outp,features,stats in; dQ,Sz,sigz,dz,alpha(,dF) out
         return f * (3 * n * D + 2 * n * H * D + 2 * n * D + feat + 2 * n * H + 2 * m + n
-                    + n * D + n * H * D + n * H + 2 * m * H + (0 if kin else dF_rw * m * D))
+                    + n * D + n * H * D + n * H + 2 * m * H + dF_rw * m * D)
     return f * (2 * n * D + 2 * m * H + 2 * m + n + 2 * n * D)  # bwd_src
 
 
-ENC_MAX_KIN = 16
-
-
-class EdgeEncoder:
-    """Edge features recomputed in the attention kernels as relu(W1 x + b1) from kin <= 16 raw
-    inputs per edge (the angle encoder's hidden layer, train.py:353-356); see
-    ``AlignnEdgeEncoder`` in include/alignn_hip.h.  x is in edge-position (target-sorted) order.
-    For the backward, dw1/db1 receive the encoder gradients (accumulated)."""
-
-    def __init__(self, x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
-                 dw1: Optional[torch.Tensor] = None, db1: Optional[torch.Tensor] = None, accumulate: bool = True):
-        _require(x, "enc.x")
-        _require(w1, "enc.w1")
-        _require(b1, "enc.b1")
-        if x.dim() != 2 or x.stride(1) != 1 or not w1.is_contiguous() or not (1 <= x.size(1) <= ENC_MAX_KIN):
-            raise ValueError("EdgeEncoder: x must be [m, kin] row-major with 1 <= kin <= 16, w1 contiguous")
-        self.x, self.w1, self.b1, self.dw1, self.db1, self.accumulate = x, w1, b1, dw1, db1, accumulate
-        self.kin = x.size(1)
-
-    def struct(self, D: int = 0, H: int = 0, backward: bool = False) -> "_lib.EdgeEncoder":
-        ws, n_ws = None, 0
-        if backward:
-            n_ws = _enc_ws_elems(D, H, self.kin)
-            ws = WS.get("tconv_enc", n_ws, self.x.device)
-        return _lib.EdgeEncoder(self.x.data_ptr(), self.x.stride(0), self.kin, 1 if self.accumulate else 0,
-                                self.w1.data_ptr(), self.b1.data_ptr(), _p(self.dw1), _p(self.db1),
-                                None if ws is None else ws.data_ptr(), n_ws)
-
-
-_ENC_WS = {}
-
-
-def _enc_ws_elems(D: int, H: int, kin: int) -> int:
-    key = (D, H, kin)
-    if key not in _ENC_WS:
-        n = int(_lib.lib().alignn_tconv_bwd_workspace(D, H, kin))
-        if n < 0:
-            raise ValueError(f"tconv: unsupported encoder shape D={D} H={H} kin={kin}")
-        _ENC_WS[key] = max(n, 1)
-    return _ENC_WS[key]
-
-
-def _check_tconv(g: GraphCSR, D: int, H: int, QKVR, F, feat_row, enc, node_out=(), node_heads=(), edge_heads=()):
+def _check_tconv(g: GraphCSR, D: int, H: int, QKVR, F, feat_row, node_out=(), node_heads=(), edge_heads=()):
     """Host check that every operand covers what the kernels index (n target/source rows, m edge
     rows) before a launch: an undersized buffer would be an out-of-bounds device access."""
     n, m = g.n, g.m
     if QKVR.size(0) < n or QKVR.size(1) < 3 * D or QKVR.stride(1) != 1:
         raise ValueError(f"tconv: QKVR {tuple(QKVR.shape)} must cover [{n}, >= {3 * D}] row-major")
-    if enc is None:
-        if F is None or F.size(1) < D or F.stride(1) != 1:
-            raise ValueError("tconv: edge features F [m, D] row-major required")
-        if m > 0 and F.size(0) < (m if feat_row is None else int(feat_row.numel())):
-            raise ValueError(f"tconv: F has {F.size(0)} rows, the graph has {m} edges")
-        if feat_row is not None and feat_row.numel() < m:
-            raise ValueError("tconv: feat_row must have one entry per edge")
-    elif enc.x.size(0) < m:
-        raise ValueError(f"tconv: encoder inputs have {enc.x.size(0)} rows, the graph has {m} edges")
+    if F is None or F.size(1) < D or F.stride(1) != 1:
+        raise ValueError("tconv: edge features F [m, D] row-major required")
+    if m > 0 and F.size(0) < (m if feat_row is None else int(feat_row.numel())):
+        raise ValueError(f"tconv: F has {F.size(0)} rows, the graph has {m} edges")
+    if feat_row is not None and feat_row.numel() < m:
+        raise ValueError("tconv: feat_row must have one entry per edge")
     for t in node_out:
         if t is not None and t.numel() < n * D:
             raise ValueError(f"tconv: per-node operand {tuple(t.shape)} smaller than [{n}, {D}]")
@@ -802,40 +748,35 @@ def _check_tconv(g: GraphCSR, D: int, H: int, QKVR, F, feat_row, enc, node_out=(
 
 def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, wbar: Optional[torch.Tensor],
               F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float,
-              seed: int, enc: Optional[EdgeEncoder] = None):
-    _check_tconv(g, D, H, QKVR, F, feat_row, enc, node_out=(aggV,), node_heads=(sumA, mstat, den))
+              seed: int):
+    _check_tconv(g, D, H, QKVR, F, feat_row, node_out=(aggV,), node_heads=(sumA, mstat, den))
     if U.numel() < g.n * H * D or S.numel() < g.n * H * D:
         raise ValueError("tconv_fwd: U and S must be [n, H, D]")
-    es = None if enc is None else enc.struct()
-    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd", enc.kin if enc else 0),
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd"),
                      lambda: check(_lib.lib().alignn_tconv_fwd(
                          g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
                          ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0), U.data_ptr(), _p(wbar),
-                         _p(F), 0 if F is None else F.stride(0), None if es is None else ctypes.byref(es),
-                         aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(), den.data_ptr(),
+                         _p(F), 0 if F is None else F.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(), den.data_ptr(),
                          float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_fwd"))
 
 
 def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, dout, outp, mstat, den,
-                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: int, drop_p: float, seed: int,
-                  enc: Optional[EdgeEncoder] = None):
-    """accumulate_dF: bit 0 add into dF, bit 1 apply the ReLU mask (F > 0) to the result.  With an
-    edge encoder, F/dF are unused and the encoder gradients go to enc.dw1/enc.db1."""
-    _check_tconv(g, D, H, QKVR, F, feat_row, enc, node_out=(dout, outp), node_heads=(mstat, den, sigz),
+                  dq, Sz, sigz, dz_e, alpha_e, dF, accumulate_dF: int, drop_p: float, seed: int):
+    """accumulate_dF: bit 0 add into dF, bit 1 apply the ReLU mask (F > 0) to the result.  dF None:
+    no edge-feature gradient (the line graph's deferred angle-encoder backward, ops.enc_bwd)."""
+    _check_tconv(g, D, H, QKVR, F, feat_row, node_out=(dout, outp), node_heads=(mstat, den, sigz),
                  edge_heads=(dz_e, alpha_e))
     if U.numel() < g.n * H * D or Vd.numel() < g.n * H * D or Sz.numel() < g.n * H * D or dq.size(0) < g.n:
         raise ValueError("tconv_bwd_dst: U, Vd, Sz must be [n, H, D] and dq [n, >= D]")
-    if enc is None and dF is not None and dF.size(0) < F.size(0):
+    if dF is not None and dF.size(0) < F.size(0):
         raise ValueError("tconv_bwd_dst: dF must cover the rows of F")
-    es = None if enc is None else enc.struct(D, H, backward=True)
     profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0,
-                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", enc.kin if enc else 0,
-                                  0 if dF is None else (2 if accumulate_dF & 1 else 1)),
+                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", 0 if dF is None else (2 if accumulate_dF & 1 else 1)),
                      lambda: check(_lib.lib().alignn_tconv_bwd_dst(
                          g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
                          ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0),
                          U.data_ptr(), Vd.data_ptr(), _p(wbar), _p(F), 0 if F is None else F.stride(0),
-                         None if es is None else ctypes.byref(es), dout.data_ptr(), outp.data_ptr(),
+                         dout.data_ptr(), outp.data_ptr(),
                          mstat.data_ptr(), den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(),
                          sigz.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF),
                          0 if dF is None else dF.stride(0), int(accumulate_dF), float(drop_p),
@@ -906,15 +847,13 @@ def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Te
     return out
 
 
-# source-side attention backward over the by-source target list (alignn_tconv_bwd_src_by)
-BWD_SRC_BY = True
-
-
-def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV):
+def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV, by_source: bool = True):
+    """Source-side attention backward.  by_source: over the by-source target list
+    (alignn_tconv_bwd_src_by, the default); False: the plain entry (alignn_tconv_bwd_src), same bits."""
     if (QKVR.size(0) < g.n or dout.numel() < g.n * D or dKV.size(0) < g.n or dKV.size(1) < 2 * D
             or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H):
         raise ValueError("tconv_bwd_src: operands do not cover the graph's n nodes / m edges")
-    if BWD_SRC_BY and g.m > 0:
+    if by_source and g.m > 0:
         ds = g.dst_src()
         fn = lambda: check(_lib.lib().alignn_tconv_bwd_src_by(  # noqa: E731
             g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(), ds.data_ptr(), QKVR.data_ptr(),

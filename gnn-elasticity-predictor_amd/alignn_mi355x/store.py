@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import json
 import os
+import warnings
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -109,7 +110,7 @@ class BatchCapacity:
     edges: int                     # bonds
     triplets: int                  # line-graph edges
     active: Optional[int] = None   # compacted line-graph nodes (PyG offset rule); None: no compaction
-    max_in_degree: int = 200       # of a ghost node (below GraphCSR.HEAVY_THRESHOLD = 256)
+    max_in_degree: int = 200       # of a ghost node (below SchedulePolicy.heavy_threshold = 256)
 
 
 def ghost_plan(cap: BatchCapacity, B: int, N: int, E: int, T: int) -> Optional[Dict[str, int]]:
@@ -429,7 +430,9 @@ class GraphStore:
         arrays, counts = {}, {}
         for k in m["fields"]:
             a = np.load(os.path.join(path, f"{k}.npy"), mmap_mode="r")      # no pickles
-            arrays[k] = torch.from_numpy(np.ascontiguousarray(a)).to(device)
+            with warnings.catch_warnings():   # a read-only map: .to(device) copies, nothing writes it
+                warnings.simplefilter("ignore", UserWarning)
+                arrays[k] = torch.from_numpy(np.ascontiguousarray(a)).to(device)
             counts[k] = np.load(os.path.join(path, f"{k}.counts.npy"))
         return cls(arrays, counts, m["fields"], m.get("extras", {}), **kw)
 

@@ -168,136 +168,6 @@ __global__ __launch_bounds__(256) void enc_bwd_kernel(EncBwdParams p) {
   }
 }
 
-// Packed variant: thread j owns the feature columns 2j and 2j + 1 (128 threads) and does every
-// per-column operation of enc_bwd_kernel as a two-wide fp32 vector op (v_pk_fma_f32 / v_pk_add_f32
-// with the per-edge LDS scalar broadcast into both halves), so each element sees exactly the same
-// fma chain — same results (bitwise, tools/encbwd_dump.py), half the VALU instructions.  Same grid,
-// chunks and partial layout.  Off: its 254 VGPRs leave 2 waves per SIMD (the scalar kernel runs 4),
-// B = 32 +0.4 % but B = 256 bf16 -0.8 % (profiles/r02/v40_ab_encbwd_pk.log).
-#ifndef ALIGNN_ENCBWD_PK
-#define ALIGNN_ENCBWD_PK 0
-#endif
-typedef float eb_f2 __attribute__((ext_vector_type(2)));
-template <int KM, int H>
-__global__ __launch_bounds__(128) void enc_bwd_pk_kernel(EncBwdParams p) {
-  constexpr int ROW = 2 * EB_HL + KM;
-  constexpr int LM = EB_HL / H < EB_LMAX ? EB_HL / H : EB_LMAX;
-  constexpr int NT = 128;
-  __shared__ __attribute__((aligned(16))) float es[EB_CHUNK * ROW];
-  const int D = p.D, kin = p.kin, L = p.L;
-  const int HL = H * L;
-  const int j = threadIdx.x;
-  const int c0 = 2 * j;                 // columns c0, c0 + 1 (D is a multiple of 4)
-  const bool act = c0 < D;
-  eb_f2 w[KM], bj = {0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    w[k].x = (act && k < kin) ? p.w1[(int64_t)c0 * kin + k] : 0.f;
-    w[k].y = (act && k < kin) ? p.w1[(int64_t)(c0 + 1) * kin + k] : 0.f;
-  }
-  if (act) bj = eb_f2{p.b1[c0], p.b1[c0 + 1]};
-
-  eb_f2 acc[KM], accb = {0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < KM; ++k) acc[k] = eb_f2{0.f, 0.f};
-  for (int i = threadIdx.x; i < EB_CHUNK * ROW; i += NT) es[i] = 0.f;
-
-  eb_f2 Pu[EB_HL], Pv[EB_HL];
-  for (int64_t d = blockIdx.x; d < p.n; d += gridDim.x) {
-    const int64_t t0 = p.off_dst[d], t1 = p.off_dst[d + 1];
-    if (t0 == t1) continue;
-    const int jc = act ? c0 : 0;
-#pragma unroll
-    for (int q = 0; q < EB_HL; ++q) {
-      const int l = q / H, h = q % H;
-      const int ls = l < L ? l : 0;
-      const eb_f2 u = *reinterpret_cast<const eb_f2*>(p.U[ls] + (d * H + h) * D + jc);
-      const eb_f2 v = *reinterpret_cast<const eb_f2*>(p.Vd[ls] + (d * H + h) * D + jc);
-      const bool on = q < HL && act;
-      Pu[q] = on ? u : eb_f2{0.f, 0.f};
-      Pv[q] = on ? v : eb_f2{0.f, 0.f};
-    }
-    constexpr int PER_L = (EB_CHUNK * H + NT - 1) / NT;
-    constexpr int PER_X = (EB_CHUNK * KM + NT - 1) / NT;
-    for (int64_t tc = t0; tc < t1; tc += EB_CHUNK) {
-      const int ne = (int)min<int64_t>(EB_CHUNK, t1 - tc);
-      float vz[LM][PER_L], va[LM][PER_L], vx[PER_X];
-#pragma unroll
-      for (int l = 0; l < LM; ++l) {
-        const float* dz = p.dz[l < L ? l : 0] + tc * H;
-        const float* al = p.al[l < L ? l : 0] + tc * H;
-#pragma unroll
-        for (int u = 0; u < PER_L; ++u) {
-          const int i = threadIdx.x + NT * u;
-          const int ic = i < ne * H ? i : 0;
-          vz[l][u] = dz[ic];
-          va[l][u] = al[ic];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < PER_X; ++u) {
-        const int i = threadIdx.x + NT * u;
-        const int e = i / KM, k = i % KM;
-        vx[u] = (i < ne * KM && k < kin) ? p.x[(tc + e) * p.ldx + k] : 0.f;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int l = 0; l < LM; ++l) {
-        if (l < L) {
-#pragma unroll
-          for (int u = 0; u < PER_L; ++u) {
-            const int i = threadIdx.x + NT * u;
-            if (i < ne * H) {
-              const int e = i / H, h = i % H;
-              es[e * ROW + l * H + h] = vz[l][u];
-              es[e * ROW + EB_HL + l * H + h] = va[l][u];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < PER_X; ++u) {
-        const int i = threadIdx.x + NT * u;
-        if (i < ne * KM) es[(i / KM) * ROW + 2 * EB_HL + i % KM] = vx[u];
-      }
-      __syncthreads();
-      if (act) {
-        for (int e = 0; e < ne; ++e) {
-          const float* r = es + e * ROW;
-          eb_f2 gq[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-          for (int q = 0; q < EB_HL; ++q) {
-            const eb_f2 sz = {r[q], r[q]}, sa = {r[EB_HL + q], r[EB_HL + q]};
-            gq[q & 3] = __builtin_elementwise_fma(sz, Pu[q], __builtin_elementwise_fma(sa, Pv[q], gq[q & 3]));
-          }
-          const eb_f2 g = (gq[0] + gq[1]) + (gq[2] + gq[3]);
-          eb_f2 pre = {0.f, 0.f};
-#pragma unroll
-          for (int k = 0; k < KM; ++k) {
-            const eb_f2 xk = {r[2 * EB_HL + k], r[2 * EB_HL + k]};
-            pre = __builtin_elementwise_fma(xk, w[k], pre);
-          }
-          const eb_f2 pb = pre + bj;
-          const eb_f2 dp = {pb.x > 0.f ? g.x : 0.f, pb.y > 0.f ? g.y : 0.f};
-          accb += dp;
-#pragma unroll
-          for (int k = 0; k < KM; ++k) {
-            const eb_f2 xk = {r[2 * EB_HL + k], r[2 * EB_HL + k]};
-            acc[k] = __builtin_elementwise_fma(dp, xk, acc[k]);
-          }
-        }
-      }
-    }
-  }
-  if (act) {
-    float* part = p.part + (int64_t)blockIdx.x * (kin + 1) * D;
-#pragma unroll
-    for (int k = 0; k < KM; ++k)
-      if (k < kin) *reinterpret_cast<eb_f2*>(part + (int64_t)k * D + c0) = acc[k];
-    *reinterpret_cast<eb_f2*>(part + (int64_t)kin * D + c0) = accb;
-  }
-}
-
 // out (j, k): sum over workgroups b of part[b][k * D + j] in workgroup order (4 chains, fixed
 // combine) -> dW1[j, k] (k < kin) or db1[j] (k == kin), written or accumulated.
 // Block: 16 row-lanes x 64 outputs; thread (ty, tx) keeps four chains over workgroups ty, ty+16,
@@ -379,15 +249,6 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
   }
   if (a->T > 0) {
     const int km = a->kin <= 8 ? 8 : a->kin <= 12 ? 12 : 16;
-#if ALIGNN_ENCBWD_PK
-#define EB_LAUNCH_H(KM_)                                                                      \
-  switch (a->H) {                                                                             \
-    case 1: launch(enc_bwd_pk_kernel<KM_, 1>, dim3(EB_BLOCKS), dim3(128), 0, s, p); break;    \
-    case 2: launch(enc_bwd_pk_kernel<KM_, 2>, dim3(EB_BLOCKS), dim3(128), 0, s, p); break;    \
-    case 4: launch(enc_bwd_pk_kernel<KM_, 4>, dim3(EB_BLOCKS), dim3(128), 0, s, p); break;    \
-    default: launch(enc_bwd_pk_kernel<KM_, 8>, dim3(EB_BLOCKS), dim3(128), 0, s, p); break;   \
-  }
-#else
 #define EB_LAUNCH_H(KM_)                                                                   \
   switch (a->H) {                                                                          \
     case 1: launch(enc_bwd_kernel<KM_, 1>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;    \
@@ -395,7 +256,6 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
     case 4: launch(enc_bwd_kernel<KM_, 4>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;    \
     default: launch(enc_bwd_kernel<KM_, 8>, dim3(EB_BLOCKS), dim3(256), 0, s, p); break;   \
   }
-#endif
     if (km == 8) {
       EB_LAUNCH_H(8)
     } else if (km == 12) {

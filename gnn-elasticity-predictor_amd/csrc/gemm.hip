@@ -63,7 +63,6 @@ struct GemmParams {
   int reduce_batch;  // sum the batch into one output: K loop runs over (batch, k), K % BK == 0
   int pad_;
   const int32_t* c_rows;  // optional scatter of C rows
-  int32_t* cnt;           // split-K tile tickets (in-launch combine) or null (separate reduce)
 };
 
 // Loads one operand tile (ROWS x BKT) into registers.  KC: load along k (general strides,
@@ -259,8 +258,9 @@ __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (
     }
 }
 
-// Sum of one output element's split-K partials in the fixed order of splitk_reduce_kernel (eight
-// chains, partial s into chain s % 8, combined as a fixed tree): both combine paths give the same bits.
+// Sum of one output element's split-K partials (eight chains, partial s into chain s % 8, combined as
+// a fixed tree).  An in-launch combine by each tile's last workgroup was measured slower than this
+// separate reduce launch (profiles/r02/v9_ab_splitk_combine.log) and removed in round 3.
 __device__ __forceinline__ float splitk_sum(const GemmParams& p, int64_t b, int64_t row, int64_t col) {
   const int64_t nb = p.reduce_batch ? 1 : p.batch;
   const int64_t stride = nb * p.M * p.N;
@@ -273,41 +273,6 @@ __device__ __forceinline__ float splitk_sum(const GemmParams& p, int64_t b, int6
   }
   for (int j = 0; k < p.split_k; ++k, ++j) s[j] += w[(int64_t)k * stride];
   return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-}
-
-// In-launch split-K combine (the hand-off of cdna_hip_programming.md §5 "Projection GEMM", in its
-// counter form): every split's workgroup has stored its partial tile; each drains its stores, the
-// workgroup synchronises, one lane releases at agent scope and takes a ticket for the tile.  The
-// workgroup that draws split_k - 1 acquires at agent scope and sums the tile's partials (correct for
-// any placement of the splits over XCDs), applies the epilogue, stores C and puts the ticket back to
-// zero for the next launch.  `flag` is the kernel's own LDS array (no second __shared__ object).
-template <int BM, int BN>
-__device__ __forceinline__ void splitk_combine(const GemmParams& p, int64_t ctile, int64_t m0, int64_t n0, int64_t b,
-                                               float* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(p.cnt + ctile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == p.split_k - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(p.cnt + ctile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    flag[0] = last ? 1.f : 0.f;
-  }
-  __syncthreads();
-  if (flag[0] == 0.f) return;
-  const int tc = threadIdx.x % BN;
-  const int64_t col = n0 + tc;
-  if (col >= p.N) return;
-  for (int r = threadIdx.x / BN; r < BM; r += 256 / BN) {
-    const int64_t row = m0 + r;
-    if (row >= p.M) break;
-    p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, splitk_sum(p, b, row, col));
-  }
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF, bool RB>
@@ -394,7 +359,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   }
 
   store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
-  if (p.split_k > 1 && p.cnt) splitk_combine<BM, BN>(p, (RB ? 0 : b) * gridDim.x + tile, m0, n0, b, smem);
 }
 
 // Pipelined variant (ALIGNN_GEMM_PIPE): two register sets of global loads in flight, so a stage's
@@ -481,7 +445,6 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
     __syncthreads();
   }
   store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
-  if (p.split_k > 1 && p.cnt) splitk_combine<BM, BN>(p, b * gridDim.x + tile, m0, n0, b, smem);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
@@ -902,14 +865,6 @@ extern "C" int64_t alignn_gemm_workspace(const AlignnGemmArgs* a) {
   return pl.split > 1 ? (int64_t)pl.split * nb * a->M * a->N : 0;
 }
 
-extern "C" int64_t alignn_gemm_counters(const AlignnGemmArgs* a) {
-  GemmPlan pl;
-  int64_t ktot, nb;
-  if (!plan_args(a, pl, ktot, nb)) return -1;
-  if (pl.split <= 1) return 0;
-  return ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn) * nb;
-}
-
 extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
@@ -958,7 +913,6 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   p.kchunk = pl.kchunk;
   p.split_k = pl.split;
   p.ws = a->workspace;
-  p.cnt = pl.split > 1 ? a->counters : nullptr;
   if (pl.split > 1 && (!a->workspace || a->workspace_elems < (int64_t)pl.split * nbatch_out * a->M * a->N)) {
     set_error("gemm: split_k=%d needs %lld workspace floats", pl.split,
               (long long)pl.split * nbatch_out * a->M * a->N);
@@ -978,7 +932,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   else if (pl.bn == 128) dispatch_layout<64, 128>(p, akc, bkc, grid, pl.bk, bf, np, s);
   else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
-  if (pl.split > 1 && !p.cnt) {
+  if (pl.split > 1) {
     int64_t total = nbatch_out * a->M * a->N;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
     launch(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);

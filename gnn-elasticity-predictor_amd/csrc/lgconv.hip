@@ -784,11 +784,9 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
 
 // Entry points used by tconv.hip's C ABI when the schedule asks for single-wave items
 // (ALIGNN_SCHED_WAVE_ITEMS) and the call is in this family's domain (lg3_supported).
-bool lg3_supported(int D, int H, const int32_t* feat_row, const AlignnEdgeEncoder* enc, const float* F,
-                   const AlignnSchedule* sched) {
+bool lg3_supported(int D, int H, const int32_t* feat_row, const float* F, const AlignnSchedule* sched) {
   // H = 8 spills at this register budget: it takes the compact-register kernels
-  return D == lg3::D && (H == 1 || H == 2 || H == 4) && feat_row == nullptr && enc == nullptr &&
-         F != nullptr && sched != nullptr && (sched->flags & ALIGNN_SCHED_WAVE_ITEMS) && sched->n_heavy == 0 &&
+  return D == lg3::D && (H == 1 || H == 2 || H == 4) && feat_row == nullptr && F != nullptr && sched != nullptr && (sched->flags & ALIGNN_SCHED_WAVE_ITEMS) && sched->n_heavy == 0 &&
          sched->light != nullptr;
 }
 

@@ -349,7 +349,7 @@ __global__ void add_noise_kernel(int64_t n, float* __restrict__ x, float stdv, u
 
 using namespace alignn;
 
-extern "C" int alignn_version(void) { return 1; }
+extern "C" int alignn_version(void) { return ALIGNN_ABI_VERSION; }
 extern "C" const char* alignn_last_error(void) { return g_err; }
 
 extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,

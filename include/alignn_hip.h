@@ -24,7 +24,9 @@ extern "C" {
 #define ALIGNN_E_HIP -3
 #define ALIGNN_E_WORKSPACE -4
 
-/* Library/version and error introspection. */
+/* Library/version and error introspection.  ABI version 2: alignn_tconv_fwd / _bwd_dst / _family
+ * lost the edge-encoder argument, AlignnGemmArgs lost `counters` (round 3). */
+#define ALIGNN_ABI_VERSION 2
 int alignn_version(void);
 const char* alignn_last_error(void);
 
@@ -68,11 +70,6 @@ typedef struct AlignnGemmArgs {
                              + ALIGNN_GEMM_BK32 / BK16 / BK64 (stage depth), + ALIGNN_GEMM_BF16 */
   const int32_t* c_rows;  /* optional: logical row r of C is stored at row c_rows[r] (scatter; beta
                              reads the same row).  bias/rowscale/mask stay indexed by r. */
-  int32_t* counters;      /* optional, split-K only: alignn_gemm_counters(args) int32 tile tickets, all
-                             ZERO before the first call (every call leaves them zero again).  Given,
-                             the split partials are combined inside the GEMM launch by each tile's
-                             last-arriving workgroup (fixed summation order, the separate reduce's);
-                             NULL: a separate reduce launch.  Same result bits either way. */
 } AlignnGemmArgs;
 
 #define ALIGNN_GEMM_BK32 16
@@ -95,9 +92,6 @@ int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 /* Workspace floats alignn_gemm_f32 needs for these arguments (split_k = 0: the automatic plan on
  * the current device); 0 when no split is used, -1 for invalid shapes. */
 int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
-/* int32 tile tickets (AlignnGemmArgs.counters) the in-launch split-K combine needs: 0 when the plan
- * does not split K. */
-int64_t alignn_gemm_counters(const AlignnGemmArgs* args);
 
 /* Which kernel alignn_gemm_f32 takes (host query, no GPU work): 0 tiled, 1 the bf16 streaming
  * kernel (ALIGNN_GEMM_NOSTREAM), -1 invalid arguments. */
@@ -223,38 +217,21 @@ int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, 
 typedef struct AlignnSchedule {
   const int32_t* light; int64_t n_light;
   const int32_t* heavy; int64_t n_heavy;
-  int32_t flags;     /* ALIGNN_SCHED_COMPACT_REGS: the compact-register kernel variants (no encoder) */
+  int32_t flags;     /* ALIGNN_SCHED_WAVE_ITEMS or 0 (bit 0 is reserved) */
   int32_t reserved;
 } AlignnSchedule;
-#define ALIGNN_SCHED_COMPACT_REGS 1
 /* ALIGNN_SCHED_WAVE_ITEMS: `light` is the list of ALL target nodes in launch order (longest
  * in-edge list first), each processed by one single-wave workgroup (lgconv.hip); `heavy` must be
- * empty.  Used for D = 256, H in {1,2,4,8}, materialised F (feat_row NULL), no encoder and, in the
- * backward, no dF; other calls take the kernels above.  Arithmetic and outputs are those of the
- * compact-register kernels (the same dropout masks); sums are formed in a different order. */
+ * empty.  Used for D = 256, H in {1,2,4}, F rows indexed by edge position (feat_row NULL) and, in
+ * the backward, no dF; other calls take the light/heavy kernels of tconv.hip.  Arithmetic and
+ * outputs are those kernels' (the same dropout masks); sums are formed in a different order. */
 #define ALIGNN_SCHED_WAVE_ITEMS 2
-
-/* Edge encoder (optional, replaces F): the edge features are the hidden layer of a
- * Linear->ReLU edge encoder, f_t = relu(W1 x[row(t)] + b1) — the angle encoder's first Linear
- * (train.py:353-356, applied at train.py:553-554; its second Linear is folded into M).  The kernels
- * recompute f_t from the kin raw features (1 <= kin <= 16) instead of reading an [m, D] array.
- * x: [*, ldx]; w1: [D, kin] (nn.Linear weight); b1: [D].
- * Backward only: dw1 [D, kin] and db1 [D] receive the encoder's weight gradients (+= when
- * accumulate), computed in-kernel from the gradient w.r.t. f_t and the ReLU mask — the [m, D]
- * gradient is never written.  workspace: >= alignn_tconv_bwd_workspace(D, H, kin) floats (fewer
- * lowers the kernel's parallelism; at least (KM+1)*D with KM = kin rounded up to 8/12/16). */
-typedef struct AlignnEdgeEncoder {
-  const float* x; int64_t ldx; int32_t kin; int32_t accumulate;
-  const float* w1; const float* b1;
-  float* dw1; float* db1;
-  float* workspace; int64_t workspace_elems;
-} AlignnEdgeEncoder;
 
 int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
                      const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
                      const AlignnSchedule* sched,
                      const float* QKVR, int64_t ldq, const float* U, const float* wbar,
-                     const float* F, int64_t ldf, const AlignnEdgeEncoder* enc,
+                     const float* F, int64_t ldf,
                      float* aggV, float* S, float* sumA, float* mstat, float* den,
                      float drop_p, uint64_t seed, void* stream);
 
@@ -267,12 +244,12 @@ int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
  *   accumulate_dF: bit 0 = add to dF, bit 1 = multiply the result by (F[row(t)] > 0) (F is a
  *   ReLU output, e.g. the angle-encoder hidden layer: its backward mask is applied in place)
  * given dout (gradient of the aggregated message, [n, D]), outp (the aggregated message),
- * Vd[d,h] = M_h^T dout[d,h].  With an edge encoder, dF is not touched (the encoder's gradients go
- * to enc->dw1/db1 instead). */
+ * Vd[d,h] = M_h^T dout[d,h].  dF may be NULL (the line graph defers the angle-encoder backward to
+ * alignn_enc_bwd_f32, which recomputes the per-edge gradient there). */
 int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H,
                          const int32_t* off_dst, const int32_t* src_at, const int32_t* feat_row,
                          const AlignnSchedule* sched, const float* QKVR, int64_t ldq, const float* U, const float* Vd,
-                         const float* wbar, const float* F, int64_t ldf, const AlignnEdgeEncoder* enc,
+                         const float* wbar, const float* F, int64_t ldf,
                          const float* dout, const float* outp, const float* mstat, const float* den,
                          float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
                          float* dF, int64_t lddf, int32_t accumulate_dF,
@@ -301,14 +278,10 @@ int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t co
                          void* stream);
 
 /* Which attention kernel family alignn_tconv_fwd / alignn_tconv_bwd_dst (with dF == NULL) run for
- * these arguments: 3 = single-wave items (lgconv.hip), 2 = compact-register, 1 = default
- * (tconv.hip), 0 = unsupported arguments.  A host query: no device work. */
-int alignn_tconv_family(int32_t D, int32_t H, const int32_t* feat_row, const AlignnEdgeEncoder* enc,
-                        const float* F, const AlignnSchedule* sched);
-
-/* Workspace (floats) alignn_tconv_bwd_dst needs for an edge encoder with kin inputs at full
- * parallelism on the current device; 0 without encoder, -1 for unsupported arguments. */
-int64_t alignn_tconv_bwd_workspace(int32_t D, int32_t H, int32_t kin);
+ * these arguments: 3 = single-wave items (lgconv.hip), 2 = light/heavy workgroups (tconv.hip),
+ * 0 = unsupported arguments.  A host query: no device work. */
+int alignn_tconv_family(int32_t D, int32_t H, const int32_t* feat_row, const float* F,
+                        const AlignnSchedule* sched);
 
 /* Backward, source side (replaces the atomic index_add of the gather backward): per source node
  *   dK[s] = sum_{t: src(t)=s} dzs_t Q[dst(t)],  dV[s] = sum alpha'_t dout[dst(t)]

@@ -236,12 +236,8 @@ def test_bwd_src_by_source_list_bitwise(n, D, H):
     al = torch.randn(m, H, generator=g).to(DEV)
     outs = []
     for by in (False, True):
-        ops.BWD_SRC_BY = by
-        try:
-            dKV = torch.full((n, 2 * D), float("nan"), device=DEV)
-            ops.tconv_bwd_src(csr, D, H, QKVR, dout, dz, al, dKV)
-        finally:
-            ops.BWD_SRC_BY = True
+        dKV = torch.full((n, 2 * D), float("nan"), device=DEV)
+        ops.tconv_bwd_src(csr, D, H, QKVR, dout, dz, al, dKV, by_source=by)
         outs.append(dKV)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])

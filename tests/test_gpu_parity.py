@@ -126,24 +126,21 @@ def _grad_tols(st, cpu_batch, num_graphs, rgrads):
     return {k: max(TOL, 1.5 * norm_err(r32[k], rgrads[k], nfloor)) for k in rgrads}
 
 
-@pytest.mark.parametrize("num_graphs,lg_offset,heavy,recompute", [
-    (1, "num_nodes", None, True), (3, "num_nodes", None, True), (2, "num_edges", None, True),
-    (8, "num_nodes", None, True), (3, "num_nodes", 0, True), (2, "num_edges", 10**9, True),
-    (32, "num_edges", None, True),
-    (3, "num_nodes", None, False), (2, "num_edges", None, False)])
-def test_full_size_model_vs_oracle(num_graphs, lg_offset, heavy, recompute, monkeypatch):
+@pytest.mark.parametrize("num_graphs,lg_offset,heavy", [
+    (1, "num_nodes", None), (3, "num_nodes", None), (2, "num_edges", None),
+    (8, "num_nodes", None), (3, "num_nodes", 0), (2, "num_edges", 10**9),
+    (32, "num_edges", None)])
+def test_full_size_model_vs_oracle(num_graphs, lg_offset, heavy, monkeypatch):
     """Production dims (D=256, H=4, L=4, 206/36/11 features) on MP-like graphs.  ``heavy`` overrides
     the in-degree threshold of the 4-wave split path (0: every node with in-edges is split;
-    10**9: none is) so both kernel variants are checked against the oracle.  ``recompute`` False
-    materialises the angle hidden layer instead of recomputing it in the line convs."""
+    10**9: none is) so both kernel variants are checked against the oracle."""
     import alignn_mi355x as A
     from alignn_mi355x import ops
     from alignn_mi355x.synthetic import mp_like_batch
     if heavy is not None:
-        monkeypatch.setattr(ops.GraphCSR, "HEAVY_THRESHOLD", heavy)
+        monkeypatch.setattr(ops, "DEFAULT_SCHEDULE", ops.SchedulePolicy(heavy_threshold=heavy))
     torch.manual_seed(5)
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
-    model._engine.recompute_angle = recompute
     st = {k: v.detach().clone() for k, v in model.state_dict().items()}
     cpu_batch = mp_like_batch(num_graphs, lg_offset=lg_offset)
     rmean, rlogvar, rloss, rgrads = _oracle_grads({k: v.double() for k, v in st.items()},

@@ -38,10 +38,8 @@ def _run(csr, m, t, D, H, drop, wave_items, xcd_items=None):
     ops = _ops()
     n = csr.n
     csr._sched = None
-    prev = ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.XCD_ITEMS
-    ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS = wave_items, True
-    if xcd_items is not None:
-        ops.GraphCSR.XCD_ITEMS = xcd_items
+    prev = csr.policy
+    csr.policy = ops.SchedulePolicy(wave_items=wave_items, xcd_items=True if xcd_items is None else xcd_items)
     try:
         fam = csr.family(D, H, t["F"])
         outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
@@ -53,7 +51,7 @@ def _run(csr, m, t, D, H, drop, wave_items, xcd_items=None):
         ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], None, t["dout"], outp,
                           mstat, den, dq, Sz, sigz, dz, al, None, 0, drop, 77)
     finally:
-        ops.GraphCSR.WAVE_ITEMS, ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.XCD_ITEMS = prev
+        csr.policy = prev
         csr._sched = None
     torch.cuda.synchronize()
     return fam, dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz[:m], al=al[:m])

@@ -1,5 +1,5 @@
-"""GPU tests of paths added after the last on-GPU verification (opt-in in the product until they
-pass here): the 32-deep GEMM stage and the forward side-stream overlap.  Kept in a file that sorts
+"""GPU tests of engine options and kernel variants: GEMM stage depths, stream-placement options
+(bitwise neutral), the HIP optimizer, tconv.hip's light/heavy attention kernels vs fp64.  Kept in a file that sorts
 after the core parity suites so a failure here cannot stop those under ``pytest -x``."""
 import pytest
 import torch
@@ -72,10 +72,10 @@ def test_forward_side_stream_is_bitwise_neutral():
     assert torch.equal(tr1.st.grad, tr2.st.grad)
 
 
-@pytest.mark.parametrize("flag", ["overlap_skip", "overlap_src", "enc_bwd_aux", "gate_reduce_side", "proj_main"])
+@pytest.mark.parametrize("flag", ["enc_bwd_aux", "gate_reduce_side"])
 def test_backward_third_stream_is_bitwise_neutral(flag):
-    """Backward branches on the third stream (the line blocks' skip-projection dX product, the
-    source-side attention backward) change no bits: dX accumulates in the same order."""
+    """Backward branches off the main stream (the deferred angle-encoder backward on the third
+    stream, the gate/LayerNorm parameter reduction on the side stream) change no bits."""
     _, tr1, b1 = _setup()
     _, tr2, b2 = _setup()
     setattr(tr2.model._engine, flag, True)
@@ -187,56 +187,104 @@ def _tconv_case(D, H, n, deg_hi, seed, with_wbar, feat_row):
     return csr, m, t
 
 
-def _run_tconv(csr, m, t, D, H, drop, compact):
+def _run_tconv(csr, m, t, D, H, drop, heavy_threshold):
+    """tconv.hip's light/heavy kernels (wave_items off: every shape takes them, D = 256 included)."""
     ops = _ops()
     n = csr.n
     csr._sched = None
-    prev = ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.WAVE_ITEMS
-    ops.GraphCSR.COMPACT_REGS = compact
-    ops.GraphCSR.WAVE_ITEMS = False  # these tests pin the tconv.hip families (lgconv.hip: test_gpu_x_lg3.py)
-    try:
-        outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
-        sumA, mstat, den = (torch.empty(n, H, device=DEV) for _ in range(3))
-        ops.tconv_fwd(csr, D, H, t["QKVR"], t["U"], t["wbar"], t["F"], t["feat_row"], outp, S, sumA, mstat, den,
-                      drop, 77)
-        dq = torch.empty(n, D, device=DEV)
-        Sz, sigz = torch.empty(n, H, D, device=DEV), torch.empty(n, H, device=DEV)
-        dz, al = torch.empty(max(m, 1), H, device=DEV), torch.empty(max(m, 1), H, device=DEV)
-        dF = t["dF0"].clone()
-        ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], t["feat_row"], t["dout"], outp,
-                          mstat, den, dq, Sz, sigz, dz, al, dF, 3, drop, 77)
-    finally:
-        ops.GraphCSR.COMPACT_REGS, ops.GraphCSR.WAVE_ITEMS = prev
-        csr._sched = None
+    csr.policy = ops.SchedulePolicy(heavy_threshold=heavy_threshold, wave_items=False)
+    assert csr.family(D, H, t["F"], t["feat_row"]) == 2
+    outp, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
+    sumA, mstat, den = (torch.empty(n, H, device=DEV) for _ in range(3))
+    ops.tconv_fwd(csr, D, H, t["QKVR"], t["U"], t["wbar"], t["F"], t["feat_row"], outp, S, sumA, mstat, den,
+                  drop, 77)
+    dq = torch.empty(n, D, device=DEV)
+    Sz, sigz = torch.empty(n, H, D, device=DEV), torch.empty(n, H, device=DEV)
+    dz, al = torch.empty(max(m, 1), H, device=DEV), torch.empty(max(m, 1), H, device=DEV)
+    dF = t["dF0"].clone()
+    ops.tconv_bwd_dst(csr, D, H, t["QKVR"], t["U"], t["Vd"], t["wbar"], t["F"], t["feat_row"], t["dout"], outp,
+                      mstat, den, dq, Sz, sigz, dz, al, dF, 3, drop, 77)
     torch.cuda.synchronize()
     return dict(outp=outp, S=S, sumA=sumA, mstat=mstat, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz[:m], al=al[:m],
                 dF=dF)
 
 
+def _attention_ref(csr, m, t, D, H):
+    """fp64 restatement of the kernels' contract (include/alignn_hip.h, alignn_tconv_fwd/_bwd_dst;
+    PyG TransformerConv.message + softmax(+1e-16) with the edge-feature algebra of DESIGN.md §3),
+    no dropout.  Edge position t: target-sorted (csr.src_at / dst_at); F row feat_row[t] or t."""
+    import math
+    n, C = csr.n, D // H
+    d64 = lambda x: x.detach().double().cpu()  # noqa: E731
+    src, dst = csr.src_at[:m].long().cpu(), csr.dst_at[:m].long().cpu()
+    row = t["feat_row"][:m].long().cpu() if t["feat_row"] is not None else torch.arange(m)
+    QKVR = d64(t["QKVR"])
+    Q, K, V = (QKVR[:, i * D:(i + 1) * D].reshape(n, H, C) for i in range(3))
+    U, Vd, F = d64(t["U"]), d64(t["Vd"]), d64(t["F"])[row]
+    wb = d64(t["wbar"]).view(H, C) if t["wbar"] is not None else torch.zeros(H, C, dtype=torch.float64)
+    dout = d64(t["dout"]).view(n, H, C)
+    z64 = lambda *s: torch.zeros(*s, dtype=torch.float64)  # noqa: E731
+    z = ((Q[dst] * K[src]).sum(-1) + torch.einsum("mhd,md->mh", U[dst], F) + (Q[dst] * wb).sum(-1)) / math.sqrt(C)
+    mst = torch.full((n, H), float("-inf"), dtype=torch.float64).scatter_reduce(
+        0, dst[:, None].expand(m, H), z, "amax", include_self=True)
+    ex = torch.exp(z - mst[dst])
+    den = z64(n, H).index_add_(0, dst, ex) + 1e-16
+    al = ex / den[dst]
+    outp = z64(n, H, C).index_add_(0, dst, al[..., None] * V[src]).view(n, D)
+    S = z64(n, H, D).index_add_(0, dst, al[..., None] * F[:, None, :])
+    sumA = z64(n, H).index_add_(0, dst, al)
+    g = (dout[dst] * V[src]).sum(-1) + torch.einsum("mhd,md->mh", Vd[dst], F) + (dout[dst] * wb).sum(-1)
+    pdl = (dout * outp.view(n, H, C)).sum(-1)
+    dz = al * (g - pdl[dst]) / math.sqrt(C)
+    dq = z64(n, H, C).index_add_(0, dst, dz[..., None] * K[src]).view(n, D)
+    Sz = z64(n, H, D).index_add_(0, dst, dz[..., None] * F[:, None, :])
+    sigz = z64(n, H).index_add_(0, dst, dz)
+    dF = d64(t["dF0"])
+    upd = torch.einsum("mh,mhd->md", dz, U[dst]) + torch.einsum("mh,mhd->md", al, Vd[dst])
+    dF[row] = (dF[row] + upd) * (F > 0)            # accumulate_dF = 3: add, then the ReLU mask
+    return dict(outp=outp, S=S, sumA=sumA, mstat=mst, den=den, dq=dq, Sz=Sz, sigz=sigz, dz=dz, al=al, dF=dF)
+
+
 @pytest.mark.parametrize("thr", [32, 256])
 @pytest.mark.parametrize("D,H", [(256, 4), (128, 2), (64, 1), (32, 4), (32, 1), (512, 8)])
-@pytest.mark.parametrize("drop", [0.0, 0.15])
-def test_compact_register_attention_kernels_match_v1(D, H, drop, thr, monkeypatch):
-    """The row-distributed (COMPACT_REGS) attention kernels vs the default ones: same math, softmax
-    sums in a different order -> 1e-5 relative; per-edge dz / alpha' and the dF rows agree too.
+def test_light_heavy_attention_kernels_vs_fp64(D, H, thr):
+    """tconv.hip's attention kernels (forward + target-side backward with the dF read-modify-write
+    path, every supported D/H) vs an fp64 restatement of their contract: 2e-5 of each output's max.
     thr: heavy-node threshold (32: in-degrees up to 70 take both the 4-wave and the 1-wave path;
     256, the default: all 1-wave)."""
-    monkeypatch.setattr(_ops().GraphCSR, "HEAVY_THRESHOLD", thr)
     for seed, (with_wbar, feat_row) in enumerate([(True, False), (False, True)]):
         csr, m, t = _tconv_case(D, H, 300, 70, 10 + seed, with_wbar, feat_row)
-        a = _run_tconv(csr, m, t, D, H, drop, False)
-        b = _run_tconv(csr, m, t, D, H, drop, True)
-        for k in a:
-            assert _rel(b[k], a[k]) < 1e-5, (k, D, H, drop, seed)
+        got = _run_tconv(csr, m, t, D, H, 0.0, thr)
+        ref = _attention_ref(csr, m, t, D, H)
+        for k in ref:
+            assert _rel(got[k].cpu(), ref[k]) < 2e-5, (k, D, H, thr, seed)
+
+
+@pytest.mark.parametrize("D,H", [(256, 4), (128, 2)])
+def test_light_heavy_attention_dropout_replays(D, H):
+    """With dropout the kernels draw the same keep mask in the forward and the backward (the alpha'
+    they write per edge sums to sumA), and a second run is bitwise identical."""
+    csr, m, t = _tconv_case(D, H, 300, 70, 21, True, False)
+    a = _run_tconv(csr, m, t, D, H, 0.15, 32)
+    b = _run_tconv(csr, m, t, D, H, 0.15, 32)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    dst = csr.dst_at[:m].long()
+    sumA = torch.zeros(csr.n, H, device=DEV, dtype=torch.float64).index_add_(0, dst, a["al"].double())
+    assert _rel(a["sumA"], sumA) < 1e-5
+    assert float((a["al"] == 0).double().mean()) > 0.1     # ~15 % of (edge, head) pairs dropped
 
 
 @pytest.mark.parametrize("lg_offset", ["num_nodes", "num_edges"])
-def test_compact_register_kernels_full_model_vs_oracle(lg_offset):
+def test_light_heavy_kernels_full_model_vs_oracle(lg_offset, monkeypatch):
+    """The production model (D = 256) with every attention on tconv.hip's kernels (wave_items off)
+    vs the fp64 oracle."""
     import alignn_mi355x as A
     from alignn_mi355x import ops
     from alignn_mi355x.synthetic import mp_like_batch
     from oracle import model_ref
     from oracle.pyg_ref import RefData
+    monkeypatch.setattr(ops, "DEFAULT_SCHEDULE", ops.SchedulePolicy(wave_items=False))
     torch.manual_seed(5)
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
     st = {k: v.detach().clone().double() for k, v in model.state_dict().items()}
@@ -246,13 +294,10 @@ def test_compact_register_kernels_full_model_vs_oracle(lg_offset):
         setattr(ref_b, k, getattr(ref_b, k).double())
     ref_b.num_graphs = 3
     rmean, rlogvar = model_ref.hetero_forward(st, ref_b, 4)
-    prev = ops.GraphCSR.COMPACT_REGS
-    ops.GraphCSR.COMPACT_REGS = True
-    try:
-        model.to(DEV)
-        mean, logvar = model(cpu_batch.to(DEV))
-    finally:
-        ops.GraphCSR.COMPACT_REGS = prev
+    model.to(DEV)
+    b = cpu_batch.to(DEV)
+    mean, logvar = model(b)
+    assert b._alignn_cache.lg.policy.wave_items is False
     assert _rel(mean.detach().cpu(), rmean) < 1e-4
     assert _rel(logvar.detach().cpu(), rlogvar) < 1e-4
 

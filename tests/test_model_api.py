@@ -89,15 +89,15 @@ def test_tconv_host_shape_checks_reject_undersized_operands():
     g = types.SimpleNamespace(n=10, m=40)
     D, H = 64, 4
     ok = dict(QKVR=torch.zeros(10, 3 * D), F=torch.zeros(40, D))
-    ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None, None)
+    ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None)
     with pytest.raises(ValueError):
-        ops._check_tconv(g, D, H, ok["QKVR"], torch.zeros(39, D), None, None)     # F short of m rows
+        ops._check_tconv(g, D, H, ok["QKVR"], torch.zeros(39, D), None)     # F short of m rows
     with pytest.raises(ValueError):
-        ops._check_tconv(g, D, H, torch.zeros(9, 3 * D), ok["F"], None, None)     # QKVR short of n rows
+        ops._check_tconv(g, D, H, torch.zeros(9, 3 * D), ok["F"], None)     # QKVR short of n rows
     with pytest.raises(ValueError):
-        ops._check_tconv(g, D, H, ok["QKVR"], None, None, None)                    # no edge features
+        ops._check_tconv(g, D, H, ok["QKVR"], None, None)                    # no edge features
     with pytest.raises(ValueError):
-        ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None, None, edge_heads=(torch.zeros(40, 3),))
+        ops._check_tconv(g, D, H, ok["QKVR"], ok["F"], None, edge_heads=(torch.zeros(40, 3),))
 
 
 def test_mp_like_line_graph_is_the_per_graph_construction():

@@ -12,7 +12,7 @@ from alignn_mi355x import ops  # noqa: E402
 from oracle.model_ref import edge_block, node_block  # noqa: E402
 
 if len(sys.argv) > 1:
-    ops.GraphCSR.HEAVY_THRESHOLD = int(sys.argv[1])
+    ops.DEFAULT_SCHEDULE = ops.SchedulePolicy(heavy_threshold=int(sys.argv[1]))
 torch.manual_seed(0)
 D, H = 256, 4
 n, m = 1000, 30000

@@ -1,6 +1,6 @@
 """Microbenchmark of the attention kernels on the bench workload's graphs (B=32 MP-like, quirk and
-fixed line-graph wiring): line graph with the in-kernel angle encoder and with materialised
-features, atom graph.  Times each call with HIP events (median of R reps) on the current stream.
+fixed line-graph wiring): line graph (materialised features, with and without the dF rows; both
+kernel families), atom graph.  Times each call with HIP events (median of R reps) on the current stream.
 
 usage: python tools/tconv_bench.py [--reps 20] [--batch 32]
 """
@@ -38,12 +38,11 @@ def timeit(fn, reps):
     return sorted(ts)[1]
 
 
-def run_graph(name, g, n, m, D, H, F, enc, reps, out, nodf=False):
+def run_graph(name, g, n, m, D, H, F, reps, out, nodf=False):
     dev = "cuda"
     # shapes the kernels assume (checked on the host before any launch)
     assert g.n == n and g.m == m, (g.n, n, g.m, m)
-    assert F is None or F.size(0) >= m, (F.size(0), m)
-    assert enc is None or enc.x.size(0) >= m
+    assert F.size(0) >= m, (F.size(0), m)
     gen = torch.Generator(device=dev).manual_seed(0)
     r = lambda *s: torch.randn(*s, device=dev, generator=gen) * 0.5
     QKVR, U, Vd = r(n, 4 * D), r(n, H, D), r(n, H, D)
@@ -54,19 +53,13 @@ def run_graph(name, g, n, m, D, H, F, enc, reps, out, nodf=False):
     Sz, sigz = torch.empty(n, H, D, device=dev), torch.empty(n, H, device=dev)
     dz, al = torch.empty(max(m, 1), H, device=dev), torch.empty(max(m, 1), H, device=dev)
     dKV = torch.empty(n, 2 * D, device=dev)
-    dF = None if (F is None or nodf) else torch.zeros_like(F)
-    ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, None, aggV, S, sumA, mstat, den, 0.15, 1, enc=enc)
-    t_f = timeit(lambda: ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, None, aggV, S, sumA, mstat, den, 0.15, 1,
-                                       enc=enc), reps)
-    bwd_enc = None
-    if enc is not None:
-        dw1, db1 = torch.zeros_like(enc.w1), torch.zeros_like(enc.b1)
-        bwd_enc = ops.EdgeEncoder(enc.x, enc.w1, enc.b1, dw1, db1)
+    dF = None if nodf else torch.zeros_like(F)
+    ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, None, aggV, S, sumA, mstat, den, 0.15, 1)
+    t_f = timeit(lambda: ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, None, aggV, S, sumA, mstat, den, 0.15, 1), reps)
     t_b = timeit(lambda: ops.tconv_bwd_dst(g, D, H, QKVR, U, Vd, wbar, F, None, dout, aggV, mstat, den, dq, Sz,
-                                           sigz, dz, al, dF, 0 if dF is None else 1, 0.15, 1, enc=bwd_enc),
-                 reps)
+                                           sigz, dz, al, dF, 0 if dF is None else 1, 0.15, 1), reps)
     t_s = timeit(lambda: ops.tconv_bwd_src(g, D, H, QKVR, dout, dz, al, dKV), reps)
-    fam = g.family(D, H, F, None, enc)
+    fam = g.family(D, H, F)
     res = {"fwd_us": t_f, "bwd_dst_us": t_b, "bwd_src_us": t_s, "n": n, "m": m, "family": fam}
     out[name] = res
     print(f"{name:28s} fam={fam} n={n:6d} m={m:7d}  fwd {t_f:8.1f} us  bwd_dst {t_b:8.1f} us  bwd_src {t_s:8.1f} us", flush=True)
@@ -90,22 +83,20 @@ def main():
         ops.gather_rows(b.lg_edge_attr, lg.perm_dst, xa)
         w1 = torch.randn(D, xa.size(1), device="cuda") * 0.3
         b1 = torch.randn(D, device="cuda") * 0.1
-        enc = ops.EdgeEncoder(xa, w1, b1)
-        run_graph(f"line/{lg_offset}/enc", lg, nl, T, D, H, None, enc, a.reps, out)
         F = torch.relu(xa @ w1.t() + b1)
-        run_graph(f"line/{lg_offset}/F", lg, nl, T, D, H, F, None, a.reps, out)
+        run_graph(f"line/{lg_offset}/F", lg, nl, T, D, H, F, a.reps, out)
         # the training step's configuration: materialised F, deferred encoder backward (no dF)
         for wave_items in (False, True):
-            ops.GraphCSR.WAVE_ITEMS = wave_items
+            lg.policy = ops.SchedulePolicy(wave_items=wave_items)
             lg._sched = None
-            run_graph(f"line/{lg_offset}/F/nodF/wi{int(wave_items)}", lg, nl, T, D, H, F, None, a.reps, out,
+            run_graph(f"line/{lg_offset}/F/nodF/wi{int(wave_items)}", lg, nl, T, D, H, F, a.reps, out,
                       nodf=True)
         lg._sched = None
         if lg_offset == "num_nodes":
             N = b.x.size(0)
             ag = ops.GraphCSR(b.edge_index, N)
             Fe = torch.randn(E, D, device="cuda")
-            run_graph("atom", ag, N, E, D, H, Fe, None, a.reps, out)
+            run_graph("atom", ag, N, E, D, H, Fe, a.reps, out)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)
