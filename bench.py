@@ -70,9 +70,6 @@ def parse():
                         "(config C5's ~10k graphs; 0 = off): device collate of a random batch + CSR/compaction + "
                         "step, at the headline config and (one GPU) at config C5's B=256 bf16 (SURVEY §8d's "
                         "'including collate' number; separate fields, never value)")
-    p.add_argument("--e2e-sync", action="store_true",
-                   help="e2e: prepare each next batch on this thread between the steps instead of on the "
-                        "prefetch thread (for comparison)")
     p.add_argument("--launch", choices=["eager", "plan", "graph"], default="plan",
                    help="eager: Python issues every launch; plan: the step is recorded once as a native launch "
                         "plan and re-issued from C++ (plan.hip; the roofline probe is a pair of plan timestamps "
@@ -200,7 +197,6 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     import numpy as np
     from alignn_mi355x.dp import max_over_ranks
     from alignn_mi355x.engine import prepare_batch
-    from alignn_mi355x.prefetch import BatchPrefetcher
 
     rng = np.random.default_rng(1234 + rank)
     # B >= 128: a high-priority loader stream, so the small collate/CSR kernels (and the host syncs of
@@ -210,27 +206,14 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     prio = getattr(args, "loader_priority", None)
     if prio is None:
         prio = -1 if B >= 128 else 0
-    draw = lambda: rng.choice(store.num_graphs, size=B, replace=False)  # noqa: E731
-    total = 1 + args.warmup + args.steps
-    if args.e2e_sync:   # the loader's host work between the steps, on this thread
-        loader = torch.cuda.Stream(device=dev, priority=prio)
+    loader = torch.cuda.Stream(device=dev, priority=prio)
 
-        def make():
-            with torch.cuda.stream(loader):
-                b = store.collate(draw(), lg_offset=args.lg_offset, capacity=capacity)
-            prepare_batch(b, loader)
-            return b
-        pf = None
-    else:               # a host thread prepares the next batches while this one re-binds and replays
-        drawn = [0]
-
-        def nxt_idx():
-            if drawn[0] >= total:
-                return None
-            drawn[0] += 1
-            return draw()
-        pf = BatchPrefetcher(store, nxt_idx, depth=2, lg_offset=args.lg_offset, capacity=capacity, priority=prio)
-        make = pf.get
+    def make():
+        with torch.cuda.stream(loader):
+            b = store.collate(rng.choice(store.num_graphs, size=B, replace=False), lg_offset=args.lg_offset,
+                              capacity=capacity)
+        prepare_batch(b, loader)
+        return b
 
     r0, m0 = trainer.rebinds, trainer.rebind_misses
     nxt = make()
@@ -262,18 +245,13 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
            "dataset_graphs_per_rank": store.num_graphs,
            "store_build_s": round(t_build, 1), "replayed_steps": trainer.rebinds - r0,
            "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
-                                ("collate_and_prepare" if args.e2e_sync else "wait_for_prefetched_batch"):
-                                    round(host_make / args.steps * 1e3, 3)},
-           "loader": ("synchronous (this thread)" if args.e2e_sync else
-                      "host thread, 2 batches ahead (prefetch.BatchPrefetcher)"),
+                                "collate_and_prepare": round(host_make / args.steps * 1e3, 3)},
            "eager_steps": trainer.rebind_misses - m0,
            "signature": ("every batch padded to one capacity (store.BatchCapacity)" if capacity is not None else
                          "fixed: every synthetic graph has 60 atoms, so every batch has the captured signature "
                          "(best case; see e2e_variable for variable-size graphs)"),
            "includes": "device collate of a random batch + CSR/compaction/schedules (loader stream) + "
                        "fwd/NLL/bwd/clip/AdamW (captured plan re-bound to the batch)"}
-    if pf is not None:
-        pf.close()
     return out
 
 

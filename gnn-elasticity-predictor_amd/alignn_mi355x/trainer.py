@@ -255,6 +255,16 @@ class FusedTrainer:
             phases = [("forward/backward layers", lambda: state.__setitem__("t", self._fb_layers(batch, 0))),
                       ("backward tail", lambda: self._fb_tail(state["t"]))]
         phases.append(("clip/AdamW", self._clip_and_update))
+        # the per-layer phase leaves weight-gradient work queued on the engine's side stream (joined by
+        # the tail); a graph capture must end with every forked stream joined, so the capture joins them
+        # here — a torch-level wait the launch plan does not record: the replayed plans keep the
+        # overlap, and their stream order is that of the uncaptured step
+        engine_ctx = self.model._engine.ctx
+
+        def join_forks():
+            cur = torch.cuda.current_stream(dev)
+            for st in list(engine_ctx._side.values()) + list(engine_ctx._aux.values()):
+                cur.wait_stream(st)
         graphs = [torch.cuda.CUDAGraph(keep_graph=keep) for _ in phases]
         plans = []
         try:
@@ -265,6 +275,8 @@ class FusedTrainer:
                             plans.append(_record_plan(fn))
                         else:
                             fn()
+                        if len(phases) == 3 and i == 0:
+                            join_forks()
             state.clear()
             torch.cuda.synchronize(dev)
             self._restore(snap)

@@ -117,42 +117,3 @@ def test_variable_batches_replay_one_plan_bitwise():
     tp.release_capture()
     ops.set_step_seed(None)
 
-
-def test_prefetched_batches_match_synchronous_loop_bitwise():
-    """prefetch.BatchPrefetcher (collate + prepare on a host thread and its own loader stream, two
-    batches ahead) yields the batches a synchronous loop over the same index draws yields, and a
-    captured trainer fed by it ends bitwise where the same trainer fed synchronously ends."""
-    from alignn_mi355x.engine import prepare_batch
-    from alignn_mi355x.prefetch import BatchPrefetcher
-    st = _store()
-    cap = st.capacity(8)
-    draws = [np.random.default_rng(40 + i).choice(st.num_graphs, size=8, replace=False) for i in range(7)]
-    it = iter(draws)
-    pf = BatchPrefetcher(st, lambda: next(it, None), depth=2, capacity=cap)
-    got = list(pf)
-    pf.close()
-    assert len(got) == len(draws) and pf.produced == len(draws)
-    loader = torch.cuda.Stream()
-    ref = []
-    for idx in draws:
-        with torch.cuda.stream(loader):
-            b = st.collate(idx, capacity=cap)
-        prepare_batch(b, loader)
-        ref.append(b)
-    torch.cuda.synchronize()
-    for a, b in zip(got, ref):
-        for k in KEYS + ("batch", "ptr"):
-            assert torch.equal(getattr(a, k), getattr(b, k)), k
-    ta, tb = _trainer(), _trainer()
-    ta.capture(st.collate(draws[0], capacity=cap))   # each trainer owns its captured batch's buffers
-    tb.capture(st.collate(draws[0], capacity=cap))
-    it2 = iter(draws[1:])
-    with BatchPrefetcher(st, lambda: next(it2, None), depth=2, capacity=cap) as pf2:
-        for i, b in enumerate(pf2):
-            ta.step(b, seed=500 + i)
-            tb.step(ref[1 + i], seed=500 + i)
-    torch.cuda.synchronize()
-    assert torch.equal(ta.st.flat, tb.st.flat)
-    assert ta.rebinds == tb.rebinds == len(draws) - 1 and ta.rebind_misses == 0
-    ta.release_capture()
-    tb.release_capture()
