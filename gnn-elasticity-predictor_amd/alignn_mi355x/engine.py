@@ -17,6 +17,7 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 
 from . import ops
@@ -118,6 +119,9 @@ class BatchCache:
     ATOM_XCD_CHUNK = 4
 
     def __init__(self, batch, validate: bool = True):
+        # a batch collated from a GraphStore whose index ranges were checked when it was built needs
+        # no per-batch check (two host syncs fewer)
+        validate = validate and not getattr(batch, "_alignn_trusted", False)
         x = batch.x
         if not x.is_cuda:
             raise ValueError("batch must be on the HIP device (batch.to('cuda')); the engine has no CPU path")
@@ -166,6 +170,18 @@ class BatchCache:
     # on: node/edge/triplet counts, the compacted line graph's size, the schedules' list lengths and
     # flags) can be copied into the captured batch's buffers and the plan replayed unchanged.
     # -------------------------------------------------------------------------------------------
+    def schedules(self) -> None:
+        """Builds the atom and line graphs' schedules with ONE device->host copy (their in-degrees
+        are needed on the host to order the work items) instead of one per graph."""
+        gs = [g for g in (self.ag, self.lg) if g._sched is None]
+        if len(gs) == 2:
+            off = torch.cat([g.off_dst for g in gs]).cpu().numpy().astype(np.int64)
+            a = gs[0].n + 1
+            for g, o in ((gs[0], off[:a]), (gs[1], off[a:])):
+                g.schedule(deg=o[1:] - o[:-1] if g.n else np.zeros(0, np.int64))
+        for g in (self.ag, self.lg):
+            g.schedule()
+
     @staticmethod
     def _graph_sig(g: ops.GraphCSR):
         sc = g.schedule()
@@ -239,14 +255,21 @@ class BatchCache:
             need = pad["active"] - active.sum()
             j = torch.arange(n, device=edge_index.device) - first
             active |= (j >= 0) & (j < need)
-        return cls._compact(active, edge_index, n, force=pad is not None)
+        return cls._compact(active, edge_index, n, force=pad is not None,
+                            na=None if pad is None else int(pad["active"]))
 
     @classmethod
-    def _compact(cls, active: torch.Tensor, edge_index: torch.Tensor, n: int, force: bool = False) -> ops.GraphCSR:
-        na = int(active.sum().item())
-        if na > cls.COMPACT_FRACTION * n and not force:
-            return ops.GraphCSR(edge_index, n)
-        rows = torch.nonzero(active).flatten()
+    def _compact(cls, active: torch.Tensor, edge_index: torch.Tensor, n: int, force: bool = False,
+                 na: Optional[int] = None) -> ops.GraphCSR:
+        """na: the active count when the caller knows it (a padded batch: its capacity's), so neither
+        the count nor the index list waits for the device."""
+        if na is None:
+            na = int(active.sum().item())
+            if na > cls.COMPACT_FRACTION * n and not force:
+                return ops.GraphCSR(edge_index, n)
+            rows = torch.nonzero(active).flatten()
+        else:
+            rows = torch.nonzero_static(active, size=na).flatten()
         cmap = torch.full((n,), -1, dtype=torch.int64, device=edge_index.device)
         cmap[rows] = torch.arange(na, dtype=torch.int64, device=edge_index.device)
         gc = ops.GraphCSR(cmap[edge_index], na)
@@ -262,12 +285,12 @@ def prepare_batch(batch, stream: Optional[torch.cuda.Stream] = None, validate: b
     for (FusedTrainer.step): a loader can prepare batch i + 1 on its own stream while step i runs."""
     if stream is None:
         bc = batch_cache(batch, validate)
-        bc.signature()       # builds the schedules too
+        bc.schedules()       # both graphs' schedules from one device->host copy of their offsets
         bc.device_tensors()  # and the by-source target lists
     else:
         with torch.cuda.stream(stream):
             bc = batch_cache(batch, validate)
-            bc.signature()
+            bc.schedules()
             bc.device_tensors()
     ev = torch.cuda.Event()
     s = stream if stream is not None else torch.cuda.current_stream()

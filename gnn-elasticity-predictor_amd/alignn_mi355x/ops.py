@@ -596,12 +596,14 @@ class GraphCSR:
             self._dst_src = self.dst_at[self.pos_src.long()].contiguous() if self.m else self.dst_at[:0].clone()
         return self._dst_src
 
-    def schedule(self):
+    def schedule(self, deg: Optional[np.ndarray] = None):
         """Light/heavy target-node lists for the attention kernels (host-built once per graph:
-        one small device->host copy of the offsets, numpy ordering, one upload)."""
+        one small device->host copy of the offsets — or the in-degrees ``deg`` the caller fetched —
+        numpy ordering, one upload)."""
         if self._sched is None:
-            off = self.off_dst.cpu().numpy().astype(np.int64)
-            deg = off[1:] - off[:-1] if self.n else np.zeros(0, np.int64)
+            if deg is None:
+                off = self.off_dst.cpu().numpy().astype(np.int64)
+                deg = off[1:] - off[:-1] if self.n else np.zeros(0, np.int64)
             po = self.policy
             light, heavy = schedule_lists(deg, po.heavy_threshold, po.wave_items, po.xcd_items and po.wave_items,
                                           po.xcds, self.xcd_chunk)

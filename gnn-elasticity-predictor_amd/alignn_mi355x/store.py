@@ -165,6 +165,9 @@ class GraphStore:
         self._configure_nodes(use_mat2vec, force_node_dim)
         self._x_stats = None   # device (mean, std) over node_dim columns, identity where a block has none
         self._g_stats = None   # device (mean, std) over the global scalars
+        # every stored graph's index fields point inside the graph (checked once here): batches collated
+        # from the store then need no per-batch index validation (engine.prepare_batch skips its syncs)
+        self.indices_checked = self._index_ranges_ok()
 
     # -------------------------------------------------------------------------------- capacity
     def field_kind(self, f: str) -> str:
@@ -181,6 +184,42 @@ class GraphStore:
             if ref in self.counts and np.array_equal(c, self.counts[ref]):
                 return kind
         raise ValueError(f"field {f!r}: rows per graph follow neither atoms, bonds, triplets nor a constant")
+
+    # index field -> the field whose rows it indexes (per graph: 0 <= index < that field's row count)
+    INDEXED = {"edge_index": "x", "lg_edge_index": "edge_index"}
+
+    def _index_ranges_ok(self) -> bool:
+        """True when every index field is one of INDEXED and every stored graph's indices lie in
+        [0, rows of the indexed field) — one pass per field on the stored arrays."""
+        for f, m in self.meta.items():
+            if m["kind"] != "index":
+                continue
+            ref = self.INDEXED.get(f)
+            if ref is None or ref not in self.counts:
+                return False
+            a = self.arrays[f]
+            cnt = self.counts[f]
+            if a.numel() == 0:
+                continue
+            lim = self.counts[ref]   # rows (atoms) or index entries (bonds) per graph
+            if a.device.type == "cuda":
+                c = torch.from_numpy(cnt).to(a.device)
+                lo = torch.segment_reduce(a.min(0).values.double(), "min", lengths=c, unsafe=True)
+                hi = torch.segment_reduce(a.max(0).values.double(), "max", lengths=c, unsafe=True)
+                lo, hi = lo.cpu().numpy(), hi.cpu().numpy()
+            else:
+                v = a.numpy()
+                st = _excl_cumsum(cnt)
+                nz = cnt > 0
+                lo = np.zeros(len(cnt))
+                hi = np.zeros(len(cnt))
+                if nz.any():
+                    lo[nz] = np.minimum.reduceat(v.min(0), st[nz])
+                    hi[nz] = np.maximum.reduceat(v.max(0), st[nz])
+            nz = cnt > 0
+            if np.any(lo[nz] < 0) or np.any(hi[nz] >= lim[nz]):
+                return False
+        return True
 
     def _lg_spans(self) -> np.ndarray:
         """Per stored graph: [lo, hi] of its local line-graph endpoint ids (the bonds it touches lie
@@ -533,6 +572,7 @@ class GraphStore:
         _lib.check(lib.alignn_collate_batchvec(len(pl.nodes), node_dst.data_ptr(), nodes.data_ptr(),
                                                int(pl.nodes.max()), batch.data_ptr(), s), "alignn_collate_batchvec")
         b.batch = batch
+        b._alignn_trusted = self.indices_checked   # index ranges checked at build (no per-batch sync)
         b.ptr = ptr.clone()
         b.sample_index = sample_index.clone()   # train.py:171 (dataset indices of the batch's graphs)
         b.num_graphs = G

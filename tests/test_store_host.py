@@ -58,3 +58,20 @@ def test_plan_rejects_bad_indices():
         st.plan([])
     with pytest.raises(ValueError):
         st.plan([0], lg_offset="bogus")
+
+
+def test_index_ranges_checked_once_at_build():
+    """GraphStore checks every stored graph's edge_index / lg_edge_index against its own atom / bond
+    counts once (so collated batches skip the per-batch check); a graph pointing outside itself
+    leaves the store unchecked, and batches are then validated as PyG would at use."""
+    from alignn_mi355x.data import Data
+    from alignn_mi355x.store import GraphStore
+    keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
+    gs = [Data(**{k: getattr(g, k) for k in keys}) for g in _graphs(4)]
+    assert GraphStore.from_data_list(gs, "cpu").indices_checked
+    bad = [Data(**{k: getattr(g, k).clone() for k in keys}) for g in _graphs(4)]
+    bad[2].edge_index[1, 3] = bad[2].x.size(0)            # one past the graph's atoms
+    assert not GraphStore.from_data_list(bad, "cpu").indices_checked
+    bad = [Data(**{k: getattr(g, k).clone() for k in keys}) for g in _graphs(4)]
+    bad[1].lg_edge_index[0, 0] = bad[1].edge_index.size(1)   # one past the graph's bonds
+    assert not GraphStore.from_data_list(bad, "cpu").indices_checked
