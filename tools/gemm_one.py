@@ -1,8 +1,7 @@
-"""One GEMM shape launched back to back (for rocprofv3 --pmc / --kernel-trace on a single kernel).
+"""One GEMM shape issued R times (for per-launch PMC traffic of a single product, e.g. config C3's
+dominant bf16 product over every bond: C[184320, 256] = A[184320, 256] . W^T).
 
-usage: python tools/gemm_one.py M N K [--layout nt|nn|tn|tt] [--batch B] [--reps R] [--tile T] [--split S]
-Layout letters: A stored [M,K] ('n') or [K,M] ('t'); B stored [K,N] ('n') or [N,K] ('t').
-Prints the median device time per call (HIP events over the reps).
+usage: python tools/gemm_one.py --M 184320 --N 256 --K 256 [--bf16] [--reps 10]
 """
 import argparse
 import os
@@ -16,39 +15,24 @@ from alignn_mi355x import ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("M", type=int)
-    ap.add_argument("N", type=int)
-    ap.add_argument("K", type=int)
-    ap.add_argument("--layout", default="nt")
-    ap.add_argument("--batch", type=int, default=1)
-    ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--tile", type=int, default=0)
-    ap.add_argument("--split", type=int, default=None)
-    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--M", type=int, default=184320)
+    ap.add_argument("--N", type=int, default=256)
+    ap.add_argument("--K", type=int, default=256)
+    ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
-    g = torch.Generator(device="cpu").manual_seed(0)
-    bt = (a.batch,) if a.batch > 1 else ()
-    A = torch.randn(*bt, a.M, a.K, generator=g).cuda()
-    B = torch.randn(*bt, a.K, a.N, generator=g).cuda()
-    Av = A if a.layout[0] == "n" else A.transpose(-1, -2).contiguous().transpose(-1, -2)
-    Bv = B if a.layout[1] == "n" else B.transpose(-1, -2).contiguous().transpose(-1, -2)
-    C = torch.empty(*bt, a.M, a.N, device="cuda")
-    run = lambda: ops.gemm(Av, Bv, C, tile=a.tile, split_k=a.split)  # noqa: E731
-    run()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    A = torch.randn(a.M, a.K, device="cuda", generator=g)
+    W = torch.randn(a.N, a.K, device="cuda", generator=g)
+    b = torch.randn(a.N, device="cuda", generator=g)
+    C = torch.empty(a.M, a.N, device="cuda")
+    tile = ops.GEMM_BF16 if a.bf16 else 0
+    path = ops.gemm(A, W.t(), C, bias=b, tile=tile, path_only=True)
+    for _ in range(a.reps):
+        ops.gemm(A, W.t(), C, bias=b, tile=tile)
     torch.cuda.synchronize()
-    if a.check:
-        ref = A.double() @ B.double()
-        print("rel err", float((C.double() - ref).abs().max() / ref.abs().max()))
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
-    for e0, e1 in ev:
-        e0.record()
-        run()
-        e1.record()
-    torch.cuda.synchronize()
-    ts = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in ev)
-    t = ts[len(ts) // 2]
-    fl = 2.0 * a.M * a.N * a.K * a.batch
-    print(f"M{a.M} N{a.N} K{a.K} b{a.batch} {a.layout}: {t:.1f} us  {fl / t / 1e6:.1f} TF/s (min {ts[0]:.1f})")
+    print(f"gemm M{a.M} N{a.N} K{a.K} {'bf16' if a.bf16 else 'fp32'}: path {path} ({'bf16 streaming' if path == 1 else 'tiled'}), "
+          f"{a.reps} launches; algorithmic bytes per launch {4 * (a.M * a.K + a.N * a.K + a.M * a.N) / 1e6:.1f} MB")
 
 
 if __name__ == "__main__":
