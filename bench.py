@@ -318,9 +318,16 @@ def pmc_traffic(kernel_key):
 
 
 def _roofline(summ, dominant, mfma_peak, probe_src):
+    """The dominant kernel against the roof that binds it: a GEMM is MFMA-bound when its arithmetic
+    intensity (algorithmic flops / bytes: A, B and C once) times the HBM peak exceeds the matrix-core
+    peak, HBM-bound otherwise (the bf16 products over every bond: 64 flop/B x 8 TB/s < 2.5 PF/s);
+    the attention kernels are HBM-bound."""
     s = summ[dominant]
     avg_s = s["avg_ms"] / 1e3
-    if s["flops_per_launch"] > 0:
+    flops, nbytes = s["flops_per_launch"], s.get("bytes_per_launch", 0.0)
+    if flops > 0 and nbytes > 0 and flops / nbytes * HBM_PEAK_GBS / 1e3 < mfma_peak:
+        flops = 0.0   # below the ridge point: report it against HBM
+    if flops > 0:
         ach = s["flops_per_launch"] / avg_s / 1e12
         return {"bound": "mfma", "achieved": round(ach, 2), "peak": mfma_peak, "unit": "TFLOP/s",
                 "frac": round(ach / mfma_peak, 4), "traffic": pmc_traffic(dominant), "kernel": dominant,

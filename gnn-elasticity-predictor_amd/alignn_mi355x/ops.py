@@ -422,7 +422,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: Opt
 
 def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
     M, N = X.shape
-    ws = WS.get("colsum", 512 * N, X.device)   # <= 512 row chunks (alignn_colsum_f32)
+    ws = WS.get("colsum", 256 * N, X.device)
     check(_lib.lib().alignn_colsum_f32(X.data_ptr(), M, N, X.stride(0), out.data_ptr(), int(accumulate),
                                        ws.data_ptr(), stream_ptr()), "alignn_colsum_f32")
     return out
@@ -438,7 +438,7 @@ def wcolsum2(X1: torch.Tensor, W1: torch.Tensor, X2: torch.Tensor, W2: torch.Ten
             or X1.stride(1) != 1 or X2.stride(1) != 1 or W1.stride(1) != 1 or W2.stride(1) != 1 or out.numel() != N
             or not out.is_contiguous()):
         raise ValueError("wcolsum2: inconsistent shapes or strides")
-    ws = WS.get("colsum", 512 * N, X1.device)
+    ws = WS.get("colsum", 256 * N, X1.device)
     check(_lib.lib().alignn_wcolsum2_f32(M, N, N // Hh, X1.data_ptr(), X1.stride(0), W1.data_ptr(), W1.stride(0),
                                          X2.data_ptr(), X2.stride(0), W2.data_ptr(), W2.stride(0), out.data_ptr(),
                                          int(accumulate), ws.data_ptr(), stream_ptr()), "alignn_wcolsum2_f32")

@@ -258,6 +258,22 @@ __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (
     }
 }
 
+// Sum of one output element's split-K partials (eight chains, partial s into chain s % 8, combined as
+// a fixed tree).  An in-launch combine by each tile's last workgroup was measured slower than this
+// separate reduce launch (profiles/r02/v9_ab_splitk_combine.log) and removed in round 3.
+__device__ __forceinline__ float splitk_sum(const GemmParams& p, int64_t b, int64_t row, int64_t col) {
+  const int64_t nb = p.reduce_batch ? 1 : p.batch;
+  const int64_t stride = nb * p.M * p.N;
+  const float* w = p.ws + (b * p.M + row) * p.N + col;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 7 < p.split_k; k += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += w[(int64_t)(k + j) * stride];
+  }
+  for (int j = 0; k < p.split_k; ++k, ++j) s[j] += w[(int64_t)k * stride];
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
 
 template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF, bool RB>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
@@ -431,47 +447,14 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
   store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
 }
 
-// Split-K reduction with TPO threads per output element (1..16, from the element count: enough loads
-// in flight for small outputs — a [256, 36] weight gradient over 63 splits, one thread per element,
-// waited on eight dependent load rounds, 48 us at the step's tail).  Thread (j, o) of a block sums
-// splits j, j + TPO, ... of element o in four chains; the TPO partials are combined in j order through
-// LDS.  The order depends only on the shape (deterministic).
-template <int TPO>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
-  constexpr int OPB = 256 / TPO;
-  __shared__ float red[256];
-  const int t = threadIdx.x, j = t / OPB, o = t % OPB;
   const int64_t total = (p.reduce_batch ? 1 : p.batch) * p.M * p.N;
-  for (int64_t base = (int64_t)blockIdx.x * OPB; base < total; base += (int64_t)gridDim.x * OPB) {
-    const int64_t i = base + o;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (i < total) {
-      const float* w = p.ws + i;
-      int k = j;
-      for (; k + 3 * TPO < p.split_k; k += 4 * TPO) {
-        s0 += w[(int64_t)k * total];
-        s1 += w[(int64_t)(k + TPO) * total];
-        s2 += w[(int64_t)(k + 2 * TPO) * total];
-        s3 += w[(int64_t)(k + 3 * TPO) * total];
-      }
-      for (; k < p.split_k; k += TPO) s0 += w[(int64_t)k * total];
-    }
-    float sum = (s0 + s1) + (s2 + s3);
-    if constexpr (TPO > 1) {
-      red[t] = sum;
-      __syncthreads();
-      if (j == 0) {
-#pragma unroll
-        for (int q = 1; q < TPO; ++q) sum += red[q * OPB + o];
-      }
-      __syncthreads();
-    }
-    if (j == 0 && i < total) {
-      const int64_t col = i % p.N;
-      const int64_t row = (i / p.N) % p.M;
-      const int64_t b = i / (p.N * p.M);
-      p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, sum);
-    }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t col = i % p.N;
+    const int64_t row = (i / p.N) % p.M;
+    const int64_t b = i / (p.N * p.M);
+    // eight independent chains (partial k goes to chain k % 8), combined in a fixed tree
+    p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, splitk_sum(p, b, row, col));
   }
 }
 
@@ -950,20 +933,9 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   else dispatch_layout<64, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {
-    // an in-launch combine by each tile's last workgroup was measured slower than this separate
-    // reduce (profiles/r02/v9_ab_splitk_combine.log) and removed in round 3
-    const int64_t total = nbatch_out * a->M * a->N;
-    int tpo = 1;
-    while (tpo < 16 && 2 * tpo <= pl.split && total * tpo < 131072) tpo *= 2;
-    const int64_t opb = 256 / tpo;
-    const unsigned blocks = (unsigned)std::min<int64_t>((total + opb - 1) / opb, 4096);
-    switch (tpo) {
-      case 1: launch(splitk_reduce_kernel<1>, dim3(blocks), dim3(256), 0, s, p); break;
-      case 2: launch(splitk_reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, p); break;
-      case 4: launch(splitk_reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, p); break;
-      case 8: launch(splitk_reduce_kernel<8>, dim3(blocks), dim3(256), 0, s, p); break;
-      default: launch(splitk_reduce_kernel<16>, dim3(blocks), dim3(256), 0, s, p); break;
-    }
+    int64_t total = nbatch_out * a->M * a->N;
+    int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    launch(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");
   }
   return ALIGNN_OK;
@@ -1037,11 +1009,9 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
   if (N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned strips = (unsigned)((N + 63) / 64);
-  // ~8 blocks per CU in stage 1, at least 64 rows per chunk, at most 512 chunks: a thread sums at
-  // most ~16 rows (four rounds of four loads in flight; 45 rows, eleven rounds, took 23 us for the
-  // [23040, 256] bias gradient at the step's tail)
-  int64_t want = std::max<int64_t>(1, 2048 / (int64_t)strips);
-  int nparts = (int)std::min<int64_t>({512, want, std::max<int64_t>(1, (M + 63) / 64)});
+  // ~2 blocks per CU in stage 1, at least 64 rows per chunk, at most 256 chunks
+  int64_t want = std::max<int64_t>(1, 512 / (int64_t)strips);
+  int nparts = (int)std::min<int64_t>({256, want, std::max<int64_t>(1, (M + 63) / 64)});
   int64_t rows_per = (M + nparts - 1) / nparts;
   if (rows_per == 0) rows_per = 1;
   nparts = (int)((M + rows_per - 1) / rows_per);
@@ -1065,9 +1035,9 @@ extern "C" int alignn_wcolsum2_f32(int64_t M, int64_t N, int32_t C, const float*
   if (N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned strips = (unsigned)((N + 63) / 64);
-  // as alignn_colsum_f32: ~8 blocks per CU, >= 64 rows per chunk, <= 512 chunks
-  int64_t want = std::max<int64_t>(1, 2048 / (int64_t)strips);
-  int nparts = (int)std::min<int64_t>({512, want, std::max<int64_t>(1, (M + 63) / 64)});
+  // as alignn_colsum_f32: ~2 blocks per CU, >= 64 rows per chunk, <= 256 chunks
+  int64_t want = std::max<int64_t>(1, 512 / (int64_t)strips);
+  int nparts = (int)std::min<int64_t>({256, want, std::max<int64_t>(1, (M + 63) / 64)});
   int64_t rows_per = std::max<int64_t>(1, (M + nparts - 1) / nparts);
   nparts = (int)std::max<int64_t>(1, (M + rows_per - 1) / rows_per);
   if (M == 0) {

@@ -24,10 +24,9 @@ extern "C" {
 #define ALIGNN_E_HIP -3
 #define ALIGNN_E_WORKSPACE -4
 
-/* Library/version and error introspection.  ABI version 3 (round 3): alignn_tconv_fwd / _bwd_dst /
- * _family lost the edge-encoder argument, AlignnGemmArgs lost `counters`, and the column-sum
- * workspaces grew to 512*N floats. */
-#define ALIGNN_ABI_VERSION 3
+/* Library/version and error introspection.  ABI version 2 (round 3): alignn_tconv_fwd / _bwd_dst /
+ * _family lost the edge-encoder argument, AlignnGemmArgs lost `counters`. */
+#define ALIGNN_ABI_VERSION 2
 int alignn_version(void);
 const char* alignn_last_error(void);
 
@@ -155,7 +154,7 @@ int64_t alignn_enc_bwd_workspace(int32_t D, int32_t kin);
 int alignn_enc_bwd_f32(const AlignnEncBwdArgs* args, void* stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
- * Two-stage, fixed order.  workspace >= 512*N floats. */
+ * Two-stage, fixed order.  workspace >= 256*N floats. */
 int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
                       float* workspace, void* stream);
 
@@ -164,7 +163,7 @@ int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* 
  *   out[j] (+)= sum_r W1[r*lw1 + j/C] X1[r*ld1 + j] + W2[r*lw2 + j/C] X2[r*ld2 + j]
  * The w-bar gradient of a TransformerConv whose edge features pass through a folded Linear
  * (edge_proj, train.py:325/:333; the angle encoder's 2nd Linear, train.py:358-364): per head,
- * sum_n Q_nh sigz_nh + dout_nh sumA_nh.  Two fixed-order stages; workspace >= 512*N floats. */
+ * sum_n Q_nh sigz_nh + dout_nh sumA_nh.  Two fixed-order stages; workspace >= 256*N floats. */
 int alignn_wcolsum2_f32(int64_t M, int64_t N, int32_t C, const float* X1, int64_t ld1, const float* W1, int64_t lw1,
                         const float* X2, int64_t ld2, const float* W2, int64_t lw2, float* out, int32_t accumulate,
                         float* workspace, void* stream);
