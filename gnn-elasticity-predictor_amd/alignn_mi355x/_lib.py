@@ -149,6 +149,7 @@ _SIGNATURES = {
     "alignn_plan_note_timestamp": ([c_vp], c_i32),
     "alignn_plan_elapsed_ms": ([c_vp, c_i32, c_i32, c_vp], c_i32),
     "alignn_plan_check_ptrs": ([c_vp, c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
+    "alignn_plan_refs": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
     "alignn_stream_create": ([c_i32, ctypes.POINTER(c_vp)], c_i32),
     "alignn_stream_destroy": ([c_vp], c_i32),

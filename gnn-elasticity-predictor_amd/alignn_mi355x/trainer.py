@@ -182,7 +182,11 @@ class FusedTrainer:
                 return False
             pairs = [(getattr(slot, k), getattr(batch, k)) for k in BATCH_FIELDS
                      if getattr(batch, k, None) is not None and getattr(batch, k).numel()]
-            ops.copy_many(pairs + bc_new.copy_pairs(bc_slot))   # one launch for the batch and its cache
+            pairs += bc_new.copy_pairs(bc_slot)
+            used = self._graph[5]   # data_ptr of every captured buffer the plans touch (None: all)
+            if used is not None:
+                pairs = [(d, s) for d, s in pairs if d.data_ptr() in used]
+            ops.copy_many(pairs)   # one launch for the batch and its cache
         self.rebinds += 1
         return True
 
@@ -289,8 +293,16 @@ class FusedTrainer:
             for pl in plans:
                 _lib.lib().alignn_plan_destroy(pl)
             raise
-        self._graph = (graphs[0], graphs[-1], batch, plans if keep else None, graphs)
+        self._graph = (graphs[0], graphs[-1], batch, plans if keep else None, graphs,
+                       _plan_refs(plans, self._rebind_targets(batch)) if keep else None)
         self.ctx.freeze()   # the plans hold the workspaces' addresses: eager steps may not replace them
+
+    @staticmethod
+    def _rebind_targets(batch):
+        """The captured batch's buffers a re-binding copy may write: its fields and its device cache."""
+        ts = [getattr(batch, k) for k in BATCH_FIELDS if getattr(batch, k, None) is not None]
+        ts += [t for t in batch_cache(batch).device_tensors() if t is not None]
+        return [t for t in ts if t.numel()]
 
     def _held_ranges(self, batch, pool_id):
         """[lo, hi) device byte ranges this trainer holds for as long as a captured plan lives: its own
@@ -389,6 +401,20 @@ def _record_plan(fn) -> int:
         check(-1, "alignn_plan_end")
     profiling.bind_plan(plan)
     return plan
+
+
+def _plan_refs(plans, tensors) -> set:
+    """data_ptr of each tensor some recorded plan points into (alignn_plan_refs over all phases):
+    a re-bound batch is copied into these buffers only — the raw line-graph index and angle
+    features, for instance, are read when the batch's cache is built, never by the step."""
+    arr = (ctypes.c_uint64 * (2 * len(tensors)))(*[v for t in tensors
+                                                    for v in (t.data_ptr(), t.data_ptr() + t.numel() * t.element_size())])
+    used = set()
+    for pl in plans:
+        hit = (ctypes.c_int32 * len(tensors))()
+        check(_lib.lib().alignn_plan_refs(pl, arr, len(tensors), hit), "alignn_plan_refs")
+        used.update(t.data_ptr() for t, h in zip(tensors, hit) if h)
+    return used
 
 
 def plan_info(plan) -> dict:

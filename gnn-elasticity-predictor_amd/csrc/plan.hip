@@ -290,6 +290,40 @@ extern "C" int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, 
   return ALIGNN_OK;
 }
 
+// Which of n caller ranges [lo, hi) the recorded plan reads or writes through any pointer argument
+// or struct-argument word: hit[i] = 1 if some such value lies in range i (a struct word that only
+// looks like an address marks a range too — harmless, the caller then copies one buffer more).
+// trainer._rebind copies a new batch only into the captured batch's buffers a plan touches.
+extern "C" int alignn_plan_refs(const void* plan, const uint64_t* ranges, int64_t n, int32_t* hit) {
+  const Plan* p = reinterpret_cast<const Plan*>(plan);
+  if (!p || n < 0 || (n > 0 && (!ranges || !hit))) return ALIGNN_E_BAD_SHAPE;
+  auto mark = [&](uint64_t v) {
+    if (!v) return;
+    for (int64_t i = 0; i < n; ++i)
+      if (v >= ranges[2 * i] && v < ranges[2 * i + 1]) hit[i] = 1;
+  };
+  for (int64_t i = 0; i < n; ++i) hit[i] = 0;
+  for (const PlanEntry& e : p->entries) {
+    if (!e.func) continue;
+    for (size_t a = 0; a < e.nargs; ++a) {
+      const size_t j = e.arg0 + a;
+      const unsigned char* b = p->args.data() + p->arg_off[j];
+      if (p->arg_kind[j] == 1) {
+        uint64_t v;
+        std::memcpy(&v, b, sizeof v);
+        mark(v);
+      } else if (p->arg_kind[j] == 2) {
+        for (size_t o = 0; o + 8 <= p->arg_size[j]; o += 8) {
+          uint64_t v;
+          std::memcpy(&v, b + o, sizeof v);
+          mark(v);
+        }
+      }
+    }
+  }
+  return ALIGNN_OK;
+}
+
 // Device time between two timestamps of the last replay (call after it has completed).
 extern "C" int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms) {
   Plan* p = reinterpret_cast<Plan*>(plan);

@@ -524,6 +524,10 @@ int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms);
  * refuses such a plan).  Recording state and the registered step seed are per host thread. */
 int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, int64_t n, uint64_t* bad_value,
                            int64_t* bad_launch, int64_t* checked);
+/* alignn_plan_refs(plan, ranges, n, hit): hit[i] = 1 when some pointer argument or struct-argument
+ * word of the recorded plan lies in [ranges[2i], ranges[2i+1]), else 0 (trainer._rebind copies a new
+ * batch only into the captured batch's buffers the plans touch). */
+int alignn_plan_refs(const void* plan, const uint64_t* ranges, int64_t n, int32_t* hit);
 int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other);
 /* A non-blocking HIP stream of the library's own at `priority` (an execution context's side / aux
  * streams: never one of torch's pooled streams, which may coincide with a capture or loader stream);

@@ -116,11 +116,27 @@ def test_colsum():
     assert _rel(out, X.double().sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("n,m", [(7, 19), (1000, 20000), (50, 0), (5, 1)])
-def test_graph_prep_bit_exact(n, m):
+def _edges(n, m, layout, g):
+    """[src; dst] lists whose keys repeat within a wave in different ways (the CSR build groups each
+    wave's lanes by key): random; a few targets interleaved (as a line graph's sources repeat in
+    target order); runs of one target whose sources come in runs of 8; one key throughout."""
+    if layout == "random":
+        return torch.randint(0, n, (2, m), generator=g)
+    i = torch.arange(m)
+    if layout == "interleaved":
+        return torch.stack([torch.randint(0, n, (m,), generator=g), (i % 12 + 12 * (i // 1200)) % n])
+    if layout == "runs":
+        return torch.stack([((i % 97) // 8 + 13 * (i // 97)) % n, (i // 97) % n])
+    return torch.stack([torch.full((m,), n // 3), torch.full((m,), n // 2)])
+
+
+@pytest.mark.parametrize("n,m,layout", [(7, 19, "random"), (1000, 20000, "random"), (50, 0, "random"),
+                                        (5, 1, "random"), (2580, 253440, "interleaved"), (2580, 253440, "runs"),
+                                        (300, 2000, "constant")])
+def test_graph_prep_bit_exact(n, m, layout):
     ops = _ops()
     g = torch.Generator().manual_seed(n + m)
-    ei = torch.randint(0, n, (2, m), generator=g)
+    ei = _edges(n, m, layout, g)
     csr = ops.GraphCSR(ei.to(DEV), n)
     torch.cuda.synchronize()
     csr.check_indices("test")
@@ -140,6 +156,12 @@ def test_graph_prep_bit_exact(n, m):
 def test_graph_prep_flags_out_of_range():
     ops = _ops()
     ei = torch.tensor([[0, 1, 5], [1, 2, 0]], device=DEV)
+    csr = ops.GraphCSR(ei, 3)
+    with pytest.raises(IndexError):
+        csr.check_indices("edge_index")
+    # an out-of-range key among lanes that share one in-range key
+    ei = torch.stack([torch.zeros(200, dtype=torch.int64), torch.full((200,), 2)]).to(DEV)
+    ei[1, 77] = 3
     csr = ops.GraphCSR(ei, 3)
     with pytest.raises(IndexError):
         csr.check_indices("edge_index")
