@@ -138,6 +138,7 @@ _SIGNATURES = {
                                    c_i64, c_vp], c_i32),
     "alignn_enc_bwd_workspace": ([c_i32, c_i32], c_i64),
     "alignn_enc_bwd_f32": ([ctypes.POINTER(EncBwdArgs), c_vp], c_i32),
+    "alignn_enc_bwd_bf16": ([ctypes.POINTER(EncBwdArgs), c_vp, c_i64, c_vp], c_i32),
     "alignn_gate_ln_bwd_workspace": ([c_i64, c_i32], c_i64),
     "alignn_plan_begin": ([c_vp], c_i32),
     "alignn_plan_note_wait": ([c_vp, c_vp], c_i32),

@@ -200,6 +200,168 @@ __global__ __launch_bounds__(1024) void enc_bwd_stage2(const float* __restrict__
   *dst = accumulate ? *dst + t : t;
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 storage (config C3, the reference's autocast, train.py:628-636): the same gradient on the
+// matrix cores.  Under autocast the hidden layer f = relu(W1 x + b1) is a bf16 Linear output, its
+// gradient reaches it through bf16 Linear backwards, ReLU's backward reads its own (bf16) output, and
+// dW1 = dpre^T x is a bf16 product with fp32 accumulation.  Per target segment d and chunk of 32
+// target-sorted edges, one wave per 64 feature columns (two 32-column tiles):
+//     G    = [dz | alpha'] (32 edges x 32)  .  [U_d ; Vd_d] (32 x 32 columns)     (2 MFMA 32x32x16)
+//     dpre = G * [f > 0]                     (f: the forward's bf16 hidden layer rows)
+//     Z   += dpre^T . [x | 1] (32 columns x 32: kin inputs, a ones column for db1, zeros)  (2 MFMA)
+// The G accumulator is the next product's A operand with no data movement: registers 8s..8s+7,
+// rounded to bf16, are k-step s of dpre^T, whose k (edge) order is 16s + 8(j>>2) + 4h + (j&3) for
+// element j of lane half h — the [x | 1] operand is loaded in that same edge order.  The 32 (layer,
+// head) slots past H*L and the edges past a chunk's end are zeros.  Z partials per workgroup,
+// reduced by enc_bwd_stage2 as in the fp32 kernel (fixed grid and orders: deterministic).  Memory
+// bound: the f rows (T x D bf16) and U/Vd (once per target) dominate; 2.03 M triplets at B = 256
+// take ~30 us of matrix-core time in all.
+typedef float ebx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 ebh8 __attribute__((ext_vector_type(8)));
+typedef uint32_t ebu4 __attribute__((ext_vector_type(4)));
+// v where keep, else +0 — a bit mask, not a select: a select on a loaded value let the compiler sink
+// the load into a branch (a branch and a full wait per element)
+__device__ __forceinline__ float keep_if(float v, bool keep) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & (keep ? 0xffffffffu : 0u));
+}
+// fixed grid of the bf16 kernel: three workgroups per CU of an MI355X (its occupancy), all resident at
+// once — a fourth, queued behind them, doubled the kernel's tail (partials: EBF_BLOCKS rows of the
+// workspace, summed by enc_bwd_stage2 in workgroup order)
+constexpr int EBF_BLOCKS = EB_BLOCKS < 768 ? EB_BLOCKS : 768;
+constexpr int EBF_FP = 256 + 8;   // LDS row of a chunk's hidden-layer rows (bf16), padded
+constexpr int EBF_XP = 17;        // LDS row of a chunk's raw inputs (kin <= 16 floats), padded
+
+// The 32 k slots of the G product: k-step s (0: dz and U, 1: alpha' and Vd), element j of lane half hh
+// is (layer j / (H/2), head hh (H/2) + j % (H/2)) — the layer depends on j only, so every per-layer
+// pointer is wave-uniform (a per-lane choice of table entry compiled to vector loads of the table and
+// a wait before every use).  Layers >= L: zeros (their table entries repeat layer 0, enc_bwd_params).
+template <int H>
+struct EbSlot {
+  static constexpr int JPL = H / 2;   // j values per layer
+  static __device__ __forceinline__ int layer(int j) { return j / JPL; }
+  static __device__ __forceinline__ int head(int hh, int j) { return hh * JPL + j % JPL; }
+};
+
+template <int H>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))  // 166 VGPRs: 3 waves/SIMD
+void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64_t ldf) {
+  constexpr int D = 256;
+  __shared__ __attribute__((aligned(16))) uint16_t fs[32 * EBF_FP];   // the chunk's f rows
+  __shared__ float xs[32 * EBF_XP];                                     // the chunk's raw inputs
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int kin = p.kin;
+  ebx16 Z[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Z[ct][i] = 0.f;
+  for (int64_t d = blockIdx.x; d < p.n; d += gridDim.x) {
+    const int64_t t0 = p.off_dst[d], t1 = p.off_dst[d + 1];
+    if (t0 == t1) continue;
+    // B operands of G: slot q = 8 hh + j of k-step s (0: U, 1: Vd), column 64 w + 32 ct + r
+    ebh8 PB[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = EbSlot<H>::layer(j);
+        const float* base = (s ? p.Vd : p.U)[l < EB_LMAX ? l : 0];
+        const bool ok = l < p.L;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {   // unconditional load (every table entry is a valid layer)
+          const float v = base[(d * H + EbSlot<H>::head(hh, j)) * D + 64 * w + 32 * ct + r];
+          PB[ct][s][j] = (__bf16)keep_if(v, ok);
+        }
+      }
+    for (int64_t tc = t0; tc < t1; tc += 32) {
+      const int ne = (int)min<int64_t>(32, t1 - tc);
+      // stage the chunk's f rows (32 x 256 bf16: four 16-byte loads per thread, rows past the chunk
+      // read a valid row and are never used) and raw inputs
+      ebu4 fv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = threadIdx.x + 256 * u, e = i >> 5, c8 = (i & 31) * 8;
+        fv[u] = *reinterpret_cast<const ebu4*>(F16 + (tc + min(e, ne - 1)) * ldf + c8);
+      }
+      float xv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = threadIdx.x + 256 * u, e = i >> 4, k = i & 15;
+        const float v = p.x[(tc + min(e, ne - 1)) * p.ldx + min(k, kin - 1)];   // unconditional load
+        xv[u] = keep_if(v, e < ne && k < kin);
+      }
+      // A operand of G: [dz | alpha'] of edge tc + r, slot 8 hh + j (k-step 0: dz, 1: alpha')
+      const bool ev = r < ne;
+      const int64_t te = tc + (ev ? r : 0);
+      float sv[2][8];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int l = EbSlot<H>::layer(j);
+          sv[s][j] = (s ? p.al : p.dz)[l < EB_LMAX ? l : 0][te * H + EbSlot<H>::head(hh, j)];
+        }
+      __syncthreads();   // the previous chunk's LDS readers are done
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = threadIdx.x + 256 * u, e = i >> 5, c8 = (i & 31) * 8;
+        *reinterpret_cast<ebu4*>(fs + e * EBF_FP + c8) = fv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = threadIdx.x + 256 * u;
+        xs[(i >> 4) * EBF_XP + (i & 15)] = xv[u];
+      }
+      __syncthreads();
+      ebh8 SA[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) SA[s][j] = (__bf16)keep_if(sv[s][j], ev && EbSlot<H>::layer(j) < p.L);
+      // B operand of Z: [x | 1 | 0] of edge 16 s + 8 (j>>2) + 4 hh + (j&3), input column r
+      ebh8 XB[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int e = 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
+          const float v = xs[e * EBF_XP + (r & 15)];   // unconditional read
+          const float one = (r == kin && e < ne) ? 1.f : 0.f;
+          XB[s][j] = (__bf16)(keep_if(v, r < kin) + one);
+        }
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        ebx16 G;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) G[i] = 0.f;
+        G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(SA[0], PB[ct][0], G, 0, 0, 0);
+        G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(SA[1], PB[ct][1], G, 0, 0, 0);
+        // ReLU backward from the bf16 output: register i is edge (i&3) + 8(i>>2) + 4 hh of the chunk
+        // (edges past the chunk's end have zero G rows: their [dz | alpha'] rows are zero)
+        const int col = 64 * w + 32 * ct + r;
+        ebh8 GA[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int e = (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const uint32_t fb = fs[e * EBF_FP + col];
+          GA[i >> 3][i & 7] = (__bf16)(__builtin_bit_cast(float, fb << 16) > 0.f ? G[i] : 0.f);
+        }
+        Z[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(GA[0], XB[0], Z[ct], 0, 0, 0);
+        Z[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(GA[1], XB[1], Z[ct], 0, 0, 0);
+      }
+    }
+  }
+  // Z[ct] register i: feature column 64 w + 32 ct + (i&3) + 8(i>>2) + 4 hh, input column r
+  if (r <= kin) {
+    float* part = p.part + (int64_t)blockIdx.x * (kin + 1) * D + (int64_t)r * D;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) part[64 * w + 32 * ct + (i & 3) + 8 * (i >> 2) + 4 * hh] = Z[ct][i];
+  }
+}
+
 }  // namespace alignn
 
 using namespace alignn;
@@ -209,7 +371,34 @@ extern "C" int64_t alignn_enc_bwd_workspace(int32_t D, int32_t kin) {
   return (int64_t)EB_BLOCKS * (kin + 1) * D;
 }
 
-extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
+static int enc_bwd_params(const AlignnEncBwdArgs* a, EncBwdParams& p);
+static int enc_bwd_stage2_launch(const AlignnEncBwdArgs* a, hipStream_t s, int blocks);
+
+extern "C" int alignn_enc_bwd_bf16(const AlignnEncBwdArgs* a, const uint16_t* F16, int64_t ldf, void* stream) {
+  EncBwdParams p;
+  const int rc = enc_bwd_params(a, p);
+  if (rc != ALIGNN_OK) return rc;
+  if (a->D != 256 || a->kin < 1 || a->H < 2 || (a->T > 0 && (!F16 || ldf < a->D || ldf % 8 != 0 || (reinterpret_cast<uintptr_t>(F16) & 15)))) {
+    set_error("enc_bwd_bf16: needs D = 256, H >= 2, kin >= 1 and 16-byte aligned bf16 hidden-layer rows (ldf >= D, "
+              "ldf %% 8 == 0; D=%d kin=%d ldf=%lld)", a->D, a->kin, (long long)ldf);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a->T > 0) {
+    switch (a->H) {
+      case 2: launch(enc_bwd_bf16_kernel<2>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+      case 4: launch(enc_bwd_bf16_kernel<4>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+      default: launch(enc_bwd_bf16_kernel<8>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+    }
+    ALIGNN_LAUNCH_CHECK("enc_bwd_bf16_kernel");
+  } else {
+    const int rc2 = alignn_fill_f32(a->workspace, (int64_t)EBF_BLOCKS * (a->kin + 1) * a->D, 0.f, stream);
+    if (rc2 != ALIGNN_OK) return rc2;
+  }
+  return enc_bwd_stage2_launch(a, s, EBF_BLOCKS);
+}
+
+static int enc_bwd_params(const AlignnEncBwdArgs* a, EncBwdParams& p) {
   if (!a || a->n < 0 || a->T < 0 || a->D <= 0 || a->H <= 0 || a->L < 1 || a->kin < 0) {
     set_error("enc_bwd: bad shape");
     return ALIGNN_E_BAD_SHAPE;
@@ -226,27 +415,41 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
     set_error("enc_bwd: needs %lld workspace floats", (long long)EB_BLOCKS * (a->kin + 1) * a->D);
     return ALIGNN_E_WORKSPACE;
   }
-  EncBwdParams p;
   std::memset(&p, 0, sizeof p);  // defined padding bytes (plan.hip scans recorded struct words)
   p.n = a->n; p.T = a->T; p.D = a->D; p.H = a->H; p.L = a->L; p.kin = a->kin;
   p.off_dst = a->off_dst; p.x = a->x; p.ldx = a->ldx; p.w1 = a->w1; p.b1 = a->b1;
-  for (int l = 0; l < EB_LMAX; ++l) {
-    const bool in = l < a->L;
-    p.U[l] = in ? a->U[l] : nullptr;
-    p.Vd[l] = in ? a->Vd[l] : nullptr;
-    p.dz[l] = in ? a->dz[l] : nullptr;
-    p.al[l] = in ? a->alpha[l] : nullptr;
-    if (in && a->T > 0 && (!p.U[l] || !p.Vd[l] || !p.dz[l] || !p.al[l])) {
-      set_error("enc_bwd: layer %d operand missing", l);
+  for (int l = 0; l < EB_LMAX; ++l) {   // entries past L repeat layer 0 (read, never used)
+    const int li = l < a->L ? l : 0;
+    p.U[l] = a->U[li];
+    p.Vd[l] = a->Vd[li];
+    p.dz[l] = a->dz[li];
+    p.al[l] = a->alpha[li];
+    if (a->T > 0 && (!p.U[l] || !p.Vd[l] || !p.dz[l] || !p.al[l])) {
+      set_error("enc_bwd: layer %d operand missing", li);
       return ALIGNN_E_BAD_SHAPE;
     }
   }
   p.part = a->workspace;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->T > 0 && !a->off_dst) {
     set_error("enc_bwd: off_dst missing");
     return ALIGNN_E_BAD_SHAPE;
   }
+  return ALIGNN_OK;
+}
+
+static int enc_bwd_stage2_launch(const AlignnEncBwdArgs* a, hipStream_t s, int blocks) {
+  const int n = (a->kin + 1) * a->D;
+  launch(enc_bwd_stage2, dim3((n + 63) / 64), dim3(1024), 0, s, a->workspace, blocks, a->D, a->kin,
+                     a->dW1, a->db1, (int)a->accumulate);
+  ALIGNN_LAUNCH_CHECK("enc_bwd_stage2");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
+  EncBwdParams p;
+  const int rc = enc_bwd_params(a, p);
+  if (rc != ALIGNN_OK) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->T > 0) {
     const int km = a->kin <= 8 ? 8 : a->kin <= 12 ? 12 : 16;
 #define EB_LAUNCH_H(KM_)                                                                   \
@@ -266,12 +469,8 @@ extern "C" int alignn_enc_bwd_f32(const AlignnEncBwdArgs* a, void* stream) {
 #undef EB_LAUNCH_H
     ALIGNN_LAUNCH_CHECK("enc_bwd_kernel");
   } else {
-    const int rc = alignn_fill_f32(a->workspace, (int64_t)EB_BLOCKS * (a->kin + 1) * a->D, 0.f, stream);
-    if (rc != ALIGNN_OK) return rc;
+    const int rc2 = alignn_fill_f32(a->workspace, (int64_t)EB_BLOCKS * (a->kin + 1) * a->D, 0.f, stream);
+    if (rc2 != ALIGNN_OK) return rc2;
   }
-  const int n = (a->kin + 1) * a->D;
-  launch(enc_bwd_stage2, dim3((n + 63) / 64), dim3(1024), 0, s, a->workspace, EB_BLOCKS, a->D, a->kin,
-                     a->dW1, a->db1, (int)a->accumulate);
-  ALIGNN_LAUNCH_CHECK("enc_bwd_stage2");
-  return ALIGNN_OK;
+  return enc_bwd_stage2_launch(a, s, EB_BLOCKS);
 }

@@ -152,6 +152,13 @@ typedef struct AlignnEncBwdArgs {
 } AlignnEncBwdArgs;
 int64_t alignn_enc_bwd_workspace(int32_t D, int32_t kin);
 int alignn_enc_bwd_f32(const AlignnEncBwdArgs* args, void* stream);
+/* bf16 storage (config C3, the reference's autocast, train.py:628-636): the same gradients on the
+ * matrix cores with bf16 operands and fp32 accumulation, as autocast runs these Linear backwards —
+ * per target and chunk of 32 edges G = [dz | alpha'] . [U ; Vd], dpre = G * [f > 0] with f the
+ * forward's bf16 hidden layer F16 [T, ldf] itself (ReLU's backward reads its output), and
+ * [dW1^T | db1] (+)= dpre^T . [x | 1].  Needs D = 256 (else ALIGNN_E_UNSUPPORTED); same workspace and
+ * determinism as alignn_enc_bwd_f32. */
+int alignn_enc_bwd_bf16(const AlignnEncBwdArgs* args, const uint16_t* F16, int64_t ldf, void* stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
  * Two-stage, fixed order.  workspace >= 256*N floats. */

@@ -75,6 +75,42 @@ def test_enc_bwd_matches_fp64(n, D, H, L, kin):
     assert torch.equal(dW3, dW1) and torch.equal(db3, db1)
 
 
+@pytest.mark.parametrize("n,H,L,kin", [(40, 4, 4, 11), (25, 8, 2, 16), (30, 2, 8, 1), (17, 2, 3, 7), (9, 4, 2, 11)])
+def test_enc_bwd_bf16_matches_fp64(n, H, L, kin):
+    """bf16 storage (config C3): the matrix-core kernel (alignn_enc_bwd_bf16) against an fp64
+    restatement of its arithmetic — [dz | alpha'], U/Vd, dpre and x rounded to bf16, the ReLU mask
+    from the bf16 hidden layer — and against the fp32 kernel at bf16 tolerance."""
+    from alignn_mi355x import ops
+    D = 256
+    csr, x, W1, b1, U, Vd, dz, al = _case(n, D, H, L, kin, seed=n * 17 + H + L + kin)
+    T = x.size(0)
+    f16 = torch.empty(T, D, dtype=torch.bfloat16, device=DEV)
+    ops.linear_smallk_bf16(x, W1, b1, f16, relu=True)
+    dW1 = torch.full((D, kin), float("nan"), device=DEV)
+    db1 = torch.full((D,), float("nan"), device=DEV)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1, db1, F16=f16)
+    bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    d = csr.dst_at[:T].long()
+    g = torch.zeros(T, D, dtype=torch.float64, device=DEV)
+    for Ul, Vl, zl, al_l in zip(U, Vd, dz, al):
+        g += torch.einsum("th,thd->td", bf(zl[:T]), bf(Ul)[d]) + torch.einsum("th,thd->td", bf(al_l[:T]), bf(Vl)[d])
+    dpre = bf(g.float() * (f16.float() > 0))
+    rW, rb = dpre.t() @ bf(x), dpre.sum(0)
+    nrel = lambda a, b: float((a.double() - b).norm() / b.norm())  # noqa: E731
+    assert nrel(dW1, rW) < 2e-3 and nrel(db1, rb) < 2e-3
+    # the fp32 kernel (exact fp32 products, mask from the recomputed pre-activation) at bf16 tolerance
+    fW, fb = torch.empty_like(dW1), torch.empty_like(db1)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, fW, fb)
+    assert nrel(dW1, fW.double()) < 3e-2 and nrel(db1, fb.double()) < 3e-2
+    # accumulate adds exactly the same partial sums; repeated launches are bitwise equal
+    dW2, db2 = dW1.clone(), db1.clone()
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW2, db2, accumulate=True, F16=f16)
+    assert torch.equal(dW2, dW1 + dW1) and torch.equal(db2, db1 + db1)
+    dW3, db3 = torch.empty_like(dW1), torch.empty_like(db1)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW3, db3, F16=f16)
+    assert torch.equal(dW3, dW1) and torch.equal(db3, db1)
+
+
 def test_enc_bwd_empty_graph_and_rejects_unsupported():
     from alignn_mi355x import ops
     csr = ops.GraphCSR(torch.zeros(2, 0, dtype=torch.int64, device=DEV), 5)
