@@ -614,9 +614,6 @@ class AlignnEngine:
         # step's last branch): +1.8 % (17,697-17,740 -> 18,027-18,051 graphs/s,
         # profiles/r02/v30_ab_enc_bwd_aux_c3.log)
         self.enc_bwd_aux = 1_000_000
-        # bf16 storage: the deferred backward on the matrix cores in bf16, its ReLU mask from the bf16
-        # hidden layer (alignn_enc_bwd_bf16) instead of the fp32 VALU kernel
-        self.enc_bwd_mfma = True
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
@@ -875,12 +872,13 @@ class AlignnEngine:
         # projection chain rules and the angle encoder's first layer: side stream (after the
         # per-layer dM/dw̄ there), overlapping the edge/node encoder backward below
         kept = [t for c in ctx.edge for t in (c.U, *c.edge_scalars)] if defer else []
-        # bf16 storage: the deferred backward runs on the matrix cores and reads the ReLU mask from the
-        # forward's bf16 hidden layer (alignn_enc_bwd_bf16)
-        f16 = (ctx.a if (defer and self.enc_bwd_mfma and ctx.a is not None and ctx.a.dtype == torch.bfloat16
-                         and ctx.a.size(1) == 256 and cfg.heads >= 2) else None)
-        if f16 is not None:
-            kept.append(f16)
+        # bf16 storage: the deferred backward on the matrix cores in bf16, its ReLU mask read from the
+        # forward's bf16 hidden layer (alignn_enc_bwd_bf16; C3 +3.7 %, profiles/r03/v14_*).  fp32 keeps
+        # the VALU kernel: exact fp32 MFMA runs at the VALU rate and measured slower (v15_*)
+        f_rows = (ctx.a if (defer and ctx.a is not None and ctx.a.dtype == torch.bfloat16 and ctx.a.dim() == 2
+                            and ctx.a.size(1) == 256 and cfg.heads % 2 == 0) else None)
+        if f_rows is not None:
+            kept.append(f_rows)
         # the deferred angle-encoder backward (the longest branch of the tail) on a third stream,
         # started as soon as the last line block is done instead of behind the side stream's queue
         use_aux = self.enc_bwd_aux == 1 or (self.enc_bwd_aux > 1 and T >= self.enc_bwd_aux)
@@ -890,7 +888,7 @@ class AlignnEngine:
                 ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
                             [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                             [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
-                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F16=f16)
+                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F=f_rows)
         with _side_work(side, (da, *kept)):
             if E > 0 and L > 0:
                 proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
@@ -902,7 +900,7 @@ class AlignnEngine:
                     ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
                                 [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                                 [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
-                                G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F16=f16)
+                                G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F=f_rows)
             elif ctx.has_angle and da_written:
                 # da is the masked hidden-layer gradient
                 if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLN_MAX:

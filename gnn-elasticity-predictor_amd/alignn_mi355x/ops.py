@@ -511,12 +511,12 @@ def enc_bwd_ok(D: int, H: int, L: int, kin: int) -> bool:
 
 def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, Us, Vds, dzs, alphas,
             dW1: torch.Tensor, db1: torch.Tensor, accumulate: bool = False,
-            F16: Optional[torch.Tensor] = None) -> None:
+            F: Optional[torch.Tensor] = None) -> None:
     """Deferred backward of the angle encoder's first Linear + ReLU over the line graph ``g``:
     dW1/db1 (+)= sum_t dpre_t x_t^T / dpre_t with dpre_t = relu'(W1 x_t + b1) * sum_l,h
-    (dz_l u_l + alpha_l Vd_l) — see include/alignn_hip.h (alignn_enc_bwd_f32).  F16: the forward's
-    bf16 hidden layer [T, D] (bf16 storage, config C3) — the products then run on the matrix cores in
-    bf16 with the ReLU mask read from F16 (alignn_enc_bwd_bf16, D = 256)."""
+    (dz_l u_l + alpha_l Vd_l) — see include/alignn_hip.h (alignn_enc_bwd_f32).  F: the forward's bf16
+    hidden layer [T, 256] (bf16 storage, config C3) — the two products then run on the matrix cores in
+    bf16 with the ReLU mask read from F (alignn_enc_bwd_bf16)."""
     L = len(Us)
     T, kin = x.shape
     D = W1.size(0)
@@ -546,14 +546,14 @@ def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, 
     a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
     # compulsory bytes: x rows, targets, 2LH scalars per edge; U/Vd rows once per target
     nbytes = 4.0 * (T * (kin + 1 + 2 * L * H) + 2 * L * g.n * H * D)
-    if F16 is not None:
-        if (F16.dtype != torch.bfloat16 or F16.dim() != 2 or F16.size(0) < T or F16.size(1) != D or F16.stride(1) != 1
-                or F16.stride(0) % 8 or F16.data_ptr() % 16 or D != 256 or H < 2 or kin < 1):
-            raise ValueError("enc_bwd: F16 must be the bf16 [T, 256] hidden layer, rows 16-byte aligned "
-                             "(and H >= 2, kin >= 1)")
+    if F is not None:
+        if (F.dtype != torch.bfloat16 or F.dim() != 2 or F.size(0) < T or F.size(1) != D or F.stride(1) != 1
+                or F.stride(0) % 8 or F.data_ptr() % 16 or D != 256 or H % 2 or kin < 1):
+            raise ValueError("enc_bwd: F must be the bf16 [T, 256] hidden layer, rows 16-byte aligned "
+                             "(and H even, kin >= 1)")
         nbytes += 2.0 * T * D
         profiling.launch(f"enc_bwd_bf16 T{T} L{L}", 0.0, nbytes,
-                         lambda: check(lib.alignn_enc_bwd_bf16(ctypes.byref(a), F16.data_ptr(), F16.stride(0),
+                         lambda: check(lib.alignn_enc_bwd_bf16(ctypes.byref(a), F.data_ptr(), F.stride(0),
                                                                stream_ptr()), "alignn_enc_bwd_bf16"))
         return
     profiling.launch(f"enc_bwd T{T} L{L}", 0.0, nbytes,

@@ -88,7 +88,7 @@ def test_enc_bwd_bf16_matches_fp64(n, H, L, kin):
     ops.linear_smallk_bf16(x, W1, b1, f16, relu=True)
     dW1 = torch.full((D, kin), float("nan"), device=DEV)
     db1 = torch.full((D,), float("nan"), device=DEV)
-    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1, db1, F16=f16)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1, db1, F=f16)
     bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
     d = csr.dst_at[:T].long()
     g = torch.zeros(T, D, dtype=torch.float64, device=DEV)
@@ -98,16 +98,16 @@ def test_enc_bwd_bf16_matches_fp64(n, H, L, kin):
     rW, rb = dpre.t() @ bf(x), dpre.sum(0)
     nrel = lambda a, b: float((a.double() - b).norm() / b.norm())  # noqa: E731
     assert nrel(dW1, rW) < 2e-3 and nrel(db1, rb) < 2e-3
-    # the fp32 kernel (exact fp32 products, mask from the recomputed pre-activation) at bf16 tolerance
+    # the fp32 VALU kernel (exact fp32 products, mask from the recomputed pre-activation) at bf16 tolerance
     fW, fb = torch.empty_like(dW1), torch.empty_like(db1)
     ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, fW, fb)
     assert nrel(dW1, fW.double()) < 3e-2 and nrel(db1, fb.double()) < 3e-2
     # accumulate adds exactly the same partial sums; repeated launches are bitwise equal
     dW2, db2 = dW1.clone(), db1.clone()
-    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW2, db2, accumulate=True, F16=f16)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW2, db2, accumulate=True, F=f16)
     assert torch.equal(dW2, dW1 + dW1) and torch.equal(db2, db1 + db1)
     dW3, db3 = torch.empty_like(dW1), torch.empty_like(db1)
-    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW3, db3, F16=f16)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW3, db3, F=f16)
     assert torch.equal(dW3, dW1) and torch.equal(db3, db1)
 
 

@@ -15,10 +15,13 @@ def main():
     ap.add_argument("--targets", type=int, default=16020)
     ap.add_argument("--deg", type=int, default=126)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--b32", action="store_true", help="B = 32 size: 2,580 targets x ~98 in-edges")
     a = ap.parse_args()
     from alignn_mi355x import ops
     dev = "cuda"
     g = torch.Generator(device="cpu").manual_seed(0)
+    if a.b32:
+        a.targets, a.deg = 2580, 98
     n, H, L, kin, D = a.targets, 4, 4, 11, 256
     deg = torch.randint(a.deg // 2, a.deg * 3 // 2 + 1, (n,), generator=g)
     dst = torch.repeat_interleave(torch.arange(n), deg)
@@ -37,7 +40,7 @@ def main():
     ops.linear_smallk_bf16(x, W1, b1, f16, relu=True)
     dW1, db1 = torch.empty(D, kin, device=dev), torch.empty(D, device=dev)
     byt = 4.0 * (T * (kin + 1 + 2 * L * H) + 2 * L * n * H * D)
-    for name, kw, extra in (("fp32 valu", {}, 0.0), ("bf16 mfma", {"F16": f16}, 2.0 * T * D)):
+    for name, kw, extra in (("fp32 valu", {}, 0.0), ("bf16 mfma", {"F": f16}, 2.0 * T * D)):
         for _ in range(2):
             ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1, db1, **kw)
         torch.cuda.synchronize()
