@@ -392,8 +392,11 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
 
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
-                  seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False):
+                  seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
+                  skip_early: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
+    skip_early: on a compacted graph with a side stream, the skip projection is queued there before
+    the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
     (no zero-filled [n, D] copy; the backward writes the compacted dout directly).
 
@@ -416,12 +419,17 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
         c.Xa, c.QKV, c.R = X, QKVR[:, :3 * D], QKVR[:, 3 * D:]
     else:
         na = g.n
+        early = skip_early and side is not None
+        c.R = torch.empty(n, D, device=dev)
+        if early:
+            with _side_work(side, (X, c.R)):   # skip projection of all rows, beside Q/K/V and the attention
+                ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
         c.Xa = ops.gather_rows(X, rows)
         c.QKV = torch.empty(na, 3 * D, device=dev)
         ops.gemm(c.Xa, cv.Wqkvr[:3 * D].t(), c.QKV, bias=cv.bqkvr[:3 * D])
-        c.R = torch.empty(n, D, device=dev)
-        with _side_work(side, (X, c.R)):   # skip projection of all rows, concurrent with the attention
-            ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+        if not early:
+            with _side_work(side, (X, c.R)):   # skip projection of all rows, concurrent with the attention
+                ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
     c.U = torch.empty(na, H, D, device=dev)
     ops.gemm(c.QKV[:, :D].view(na, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
     c.outp_a = torch.empty(na, D, device=dev)
@@ -467,7 +475,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
 def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, dF: Optional[torch.Tensor],
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
-                   keep_edge_scalars: bool = False, gate_reduce_side: bool = False) -> None:
+                   keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
+                   wgrad_early: int = 0) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -477,7 +486,10 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     caller joins the side stream before reading those gradients.
     keep_edge_scalars: leave (Vd, dz_e, alpha_e) on ``c.edge_scalars`` for the deferred angle-encoder
     backward (ops.enc_bwd; then dF is None).
-    gate_reduce_side: the gate/LayerNorm parameter-gradient reduction on the side stream."""
+    gate_reduce_side: the gate/LayerNorm parameter-gradient reduction on the side stream.
+    wgrad_early: where the side stream's weight-gradient products are queued — 0: after the dX
+    products; 1: once dQ is final, before the dX products; 2: those final after the target-side
+    kernel (dM, dw̄, the skip projection's) right after it, the rest once dQ is final."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -509,11 +521,15 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     else:
         ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
                           dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att)
+    Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
+    Oh = dout_a.view(na, H, C).permute(1, 2, 0)
+    wg = (cv, gv, c, side, Qh, Oh, Sz, sigz, dout_a, dQKV, dR, dQKVR if rows is None else None, dM, dwbar, H, C, D)
+    early = wgrad_early if side is not None else 0
+    if early >= 2:
+        _weight_grads(*wg, part="a")     # final once the target-side kernel is done
     ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
     if keep_edge_scalars:
         c.edge_scalars = (Vd, dz_e, al_e)
-    Qh = c.QKV[:, :D].view(na, H, C).permute(1, 2, 0)
-    Oh = dout_a.view(na, H, C).permute(1, 2, 0)
     dQv = dQKV[:, :D].view(na, H, C).transpose(0, 1)
     Mt = c.M.view(H, C, D).transpose(1, 2)
     # critical path: dQ (+ its edge-projection terms), then dX
@@ -521,29 +537,44 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0, rowscale=sigz.t(), bias2=c.wbar.view(H, C))
     else:
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0)
+    if early:
+        _weight_grads(*wg, part="b" if early >= 2 else "ab")
     if rows is None:
         ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
     else:
         ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                    # residual + skip projection
         ops.gemm(dQKV, cv.Wqkvr[:3 * D], dX, beta=1.0, c_rows=rows)     # + Q/K/V projections (active rows)
-    # weight gradients: off the critical path
+    if not early:
+        _weight_grads(*wg, part="ab")
+
+
+def _weight_grads(cv, gv, c, side, Qh, Oh, Sz, sigz, dout_a, dQKV, dR, dQKVR, dM, dwbar, H, C, D,
+                  part: str = "ab") -> None:
+    """A conv block's weight-gradient products (dM, dw̄ or dW_edge, dW, db): off the critical path.
+    part "a": those final after the target-side attention backward (dM / dw̄ / dW_edge and, on a
+    compacted graph, the skip projection's dW, db); "b": the rest (the Q/K/V projections' dW, db,
+    which read dQ and dK/dV)."""
+    rows = c.rows
     with _side_work(side, (c.QKV, dout_a, Sz, sigz, c.S, c.sumA, dQKV, dR, c.X, c.Xa)):
-        if c.with_proj:
-            ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
-            ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
-            # dw̄_h = Σ Q_h σz_h + dout_h ΣA_h in one weighted column-sum kernel
-            ops.wcolsum2(c.QKV[:, :D], sigz, dout_a, c.sumA, dwbar)
-        else:
-            ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
-            ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
-        if rows is None:
-            ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
-            ops.colsum(dQKVR, gv.bqkvr)
-        else:
-            ops.gemm(dR.t(), c.X, gv.Wqkvr[3 * D:])
-            ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D])
-            ops.colsum(dR, gv.bqkvr[3 * D:])
-            ops.colsum(dQKV, gv.bqkvr[:3 * D])
+        if "a" in part:
+            if c.with_proj:
+                ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
+                ops.gemm(Oh, c.S.transpose(0, 1), dM.view(H, C, D), beta=1.0)
+                # dw̄_h = Σ Q_h σz_h + dout_h ΣA_h in one weighted column-sum kernel
+                ops.wcolsum2(c.QKV[:, :D], sigz, dout_a, c.sumA, dwbar)
+            else:
+                ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
+                ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
+            if rows is not None:
+                ops.gemm(dR.t(), c.X, gv.Wqkvr[3 * D:])
+                ops.colsum(dR, gv.bqkvr[3 * D:])
+        if "b" in part:
+            if rows is None:
+                ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
+                ops.colsum(dQKVR, gv.bqkvr)
+            else:
+                ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D])
+                ops.colsum(dQKV, gv.bqkvr[:3 * D])
 
 
 class _side_work:
@@ -577,6 +608,8 @@ class _side_work:
 class AlignnEngine:
     """``mode``: 'hetero' -> [B, 2T] = [mean | logvar] (HeteroAlignnRegressor.forward),
     'base' -> [B, T] (AlignnRegressor.forward), 'embed' -> shared [B, D] (embed)."""
+
+    WGRAD_SPLIT_MAX_T = 1_000_000
 
     def __init__(self, cfg: AlignnConfig):
         cfg.validate()
@@ -614,6 +647,17 @@ class AlignnEngine:
         # step's last branch): +1.8 % (17,697-17,740 -> 18,027-18,051 graphs/s,
         # profiles/r02/v30_ab_enc_bwd_aux_c3.log)
         self.enc_bwd_aux = 1_000_000
+        # forward: each line block's skip projection queued on the side stream before its active-row
+        # gather and Q/K/V product (else after them), and the angle encoder's first Linear on the side
+        # stream beside the node/edge encoders (bitwise neutral; with wgrad_early B = 32
+        # 8,788 -> 8,986 graphs/s, profiles/r03/v19_ab_stream_order.log)
+        self.skip_early = True
+        self.angle_side = True
+        # backward: where each block's weight-gradient products are queued on the side stream (see
+        # block_backward: 0 after its dX products, 1 before them, 2 split at the target-side kernel);
+        # -1: 2 below WGRAD_SPLIT_MAX_T line-graph edges, else 1.  B = 32: 0 -> 2 +2.3 % (8,842 ->
+        # 9,043 graphs/s); B = 256 bf16: 2 measured -0.7 %, 1 +0.3 % (v20_ab_wgrad_levels.log)
+        self.wgrad_early = -1
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
@@ -624,6 +668,23 @@ class AlignnEngine:
                 and ops.enc_bwd_ok(D, self.cfg.heads, self.cfg.layers, bc.xa.size(1))):
             return False
         return bc.lg.schedule().n_heavy == 0
+
+    def _angle_hidden(self, P: FlatViews, bc: BatchCache, D: int, dev, a: torch.Tensor) -> None:
+        """a = relu(x_angle W1^T + b1), the angle encoder's hidden layer (its 2nd Linear is folded).
+        bf16 ``a``: config C3 (autocast) — a bf16 Linear output, read by the bf16-storage line-graph
+        attention (its backward is the deferred enc_bwd)."""
+        W1, b1 = P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias")
+        if a.dtype == torch.bfloat16:
+            if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLK_MAX and D % 4 == 0:
+                ops.linear_smallk_bf16(bc.xa, W1, b1, a, relu=True)
+            else:
+                a32 = torch.empty(a.shape, device=dev)
+                ops.gemm(bc.xa, W1.t(), a32, bias=b1, relu=True)
+                ops.cast_bf16(a32, a)
+        elif self.skinny_encoder and ops.linear_smallk_ok(bc.xa, W1, a):
+            ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
+        else:
+            ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -685,6 +746,21 @@ class AlignnEngine:
         ctx.x = x
         edge_attr = batch.edge_attr.contiguous()
         ctx.edge_attr = edge_attr
+        # Angle encoder (train.py:553-554): only its hidden layer is materialised.  Its second Linear
+        # (W2, b2) is folded into every line-graph conv's edge projection, M_l = W_edge,l W2 and
+        # w̄_l = W_edge,l b2 — exact algebra (DESIGN.md §3), so the [T, D] x [D, D] GEMM and its two
+        # backward GEMMs never run.
+        ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
+        side = ops.side_stream(dev) if (self.overlap and self.overlap_forward) else None
+        angle_side = self.angle_side and side is not None and ctx.has_angle
+        if ctx.has_angle:
+            a = torch.empty(T, D, device=dev, dtype=torch.bfloat16 if self._bf16_angle(bc, D) else torch.float32)
+        else:
+            a = ops.zeros(T, D, device=dev)
+        if angle_side:
+            # beside the node/edge encoders; the main stream waits for it before the first line block
+            with _side_work(side, (a,)):
+                self._angle_hidden(P, bc, D, dev, a)
         # encoders (train.py:547-556)
         ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
                                    P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
@@ -693,35 +769,12 @@ class AlignnEngine:
                                        P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
         else:
             ctx.h1e, e = None, ops.zeros(E, D, device=dev)
-        # Angle encoder (train.py:553-554): only its hidden layer is materialised.  Its second Linear
-        # (W2, b2) is folded into every line-graph conv's edge projection, M_l = W_edge,l W2 and
-        # w̄_l = W_edge,l b2 — exact algebra (DESIGN.md §3), so the [T, D] x [D, D] GEMM and its two
-        # backward GEMMs never run.
-        ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
-        a = None
-        if ctx.has_angle:
-            W1, b1 = P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias")
-            if self._bf16_angle(bc, D):
-                # config C3 (autocast): the hidden layer is a bf16 Linear output, stored as bf16 and read
-                # by the bf16-storage line-graph attention (its backward is the deferred enc_bwd)
-                a = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
-                if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLK_MAX and D % 4 == 0:
-                    ops.linear_smallk_bf16(bc.xa, W1, b1, a, relu=True)
-                else:
-                    a32 = torch.empty(T, D, device=dev)
-                    ops.gemm(bc.xa, W1.t(), a32, bias=b1, relu=True)
-                    ops.cast_bf16(a32, a)
-            else:
-                a = torch.empty(T, D, device=dev)
-                if self.skinny_encoder and ops.linear_smallk_ok(bc.xa, W1, a):
-                    ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
-                else:
-                    ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
-        else:
-            a = ops.zeros(T, D, device=dev)
+        if angle_side:
+            ops.stream_wait(torch.cuda.current_stream(dev), side)
+        elif ctx.has_angle:
+            self._angle_hidden(P, bc, D, dev, a)
         ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
-        side = ops.side_stream(dev) if (self.overlap and self.overlap_forward) else None
         if T > 0 and E > 0 and L > 0 and ctx.has_angle:
             W2, b2 = P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias")
             ctx.Ml_all, ctx.wl_all = proj_weights(P.edge_We, W2.expand(L, D, D), b2.expand(L, D))
@@ -732,7 +785,8 @@ class AlignnEngine:
             if T > 0 and E > 0:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
-                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate)
+                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
+                                     skip_early=self.skip_early)
             else:
                 c = None
             ctx.edge.append(c)
@@ -822,6 +876,7 @@ class AlignnEngine:
             dwbar_all = torch.empty(L, D, device=dev)
         line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
         side = ops.side_stream(dev) if self.overlap else None
+        wgrad = self.wgrad_early if self.wgrad_early >= 0 else (2 if T < self.WGRAD_SPLIT_MAX_T else 1)
         if line_proj:
             dMl_all = torch.empty(L, D, D, device=dev)
             dwl_all = torch.empty(L, D, device=dev)
@@ -831,7 +886,8 @@ class AlignnEngine:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
             if c is not None:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               gate_reduce_side=self.gate_reduce_side)
+                               gate_reduce_side=self.gate_reduce_side,
+                                   wgrad_early=wgrad)
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -841,10 +897,12 @@ class AlignnEngine:
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
-                                   keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side)
+                                   keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
+                                   wgrad_early=wgrad)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
-                                   gate_reduce_side=self.gate_reduce_side)
+                                   gate_reduce_side=self.gate_reduce_side,
+                                   wgrad_early=wgrad)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

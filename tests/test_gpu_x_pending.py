@@ -72,13 +72,17 @@ def test_forward_side_stream_is_bitwise_neutral():
     assert torch.equal(tr1.st.grad, tr2.st.grad)
 
 
-@pytest.mark.parametrize("flag", ["enc_bwd_aux", "gate_reduce_side"])
-def test_backward_third_stream_is_bitwise_neutral(flag):
-    """Backward branches off the main stream (the deferred angle-encoder backward on the third
-    stream, the gate/LayerNorm parameter reduction on the side stream) change no bits."""
+@pytest.mark.parametrize("flag,value", [("enc_bwd_aux", 1), ("gate_reduce_side", True), ("skip_early", True),
+                                        ("angle_side", True), ("wgrad_early", 1), ("wgrad_early", 2)])
+def test_backward_third_stream_is_bitwise_neutral(flag, value):
+    """Branches off the main stream (the deferred angle-encoder backward on the third stream, the
+    gate/LayerNorm parameter reduction on the side stream, the skip projection queued before Q/K/V,
+    the angle encoder beside the node/edge encoders, the weight gradients queued before dX) change
+    no bits."""
     _, tr1, b1 = _setup()
     _, tr2, b2 = _setup()
-    setattr(tr2.model._engine, flag, True)
+    setattr(tr1.model._engine, flag, type(value)(0))
+    setattr(tr2.model._engine, flag, value)
     l1 = tr1.forward_backward(b1, 9)
     l2 = tr2.forward_backward(b2, 9)
     torch.cuda.synchronize()

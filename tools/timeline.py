@@ -21,6 +21,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--by-kernel", action="store_true", help="per-queue time by kernel (name, grid) in the step")
+    ap.add_argument("--sequence", action="store_true", help="every kernel of the step in start order")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -73,6 +74,11 @@ def main():
             print(f"queue {q} by kernel:")
             for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top * 2]:
                 print(f"  {t/1e3:8.1f} us  n={c:3d}  {k}")
+    if a.sequence:
+        # every kernel of the step in start order: queue, start and end (us from the step start)
+        print("sequence (queue, start, end, duration us):")
+        for s, e, q, n in ks:
+            print(f"  q{q} {(s - t0)/1e3:8.1f} {(e - t0)/1e3:8.1f} {(e - s)/1e3:7.1f}  {short(n)}")
 
 
 if __name__ == "__main__":
