@@ -104,6 +104,8 @@ _SIGNATURES = {
                                  c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_gate_ln_bwd_partials": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_gate_ln_bwd_partials_add": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_gate_ln_bwd_reduce": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_readout_feats_fwd": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_f32, c_u64, c_vp],
                                  c_i32),
@@ -155,6 +157,7 @@ _SIGNATURES = {
     "alignn_stream_create": ([c_i32, ctypes.POINTER(c_vp)], c_i32),
     "alignn_stream_destroy": ([c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
+    "alignn_add_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_set_i64": ([c_vp, c_i64, c_vp], c_i32),
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,

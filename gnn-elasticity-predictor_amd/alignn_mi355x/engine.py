@@ -476,7 +476,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
-                   wgrad_early: int = 0) -> None:
+                   wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -489,7 +489,9 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     gate_reduce_side: the gate/LayerNorm parameter-gradient reduction on the side stream.
     wgrad_early: where the side stream's weight-gradient products are queued — 0: after the dX
     products; 1: once dQ is final, before the dX products; 2: those final after the target-side
-    kernel (dM, dw̄, the skip projection's) right after it, the rest once dQ is final."""
+    kernel (dM, dw̄, the skip projection's) right after it, the rest once dQ is final.
+    dX_add: a second part of the incoming gradient (the atom block's edge-feature gradient), added
+    to dX by the gate kernel (ops.gate_ln_bwd)."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -505,7 +507,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         dQKV = torch.empty(na, 3 * D, device=dev)
         dR = torch.empty(n, D, device=dev)
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
-                    gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None)
+                    gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None,
+                    dX_add=dX_add)
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
     Vd = torch.empty(na, H, D, device=dev)
     ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
@@ -582,13 +585,14 @@ class _side_work:
     stream (no-op context without a side stream).  The tensors are marked as used by the side
     stream so the caching allocator does not hand their memory to the main stream early."""
 
-    def __init__(self, side: Optional[torch.cuda.Stream], tensors):
-        self.side, self.tensors, self.ctx = side, tensors, None
+    def __init__(self, side: Optional[torch.cuda.Stream], tensors, wait: bool = True):
+        self.side, self.tensors, self.ctx, self.wait = side, tensors, None, wait
 
     def __enter__(self):
         if self.side is None:
             return self
-        ops.stream_wait(self.side, torch.cuda.current_stream(self.side.device))
+        if self.wait:   # else the caller has ordered ``side`` after what the enclosed work reads
+            ops.stream_wait(self.side, torch.cuda.current_stream(self.side.device))
         for t in self.tensors:
             if t is not None:
                 t.record_stream(self.side)
@@ -610,6 +614,12 @@ class AlignnEngine:
     'base' -> [B, T] (AlignnRegressor.forward), 'embed' -> shared [B, D] (embed)."""
 
     WGRAD_SPLIT_MAX_T = 1_000_000
+    ATOM_STREAM_MIN_T = 1_000_000
+
+    def _atom_mode(self, T: int, E: int) -> int:
+        if E <= 0:
+            return 0
+        return self.atom_stream if self.atom_stream >= 0 else (2 if T >= self.ATOM_STREAM_MIN_T else 0)
 
     def __init__(self, cfg: AlignnConfig):
         cfg.validate()
@@ -658,6 +668,15 @@ class AlignnEngine:
         # -1: 2 below WGRAD_SPLIT_MAX_T line-graph edges, else 1.  B = 32: 0 -> 2 +2.3 % (8,842 ->
         # 9,043 graphs/s); B = 256 bf16: 2 measured -0.7 %, 1 +0.3 % (v20_ab_wgrad_levels.log)
         self.wgrad_early = -1
+        # atom-graph blocks (NodeUpdateBlock) beside the line-graph blocks they do not depend on
+        # (forward: atom block l || line block l+1; backward: atom block l-1 || line block l).  0:
+        # inline, their edge-feature gradient accumulated into the bond-state gradient by the
+        # attention kernel; 1: inline, that gradient into a buffer of its own, added by the next line
+        # block's gate kernel (ops.gate_ln_bwd dX_add); 2: as 1 with the atom blocks on the aux stream
+        # (bitwise equal to 1); -1: 2 from ATOM_STREAM_MIN_T line-graph edges on, else 0.  B = 256
+        # bf16: 0 -> 2 +2.6 % (18,963 -> 19,458 graphs/s); B = 32: 2 within noise of 0 (-0.5 %),
+        # 1 -0.6 % (profiles/r03/v21_ab_atom_stream.log)
+        self.atom_stream = -1
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
@@ -780,6 +799,9 @@ class AlignnEngine:
             ctx.Ml_all, ctx.wl_all = proj_weights(P.edge_We, W2.expand(L, D, D), b2.expand(L, D))
         if E > 0 and L > 0:
             ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
+        # atom blocks on the aux stream: atom block l waits for line block l, line block l+1 does not
+        # wait for it (it reads only the bond states); the readout joins the aux stream
+        aux = ops.aux_stream(dev) if (self._atom_mode(T, E) == 2 and side is not None) else None
         for l in range(L):
             # EdgeUpdateBlock (train.py:312-317): line graph, angle embedding in target-sorted order
             if T > 0 and E > 0:
@@ -792,11 +814,14 @@ class AlignnEngine:
             ctx.edge.append(c)
             # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
             if E > 0:
-                h, c = block_forward(P.node[l], h, bc.ag, e, bc.ag.perm_dst, ctx.M_all[l], ctx.wbar_all[l], H,
-                                     p_drop, site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
+                with _side_work(aux, (e, h, ctx.M_all, ctx.wbar_all)):
+                    h, c = block_forward(P.node[l], h, bc.ag, e, bc.ag.perm_dst, ctx.M_all[l], ctx.wbar_all[l], H,
+                                         p_drop, site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
             else:
                 c = None
             ctx.node.append(c)
+        if aux is not None:
+            ops.stream_wait(torch.cuda.current_stream(dev), aux)
         ctx.h = h
         # readout (train.py:562-574)
         gdim = global_x.numel() // max(B, 1)
@@ -880,14 +905,41 @@ class AlignnEngine:
         if line_proj:
             dMl_all = torch.empty(L, D, D, device=dev)
             dwl_all = torch.empty(L, D, device=dev)
-        for l in reversed(range(L)):
+        atom_mode = self._atom_mode(T, E)
+        # atom_stream 1/2: each atom block's edge-feature gradient into a buffer of its own, added to
+        # the bond-state gradient before the line block's backward; 2: the atom blocks on the aux
+        # stream, atom block l-1 beside line block l (it reads only dh and its own forward state)
+        dF_atom = torch.empty(L, E, D, device=dev) if atom_mode else None
+        aux = ops.aux_stream(dev) if (atom_mode == 2 and side is not None) else None
+
+        def atom_bwd(l):
             c = ctx.node[l]
+            if c is None:
+                return
+            if atom_mode:
+                block_backward(P.node[l], G.node[l], c, bc.ag, dh, dF_atom[l], 0, dM_all[l], dwbar_all[l],
+                               side=side, gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad)
+            else:
+                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
+                               gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad)
+
+        if aux is not None and L > 0:
+            with _side_work(aux, (dh, dF_atom, dM_all, dwbar_all)):
+                atom_bwd(L - 1)
+        for l in reversed(range(L)):
             if self.debug is not None:
                 self.debug[f"dh{l + 1}"], self.debug[f"de{l + 1}_pre"] = dh.clone(), de.clone()
-            if c is not None:
-                block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad)
+            if aux is None:
+                atom_bwd(l)
+            else:
+                ops.stream_wait(torch.cuda.current_stream(dev), aux)   # atom block l is done
+                if l > 0:
+                    with _side_work(aux, (), wait=False):   # ordered after atom block l on aux
+                        atom_bwd(l - 1)
+            add = dF_atom[l] if (atom_mode and ctx.node[l] is not None) else None
+            if add is not None and (ctx.edge[l] is None or self.debug is not None):
+                ops.add_(de, add)   # no line block to fold it into (or debug wants de complete here)
+                add = None
             if self.debug is not None:
                 self.debug[f"de{l + 1}"] = de.clone()
             c = ctx.edge[l]
@@ -898,11 +950,11 @@ class AlignnEngine:
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad)
+                                   wgrad_early=wgrad, dX_add=add)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad)
+                                   wgrad_early=wgrad, dX_add=add)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

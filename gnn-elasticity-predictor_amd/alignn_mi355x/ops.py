@@ -258,6 +258,16 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def add_(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """x += y (contiguous fp32, same element count) by a library kernel (alignn_add_f32)."""
+    _require(x, "add_ x")
+    _require(y, "add_ y")
+    if not (x.is_contiguous() and y.is_contiguous()) or x.numel() != y.numel():
+        raise ValueError("add_: contiguous tensors with equal element counts only")
+    check(_lib.lib().alignn_add_f32(x.data_ptr(), y.data_ptr(), x.numel(), stream_ptr()), "alignn_add_f32")
+    return x
+
+
 def zeros(*shape, device) -> torch.Tensor:
     return zero_(torch.empty(*shape, device=device))
 
@@ -907,15 +917,39 @@ def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, see
 
 
 def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_wbeta, d_ln_w, d_ln_b, drop_p, seed,
-                outp_rows=None, reduce_stream: Optional[torch.cuda.Stream] = None):
+                outp_rows=None, reduce_stream: Optional[torch.cuda.Stream] = None,
+                dX_add: Optional[torch.Tensor] = None):
     """outp_rows: as in gate_ln_fwd; dout then has outp's (compacted) rows and only those are written.
     reduce_stream: run the parameter-gradient reduction (d_wbeta, d_ln_w, d_ln_b) there, after the
-    row kernel, off the current stream (nothing on it reads those gradients)."""
+    row kernel, off the current stream (nothing on it reads those gradients).
+    dX_add: [n, D] contiguous addend of the incoming gradient; dXnew += dX_add is written back
+    (alignn_gate_ln_bwd_partials_add)."""
     n, D = R.shape
     rp = _check_outp_rows(outp, outp_rows, n)
     if dout.shape != outp.shape:
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
     wsize = int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D))
+    if dX_add is not None:
+        _require(dX_add, "gate_ln_bwd dX_add")
+        if tuple(dX_add.shape) != (n, D) or not dX_add.is_contiguous():
+            raise ValueError("gate_ln_bwd: dX_add must be a contiguous [n, D] tensor")
+        red = reduce_stream if reduce_stream is not None else torch.cuda.current_stream(outp.device)
+        ws = (current().fresh("gate_ln_red", wsize, outp.device) if reduce_stream is not None
+              else WS.get("gate_ln", wsize, outp.device))
+        check(_lib.lib().alignn_gate_ln_bwd_partials_add(n, D, dXnew.data_ptr(), dXnew.stride(0), dX_add.data_ptr(),
+                                                         outp.data_ptr(), rp, R.data_ptr(), R.stride(0),
+                                                         wbeta.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+                                                         beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),
+                                                         dout.data_ptr(), dR.data_ptr(), dR.stride(0), ws.data_ptr(),
+                                                         float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+              "alignn_gate_ln_bwd_partials_add")
+        if reduce_stream is not None:
+            stream_wait(reduce_stream, torch.cuda.current_stream(outp.device))
+            ws.record_stream(reduce_stream)
+        check(_lib.lib().alignn_gate_ln_bwd_reduce(n, D, ws.data_ptr(), d_wbeta.data_ptr(), d_ln_w.data_ptr(),
+                                                   d_ln_b.data_ptr(), red.cuda_stream),
+              "alignn_gate_ln_bwd_reduce")
+        return
     if reduce_stream is not None:
         ws = current().fresh("gate_ln_red", wsize, outp.device)   # its own buffer: read later on reduce_stream
         check(_lib.lib().alignn_gate_ln_bwd_partials(n, D, dXnew.data_ptr(), dXnew.stride(0), outp.data_ptr(), rp,

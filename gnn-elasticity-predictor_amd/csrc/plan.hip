@@ -109,6 +109,21 @@ __global__ __launch_bounds__(256) void copy_f32_kernel(float* __restrict__ dst, 
     dst[i] = src[i];
 }
 
+// x += y elementwise (one add per element: the atom-graph blocks' edge-feature gradient, produced
+// on their own stream, folded into the bond-state gradient before the line block's backward)
+__global__ __launch_bounds__(256) void add_f32_kernel(float* __restrict__ x, const float* __restrict__ y, int64_t n) {
+  const int64_t n4 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) ? 0 : n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 a = reinterpret_cast<float4*>(x)[i];
+    const float4 b = reinterpret_cast<const float4*>(y)[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    reinterpret_cast<float4*>(x)[i] = a;
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] += y[i];
+}
+
 static unsigned blocks_for(int64_t n) { return (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 255) / 256), 8192); }
 
 }  // namespace alignn
@@ -381,6 +396,14 @@ extern "C" int alignn_copy_f32(float* dst, const float* src, int64_t n, void* st
   launch(copy_f32_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dst,
          src, n);
   ALIGNN_LAUNCH_CHECK("copy_f32_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_add_f32(float* x, const float* y, int64_t n, void* stream) {
+  if (n < 0) return ALIGNN_E_BAD_SHAPE;
+  if (n == 0) return ALIGNN_OK;
+  launch(add_f32_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, y, n);
+  ALIGNN_LAUNCH_CHECK("add_f32_kernel");
   return ALIGNN_OK;
 }
 

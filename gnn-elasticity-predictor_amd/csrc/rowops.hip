@@ -119,6 +119,7 @@ struct GateBwdParams {
   int nwaves, pad2_;
   DropParams drop;
   const int32_t* orow;  // optional: o and dout rows through this map (-1: o = 0, dout not written)
+  const float* dX2;     // optional [n, D] addend: the incoming gradient is dXn + dX2, written back to dXn
 };
 
 template <int VPL>
@@ -147,6 +148,13 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
       if (orow >= 0) vload(p.outp + orow * D + j0, o);
       vload(p.R + row * p.ldr + j0, r);
       vload(p.dXn + row * p.lddx + j0, gx);
+      if (p.dX2) {   // one add per element, the sum kept as the residual's gradient
+        float x2[VPL];
+        vload(p.dX2 + row * D + j0, x2);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) gx[i] += x2[i];
+        vstore(const_cast<float*>(p.dXn) + row * p.lddx + j0, gx);
+      }
     }
     const float b = p.beta[row], mean = p.mu[row], rs = p.rstd[row];
     float yh[VPL], gyh[VPL];
@@ -395,11 +403,12 @@ extern "C" int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D) {
   return std::max<int64_t>(1, std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n)) * 5 * D;
 }
 
-extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
-                                           const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
-                                           const float* ln_w, const float* ln_b, const float* beta, const float* mu,
-                                           const float* rstd, float* dout, float* dR, int64_t lddr, float* workspace,
-                                           float drop_p, uint64_t seed, void* stream) {
+extern "C" int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
+                                               const float* outp, const int32_t* outp_rows, const float* R, int64_t ldr,
+                                               const float* wbeta, const float* ln_w, const float* ln_b,
+                                               const float* beta, const float* mu, const float* rstd, float* dout,
+                                               float* dR, int64_t lddr, float* workspace, float drop_p, uint64_t seed,
+                                               void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_bwd: unsupported hidden %d", D);
@@ -408,7 +417,7 @@ extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dX
   if (n == 0) return ALIGNN_OK;
   const int nwaves = (int)std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n);
   GateBwdParams p{n, D, 0, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
-                  nwaves, 0, make_drop(drop_p, seed), outp_rows};
+                  nwaves, 0, make_drop(drop_p, seed), outp_rows, dX_add};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
   switch (vpl) {
@@ -419,6 +428,15 @@ extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dX
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,
+                                           const int32_t* outp_rows, const float* R, int64_t ldr, const float* wbeta,
+                                           const float* ln_w, const float* ln_b, const float* beta, const float* mu,
+                                           const float* rstd, float* dout, float* dR, int64_t lddr, float* workspace,
+                                           float drop_p, uint64_t seed, void* stream) {
+  return alignn_gate_ln_bwd_partials_add(n, D, const_cast<float*>(dXnew), lddx, nullptr, outp, outp_rows, R, ldr, wbeta,
+                                         ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace, drop_p, seed, stream);
 }
 
 extern "C" int alignn_gate_ln_bwd_reduce(int64_t n, int32_t D, const float* workspace, float* d_wbeta, float* d_ln_w,

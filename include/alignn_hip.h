@@ -351,6 +351,16 @@ int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dXnew, int64_
                                 float drop_p, uint64_t seed, void* stream);
 int alignn_gate_ln_bwd_reduce(int64_t n, int32_t D, const float* workspace, float* d_wbeta, float* d_ln_w,
                               float* d_ln_b, void* stream);
+/* _partials with an addend: the incoming gradient is dXnew + dX_add ([n, D] contiguous, one fp32 add
+ * per element), and that sum is written back to dXnew (it is also the residual's gradient).  The
+ * bond state e feeds both the atom block and the next line block (train.py:570-573): the line
+ * block's backward folds the atom block's edge-feature gradient in here, so the atom block can run
+ * on its own stream (write-only dF) beside the later line block. */
+int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
+                                    const float* outp, const int32_t* outp_rows, const float* R, int64_t ldr,
+                                    const float* wbeta, const float* ln_w, const float* ln_b, const float* beta,
+                                    const float* mu, const float* rstd, float* dout, float* dR, int64_t lddr,
+                                    float* workspace, float drop_p, uint64_t seed, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Readout (train.py:562-586): global_mean_pool over ptr (PyG, train.py:562), concat with
@@ -511,6 +521,9 @@ int alignn_knn_select_weights(const float* G, int64_t ldg, const float* r, int64
  *   that a plan recorded during that capture holds every kernel (other == 0).
  * alignn_fill_f32 / alignn_copy_f32: x[0:n] = value; dst[0:n] = src[0:n] (plan-recordable
  *   replacements for torch's zero_/copy_ inside the step).
+ * alignn_add_f32: x[0:n] += y[0:n], one fp32 add per element (the atom-graph blocks' edge-feature
+ *   gradient folded into the bond-state gradient; replaces the `+=` autograd does where the bond
+ *   state e feeds both the atom block and the next line block, train.py:570-573).
  * alignn_set_i64: x[0] = value on the stream — the per-step device seed written before a plan
  *   replay (the reference draws fresh dropout masks every step, train.py:655).
  * ---------------------------------------------------------------------------------------- */
@@ -543,6 +556,7 @@ int alignn_stream_create(int32_t priority, void** out);
 int alignn_stream_destroy(void* stream);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);
+int alignn_add_f32(float* x, const float* y, int64_t n, void* stream);
 int alignn_set_i64(int64_t* x, int64_t value, void* stream);
 
 #ifdef __cplusplus
