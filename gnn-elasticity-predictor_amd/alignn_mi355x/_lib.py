@@ -158,6 +158,7 @@ _SIGNATURES = {
     "alignn_stream_destroy": ([c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
     "alignn_add_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
+    "alignn_transpose_f32": ([c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
     "alignn_set_i64": ([c_vp, c_i64, c_vp], c_i32),
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,

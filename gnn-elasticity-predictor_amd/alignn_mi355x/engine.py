@@ -57,6 +57,9 @@ class FlatViews:
         self.node_We = self._stack(offs, "node_blocks.{}.conv.lin_edge.weight", (D, D))
         self.node_Wp = self._stack(offs, "node_blocks.{}.edge_proj.weight", (D, D))
         self.node_bp = self._stack(offs, "node_blocks.{}.edge_proj.bias", (D,))
+        # [L, 4D, D] stacks of each conv's [Wq; Wk; Wv; Wskip] block
+        self.edge_Wqkvr = self._stack(offs, "edge_blocks.{}.conv.lin_query.weight", (4 * D, D))
+        self.node_Wqkvr = self._stack(offs, "node_blocks.{}.conv.lin_query.weight", (4 * D, D))
         T = cfg.target_dim
 
         def rows(name, k):
@@ -476,7 +479,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dF_accumulate: int, dM: Optional[torch.Tensor] = None,
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
-                   wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None) -> None:
+                   wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None,
+                   Wt: Optional[torch.Tensor] = None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -491,7 +495,9 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     products; 1: once dQ is final, before the dX products; 2: those final after the target-side
     kernel (dM, dw̄, the skip projection's) right after it, the rest once dQ is final.
     dX_add: a second part of the incoming gradient (the atom block's edge-feature gradient), added
-    to dX by the gate kernel (ops.gate_ln_bwd)."""
+    to dX by the gate kernel (ops.gate_ln_bwd).
+    Wt: [D, 4D] transposed copy of cv.Wqkvr — the dX products then read the weights K-contiguous
+    (bitwise the same products, fewer cycles)."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -542,11 +548,12 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0)
     if early:
         _weight_grads(*wg, part="b" if early >= 2 else "ab")
+    Wb = cv.Wqkvr if Wt is None else Wt.t()   # B operand [4D, D]
     if rows is None:
-        ops.gemm(dQKVR, cv.Wqkvr, dX, beta=1.0)                         # residual + projections
+        ops.gemm(dQKVR, Wb, dX, beta=1.0)                               # residual + projections
     else:
-        ops.gemm(dR, cv.Wqkvr[3 * D:], dX, beta=1.0)                    # residual + skip projection
-        ops.gemm(dQKV, cv.Wqkvr[:3 * D], dX, beta=1.0, c_rows=rows)     # + Q/K/V projections (active rows)
+        ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                          # residual + skip projection
+        ops.gemm(dQKV, Wb[:3 * D], dX, beta=1.0, c_rows=rows)           # + Q/K/V projections (active rows)
     if not early:
         _weight_grads(*wg, part="ab")
 
@@ -677,6 +684,9 @@ class AlignnEngine:
         # bf16: 0 -> 2 +2.6 % (18,963 -> 19,458 graphs/s); B = 32: 2 within noise of 0 (-0.5 %),
         # 1 -0.6 % (profiles/r03/v21_ab_atom_stream.log)
         self.atom_stream = -1
+        # fp32: the backward's dX products read transposed (K-contiguous) copies of the projection
+        # weights, made beside the encoders at the start of the forward
+        self.wt_copies = False
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
@@ -776,10 +786,20 @@ class AlignnEngine:
             a = torch.empty(T, D, device=dev, dtype=torch.bfloat16 if self._bf16_angle(bc, D) else torch.float32)
         else:
             a = ops.zeros(T, D, device=dev)
+        # transposed copies of the conv blocks' projection weights for the backward's dX products
+        wt = self.wt_copies and self.precision == "fp32" and L > 0
+        ctx.Wt_edge = torch.empty(L, D, 4 * D, device=dev) if wt else None
+        ctx.Wt_node = torch.empty(L, D, 4 * D, device=dev) if wt else None
         if angle_side:
             # beside the node/edge encoders; the main stream waits for it before the first line block
-            with _side_work(side, (a,)):
+            with _side_work(side, (a, ctx.Wt_edge, ctx.Wt_node)):
                 self._angle_hidden(P, bc, D, dev, a)
+                if wt:
+                    ops.transpose_(ctx.Wt_edge, P.edge_Wqkvr)
+                    ops.transpose_(ctx.Wt_node, P.node_Wqkvr)
+        elif wt:
+            ops.transpose_(ctx.Wt_edge, P.edge_Wqkvr)
+            ops.transpose_(ctx.Wt_node, P.node_Wqkvr)
         # encoders (train.py:547-556)
         ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
                                    P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
@@ -918,10 +938,12 @@ class AlignnEngine:
                 return
             if atom_mode:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, dF_atom[l], 0, dM_all[l], dwbar_all[l],
-                               side=side, gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad)
+                               side=side, gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad,
+                               Wt=None if ctx.Wt_node is None else ctx.Wt_node[l])
             else:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad)
+                               gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad,
+                               Wt=None if ctx.Wt_node is None else ctx.Wt_node[l])
 
         if aux is not None and L > 0:
             with _side_work(aux, (dh, dF_atom, dM_all, dwbar_all)):
@@ -950,11 +972,13 @@ class AlignnEngine:
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add)
+                                   wgrad_early=wgrad, dX_add=add,
+                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l])
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add)
+                                   wgrad_early=wgrad, dX_add=add,
+                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l])
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

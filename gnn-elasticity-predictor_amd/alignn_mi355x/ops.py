@@ -268,6 +268,20 @@ def add_(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def transpose_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst [nb, C, R] (contiguous) = src [nb, R, C] transposed (src rows unit-stride, any row and
+    batch strides) by a library kernel (alignn_transpose_f32)."""
+    _require(dst, "transpose_ dst")
+    _require(src, "transpose_ src")
+    if src.dim() != 3 or dst.dim() != 3 or src.stride(2) != 1 or not dst.is_contiguous() or \
+            tuple(dst.shape) != (src.size(0), src.size(2), src.size(1)):
+        raise ValueError("transpose_: dst must be a contiguous [nb, C, R] for a row-major src [nb, R, C]")
+    nb, R, C = src.shape
+    check(_lib.lib().alignn_transpose_f32(dst.data_ptr(), src.data_ptr(), nb, R, C, src.stride(1),
+                                          src.stride(0) if nb > 1 else 0, stream_ptr()), "alignn_transpose_f32")
+    return dst
+
+
 def zeros(*shape, device) -> torch.Tensor:
     return zero_(torch.empty(*shape, device=device))
 

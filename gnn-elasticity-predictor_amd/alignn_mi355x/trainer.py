@@ -256,19 +256,25 @@ class FusedTrainer:
         if self.grad_buckets is None:
             phases = [("forward/backward", lambda: self._fb_tail(self._fb_layers(batch, 0)))]
         else:
-            phases = [("forward/backward layers", lambda: state.__setitem__("t", self._fb_layers(batch, 0))),
+            def layers_phase():
+                state["t"] = self._fb_layers(batch, 0)
+                join_forks()
+            phases = [("forward/backward layers", layers_phase),
                       ("backward tail", lambda: self._fb_tail(state["t"]))]
         phases.append(("clip/AdamW", self._clip_and_update))
-        # the per-layer phase leaves weight-gradient work queued on the engine's side stream (joined by
-        # the tail); a graph capture must end with every forked stream joined, so the capture joins them
-        # here — a torch-level wait the launch plan does not record: the replayed plans keep the
-        # overlap, and their stream order is that of the uncaptured step
+        # the per-layer phase leaves weight-gradient work queued on the engine's side stream; a graph
+        # capture must end with every forked stream joined, and the join is part of the recorded plan
+        # too: the next phase's allocations may reuse memory that this work still reads (the capture's
+        # allocator releases cross-stream blocks at the end of each captured phase), so a replay
+        # without the join let the tail overwrite the last blocks' weight-gradient inputs
+        # (test_bucketed_dp_plan_replay_bitwise, intermittent).  The first bucket's exchange, issued
+        # after the phase, still overlaps the tail.
         engine_ctx = self.model._engine.ctx
 
         def join_forks():
             cur = torch.cuda.current_stream(dev)
             for st in list(engine_ctx._side.values()) + list(engine_ctx._aux.values()):
-                cur.wait_stream(st)
+                ops.stream_wait(cur, st)   # a torch wait, noted in the plan being recorded
         graphs = [torch.cuda.CUDAGraph(keep_graph=keep) for _ in phases]
         plans = []
         try:
@@ -279,8 +285,6 @@ class FusedTrainer:
                             plans.append(_record_plan(fn))
                         else:
                             fn()
-                        if len(phases) == 3 and i == 0:
-                            join_forks()
             state.clear()
             torch.cuda.synchronize(dev)
             self._restore(snap)

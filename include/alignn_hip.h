@@ -557,6 +557,11 @@ int alignn_stream_destroy(void* stream);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);
 int alignn_add_f32(float* x, const float* y, int64_t n, void* stream);
+/* alignn_transpose_f32: dst[b][c][r] = src[b][r][c] for b < nb (src rows ld_src apart, batches sb_src
+ * apart; dst contiguous [nb, cols, rows]) — the transposed copies of the conv blocks' projection
+ * weights the backward's dX products read K-contiguous (bitwise the same products). */
+int alignn_transpose_f32(float* dst, const float* src, int64_t nb, int64_t rows, int64_t cols, int64_t ld_src,
+                         int64_t sb_src, void* stream);
 int alignn_set_i64(int64_t* x, int64_t value, void* stream);
 
 #ifdef __cplusplus

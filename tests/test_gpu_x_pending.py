@@ -73,7 +73,8 @@ def test_forward_side_stream_is_bitwise_neutral():
 
 
 @pytest.mark.parametrize("flag,value", [("enc_bwd_aux", 1), ("gate_reduce_side", True), ("skip_early", True),
-                                        ("angle_side", True), ("wgrad_early", 1), ("wgrad_early", 2)])
+                                        ("angle_side", True), ("wgrad_early", 1), ("wgrad_early", 2),
+                                        ("wt_copies", True)])
 def test_backward_third_stream_is_bitwise_neutral(flag, value):
     """Branches off the main stream (the deferred angle-encoder backward on the third stream, the
     gate/LayerNorm parameter reduction on the side stream, the skip projection queued before Q/K/V,
