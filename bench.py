@@ -32,6 +32,7 @@ METRIC = "graphs/sec fwd+bwd (ALIGNN, ~60-atom MP crystals) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
 BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
+PROBE_STEPS = 3            # untimed replays the dominant-kernel ranking sums over
 
 
 def parse():
@@ -363,17 +364,37 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
     def step(i):
         trainer.step(batch, seed=1000003 * rank + i)
 
-    # pick the dominant kernel (untimed eager probe step with events around every launch)
+    # pick the dominant kernel: the probed family (GEMM shape / attention launch) with the largest
+    # total device time summed over PROBE_STEPS untimed steps.  With native plans the probe is a
+    # separate capture whose every probed launch is bracketed by plan timestamps, so the ranking is
+    # taken on the replayed step itself (the concurrency of the timed region and of a rocprofv3 trace
+    # of it), not on an eager step whose overlap differs (round 3: the eager probe flipped between two
+    # GEMM families from run to run).
     dominant, step_work = None, None
     if roofline:
-        step(0)
-        torch.cuda.synchronize()
-        profiling.enable(None)
-        step(1)
-        torch.cuda.synchronize()
-        summ = profiling.summary()
-        profiling.disable()
-        dominant = max(summ, key=lambda k: summ[k]["total_ms"])
+        totals, summ = {}, {}
+        plan_probe = args.launch == "plan"
+        if plan_probe:
+            profiling.enable(None)
+            trainer.capture(batch, mode="plan")
+            profiling.disable()
+        else:
+            step(0)
+            torch.cuda.synchronize()
+        for i in range(PROBE_STEPS):
+            if not plan_probe:
+                profiling.enable(None)
+            step(1 + i)
+            torch.cuda.synchronize()
+            summ = profiling.summary()
+            if not plan_probe:
+                profiling.disable()
+            for k, v in summ.items():
+                totals[k] = totals.get(k, 0.0) + v["total_ms"]
+        if plan_probe:
+            trainer.release_capture()
+        profiling.clear()
+        dominant = max(totals, key=lambda k: (totals[k], k))
         # whole-step algorithmic work of this formulation (one probe step): GEMM flops, attention bytes
         step_work = {"gemm_gflop": sum(v["flops_per_launch"] * v["count"] for v in summ.values()) / 1e9,
                      "tconv_gbyte": sum(v["bytes_per_launch"] * v["count"] for k, v in summ.items()
@@ -381,7 +402,8 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
         if args.dump_probes and rank == 0 and (B, lg_offset, precision) == (args.batch, args.lg_offset,
                                                                              args.precision):
             with open(args.dump_probes, "w") as f:
-                json.dump(dict(sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"])), f, indent=1)
+                json.dump({k: dict(summ[k], total_ms_probe_steps=totals[k]) for k in
+                           sorted(summ, key=lambda k: -totals[k])}, f, indent=1)
 
     # captured step: in a plan the dominant kernel's launches are bracketed by plan timestamps, so
     # every replay re-times them; the timed region's last replay is read back afterwards

@@ -154,6 +154,7 @@ _SIGNATURES = {
     "alignn_plan_check_ptrs": ([c_vp, c_vp, c_i64, c_vp, c_vp, c_vp], c_i32),
     "alignn_plan_refs": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
+    "alignn_plan_check_deps": ([c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_stream_create": ([c_i32, ctypes.POINTER(c_vp)], c_i32),
     "alignn_stream_destroy": ([c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
@@ -165,6 +166,9 @@ _SIGNATURES = {
                           c_vp, c_vp], c_i32),
     "alignn_adamw_f32_dev": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                               c_vp, c_vp], c_i32),
+    "alignn_grad_norm_amp_f32": ([c_vp, c_i64, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "alignn_adamw_amp_f32_dev": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
+                                  c_vp, c_vp, c_i32, c_vp], c_i32),
 }
 
 EXPORTED = tuple(_SIGNATURES.keys())

@@ -254,12 +254,28 @@ class BatchCache:
         active[edge_index[0]] = True
         active[edge_index[1]] = True
         if pad is not None:
-            first = pad["edges"] + pad["kg"]
-            need = pad["active"] - active.sum()
-            j = torch.arange(n, device=edge_index.device) - first
-            active |= (j >= 0) & (j < need)
+            active = cls._fill_active(active, pad["edges"] + pad["kg"], int(pad["active"]))
         return cls._compact(active, edge_index, n, force=pad is not None,
                             na=None if pad is None else int(pad["active"]))
+
+    @staticmethod
+    def _fill_active(active: torch.Tensor, first: int, na: int) -> torch.Tensor:
+        """Marks inactive bonds until ``na`` are active (device arithmetic, no host round trip): the
+        unused ghost bonds (index >= first) first, so the real rows keep their order and positions in
+        every compacted product, then any other inactive bond — a bond without line-graph edges is an
+        empty segment and never a source, so it is inert in the compacted graph.  The batch's real
+        active count is only bounded on the host (store.batch_sizes); taking from every inactive bond
+        keeps exactly ``na`` marked whenever n >= na, so the compaction's fixed-size index list
+        (nonzero_static) is never padded with -1."""
+        n = active.numel()
+        inactive = ~active
+        ghost = torch.arange(n, device=active.device) >= first
+        need = na - active.sum()
+        c1 = inactive & ghost
+        take1 = c1 & (torch.cumsum(c1, 0) <= need)
+        c2 = inactive & ~ghost
+        take2 = c2 & (torch.cumsum(c2, 0) <= need - take1.sum())
+        return active | take1 | take2
 
     @classmethod
     def _compact(cls, active: torch.Tensor, edge_index: torch.Tensor, n: int, force: bool = False,

@@ -1039,16 +1039,46 @@ def grad_norm(g: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _check_scaler(scaler: torch.Tensor) -> None:
+    _require(scaler, "scaler")
+    if scaler.numel() != 4 or not scaler.is_contiguous():
+        raise ValueError("scaler must be a contiguous float32 device tensor [scale, growth_tracker, found_inf, skipped]")
+
+
+def grad_norm_amp(g: torch.Tensor, out: torch.Tensor, scaler: torch.Tensor) -> torch.Tensor:
+    """grad_norm plus GradScaler.unscale_'s found-inf flag in scaler[2] (alignn_grad_norm_amp_f32)."""
+    _require(g, "g")
+    _check_scaler(scaler)
+    ws = WS.get("gnorm", 2048, g.device)
+    check(_lib.lib().alignn_grad_norm_amp_f32(g.data_ptr(), g.numel(), out.data_ptr(), scaler.data_ptr(), ws.data_ptr(),
+                                              stream_ptr()), "alignn_grad_norm_amp_f32")
+    return out
+
+
 def adamw_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, split: int, lr0: float,
                lr1: float, weight_decay: float, betas=(0.9, 0.999), eps: float = 1e-8,
                norm: Optional[torch.Tensor] = None, max_norm: float = 5.0, step: torch.Tensor = None,
-               lr_dev: Optional[torch.Tensor] = None) -> None:
+               lr_dev: Optional[torch.Tensor] = None, scaler: Optional[torch.Tensor] = None,
+               growth_interval: int = 2000) -> None:
     """lr_dev: device float64 [2] = (lr0, lr1) read by the kernel when it runs (lr0/lr1 ignored), so a
-    recorded plan follows learning-rate changes (alignn_adamw_f32_dev)."""
+    recorded plan follows learning-rate changes (alignn_adamw_f32_dev).  scaler (with lr_dev): the
+    GradScaler state of grad_norm_amp — a flagged step is skipped and the scale backs off
+    (alignn_adamw_amp_f32_dev)."""
     for t, n in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _require(t, n)
         if not t.is_contiguous() or t.numel() != p.numel():
             raise ValueError(f"adamw_step: {n} must be contiguous with {p.numel()} elements")
+    if scaler is not None:
+        _check_scaler(scaler)
+        if lr_dev is None:
+            raise ValueError("adamw_step: the GradScaler form reads device learning rates (lr_dev)")
+        _require(lr_dev, "lr_dev", torch.float64)
+        check(_lib.lib().alignn_adamw_amp_f32_dev(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                                                  int(split), lr_dev.data_ptr(), float(weight_decay), float(betas[0]),
+                                                  float(betas[1]), float(eps), _p(norm), float(max_norm),
+                                                  step.data_ptr(), scaler.data_ptr(), int(growth_interval),
+                                                  stream_ptr()), "alignn_adamw_amp_f32_dev")
+        return
     if lr_dev is not None:
         _require(lr_dev, "lr_dev", torch.float64)
         if lr_dev.numel() != 2 or not lr_dev.is_contiguous():

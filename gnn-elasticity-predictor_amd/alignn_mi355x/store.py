@@ -232,6 +232,18 @@ class GraphStore:
             self._spans = torch.stack([lo, hi], 1).cpu().numpy().astype(np.int64)
         return self._spans
 
+    def _lg_bound_ok(self, gids: np.ndarray, lg_offset: str) -> bool:
+        """Stored graphs ``gids`` collated in this order: every collated lg_edge_index entry (local
+        index + PyG increment) is below the batch's bond count.  Implied for lg_offset='num_edges'."""
+        if lg_offset != "num_nodes" or "lg_edge_index" not in self.counts:
+            return True
+        n, e, t = (self.counts[f][gids].astype(np.int64) for f in ("x", "edge_index", "lg_edge_index"))
+        has = t > 0
+        if not has.any():
+            return True
+        hi = (_excl_cumsum(n) + self._lg_spans()[gids][:, 1])[has]
+        return int(hi.max()) < int(e.sum())
+
     def batch_sizes(self, indices, lg_offset: str = "num_nodes") -> Dict[str, int]:
         """Host sizes of a batch: atoms, bonds, triplets, and an upper bound of the line graph's active
         bonds (union of each graph's touched-bond span shifted by its PyG increment)."""
@@ -250,15 +262,16 @@ class GraphStore:
 
     def fits(self, indices, capacity: BatchCapacity, lg_offset: str = "num_nodes") -> Optional[Dict[str, int]]:
         """The ghost plan padding this batch to ``capacity``, or None when it does not fit (then the
-        batch runs uncaptured).  With a compacted capacity the ghost bonds must be able to fill the
-        line graph up to ``capacity.active``: real active bonds + kg <= active <= real active bonds +
-        ghost bonds (real active bonds: the span bound of batch_sizes, exact when every bond has
-        line-graph edges; if the true count is lower the batch's signature misses and it runs eagerly)."""
+        batch runs uncaptured).  With a compacted capacity the batch's active bonds (real ones — at most
+        the span bound of batch_sizes — plus the kg ghost bonds its ghost triplets use) must not
+        exceed ``capacity.active``; the compaction then marks inactive bonds (unused ghost bonds first,
+        then real bonds without line-graph edges: engine.BatchCache._fill_active) until exactly
+        ``capacity.active`` are active, which every batch of ``capacity.edges`` >= that many bonds allows."""
         sz = self.batch_sizes(indices, lg_offset)
         gp = ghost_plan(capacity, len(np.asarray(indices).reshape(-1)), sz["nodes"], sz["edges"], sz["triplets"])
         if gp is None or capacity.active is None:
             return gp
-        if sz["active"] + gp["kg"] > capacity.active or capacity.active - sz["active"] > gp["ge"]:
+        if sz["active"] + gp["kg"] > capacity.active or capacity.active > capacity.edges:
             return None
         return gp
 
@@ -572,7 +585,11 @@ class GraphStore:
         _lib.check(lib.alignn_collate_batchvec(len(pl.nodes), node_dst.data_ptr(), nodes.data_ptr(),
                                                int(pl.nodes.max()), batch.data_ptr(), s), "alignn_collate_batchvec")
         b.batch = batch
-        b._alignn_trusted = self.indices_checked   # index ranges checked at build (no per-batch sync)
+        # index ranges checked at build (no per-batch sync).  Each graph's local indices lie below its
+        # own row counts; the collated line-graph index (+ the PyG increment) must also lie below the
+        # batch's bond count, which lg_offset='num_nodes' does not imply (a graph with fewer bonds than
+        # atoms): checked here on the host from the per-graph spans
+        b._alignn_trusted = self.indices_checked and self._lg_bound_ok(pl.idx, lg_offset)
         b.ptr = ptr.clone()
         b.sample_index = sample_index.clone()   # train.py:171 (dataset indices of the batch's graphs)
         b.num_graphs = G

@@ -32,7 +32,8 @@ class FusedTrainer:
                  feature_jitter_std: float = 0.1, min_logvar_floor: float = MIN_LOGVAR_FLOOR,
                  target_log_means: Sequence[float] = TARGET_LOG_MEANS,
                  target_log_stds: Sequence[float] = TARGET_LOG_STDS, fused_adamw: bool = True,
-                 optimizer: str = "hip", precision: Optional[str] = None):
+                 optimizer: str = "hip", precision: Optional[str] = None, grad_scaler: Optional[bool] = None,
+                 init_scale: float = 65536.0, growth_interval: int = 2000):
         self.model = model
         if precision is not None:
             model.set_precision(precision)
@@ -59,6 +60,16 @@ class FusedTrainer:
             self.exp_avg_sq = torch.zeros_like(st.flat)
             self.hip_step = torch.zeros(1, device=st.flat.device)
             self.gnorm = torch.zeros(1, device=st.flat.device)
+        # GradScaler (train.py:690-695, built at :1475-1476 whenever the reference runs on the GPU,
+        # i.e. with autocast: our bf16 precision): a step with non-finite (scaled) gradients is skipped
+        # and the scale halves; device state [scale, growth_tracker, found_inf, skipped steps]
+        if grad_scaler is None:
+            grad_scaler = model._engine.precision == "bf16"
+        if grad_scaler and optimizer != "hip":
+            raise ValueError("grad_scaler needs optimizer='hip'")
+        self.growth_interval = int(growth_interval)
+        self.scaler = (torch.tensor([float(init_scale), 0.0, 0.0, 0.0], device=st.flat.device) if grad_scaler
+                       else None)
         self.max_norm = max_norm
         self.l2 = log_sigma_l2
         self.jitter = feature_jitter_std
@@ -80,9 +91,16 @@ class FusedTrainer:
         # re-binding (step() on a batch other than the captured one): copy it into the captured
         # batch's buffers and replay when its signature matches (BatchCache.signature), else eager
         self.rebind = True
+        # check mode of the filtered re-binding copy: copy every buffer of the batch and its cache, not
+        # only those alignn_plan_refs finds among the recorded arguments (a test replays both ways and
+        # compares: a recorded kernel reaching batch memory some other way would show up there)
+        self.rebind_copy_all = False
         self.rebinds = 0
         self.rebind_misses = 0
+        self.replays = 0
         self.lr_dev = None
+        self._wbuf = None      # a weighted capture's per-graph weights (device [real graphs])
+        self._exchange = ("none", None)   # the gradient exchange the captured phases were cut for
 
     def use_step_seed(self, t: Optional[torch.Tensor]) -> None:
         """Device int64[1] step seed the dropout/jitter kernels of this trainer mix in (None: host
@@ -150,8 +168,16 @@ class FusedTrainer:
         if seed is None:
             seed = int(torch.randint(0, 2**62, (1,)).item())
         adopt(batch)   # a loader-prepared batch: wait for it and mark its buffers as used here (any path)
-        if self._graph is not None and sample_weights is None:
-            if self._graph[2] is batch or (self.rebind and self._rebind(batch)):
+        if self._graph is not None and self._weights_match(sample_weights):
+            # a weighted capture (KNN weights, train.py:660-674) reads the per-graph weights from its
+            # own device buffer: the step's weights are copied there in the re-binding launch
+            extra = [] if sample_weights is None else [(self._wbuf, sample_weights)]
+            if self._graph[2] is batch:
+                if extra:
+                    with ops.using(self.ctx):
+                        ops.copy_many(extra)
+                return self._replay(seed)
+            if self.rebind and self._rebind(batch, extra):
                 return self._replay(seed)
         loss = self.forward_backward(batch, seed, sample_weights=sample_weights)
         if self.grad_buckets is not None:
@@ -162,7 +188,15 @@ class FusedTrainer:
         self.step_count += 1
         return loss
 
-    def _rebind(self, batch) -> bool:
+    def _weights_match(self, w: Optional[torch.Tensor]) -> bool:
+        """The step's sample weights fit the captured step: none for an unweighted capture; for a
+        weighted one, a float32 device tensor of the captured batch's real-graph count."""
+        if (w is None) != (self._wbuf is None):
+            return False
+        return w is None or (w.dtype == torch.float32 and w.is_cuda and w.shape == self._wbuf.shape
+                             and w.device == self._wbuf.device)
+
+    def _rebind(self, batch, extra=()) -> bool:
         """Copies ``batch`` into the captured batch's buffers (fields and device cache) when every
         size the recorded launches depend on matches; False (nothing copied) otherwise.  A batch
         prepared on another stream (engine.prepare_batch) was adopted by step() (engine.adopt)."""
@@ -184,9 +218,9 @@ class FusedTrainer:
                      if getattr(batch, k, None) is not None and getattr(batch, k).numel()]
             pairs += bc_new.copy_pairs(bc_slot)
             used = self._graph[5]   # data_ptr of every captured buffer the plans touch (None: all)
-            if used is not None:
+            if used is not None and not self.rebind_copy_all:
                 pairs = [(d, s) for d, s in pairs if d.data_ptr() in used]
-            ops.copy_many(pairs)   # one launch for the batch and its cache
+            ops.copy_many(pairs + list(extra))   # one launch for the batch, its cache and the weights
         self.rebinds += 1
         return True
 
@@ -197,10 +231,14 @@ class FusedTrainer:
                 self.lr_dev = torch.tensor([float(self.lr), float(self.sigma_lr)], dtype=torch.float64,
                                            device=st.flat.device)
             with ops.using(self.ctx):
-                ops.grad_norm(st.grad, self.gnorm)
+                if self.scaler is not None:
+                    ops.grad_norm_amp(st.grad, self.gnorm, self.scaler)
+                else:
+                    ops.grad_norm(st.grad, self.gnorm)
                 ops.adamw_step(st.flat, st.grad, self.exp_avg, self.exp_avg_sq, st.P.sigma_start, self.lr,
                                self.sigma_lr, self.weight_decay, norm=self.gnorm, max_norm=self.max_norm,
-                               step=self.hip_step, lr_dev=self.lr_dev)
+                               step=self.hip_step, lr_dev=self.lr_dev, scaler=self.scaler,
+                               growth_interval=self.growth_interval)
             return
         torch.nn.utils.clip_grad_norm_([self.p_base, self.p_sigma], max_norm=self.max_norm)
         self.opt.step()
@@ -223,9 +261,11 @@ class FusedTrainer:
     # A new batch of the same signature is copied into the captured batch (``_rebind``), so the
     # reference's loop over fresh batches (train.py:639-711) replays the plan every step.
     # --------------------------------------------------------------------------------------------
-    def capture(self, batch, mode: str = "plan") -> None:
+    def capture(self, batch, mode: str = "plan", weighted: bool = False) -> None:
         """Capture the training step on ``batch`` (which must stay alive with unchanged shapes; its
-        tensors may be refilled in place).  Model and optimizer state are left as they were."""
+        tensors may be refilled in place).  Model and optimizer state are left as they were.
+        weighted: the step of the reference's KNN-weighted epochs (train.py:660-674) — the loss reads
+        per-graph weights from a device buffer of this trainer that step(sample_weights=w) fills."""
         if mode not in ("plan", "graph"):
             raise ValueError("capture mode must be 'plan' or 'graph'")
         if mode == "plan" and self.optimizer != "hip":
@@ -236,7 +276,12 @@ class FusedTrainer:
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         self.use_step_seed(self._seed_dev)
         with ops.using(self.ctx):
-            batch_cache(batch)
+            bc = batch_cache(batch)
+        self._wbuf = None
+        if weighted:
+            nr = bc.real_graphs if bc.real_graphs is not None else bc.B
+            self._wbuf = torch.ones(nr, device=dev)
+        w = self._wbuf
         # warm-up (allocations, optimizer state, every workspace at this batch's sizes) on a side
         # stream, then restore the state
         snap = self._snapshot()
@@ -244,7 +289,7 @@ class FusedTrainer:
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._fb_tail(self._fb_layers(batch, 0))   # (no gradient exchange in the warm-up)
+                self._fb_tail(self._fb_layers(batch, 0, sample_weights=w))   # (no gradient exchange here)
                 self._clip_and_update()
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
@@ -254,10 +299,10 @@ class FusedTrainer:
         # the per-layer part, where the first bucket's all_reduce is issued between the two phases
         state = {}
         if self.grad_buckets is None:
-            phases = [("forward/backward", lambda: self._fb_tail(self._fb_layers(batch, 0)))]
+            phases = [("forward/backward", lambda: self._fb_tail(self._fb_layers(batch, 0, sample_weights=w)))]
         else:
             def layers_phase():
-                state["t"] = self._fb_layers(batch, 0)
+                state["t"] = self._fb_layers(batch, 0, sample_weights=w)
                 join_forks()
             phases = [("forward/backward layers", layers_phase),
                       ("backward tail", lambda: self._fb_tail(state["t"]))]
@@ -292,14 +337,24 @@ class FusedTrainer:
                 ranges = self._held_ranges(batch, graphs[0].pool())
                 for g, pl, (what, _) in zip(graphs, plans, phases):
                     _check_census(g, pl, what)
+                    _check_deps(g, pl, what)
                     _check_ownership(pl, ranges, what)
         except Exception:
             for pl in plans:
                 _lib.lib().alignn_plan_destroy(pl)
+            self._wbuf = None
             raise
         self._graph = (graphs[0], graphs[-1], batch, plans if keep else None, graphs,
                        _plan_refs(plans, self._rebind_targets(batch)) if keep else None)
+        # the gradient exchange the phases were cut for (the bucketed exchange needs three phases, a
+        # hook or none two): a replay checks that it is still the one in place
+        self._exchange = self._exchange_mode()
         self.ctx.freeze()   # the plans hold the workspaces' addresses: eager steps may not replace them
+
+    def _exchange_mode(self):
+        if self.grad_buckets is not None:
+            return ("buckets", self.grad_buckets)
+        return ("hook", self.grad_hook) if self.grad_hook is not None else ("none", None)
 
     @staticmethod
     def _rebind_targets(batch):
@@ -315,8 +370,8 @@ class FusedTrainer:
         ranges = []
         for t in _cuda_tensors((self.st.flat, self.st.grad, getattr(self, "exp_avg", None),
                                 getattr(self, "exp_avg_sq", None), getattr(self, "hip_step", None),
-                                getattr(self, "gnorm", None), self.lr_dev, self.loss, self.log_means, self.log_stds,
-                                self._seed_dev, self.ctx.tensors(), batch, list(self.model.buffers()))):
+                                getattr(self, "gnorm", None), self.scaler, self.lr_dev, self.loss, self.log_means, self.log_stds,
+                                self._seed_dev, self._wbuf, self.ctx.tensors(), batch, list(self.model.buffers()))):
             s = t.untyped_storage()
             ranges.append((s.data_ptr(), s.data_ptr() + s.nbytes()))
         pool = tuple(pool_id)
@@ -326,6 +381,7 @@ class FusedTrainer:
         return ranges
 
     def release_capture(self) -> None:
+        self._wbuf = None
         if self._graph is not None:
             if self._graph[3]:
                 for pl in self._graph[3]:
@@ -340,6 +396,10 @@ class FusedTrainer:
             pass
 
     def _replay(self, seed: int) -> torch.Tensor:
+        mode = self._exchange_mode()
+        if mode[0] != self._exchange[0] or mode[1] is not self._exchange[1]:
+            raise RuntimeError(f"gradient exchange changed after capture (captured: {self._exchange[0]}, now: "
+                               f"{mode[0]}): set grad_buckets / grad_hook before capture(), or capture again")
         check(_lib.lib().alignn_set_i64(self._seed_dev.data_ptr(), int(seed) & (2**63 - 1), ops.stream_ptr()),
               "alignn_set_i64")
         plans = self._graph[3]
@@ -361,6 +421,7 @@ class FusedTrainer:
             self.grad_hook(self.st.grad)
         run(n - 1)
         self.step_count += 1
+        self.replays += 1
         return self.loss
 
     def _snapshot(self):
@@ -368,7 +429,8 @@ class FusedTrainer:
                      for p, st in self.opt.state.items()}
         hip = None
         if self.optimizer == "hip":
-            hip = (self.exp_avg.clone(), self.exp_avg_sq.clone(), self.hip_step.clone())
+            hip = (self.exp_avg.clone(), self.exp_avg_sq.clone(), self.hip_step.clone(),
+                   None if self.scaler is None else self.scaler.clone())
         return self.st.flat.clone(), opt_state, hip
 
     def _restore(self, snap) -> None:
@@ -378,6 +440,8 @@ class FusedTrainer:
             self.exp_avg.copy_(hip[0])
             self.exp_avg_sq.copy_(hip[1])
             self.hip_step.copy_(hip[2])
+            if hip[3] is not None:
+                self.scaler.copy_(hip[3])
         for p, st in self.opt.state.items():
             saved = opt_state.get(id(p))
             for k, v in st.items():
@@ -465,6 +529,21 @@ def _check_ownership(plan, ranges, what: str) -> None:
         msg = _lib.lib().alignn_last_error()
         raise RuntimeError(f"launch plan of the {what} phase references memory the trainer does not hold "
                            f"(launch {idx.value}, 0x{bad.value:x}): {msg.decode() if msg else ''}")
+
+
+def _check_deps(graph: torch.cuda.CUDAGraph, plan, what: str) -> int:
+    """Every ordering the captured graph has between two kernels must be one the plan replays (its
+    slot order + the waits noted by ops.stream_wait), and the plan must end with every stream joined
+    (alignn_plan_check_deps).  A torch-level wait that bypassed ops.stream_wait fails the capture here
+    instead of racing on replay.  Returns the number of kernel dependencies checked."""
+    a, b, e = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = _lib.lib().alignn_plan_check_deps(plan, ctypes.c_void_p(graph.raw_cuda_graph()), ctypes.byref(a),
+                                           ctypes.byref(b), ctypes.byref(e))
+    if rc != 0:
+        msg = _lib.lib().alignn_last_error()
+        raise RuntimeError(f"launch plan of the {what} phase misses a stream dependency of its capture "
+                           f"(launches {a.value} -> {b.value}): {msg.decode() if msg else ''}")
+    return e.value
 
 
 def _check_census(graph: torch.cuda.CUDAGraph, plan, what: str) -> None:

@@ -19,6 +19,7 @@
 // a range the caller declares it holds for the plan's lifetime.
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "common.h"
@@ -390,6 +391,173 @@ extern "C" int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other
   }
   *kernels = k;
   *other = o;
+  return ALIGNN_OK;
+}
+
+// Dependency check of a recorded plan against the HIP graph captured while it was recorded.  The
+// plan orders work by its per-slot program order and the cross-stream edges noted with
+// alignn_plan_note_wait; the captured graph by the dependencies the stream capture derived from
+// every event wait — including waits issued without noting them (a torch-level wait_stream), which
+// a replayed plan silently drops (round 3: an un-noted join let the next phase overwrite buffers the
+// side stream still read).  Checks, with the kernel nodes matched to the recorded launches in
+// creation order (same kernel function, grid and block required):
+//   1. every graph dependency between two kernels (directly or through empty / event nodes) is a
+//      happens-before of the plan (vector clocks over the slots);
+//   2. the plan ends joined: every slot's last kernel happens before the end of slot 0 (a stream
+//      capture must end with every forked stream joined; the next phase starts on slot 0 alone).
+// On failure: ALIGNN_E_BAD_SHAPE, *bad_from / *bad_to = the launch indices of the first edge the
+// plan lacks (bad_to = -1: an unjoined slot, bad_from = its last launch).
+extern "C" int alignn_plan_check_deps(const void* plan, void* graph, int64_t* bad_from, int64_t* bad_to,
+                                      int64_t* graph_edges) {
+  const Plan* p = reinterpret_cast<const Plan*>(plan);
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  if (!p || !g) return ALIGNN_E_BAD_SHAPE;
+  if (bad_from) *bad_from = -1;
+  if (bad_to) *bad_to = -1;
+  // plan happens-before: vector clocks over the stream slots
+  const size_t S = p->streams.size();
+  std::vector<std::vector<int64_t>> clk(S, std::vector<int64_t>(S, 0));
+  std::vector<std::vector<int64_t>> vc;      // per launch: clock of its slot when it was issued
+  std::vector<int> lslot;
+  std::vector<int64_t> lseq;
+  std::vector<const void*> lfunc;
+  std::vector<dim3> lgrid, lblock;
+  for (const PlanEntry& e : p->entries) {
+    if (e.func) {
+      clk[e.slot][e.slot] += 1;
+      vc.push_back(clk[e.slot]);
+      lslot.push_back(e.slot);
+      lseq.push_back(clk[e.slot][e.slot]);
+      lfunc.push_back(e.func);
+      lgrid.push_back(e.grid);
+      lblock.push_back(e.block);
+    } else if (e.event >= 0) {
+      for (size_t k = 0; k < S; ++k) clk[e.slot][k] = std::max(clk[e.slot][k], clk[e.src][k]);
+    }
+  }
+  auto hb = [&](int64_t a, int64_t b) { return vc[b][lslot[a]] >= lseq[a]; };
+  // graph nodes, kernel nodes in creation order
+  size_t n = 0;
+  hipError_t r = hipGraphGetNodes(g, nullptr, &n);
+  if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphGetNodes");
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) {
+    r = hipGraphGetNodes(g, nodes.data(), &n);
+    if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphGetNodes");
+  }
+  std::vector<int64_t> launch_of;   // node index -> launch index (-1: not a kernel)
+  std::vector<std::pair<hipGraphNode_t, int64_t>> index;
+  int64_t k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    r = hipGraphNodeGetType(nodes[i], &t);
+    if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphNodeGetType");
+    if (t != hipGraphNodeTypeKernel) {
+      launch_of.push_back(-1);
+      index.emplace_back(nodes[i], (int64_t)i);
+      continue;
+    }
+    if (k >= (int64_t)lfunc.size()) {
+      set_error("plan_check_deps: the graph holds more kernel nodes than the plan has launches");
+      return ALIGNN_E_BAD_SHAPE;
+    }
+    hipKernelNodeParams kp{};
+    r = hipGraphKernelNodeGetParams(nodes[i], &kp);
+    if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphKernelNodeGetParams");
+    if (kp.func != lfunc[k] || kp.gridDim.x != lgrid[k].x || kp.gridDim.y != lgrid[k].y ||
+        kp.gridDim.z != lgrid[k].z || kp.blockDim.x != lblock[k].x || kp.blockDim.y != lblock[k].y ||
+        kp.blockDim.z != lblock[k].z) {
+      set_error("plan_check_deps: kernel node %lld does not match launch %lld of the plan (func %p vs %p)",
+                (long long)k, (long long)k, kp.func, lfunc[k]);
+      return ALIGNN_E_BAD_SHAPE;
+    }
+    launch_of.push_back(k++);
+    index.emplace_back(nodes[i], (int64_t)i);
+  }
+  if (k != (int64_t)lfunc.size()) {
+    set_error("plan_check_deps: the graph holds %lld kernel nodes, the plan %zu launches", (long long)k, lfunc.size());
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  std::sort(index.begin(), index.end());
+  auto node_idx = [&](hipGraphNode_t h) -> int64_t {
+    auto it = std::lower_bound(index.begin(), index.end(), std::make_pair(h, (int64_t)-1));
+    return (it != index.end() && it->first == h) ? it->second : -1;
+  };
+  // nearest kernel ancestors through non-kernel nodes (memoised per node)
+  std::vector<std::vector<int64_t>> kanc(n);
+  std::vector<char> done(n, 0);
+  std::vector<hipGraphNode_t> deps;
+  auto direct = [&](size_t i, std::vector<int64_t>& out) -> int {
+    size_t nd = 0;
+    hipError_t rr = hipGraphNodeGetDependencies(nodes[i], nullptr, &nd);
+    if (rr != hipSuccess) return hip_status(rr, "plan_check_deps: hipGraphNodeGetDependencies");
+    deps.resize(nd);
+    if (nd) {
+      rr = hipGraphNodeGetDependencies(nodes[i], deps.data(), &nd);
+      if (rr != hipSuccess) return hip_status(rr, "plan_check_deps: hipGraphNodeGetDependencies");
+    }
+    for (size_t j = 0; j < nd; ++j) {
+      const int64_t d = node_idx(deps[j]);
+      if (d < 0) {
+        set_error("plan_check_deps: a dependency outside the graph's node list");
+        return ALIGNN_E_BAD_SHAPE;
+      }
+      out.push_back(d);
+    }
+    return ALIGNN_OK;
+  };
+  // kernel ancestors of node i: iterative DFS over non-kernel predecessors
+  std::function<int(size_t)> resolve = [&](size_t i) -> int {
+    if (done[i]) return ALIGNN_OK;
+    std::vector<int64_t> ds;
+    int rc = direct(i, ds);
+    if (rc) return rc;
+    std::vector<int64_t> acc;
+    for (int64_t d : ds) {
+      if (launch_of[d] >= 0) {
+        acc.push_back(launch_of[d]);
+      } else {
+        rc = resolve((size_t)d);
+        if (rc) return rc;
+        acc.insert(acc.end(), kanc[d].begin(), kanc[d].end());
+      }
+    }
+    std::sort(acc.begin(), acc.end());
+    acc.erase(std::unique(acc.begin(), acc.end()), acc.end());
+    kanc[i] = std::move(acc);
+    done[i] = 1;
+    return ALIGNN_OK;
+  };
+  int64_t edges = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (launch_of[i] < 0) continue;
+    int rc = resolve(i);
+    if (rc) return rc;
+    for (int64_t a : kanc[i]) {
+      ++edges;
+      if (!hb(a, launch_of[i])) {
+        if (bad_from) *bad_from = a;
+        if (bad_to) *bad_to = launch_of[i];
+        set_error("plan_check_deps: the captured graph orders launch %lld (slot %d) before launch %lld (slot %d), "
+                  "the plan does not (a cross-stream wait that was not noted)", (long long)a, lslot[a],
+                  (long long)launch_of[i], lslot[launch_of[i]]);
+        return ALIGNN_E_BAD_SHAPE;
+      }
+    }
+  }
+  if (graph_edges) *graph_edges = edges;
+  // ends joined: slot 0's final clock covers every slot's last launch
+  for (size_t s = 1; s < S; ++s) {
+    if (clk[0][s] < clk[s][s]) {
+      int64_t last = -1;
+      for (size_t a = 0; a < lslot.size(); ++a)
+        if (lslot[a] == (int)s) last = (int64_t)a;
+      if (bad_from) *bad_from = last;
+      set_error("plan_check_deps: stream slot %zu's last launch (%lld) is not joined into slot 0 at the end of the "
+                "plan (the next phase could overtake it)", s, (long long)last);
+      return ALIGNN_E_BAD_SHAPE;
+    }
+  }
   return ALIGNN_OK;
 }
 

@@ -432,6 +432,21 @@ int alignn_adamw_f32(float* p, float* g, float* m, float* v, int64_t n, int64_t 
 int alignn_adamw_f32_dev(float* p, float* g, float* m, float* v, int64_t n, int64_t split, const double* lr,
                          double weight_decay, double beta1, double beta2, double eps, const float* norm,
                          float max_norm, float* step, void* stream);
+/* GradScaler semantics of the reference's CUDA step (train.py:690-695: scaler.scale(loss).backward();
+ * unscale_; clip_grad_norm_; scaler.step; scaler.update(); scaler built at :1475-1476 with torch's
+ * defaults).  scaler: device float[4] = {scale (initially 65536), growth_tracker, found_inf, skipped}.
+ * The gradients handed in are the unscaled ones (a power-of-two scale is exact in fp32, so
+ * scale-then-unscale only matters where the scaled value overflows).
+ * alignn_grad_norm_amp_f32: *norm as alignn_grad_norm_f32 (bitwise the same), and found_inf =
+ *   1 if some g[i] * scale is inf or NaN (unscale_'s check), else 0 (workspace >= 2048 floats).
+ * alignn_adamw_amp_f32_dev: found_inf set -> no update at all (p, g, m, v and *step unchanged),
+ *   scale *= 0.5, growth_tracker = 0, skipped += 1 (scaler.step skips optimizer.step; update backs
+ *   off); else the alignn_adamw_f32_dev update, then growth_tracker += 1 and, when it reaches
+ *   growth_interval (torch: 2000), scale *= 2 and growth_tracker = 0.  No host synchronisation. */
+int alignn_grad_norm_amp_f32(const float* g, int64_t n, float* norm, float* scaler, float* workspace, void* stream);
+int alignn_adamw_amp_f32_dev(float* p, float* g, float* m, float* v, int64_t n, int64_t split, const double* lr,
+                             double weight_decay, double beta1, double beta2, double eps, const float* norm,
+                             float max_norm, float* step, float* scaler, int32_t growth_interval, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Batch assembly from a dataset resident in HBM (replaces PyG Collater /
@@ -549,6 +564,14 @@ int alignn_plan_check_ptrs(const void* plan, const uint64_t* ranges, int64_t n, 
  * batch only into the captured batch's buffers the plans touch). */
 int alignn_plan_refs(const void* plan, const uint64_t* ranges, int64_t n, int32_t* hit);
 int alignn_graph_census(void* graph, int64_t* kernels, int64_t* other);
+/* alignn_plan_check_deps(plan, hipGraph_t, &bad_from, &bad_to, &edges): the plan's ordering against the
+ * graph captured during its recording (kernel nodes matched to launches in creation order): every
+ * kernel-to-kernel dependency of the graph (through empty / event nodes too) must be a happens-before
+ * of the plan's slot order + noted waits, and every stream slot must be joined into slot 0 at the
+ * plan's end.  A cross-stream wait issued without alignn_plan_note_wait fails here (bad_from/bad_to =
+ * the launches the plan leaves unordered; bad_to = -1 for an unjoined slot); edges = the kernel
+ * dependencies checked. */
+int alignn_plan_check_deps(const void* plan, void* graph, int64_t* bad_from, int64_t* bad_to, int64_t* edges);
 /* A non-blocking HIP stream of the library's own at `priority` (an execution context's side / aux
  * streams: never one of torch's pooled streams, which may coincide with a capture or loader stream);
  * destroy synchronises it first. */

@@ -172,6 +172,7 @@ def _trainer_worker(rank, world, port, out_dir):
         tr._seed_dev = torch.zeros(1, dtype=torch.int64)
         batch = object()
         tr._graph = (None, None, batch, [1, 2])   # two captured plans, as capture(mode="plan") leaves them
+        tr._exchange = tr._exchange_mode()        # and the exchange they were captured for
         before = tr.st.flat.clone()
         tr.step(batch, seed=3)
         torch.save({"log": log, "before": before, "after": tr.st.flat.clone(), "grad": tr.st.grad.clone(),
@@ -251,6 +252,7 @@ def _bucket_worker(rank, world, port, out_dir):
         tr.ctx.side = lambda dev: None
         batch = object()
         tr._graph = (None, None, batch, [1, 2, 3])
+        tr._exchange = tr._exchange_mode()
         before = tr.st.flat.clone()
         tr.step(batch, seed=3)
         torch.save({"log": log, "before": before, "after": tr.st.flat.clone(), "grad": tr.st.grad.clone(),

@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-4 GPU job: named steps in order, each under its own time limit; stops at the first step that
+# crashed or timed out (exit codes other than 0 = ok and 1 = test failures).
+#   usage: bash tools/job_r4.sh OUTDIR STEP...
+#   STEP: new | tests | smoke | bench | quick | c3 | probes | rocprof-c2 | rocprof-c3 | pmc-c2 | pmc-c3
+O=${1:?outdir}; shift
+mkdir -p "$O"
+PT=(python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider)
+Q=(bench.py --no-secondary --no-cpu-baseline --e2e 0)
+C3=(bench.py --no-secondary --no-cpu-baseline --e2e 0 --batch 256 --precision bf16)
+run() {
+  local name=$1 lim=$2; shift 2
+  echo "=== $name: $*" | tee -a "$O/run.log"
+  timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$O/run.log"
+  tail -4 "$O/$name.log" | cut -c1-400
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop after $name (rc=$rc)"; exit $rc; fi
+}
+pmc() {   # pmc NAME COUNTERS BENCHARGS...
+  local name=$1 ctr=$2; shift 2
+  echo "=== $name" | tee -a "$O/run.log"
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d "$O/$name" -o run --output-format csv -- python "$@" \
+    --steps 3 --warmup 1 --no-roofline > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$O/run.log"
+  [ $rc -eq 0 ] || { tail -5 "$O/$name.log"; exit $rc; }
+}
+for st in "$@"; do
+  case "$st" in
+    new) run new 600 "${PT[@]}" -x tests/test_gpu_x_round4.py ;;
+    tests) run tests 1000 "${PT[@]}" tests ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    quick) run quick 300 python "${Q[@]}" --steps 20 --warmup 5 --dump-probes "$O/probes_c2.json" ;;
+    c3) run c3 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_c3.json" ;;
+    rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
+                  python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
+    rocprof-c3) run rocprof-c3 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c3" -o run --output-format csv -- \
+                  python "${C3[@]}" --steps 5 --warmup 2 --no-roofline ;;
+    pmc-c2) pmc pmc_c2_fetch FETCH_SIZE "${Q[@]}"; pmc pmc_c2_write WRITE_SIZE "${Q[@]}"
+            pmc pmc_c2_mfma "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "${Q[@]}" ;;
+    pmc-c3) pmc pmc_c3_fetch FETCH_SIZE "${C3[@]}"; pmc pmc_c3_write WRITE_SIZE "${C3[@]}"
+            pmc pmc_c3_mfma "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "${C3[@]}" ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo done
