@@ -166,6 +166,11 @@ _SIGNATURES = {
                           c_vp, c_vp], c_i32),
     "alignn_adamw_f32_dev": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                               c_vp, c_vp], c_i32),
+    "alignn_colsum_bf16": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
+    "alignn_gate_ln_fwd_ex": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                               c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_gate_ln_bwd_partials_ex": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_grad_norm_amp_f32": ([c_vp, c_i64, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_adamw_amp_f32_dev": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,
                                   c_vp, c_vp, c_i32, c_vp], c_i32),

@@ -412,8 +412,14 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
-                  skip_early: bool = False):
+                  skip_early: bool = False, bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
+                  want_X16: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
+    bf16_io (bf16 storage, config C3 — the tensor dtypes of the reference's autocast, train.py:632-636):
+    on a compacted graph the skip projection's output R and, in the backward, its gradient dR are
+    bf16 (Linear outputs and their gradients); X16: a bf16 copy of X (the Linear's input as autocast
+    casts it: bitwise the operand the bf16 matrix cores round X to) read by the skip projection and its
+    weight gradient; want_X16: the gate kernel also writes a bf16 copy of the new state (c.Xn16).
     skip_early: on a compacted graph with a side stream, the skip projection is queued there before
     the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
@@ -439,16 +445,18 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     else:
         na = g.n
         early = skip_early and side is not None
-        c.R = torch.empty(n, D, device=dev)
+        c.R = torch.empty(n, D, device=dev, dtype=torch.bfloat16 if bf16_io else torch.float32)
+        Xs = X16 if (bf16_io and X16 is not None) else X   # the skip projection's A operand
         if early:
-            with _side_work(side, (X, c.R)):   # skip projection of all rows, beside Q/K/V and the attention
-                ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+            with _side_work(side, (X, Xs, c.R)):   # skip projection of all rows, beside Q/K/V and the attention
+                ops.gemm(Xs, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
         c.Xa = ops.gather_rows(X, rows)
         c.QKV = torch.empty(na, 3 * D, device=dev)
         ops.gemm(c.Xa, cv.Wqkvr[:3 * D].t(), c.QKV, bias=cv.bqkvr[:3 * D])
         if not early:
-            with _side_work(side, (X, c.R)):   # skip projection of all rows, concurrent with the attention
-                ops.gemm(X, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+            with _side_work(side, (X, Xs, c.R)):   # skip projection of all rows, concurrent with the attention
+                ops.gemm(Xs, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+    c.X16 = X16 if (bf16_io and rows is not None) else None
     c.U = torch.empty(na, H, D, device=dev)
     ops.gemm(c.QKV[:, :D].view(na, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
     c.outp_a = torch.empty(na, D, device=dev)
@@ -482,11 +490,12 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     if side is not None and rows is not None:
         ops.stream_wait(torch.cuda.current_stream(dev), side)
     X_new = torch.empty(n, D, device=dev)
+    c.Xn16 = torch.empty(n, D, device=dev, dtype=torch.bfloat16) if want_X16 else None
     c.beta = torch.empty(n, device=dev)
     c.mu = torch.empty(n, device=dev)
     c.rstd = torch.empty(n, device=dev)
     ops.gate_ln_fwd(c.outp, c.R, cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop, seed_blk,
-                    outp_rows=c.outp_rows)
+                    outp_rows=c.outp_rows, Xnew16=c.Xn16)
     c.p, c.seed_att, c.seed_blk, c.H, c.with_proj = p_drop, seed_att, seed_blk, H, with_proj
     return X_new, c
 
@@ -527,7 +536,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         dQKV, dR = dQKVR[:, :3 * D], dQKVR[:, 3 * D:]
     else:
         dQKV = torch.empty(na, 3 * D, device=dev)
-        dR = torch.empty(n, D, device=dev)
+        dR = torch.empty(n, D, device=dev, dtype=c.R.dtype)   # bf16 storage: the gradient of a bf16 output
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
                     gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None,
                     dX_add=dX_add)
@@ -581,7 +590,7 @@ def _weight_grads(cv, gv, c, side, Qh, Oh, Sz, sigz, dout_a, dQKV, dR, dQKVR, dM
     compacted graph, the skip projection's dW, db); "b": the rest (the Q/K/V projections' dW, db,
     which read dQ and dK/dV)."""
     rows = c.rows
-    with _side_work(side, (c.QKV, dout_a, Sz, sigz, c.S, c.sumA, dQKV, dR, c.X, c.Xa)):
+    with _side_work(side, (c.QKV, dout_a, Sz, sigz, c.S, c.sumA, dQKV, dR, c.X, c.X16, c.Xa)):
         if "a" in part:
             if c.with_proj:
                 ops.gemm(Qh, Sz.transpose(0, 1), dM.view(H, C, D))
@@ -592,7 +601,7 @@ def _weight_grads(cv, gv, c, side, Qh, Oh, Sz, sigz, dout_a, dQKV, dR, dQKVR, dM
                 ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
                 ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
             if rows is not None:
-                ops.gemm(dR.t(), c.X, gv.Wqkvr[3 * D:])
+                ops.gemm(dR.t(), c.X if c.X16 is None else c.X16, gv.Wqkvr[3 * D:])
                 ops.colsum(dR, gv.bqkvr[3 * D:])
         if "b" in part:
             if rows is None:
@@ -703,6 +712,11 @@ class AlignnEngine:
         # fp32: the backward's dX products read transposed (K-contiguous) copies of the projection
         # weights, made beside the encoders at the start of the forward
         self.wt_copies = False
+
+    def _bf16_io(self, D: int) -> bool:
+        """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
+        (precision "bf16" with bf16_storage: autocast's dtypes, train.py:632-636)."""
+        return self.precision == "bf16" and self.bf16_storage and D % 4 == 0
 
     def _bf16_angle(self, bc, D: int) -> bool:
         """bf16 storage of the angle hidden layer and the line graph's K|V rows: precision "bf16", the
@@ -838,13 +852,17 @@ class AlignnEngine:
         # atom blocks on the aux stream: atom block l waits for line block l, line block l+1 does not
         # wait for it (it reads only the bond states); the readout joins the aux stream
         aux = ops.aux_stream(dev) if (self._atom_mode(T, E) == 2 and side is not None) else None
+        bf16_io = self._bf16_io(D) and bc.lg is not None and bc.lg.rows is not None
+        e16 = None   # bf16 copy of the bond state (written by the previous line block's gate kernel)
         for l in range(L):
             # EdgeUpdateBlock (train.py:312-317): line graph, angle embedding in target-sorted order
             if T > 0 and E > 0:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
-                                     skip_early=self.skip_early)
+                                     skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
+                                     want_X16=bf16_io and l + 1 < L)
+                e16 = c.Xn16
             else:
                 c = None
             ctx.edge.append(c)

@@ -341,6 +341,7 @@ _GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
 GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
 GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
+GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an operand / the output
 
 
 @contextmanager
@@ -374,7 +375,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
          c_rows: Optional[torch.Tensor] = None, tile: int = 0, path_only: bool = False):
     """C = act(alpha * A @ B + beta * C + bias + rowscale[:,None] * bias2) [* (mask > 0)].
 
-    A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D);
+    A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D), fp32 or
+    bf16 (bf16 storage, config C3: an operand widened exactly as it is staged, C rounded RNE and
+    write-only; bf16 tensors need bf16 arithmetic, gemm_precision("bf16"));
     bias/bias2 [.., N], rowscale [.., M] (strided views too).  ``reduce_batch``: A/B batched, C is
     2-D and receives the sum over the batch (K must be a multiple of 16).  ``c_rows`` (int32 [M]):
     logical row r of C is stored at C[c_rows[r]] (C then has any number of rows >= max index)."""
@@ -414,7 +417,15 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if c_rows is not None:
         a.c_rows = c_rows.data_ptr()
     a.split_k = 0 if split_k is None else int(split_k)   # 0: the library plans tile shape and split-K
-    a.tile = int(tile) | _GEMM_FLAGS
+    io = 0
+    for t, flag in ((A, GEMM_A_BF16), (B, GEMM_B_BF16), (C, GEMM_C_BF16)):
+        if t.dtype == torch.bfloat16:
+            io |= flag
+        elif t.dtype != torch.float32:
+            raise TypeError(f"gemm: operands must be float32 or bfloat16, got {t.dtype}")
+    if io and not ((_GEMM_FLAGS | int(tile)) & GEMM_BF16):
+        raise ValueError("gemm: bf16 operands need bf16 arithmetic (ops.gemm_precision('bf16'))")
+    a.tile = int(tile) | _GEMM_FLAGS | io
     if path_only:   # which kernel the library takes (0 tiled, 1 bf16 streaming); nothing runs
         return int(_lib.lib().alignn_gemm_path(ctypes.byref(a)))
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
@@ -426,9 +437,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if GEMM_TRACE is not None:   # tuning hook (tools/gemm_bench.py): record the call's operands
         GEMM_TRACE.append(dict(A=A, B=B, C=C, alpha=alpha, beta=beta, bias=bias, rowscale=rowscale, bias2=bias2,
                                relu=relu, mask=mask, reduce_batch=reduce_batch, c_rows=c_rows))
-    key = f"gemm_f32 M{M} N{N} K{K} b{batch}"
+    key = f"gemm_f32 M{M} N{N} K{K} b{batch}" + "".join(f" {n}16" for t, n in ((A, "A"), (B, "B"), (C, "C"))
+                                                      if t.dtype == torch.bfloat16)
     if profiling.active(key) or profiling.active("*gemm"):
-        nbytes = 4.0 * batch * (M * K + K * N + M * N * (2 if beta else 1))
+        nbytes = batch * (A.element_size() * M * K + B.element_size() * K * N
+                          + C.element_size() * M * N * (2 if beta else 1))
         profiling.launch(key, 2.0 * M * N * K * batch, nbytes,
                          lambda: check(_lib.lib().alignn_gemm_f32(ctypes.byref(a), stream_ptr()), "alignn_gemm_f32"))
     else:
@@ -445,10 +458,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: Opt
 
 
 def colsum(X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """out (+)= X.sum(0) (fp32 sums of fp32 or bf16 rows)."""
     M, N = X.shape
+    if X.stride(1) != 1:
+        raise ValueError("colsum: rows must be unit-stride")
     ws = WS.get("colsum", 256 * N, X.device)
-    check(_lib.lib().alignn_colsum_f32(X.data_ptr(), M, N, X.stride(0), out.data_ptr(), int(accumulate),
-                                       ws.data_ptr(), stream_ptr()), "alignn_colsum_f32")
+    fn = _lib.lib().alignn_colsum_bf16 if X.dtype == torch.bfloat16 else _lib.lib().alignn_colsum_f32
+    check(fn(X.data_ptr(), M, N, X.stride(0), out.data_ptr(), int(accumulate), ws.data_ptr(), stream_ptr()),
+          "alignn_colsum")
     return out
 
 
@@ -919,10 +936,23 @@ def _check_outp_rows(outp, outp_rows, n):
     return outp_rows.data_ptr()
 
 
-def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed, outp_rows=None):
-    """outp_rows (int32 [n], -1 = zero row): o of row r is outp[outp_rows[r]] (compacted conv output)."""
+def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed, outp_rows=None, Xnew16=None):
+    """outp_rows (int32 [n], -1 = zero row): o of row r is outp[outp_rows[r]] (compacted conv output).
+    R may be bf16 (the skip projection's bf16 output); Xnew16 (bf16 [n, D], optional) receives a bf16
+    copy of the new state (alignn_gate_ln_fwd_ex)."""
     n, D = X.shape
     rp = _check_outp_rows(outp, outp_rows, n)
+    if R.dtype == torch.bfloat16 or Xnew16 is not None:
+        if Xnew16 is not None and (Xnew16.dtype != torch.bfloat16 or tuple(Xnew16.shape) != (n, D)
+                                   or Xnew16.stride(1) != 1):
+            raise ValueError("gate_ln_fwd: Xnew16 must be a bf16 [n, D] row-major tensor")
+        check(_lib.lib().alignn_gate_ln_fwd_ex(n, D, outp.data_ptr(), rp, R.data_ptr(), R.stride(0),
+                                               int(R.dtype == torch.bfloat16), wbeta.data_ptr(), X.data_ptr(),
+                                               X.stride(0), ln_w.data_ptr(), ln_b.data_ptr(), Xnew.data_ptr(),
+                                               Xnew.stride(0), _p(Xnew16), 0 if Xnew16 is None else Xnew16.stride(0),
+                                               beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(), float(drop_p),
+                                               int(seed) & (2**64 - 1), stream_ptr()), "alignn_gate_ln_fwd_ex")
+        return
     check(_lib.lib().alignn_gate_ln_fwd_rows(n, D, outp.data_ptr(), rp, R.data_ptr(), R.stride(0), wbeta.data_ptr(),
                                              X.data_ptr(), X.stride(0), ln_w.data_ptr(), ln_b.data_ptr(),
                                              Xnew.data_ptr(), Xnew.stride(0), beta.data_ptr(), mu.data_ptr(),
@@ -943,6 +973,29 @@ def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_w
     if dout.shape != outp.shape:
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
     wsize = int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D))
+    if R.dtype == torch.bfloat16 or dR.dtype == torch.bfloat16:
+        # bf16 storage: R read / dR written in bf16 (alignn_gate_ln_bwd_partials_ex + _reduce)
+        if dX_add is not None:
+            _require(dX_add, "gate_ln_bwd dX_add")
+            if tuple(dX_add.shape) != (n, D) or not dX_add.is_contiguous():
+                raise ValueError("gate_ln_bwd: dX_add must be a contiguous [n, D] tensor")
+        red = reduce_stream if reduce_stream is not None else torch.cuda.current_stream(outp.device)
+        ws = (current().fresh("gate_ln_red", wsize, outp.device) if reduce_stream is not None
+              else WS.get("gate_ln", wsize, outp.device))
+        check(_lib.lib().alignn_gate_ln_bwd_partials_ex(n, D, dXnew.data_ptr(), dXnew.stride(0), _p(dX_add),
+                                                        outp.data_ptr(), rp, R.data_ptr(), R.stride(0),
+                                                        int(R.dtype == torch.bfloat16), wbeta.data_ptr(),
+                                                        ln_w.data_ptr(), ln_b.data_ptr(), beta.data_ptr(),
+                                                        mu.data_ptr(), rstd.data_ptr(), dout.data_ptr(), dR.data_ptr(),
+                                                        dR.stride(0), int(dR.dtype == torch.bfloat16), ws.data_ptr(),
+                                                        float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+              "alignn_gate_ln_bwd_partials_ex")
+        if reduce_stream is not None:
+            stream_wait(reduce_stream, torch.cuda.current_stream(outp.device))
+            ws.record_stream(reduce_stream)
+        check(_lib.lib().alignn_gate_ln_bwd_reduce(n, D, ws.data_ptr(), d_wbeta.data_ptr(), d_ln_w.data_ptr(),
+                                                   d_ln_b.data_ptr(), red.cuda_stream), "alignn_gate_ln_bwd_reduce")
+        return
     if dX_add is not None:
         _require(dX_add, "gate_ln_bwd dX_add")
         if tuple(dX_add.shape) != (n, D) or not dX_add.is_contiguous():

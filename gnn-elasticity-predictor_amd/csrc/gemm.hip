@@ -63,7 +63,21 @@ struct GemmParams {
   int reduce_batch;  // sum the batch into one output: K loop runs over (batch, k), K % BK == 0
   int pad_;
   const int32_t* c_rows;  // optional scatter of C rows
+  // bf16 storage (ALIGNN_GEMM_A_BF16 / _B_BF16 / _C_BF16): the pointer holds bf16 elements (strides
+  // still in elements); A / B are widened to fp32 exactly as they are staged, C is rounded (RNE)
+  int abf, bbf, cbf, pad3_;
 };
+
+// Element pointer arithmetic for an operand that holds fp32 or (bf) bf16 elements.
+__device__ __forceinline__ const float* eoff(const float* p, int64_t off, int bf) {
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(p) + off * (bf ? 2 : 4));
+}
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+__device__ __forceinline__ float bf_at(const float* p, int64_t i) {
+  return __builtin_bit_cast(float, (uint32_t)reinterpret_cast<const uint16_t*>(p)[i] << 16);
+}
+__device__ __forceinline__ uint16_t bf_rne(float v) { return __builtin_bit_cast(uint16_t, (__bf16)v); }
 
 // Loads one operand tile (ROWS x BKT) into registers.  KC: load along k (general strides,
 // float4 when stride_k==1 and aligned); !KC: load along rows (stride_row == 1).
@@ -73,32 +87,66 @@ struct TileLoader {
   static constexpr int KP = BKT + 4;               // padded k-row of the [row][k] image
   float4 r[F4];
   const float* base[F4];                           // fast path: this thread's float4 at k = kb
+  bool raw = false;                                // r[] holds 4 bf16 values in .x/.y (widened by store)
 
   // Fast path (vectorisable operand, full stage): per-thread addresses are formed once; a stage
   // is F4 plain float4 loads, no bounds branches.  KC: rows past the end are clamped to the last
   // row (they only feed output rows that are never stored).  !KC: only for interior tiles
   // (row0 + ROWS <= rows), the caller checks.
   __device__ __forceinline__ void setup_fast(const float* __restrict__ P, int64_t srow, int64_t sk, int64_t row0,
-                                             int64_t rows, int64_t kb) {
+                                             int64_t rows, int64_t kb, int bf = 0) {
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
       const int idx = threadIdx.x + NT * i;
       if (KC) {
         const int64_t gr = min(row0 + idx / (BKT / 4), rows - 1);
-        base[i] = P + gr * srow + kb + (idx % (BKT / 4)) * 4;
+        base[i] = eoff(P, gr * srow + kb + (idx % (BKT / 4)) * 4, bf);
       } else {
-        base[i] = P + (kb + idx / (ROWS / 4)) * sk + row0 + (idx % (ROWS / 4)) * 4;
+        base[i] = eoff(P, (kb + idx / (ROWS / 4)) * sk + row0 + (idx % (ROWS / 4)) * 4, bf);
       }
     }
   }
-  // k0 - kb = koff; KC operands have sk == 1 on the fast path
-  __device__ __forceinline__ void load_fast(int64_t koff, int64_t sk) {
+  // k0 - kb = koff; KC operands have sk == 1 on the fast path.  bf: 8-byte loads of four bf16
+  // values kept raw until store() (a conversion here would wait for the load: no prefetch)
+  __device__ __forceinline__ void load_fast(int64_t koff, int64_t sk, int bf = 0) {
+    if (bf) {
+#pragma unroll
+      for (int i = 0; i < F4; ++i) {
+        const uint2 u = *reinterpret_cast<const uint2*>(eoff(base[i], KC ? koff : koff * sk, 1));
+        r[i] = make_float4(__builtin_bit_cast(float, u.x), __builtin_bit_cast(float, u.y), 0.f, 0.f);
+      }
+      raw = true;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < F4; ++i) r[i] = *reinterpret_cast<const float4*>(base[i] + (KC ? koff : koff * sk));
+    raw = false;
   }
 
   __device__ __forceinline__ void load(const float* __restrict__ P, int64_t srow, int64_t sk, int64_t row0,
-                                       int64_t rows, int64_t k0, int64_t kend, int vec) {
+                                       int64_t rows, int64_t k0, int64_t kend, int vec, int bf = 0) {
+    raw = false;
+    if (bf) {   // bf16 edge tiles: element loads, widened here
+#pragma unroll
+      for (int i = 0; i < F4; ++i) {
+        const int idx = threadIdx.x + NT * i;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int64_t gr, gk;
+          if (KC) {
+            gr = row0 + (idx / (BKT / 4));
+            gk = k0 + (idx % (BKT / 4)) * 4 + j;
+          } else {
+            gk = k0 + (idx / (ROWS / 4));
+            gr = row0 + (idx % (ROWS / 4)) * 4 + j;
+          }
+          if (gr < rows && gk < kend) v[j] = bf_at(P, KC ? gr * srow + gk * sk : gk * sk + gr);
+        }
+        r[i] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
       int idx = threadIdx.x + NT * i;
@@ -138,7 +186,15 @@ struct TileLoader {
     }
   }
 
-  __device__ __forceinline__ void store(float* __restrict__ lds) const {
+  __device__ __forceinline__ void store(float* __restrict__ lds) {
+    if (raw) {
+#pragma unroll
+      for (int i = 0; i < F4; ++i) {
+        const uint32_t a = __builtin_bit_cast(uint32_t, r[i].x), b = __builtin_bit_cast(uint32_t, r[i].y);
+        r[i] = make_float4(bf_lo(a), bf_hi(a), bf_lo(b), bf_hi(b));
+      }
+      raw = false;
+    }
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
       int idx = threadIdx.x + NT * i;
@@ -234,6 +290,12 @@ __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], con
   }
 }
 
+__device__ __forceinline__ void store_c(const GemmParams& p, int64_t b, int64_t row, int64_t col, float v) {
+  const int64_t i = b * p.scb + c_row(p, row) * p.scm + col * p.scn;
+  if (p.cbf) reinterpret_cast<uint16_t*>(p.C)[i] = bf_rne(v);
+  else p.C[i] = v;
+}
+
 // Epilogue. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
 template <int BM, int BN>
 __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (&acc)[BM / 64][BN / 64], int64_t m0,
@@ -252,7 +314,7 @@ __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (
         if (p.split_k > 1) {
           p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
         } else {
-          p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, acc[i][j][r]);
+          store_c(p, b, row, col, epilogue_value(p, b, row, col, acc[i][j][r]));
         }
       }
     }
@@ -304,11 +366,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int64_t kb = (int64_t)sidx * p.kchunk;
   const int64_t ke = min(Ktot, kb + p.kchunk);
 
-  const float* A = p.A + b * p.sab;
-  const float* B = p.B + b * p.sbb;
+  const float* A = eoff(p.A, b * p.sab, p.abf);
+  const float* B = eoff(p.B, b * p.sbb, p.bbf);
   // (batch, local k) of a global k index; identity unless the batch is reduced (RB)
-  auto tileA = [&](int64_t k0) { return RB ? p.A + (k0 / p.K) * p.sab : A; };
-  auto tileB = [&](int64_t k0) { return RB ? p.B + (k0 / p.K) * p.sbb : B; };
+  auto tileA = [&](int64_t k0) { return RB ? eoff(p.A, (k0 / p.K) * p.sab, p.abf) : A; };
+  auto tileB = [&](int64_t k0) { return RB ? eoff(p.B, (k0 / p.K) * p.sbb, p.bbf) : B; };
   auto kloc = [&](int64_t k0) { return RB ? k0 % p.K : k0; };
   auto kend = [&](int64_t k0) { return RB ? p.K : ke; };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -328,15 +390,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   // row-contiguous operand; then every full stage [k0, k0 + BKT) <= ke takes them
   const bool fastA = !RB && p.vecA && (A_KC || m0 + BM <= p.M);
   const bool fastB = !RB && p.vecB && (B_KC || n0 + BN <= p.N);
-  if (fastA) la.setup_fast(A, p.sam, p.sak, m0, p.M, kb);
-  if (fastB) lb.setup_fast(B, p.sbn, p.sbk, n0, p.N, kb);
+  if (fastA) la.setup_fast(A, p.sam, p.sak, m0, p.M, kb, p.abf);
+  if (fastB) lb.setup_fast(B, p.sbn, p.sbk, n0, p.N, kb, p.bbf);
   auto load_stage = [&](int64_t k0) {
     const bool full = k0 + BKT <= ke;
     // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
-    if (fastA && full) la.load_fast(k0 - kb, p.sak);
-    else la.load(tileA(k0), p.sam, p.sak, m0, p.M, kloc(k0), kend(k0), p.vecA);
-    if (fastB && full) lb.load_fast(k0 - kb, p.sbk);
-    else lb.load(tileB(k0), p.sbn, p.sbk, n0, p.N, kloc(k0), kend(k0), p.vecB);
+    if (fastA && full) la.load_fast(k0 - kb, p.sak, p.abf);
+    else la.load(tileA(k0), p.sam, p.sak, m0, p.M, kloc(k0), kend(k0), p.vecA, p.abf);
+    if (fastB && full) lb.load_fast(k0 - kb, p.sbk, p.bbf);
+    else lb.load(tileB(k0), p.sbn, p.sbk, n0, p.N, kloc(k0), kend(k0), p.vecB, p.bbf);
   };
   load_stage(kb);
   la.store(smem);
@@ -406,15 +468,24 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
 
   TileLoader<BM, A_KC, BKT> la;
   TileLoader<BN, B_KC, BKT> lb;
-  la.setup_fast(p.A + b * p.sab, p.sam, p.sak, m0, p.M, kb);
-  lb.setup_fast(p.B + b * p.sbb, p.sbn, p.sbk, n0, p.N, kb);
+  la.setup_fast(eoff(p.A, b * p.sab, p.abf), p.sam, p.sak, m0, p.M, kb, p.abf);
+  lb.setup_fast(eoff(p.B, b * p.sbb, p.bbf), p.sbn, p.sbk, n0, p.N, kb, p.bbf);
+  const bool abf = p.abf != 0, bbf = p.bbf != 0;
   gf4 pa[FA], pb[FB], qa[FA], qb[FB];
+  // bf16 operands: 8-byte loads into the first two words, widened when the stage is stored
+  auto ld = [](const float* ptr, bool bf) -> gf4 {
+    if (bf) {
+      const uint2 u = *reinterpret_cast<const uint2*>(ptr);
+      return gf4{__builtin_bit_cast(float, u.x), __builtin_bit_cast(float, u.y), 0.f, 0.f};
+    }
+    return *reinterpret_cast<const gf4*>(ptr);
+  };
   auto load = [&](gf4 (&ra)[FA], gf4 (&rb)[FB], int st) {
     const int64_t koff = (int64_t)min(st, nst - 1) * BKT;
 #pragma unroll
-    for (int i = 0; i < FA; ++i) ra[i] = *reinterpret_cast<const gf4*>(la.base[i] + (A_KC ? koff : koff * p.sak));
+    for (int i = 0; i < FA; ++i) ra[i] = ld(eoff(la.base[i], A_KC ? koff : koff * p.sak, abf), abf);
 #pragma unroll
-    for (int i = 0; i < FB; ++i) rb[i] = *reinterpret_cast<const gf4*>(lb.base[i] + (B_KC ? koff : koff * p.sbk));
+    for (int i = 0; i < FB; ++i) rb[i] = ld(eoff(lb.base[i], B_KC ? koff : koff * p.sbk, bbf), bbf);
     asm volatile("" ::: "memory");  // keep the loads here (not sunk to their first use)
   };
   auto store = [&](const gf4 (&ra)[FA], const gf4 (&rb)[FB], float* buf) {
@@ -422,6 +493,8 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
     for (int i = 0; i < FA; ++i) la.r[i] = make_float4(ra[i].x, ra[i].y, ra[i].z, ra[i].w);
 #pragma unroll
     for (int i = 0; i < FB; ++i) lb.r[i] = make_float4(rb[i].x, rb[i].y, rb[i].z, rb[i].w);
+    la.raw = abf;
+    lb.raw = bbf;
     la.store(buf);
     lb.store(buf + LA);
   };
@@ -454,7 +527,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
     const int64_t row = (i / p.N) % p.M;
     const int64_t b = i / (p.N * p.M);
     // eight independent chains (partial k goes to chain k % 8), combined in a fixed tree
-    p.C[b * p.scb + c_row(p, row) * p.scm + col * p.scn] = epilogue_value(p, b, row, col, splitk_sum(p, b, row, col));
+    store_c(p, b, row, col, epilogue_value(p, b, row, col, splitk_sum(p, b, row, col)));
   }
 }
 
@@ -530,6 +603,7 @@ static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, 
 }
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+static bool aligned8(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 7u) == 0; }
 
 static int g_cus = 0;
 static int device_cus() {
@@ -680,7 +754,16 @@ __device__ __forceinline__ void load_band(gf4 (&a)[KT / 8], const float* __restr
   asm volatile("" ::: "memory");  // a prefetch: issued here, not sunk to its first use
 }
 
+// bf16 A rows (ABF): one 16-byte load per 16-deep slice holds the lane half's eight k-values, already
+// the MFMA operand; kept in the first KT / 16 entries of the same register array
 template <int KT>
+__device__ __forceinline__ void load_band_bf(gf4 (&a)[KT / 8], const uint16_t* __restrict__ Arow, int h) {
+#pragma unroll
+  for (int t = 0; t < KT / 16; ++t) a[t] = *reinterpret_cast<const gf4*>(Arow + 16 * t + 8 * h);
+  asm volatile("" ::: "memory");
+}
+
+template <int KT, bool ABF>
 __device__ __forceinline__ void band_mma(floatx16 (&acc)[4], const gf4 (&a)[KT / 8], const __bf16* __restrict__ Bs,
                                          int col0, int l32, int h) {
   constexpr int KP = KT + 8;
@@ -692,10 +775,14 @@ __device__ __forceinline__ void band_mma(floatx16 (&acc)[4], const gf4 (&a)[KT /
 #pragma unroll
   for (int t = 0; t < KT / 16; ++t) {
     bf16x8 ha;
+    if constexpr (ABF) {
+      ha = __builtin_bit_cast(bf16x8, a[t]);
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ha[q] = (__bf16)a[2 * t][q];
-      ha[4 + q] = (__bf16)a[2 * t + 1][q];
+      for (int q = 0; q < 4; ++q) {
+        ha[q] = (__bf16)a[2 * t][q];
+        ha[4 + q] = (__bf16)a[2 * t + 1][q];
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -715,7 +802,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_
 // alpha acc (column layout) -> LDS tile -> rows: fma(beta, C, .), + bias, ReLU, mask, 16-byte stores
 // (epilogue_value's order).  Rows past M fall outside the store descriptor and are dropped; beta == 0
 // reads an empty descriptor.
-template <bool BETA, bool MASK>
+template <bool BETA, bool MASK, bool CBF>
 __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], const float* __restrict__ bptr,
                                            float* __restrict__ Ls, __amdgpu_buffer_rsrc_t cst,
                                            __amdgpu_buffer_rsrc_t cld, __amdgpu_buffer_rsrc_t cmk, int64_t row0,
@@ -729,7 +816,7 @@ __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       gf4 v = *reinterpret_cast<const gf4*>(Ls + rr * EPI_LD + cc + 4 * i);
-      const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * 4);
+      const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * (CBF ? 2 : 4));
       if constexpr (BETA) {   // the tiled epilogue's order: fma(beta, C, alpha acc), then + bias
         const gf4 c = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
         v = gf4{fmaf(p.beta, c.x, v.x), fmaf(p.beta, c.y, v.y), fmaf(p.beta, c.z, v.z), fmaf(p.beta, c.w, v.w)};
@@ -746,15 +833,23 @@ __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (
         v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
         v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cst, off, 0, 0);
+      if constexpr (CBF) {   // bf16 C rows (RNE): four values in 8 bytes
+        const uint32_t lo = (uint32_t)bf_rne(v.x) | ((uint32_t)bf_rne(v.y) << 16);
+        const uint32_t hi = (uint32_t)bf_rne(v.z) | ((uint32_t)bf_rne(v.w) << 16);
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, cst, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cst, off, 0, 0);
+      }
     }
   }
 }
 
 // grid: G workgroups (<= one per CU), G a multiple of nslices = N / 256; workgroup g serves slice
 // g % nslices and bands q, q + Q, ... (q = g / nslices, Q = G / nslices).
-template <int KT, bool BETA, bool MASK>
+template <int KT, bool BETA, bool MASK, bool ABF = false, bool CBF = false>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, int nslices, int64_t nbands) {
+  static_assert(!(CBF && BETA), "bf16 C is write-only");
   constexpr int KP = KT + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NB * KP];
   __shared__ __attribute__((aligned(16))) float Lepi[4 * 32 * EPI_LD];
@@ -785,8 +880,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
   const int wr = wave >> 1, wc = wave & 1;
   const int col0 = wc * 128;
   const float* bias = p.bias ? p.bias + n0 + col0 : nullptr;   // this wave's 128 columns
-  const float* Cw = p.C + n0 + col0;
-  const int64_t cbytes = (p.M * p.scm - (n0 + col0)) * 4;
+  float* Cw = const_cast<float*>(eoff(p.C, n0 + col0, CBF));
+  const int64_t cbytes = (p.M * p.scm - (n0 + col0)) * (CBF ? 2 : 4);
   const __amdgpu_buffer_rsrc_t cst = rsrc(Cw, cbytes);
   const __amdgpu_buffer_rsrc_t cld = rsrc(Cw, (BETA && p.beta != 0.f) ? cbytes : 0);
   const __amdgpu_buffer_rsrc_t cmk = rsrc(MASK ? p.mask + n0 + col0 : Cw, MASK ? (p.M * p.smk_m - (n0 + col0)) * 4 : 0);
@@ -794,23 +889,27 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
   __syncthreads();
   auto arow = [&](int64_t band) {
     const int64_t row = min(band * ROWS + wr * 32 + l32, p.M - 1);
-    return p.A + row * p.sam;
+    return eoff(p.A, row * p.sam, ABF);
+  };
+  auto lband = [&](gf4 (&a)[KT / 8], const float* r) {
+    if constexpr (ABF) load_band_bf<KT>(a, reinterpret_cast<const uint16_t*>(r), h);
+    else load_band<KT>(a, r, h);
   };
   gf4 a0[KT / 8], a1[KT / 8];
   floatx16 acc[4];
   int64_t band = q;
   if (band >= nbands) return;
-  load_band<KT>(a0, arow(band), h);
+  lband(a0, arow(band));
   while (true) {  // two bands per iteration: the register sets keep fixed names
     const int64_t b1 = band + Q;
-    load_band<KT>(a1, arow(min(b1, nbands - 1)), h);
-    band_mma<KT>(acc, a0, Bs, col0, l32, h);
-    band_store<BETA, MASK>(p, acc, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane);
+    lband(a1, arow(min(b1, nbands - 1)));
+    band_mma<KT, ABF>(acc, a0, Bs, col0, l32, h);
+    band_store<BETA, MASK, CBF>(p, acc, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane);
     if (b1 >= nbands) break;
     const int64_t b2 = b1 + Q;
-    load_band<KT>(a0, arow(min(b2, nbands - 1)), h);
-    band_mma<KT>(acc, a1, Bs, col0, l32, h);
-    band_store<BETA, MASK>(p, acc, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane);
+    lband(a0, arow(min(b2, nbands - 1)));
+    band_mma<KT, ABF>(acc, a1, Bs, col0, l32, h);
+    band_store<BETA, MASK, CBF>(p, acc, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane);
     if (b2 >= nbands) break;
     band = b2;
   }
@@ -826,12 +925,16 @@ static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
   if (a->batch != 1 || a->reduce_batch || split != 1) return false;
   if (a->K != 64 && a->K != 128 && a->K != 256) return false;
   if (a->N % bst::NB != 0 || a->M < 4096) return false;
-  if (a->sak != 1 || a->sam % 4 || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
+  const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, cbf = (a->tile & ALIGNN_GEMM_C_BF16) != 0;
+  if (a->tile & ALIGNN_GEMM_B_BF16) return false;
+  // bf16 A or C: K = 256 instantiations only, no mask; bf16 C without beta (write-only)
+  if ((abf || cbf) && (a->K != 256 || a->mask || (cbf && a->beta != 0.f))) return false;
+  if (a->sak != 1 || a->sam % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
   if (a->c_rows || a->rowscale || a->scn != 1 || a->scm < a->N) return false;
   if (a->mask && (a->smk_n != 1 || a->smk_m < a->N || (reinterpret_cast<uintptr_t>(a->mask) & 15) || a->smk_m % 4))
     return false;
   if ((a->M + 64) * std::max(a->scm, a->mask ? a->smk_m : 0) * 4 >= ((int64_t)1 << 31)) return false;
-  if (a->scm % 4 || (reinterpret_cast<uintptr_t>(a->C) & 15)) return false;  // 16-byte row segments
+  if (a->scm % 4 || (reinterpret_cast<uintptr_t>(a->C) & (cbf ? 7 : 15))) return false;  // 16 / 8-byte row segments
   return true;
 }
 
@@ -849,6 +952,14 @@ static void bf16_stream_launch(const GemmParams& p, int cus, hipStream_t s) {
   const int64_t nbands = (p.M + bst::ROWS - 1) / bst::ROWS;
   const int G = (int)(std::min<int64_t>(cus, nslices * nbands) / nslices * nslices);
   const dim3 grid((unsigned)std::max(G, nslices));
+  if (p.abf || p.cbf) {   // bf16 storage (K = 256, no mask: bf16_stream_ok)
+    const bool beta = p.beta != 0.f;
+    if (p.abf && p.cbf) launch(bst::gemm_bf16_stream_kernel<256, false, false, true, true>, grid, dim3(256), 0, s, p, nslices, nbands);
+    else if (p.cbf) launch(bst::gemm_bf16_stream_kernel<256, false, false, false, true>, grid, dim3(256), 0, s, p, nslices, nbands);
+    else if (beta) launch(bst::gemm_bf16_stream_kernel<256, true, false, true, false>, grid, dim3(256), 0, s, p, nslices, nbands);
+    else launch(bst::gemm_bf16_stream_kernel<256, false, false, true, false>, grid, dim3(256), 0, s, p, nslices, nbands);
+    return;
+  }
   if (p.K == 256) bf16_stream_launch_k<256>(p, grid, nslices, nbands, s);
   else if (p.K == 128) bf16_stream_launch_k<128>(p, grid, nslices, nbands, s);
   else bf16_stream_launch_k<64>(p, grid, nslices, nbands, s);
@@ -896,6 +1007,13 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   p.alpha = a->alpha; p.beta = a->beta; p.relu = a->relu;
   p.reduce_batch = a->reduce_batch && a->batch > 1;
   p.c_rows = a->c_rows;
+  p.abf = (a->tile & ALIGNN_GEMM_A_BF16) ? 1 : 0;
+  p.bbf = (a->tile & ALIGNN_GEMM_B_BF16) ? 1 : 0;
+  p.cbf = (a->tile & ALIGNN_GEMM_C_BF16) ? 1 : 0;
+  if (p.cbf && (a->beta != 0.f || a->mask)) {
+    set_error("gemm: a bf16 C is write-only (no beta, no mask)");
+    return ALIGNN_E_UNSUPPORTED;
+  }
   if (p.reduce_batch && a->K % BK != 0) {
     set_error("gemm: reduce_batch needs K %% %d == 0 (K=%lld)", BK, (long long)a->K);
     return ALIGNN_E_UNSUPPORTED;
@@ -906,10 +1024,12 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   // A is "k-contiguous" unless it is contiguous along m only.
   const bool akc = !(a->sam == 1 && a->sak != 1);
   const bool bkc = !(a->sbn == 1 && a->sbk != 1);
-  p.vecA = akc ? (a->sak == 1 && a->sam % 4 == 0 && a->sab % 4 == 0 && aligned16(a->A))
-               : (a->sak % 4 == 0 && a->sab % 4 == 0 && aligned16(a->A));
-  p.vecB = bkc ? (a->sbk == 1 && a->sbn % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B))
-               : (a->sbk % 4 == 0 && a->sbb % 4 == 0 && aligned16(a->B));
+  // vector loads: four elements per load (16 bytes fp32, 8 bytes bf16), aligned
+  const bool alA = p.abf ? aligned8(a->A) : aligned16(a->A), alB = p.bbf ? aligned8(a->B) : aligned16(a->B);
+  p.vecA = akc ? (a->sak == 1 && a->sam % 4 == 0 && a->sab % 4 == 0 && alA)
+               : (a->sak % 4 == 0 && a->sab % 4 == 0 && alA);
+  p.vecB = bkc ? (a->sbk == 1 && a->sbn % 4 == 0 && a->sbb % 4 == 0 && alB)
+               : (a->sbk % 4 == 0 && a->sbb % 4 == 0 && alB);
   p.kchunk = pl.kchunk;
   p.split_k = pl.split;
   p.ws = a->workspace;
@@ -949,22 +1069,25 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
 //   stage 2: one block per 64-column strip sums the R partials the same way.
 // -------------------------------------------------------------------------------------------
 namespace alignn {
+// BF: X holds bf16 elements (the bias gradient of a Linear whose output gradient is stored in bf16)
+template <bool BF = false>
 __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ X, int64_t M, int64_t N, int64_t ldx,
                                                      int64_t rows_per, float* __restrict__ part) {
   __shared__ float red[4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.y * 64 + tx;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  auto at = [&](int64_t i) { return BF ? bf_at(X, i) : X[i]; };
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int64_t r = r0 + ty;
     for (; r + 12 < r1; r += 16) {
-      s0 += X[r * ldx + col];
-      s1 += X[(r + 4) * ldx + col];
-      s2 += X[(r + 8) * ldx + col];
-      s3 += X[(r + 12) * ldx + col];
+      s0 += at(r * ldx + col);
+      s1 += at((r + 4) * ldx + col);
+      s2 += at((r + 8) * ldx + col);
+      s3 += at((r + 12) * ldx + col);
     }
-    for (; r < r1; r += 4) s0 += X[r * ldx + col];
+    for (; r < r1; r += 4) s0 += at(r * ldx + col);
   }
   red[ty][tx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -1003,8 +1126,8 @@ __global__ __launch_bounds__(256) void wcolsum2_stage1(const float* __restrict__
 }
 }  // namespace alignn
 
-extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
-                                 float* workspace, void* stream) {
+static int colsum(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
+                  float* workspace, bool bf, void* stream) {
   if (M < 0 || N < 0) return ALIGNN_E_BAD_SHAPE;
   if (N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1021,11 +1144,22 @@ extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t l
     ALIGNN_LAUNCH_CHECK("colsum_stage2");
     return ALIGNN_OK;
   }
-  launch(colsum_stage1, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
+  if (bf) launch(colsum_stage1<true>, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
+  else launch(colsum_stage1<false>, dim3(nparts, strips), dim3(256), 0, s, X, M, N, ldx, rows_per, workspace);
   ALIGNN_LAUNCH_CHECK("colsum_stage1");
   launch(colsum_stage2<0>, dim3(colsum_blocks(N)), dim3(kColsumThreads), 0, s, workspace, nparts, N, out, accumulate);
   ALIGNN_LAUNCH_CHECK("colsum_stage2");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
+                                 float* workspace, void* stream) {
+  return colsum(X, M, N, ldx, out, accumulate, workspace, false, stream);
+}
+
+extern "C" int alignn_colsum_bf16(const uint16_t* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
+                                  float* workspace, void* stream) {
+  return colsum(reinterpret_cast<const float*>(X), M, N, ldx, out, accumulate, workspace, true, stream);
 }
 
 extern "C" int alignn_wcolsum2_f32(int64_t M, int64_t N, int32_t C, const float* X1, int64_t ld1, const float* W1,

@@ -46,6 +46,10 @@ struct GateFwdParams {
   float* beta; float* mu; float* rstd;
   DropParams drop;
   const int32_t* orow;  // optional: row r of o is outp[orow[r]] (-1: o = 0) — compacted conv outputs
+  // bf16 storage (the reference's autocast, train.py:632-636): R is the skip projection's bf16 output
+  // (rbf); Xn16, if set, receives a bf16 copy of the new state (the next Linear's bf16 input)
+  int rbf, pad2_;
+  uint16_t* Xn16; int64_t ldxn16;
 };
 
 template <int VPL>
@@ -61,7 +65,8 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
   if (act) {
     if (orow >= 0) vload(p.outp + orow * D + j0, o);
-    vload(p.R + row * p.ldr + j0, r);
+    if (p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
+    else vload(p.R + row * p.ldr + j0, r);
     vload(p.wbeta + j0, w1);
     vload(p.wbeta + D + j0, w2);
     vload(p.wbeta + 2 * D + j0, w3);
@@ -99,6 +104,7 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
       out[i] = x[i] + a;
     }
     vstore(p.Xn + row * p.ldxn + j0, out);
+    if (p.Xn16) vstore_bf(p.Xn16 + row * p.ldxn16 + j0, out);
   }
   if (lane == 0) {
     p.beta[row] = b;
@@ -120,6 +126,7 @@ struct GateBwdParams {
   DropParams drop;
   const int32_t* orow;  // optional: o and dout rows through this map (-1: o = 0, dout not written)
   const float* dX2;     // optional [n, D] addend: the incoming gradient is dXn + dX2, written back to dXn
+  int rbf, drbf;        // bf16 storage: R read as bf16, dR written as bf16 (autocast: grad of a bf16 output)
 };
 
 template <int VPL>
@@ -146,7 +153,8 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
     const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
     if (act) {
       if (orow >= 0) vload(p.outp + orow * D + j0, o);
-      vload(p.R + row * p.ldr + j0, r);
+      if (p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
+      else vload(p.R + row * p.ldr + j0, r);
       vload(p.dXn + row * p.lddx + j0, gx);
       if (p.dX2) {   // one add per element, the sum kept as the residual's gradient
         float x2[VPL];
@@ -195,7 +203,8 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
         a_w3[i] = fmaf(dl, o[i] - r[i], a_w3[i]);
       }
       if (orow >= 0) vstore(p.dout + orow * D + j0, dov);
-      vstore(p.dR + row * p.lddr + j0, drv);
+      if (p.drbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dR) + row * p.lddr + j0, drv);
+      else vstore(p.dR + row * p.lddr + j0, drv);
     }
   }
   // one partial row per workgroup: the 4 waves' sums merged in LDS in wave order (fixed)
@@ -360,18 +369,24 @@ using namespace alignn;
 extern "C" int alignn_version(void) { return ALIGNN_ABI_VERSION; }
 extern "C" const char* alignn_last_error(void) { return g_err; }
 
-extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
-                                       const float* R, int64_t ldr, const float* wbeta, const float* X, int64_t ldx,
-                                       const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, float* beta,
-                                       float* mu, float* rstd, float drop_p, uint64_t seed, void* stream) {
+extern "C" int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
+                                     const void* R, int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X,
+                                     int64_t ldx, const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn,
+                                     uint16_t* Xnew16, int64_t ldxn16, float* beta, float* mu, float* rstd,
+                                     float drop_p, uint64_t seed, void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_fwd: unsupported hidden %d", D);
     return ALIGNN_E_UNSUPPORTED;
   }
+  if ((r_bf16 && (ldr % 4 || (reinterpret_cast<uintptr_t>(R) & 7))) ||
+      (Xnew16 && (ldxn16 % 4 || (reinterpret_cast<uintptr_t>(Xnew16) & 7)))) {
+    set_error("gate_ln_fwd: bf16 rows must be 8-byte aligned (leading dimension %% 4 == 0)");
+    return ALIGNN_E_BAD_SHAPE;
+  }
   if (n == 0) return ALIGNN_OK;
-  GateFwdParams p{n, D, 0, outp, R, ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta, mu, rstd, make_drop(drop_p, seed),
-                  outp_rows};
+  GateFwdParams p{n, D, 0, outp, reinterpret_cast<const float*>(R), ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta,
+                  mu, rstd, make_drop(drop_p, seed), outp_rows, r_bf16 ? 1 : 0, 0, Xnew16, ldxn16};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((n + 3) / 4));
   switch (vpl) {
@@ -382,6 +397,14 @@ extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, 
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_fwd_kernel");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
+                                       const float* R, int64_t ldr, const float* wbeta, const float* X, int64_t ldx,
+                                       const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, float* beta,
+                                       float* mu, float* rstd, float drop_p, uint64_t seed, void* stream) {
+  return alignn_gate_ln_fwd_ex(n, D, outp, outp_rows, R, ldr, 0, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, nullptr, 0,
+                               beta, mu, rstd, drop_p, seed, stream);
 }
 
 extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const float* R, int64_t ldr,
@@ -403,21 +426,27 @@ extern "C" int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D) {
   return std::max<int64_t>(1, std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n)) * 5 * D;
 }
 
-extern "C" int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
-                                               const float* outp, const int32_t* outp_rows, const float* R, int64_t ldr,
-                                               const float* wbeta, const float* ln_w, const float* ln_b,
-                                               const float* beta, const float* mu, const float* rstd, float* dout,
-                                               float* dR, int64_t lddr, float* workspace, float drop_p, uint64_t seed,
-                                               void* stream) {
+extern "C" int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
+                                              const float* outp, const int32_t* outp_rows, const void* R, int64_t ldr,
+                                              int32_t r_bf16, const float* wbeta, const float* ln_w, const float* ln_b,
+                                              const float* beta, const float* mu, const float* rstd, float* dout,
+                                              void* dR, int64_t lddr, int32_t dr_bf16, float* workspace, float drop_p,
+                                              uint64_t seed, void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_bwd: unsupported hidden %d", D);
     return ALIGNN_E_UNSUPPORTED;
   }
+  if ((r_bf16 && (ldr % 4 || (reinterpret_cast<uintptr_t>(R) & 7))) ||
+      (dr_bf16 && (lddr % 4 || (reinterpret_cast<uintptr_t>(dR) & 7)))) {
+    set_error("gate_ln_bwd: bf16 rows must be 8-byte aligned (leading dimension %% 4 == 0)");
+    return ALIGNN_E_BAD_SHAPE;
+  }
   if (n == 0) return ALIGNN_OK;
   const int nwaves = (int)std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n);
-  GateBwdParams p{n, D, 0, dXnew, lddx, outp, R, ldr, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, lddr, workspace,
-                  nwaves, 0, make_drop(drop_p, seed), outp_rows, dX_add};
+  GateBwdParams p{n, D, 0, dXnew, lddx, outp, reinterpret_cast<const float*>(R), ldr, wbeta, ln_w, ln_b, beta, mu, rstd,
+                  dout, reinterpret_cast<float*>(dR), lddr, workspace, nwaves, 0, make_drop(drop_p, seed), outp_rows,
+                  dX_add, r_bf16 ? 1 : 0, dr_bf16 ? 1 : 0};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
   switch (vpl) {
@@ -428,6 +457,16 @@ extern "C" int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXne
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
+                                               const float* outp, const int32_t* outp_rows, const float* R, int64_t ldr,
+                                               const float* wbeta, const float* ln_w, const float* ln_b,
+                                               const float* beta, const float* mu, const float* rstd, float* dout,
+                                               float* dR, int64_t lddr, float* workspace, float drop_p, uint64_t seed,
+                                               void* stream) {
+  return alignn_gate_ln_bwd_partials_ex(n, D, dXnew, lddx, dX_add, outp, outp_rows, R, ldr, 0, wbeta, ln_w, ln_b, beta,
+                                        mu, rstd, dout, dR, lddr, 0, workspace, drop_p, seed, stream);
 }
 
 extern "C" int alignn_gate_ln_bwd_partials(int64_t n, int32_t D, const float* dXnew, int64_t lddx, const float* outp,

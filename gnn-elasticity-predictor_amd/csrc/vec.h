@@ -37,6 +37,42 @@ __device__ __forceinline__ void vstore(float* __restrict__ p, const float (&v)[V
   }
 }
 
+// VPL bf16 values (contiguous) widened to fp32 (exact); VPL % 4 == 0 loads 8 bytes per four
+template <int VPL>
+__device__ __forceinline__ void vload_bf(const uint16_t* __restrict__ p, float (&v)[VPL]) {
+  if constexpr (VPL % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < VPL / 4; ++q) {
+      const uint2 u = *reinterpret_cast<const uint2*>(p + 4 * q);
+      v[4 * q] = __builtin_bit_cast(float, u.x << 16);
+      v[4 * q + 1] = __builtin_bit_cast(float, u.x & 0xffff0000u);
+      v[4 * q + 2] = __builtin_bit_cast(float, u.y << 16);
+      v[4 * q + 3] = __builtin_bit_cast(float, u.y & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] = __builtin_bit_cast(float, (uint32_t)p[i] << 16);
+  }
+}
+
+// VPL fp32 values rounded to bf16 (RNE) and stored contiguously
+template <int VPL>
+__device__ __forceinline__ void vstore_bf(uint16_t* __restrict__ p, const float (&v)[VPL]) {
+  auto rne = [](float x) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x); };
+  if constexpr (VPL % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < VPL / 4; ++q) {
+      uint2 u;
+      u.x = rne(v[4 * q]) | (rne(v[4 * q + 1]) << 16);
+      u.y = rne(v[4 * q + 2]) | (rne(v[4 * q + 3]) << 16);
+      *reinterpret_cast<uint2*>(p + 4 * q) = u;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) p[i] = (uint16_t)rne(v[i]);
+  }
+}
+
 template <int VPL>
 __device__ __forceinline__ void vzero(float (&v)[VPL]) {
 #pragma unroll

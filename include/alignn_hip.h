@@ -86,6 +86,13 @@ typedef struct AlignnGemmArgs {
 /* bf16 only: never the streaming kernel (the large-M products K in {64, 128, 256}, N % 256 == 0,
  * M >= 4096 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
 #define ALIGNN_GEMM_NOSTREAM 512
+/* bf16 storage (config C3, autocast's tensor dtypes, train.py:632-636): the A / B pointer holds bf16
+ * elements (widened exactly as they are staged; strides stay in elements, vector loads need 8-byte
+ * alignment), or C receives bf16 (RNE of the fp32 epilogue value; write-only: no beta, no mask).
+ * Pointers in AlignnGemmArgs are reinterpreted; combine with ALIGNN_GEMM_BF16 arithmetic. */
+#define ALIGNN_GEMM_A_BF16 1024
+#define ALIGNN_GEMM_B_BF16 2048
+#define ALIGNN_GEMM_C_BF16 4096
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
@@ -164,6 +171,10 @@ int alignn_enc_bwd_bf16(const AlignnEncBwdArgs* args, const uint16_t* F16, int64
  * Two-stage, fixed order.  workspace >= 256*N floats. */
 int alignn_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
                       float* workspace, void* stream);
+/* The same over bf16 X (fp32 sums): the bias gradient of a Linear whose output gradient is stored in
+ * bf16 (the skip projection under bf16 storage). */
+int alignn_colsum_bf16(const uint16_t* X, int64_t M, int64_t N, int64_t ldx, float* out, int32_t accumulate,
+                       float* workspace, void* stream);
 
 /* Weighted column sums of two row-strided [M, N] matrices with per-row weights per column group
  * of width C (N % C == 0; W rows hold N / C weights):
@@ -361,6 +372,22 @@ int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t 
                                     const float* wbeta, const float* ln_w, const float* ln_b, const float* beta,
                                     const float* mu, const float* rstd, float* dout, float* dR, int64_t lddr,
                                     float* workspace, float drop_p, uint64_t seed, void* stream);
+/* bf16 storage forms (config C3; autocast keeps Linear outputs and their gradients in bf16,
+ * train.py:632-636): r_bf16 = R is the skip projection's bf16 output; Xnew16 (may be NULL) receives
+ * a bf16 copy of the new state, the next Linear's input as autocast casts it; dr_bf16 = dR is written
+ * as bf16.  LayerNorm, the gate and every accumulation stay fp32.  bf16 rows: 8-byte aligned,
+ * leading dimension % 4 == 0. */
+int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows, const void* R,
+                          int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X, int64_t ldx,
+                          const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, uint16_t* Xnew16,
+                          int64_t ldxn16, float* beta, float* mu, float* rstd, float drop_p, uint64_t seed,
+                          void* stream);
+int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
+                                   const float* outp, const int32_t* outp_rows, const void* R, int64_t ldr,
+                                   int32_t r_bf16, const float* wbeta, const float* ln_w, const float* ln_b,
+                                   const float* beta, const float* mu, const float* rstd, float* dout, void* dR,
+                                   int64_t lddr, int32_t dr_bf16, float* workspace, float drop_p, uint64_t seed,
+                                   void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Readout (train.py:562-586): global_mean_pool over ptr (PyG, train.py:562), concat with

@@ -28,7 +28,7 @@ pmc() {   # pmc NAME COUNTERS BENCHARGS...
 }
 for st in "$@"; do
   case "$st" in
-    new) run new 600 "${PT[@]}" -x tests/test_gpu_x_round4.py ;;
+    new) run new 600 "${PT[@]}" -x tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py ;;
     tests) run tests 1000 "${PT[@]}" tests ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
