@@ -874,6 +874,22 @@ def lg_fwd_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, wbar, F16, aggV, S, s
                          "alignn_lg_fwd_bf16"))
 
 
+def lg_fwd_mfma(g: GraphCSR, D: int, H: int, QKV, KV16, U, wbar, F16, aggV, S, sumA, mstat, den, drop_p: float,
+                seed: int):
+    """alignn_lg_fwd_mfma: lg_fwd_bf16 on the matrix cores (D = 256, H = 4; scores and weighted sums
+    as bf16 MFMA products, softmax and accumulation in fp32)."""
+    _check_lg_bf16(g, D, H, QKV, KV16, F16)
+    if U.numel() < g.n * H * D or S.numel() < g.n * H * D or aggV.numel() < g.n * D:
+        raise ValueError("lg_fwd_mfma: U and S must be [n, H, D], aggV [n, D]")
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m} bf16", 0.0, _lg_bf16_bytes(g.n, g.m, D, H, "fwd"),
+                     lambda: check(_lib.lib().alignn_lg_fwd_mfma(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
+                         QKV.data_ptr(), QKV.stride(0), KV16.data_ptr(), KV16.stride(0), U.data_ptr(), _p(wbar),
+                         F16.data_ptr(), F16.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(),
+                         mstat.data_ptr(), den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+                         "alignn_lg_fwd_mfma"))
+
+
 def lg_bwd_dst_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz,
                     sigz, dz_e, alpha_e, drop_p: float, seed: int):
     """alignn_lg_bwd_dst_bf16: the target-side attention backward with bf16 K|V and feature rows."""

@@ -445,34 +445,51 @@ extern "C" int alignn_plan_check_deps(const void* plan, void* graph, int64_t* ba
     r = hipGraphGetNodes(g, nodes.data(), &n);
     if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphGetNodes");
   }
+  // kernel nodes -> recorded launches: the same kernel, grid and block and the same argument bytes
+  // (the node's kernelParams); among identical launches, in order.  hipGraphGetNodes does not list
+  // the nodes of a multi-stream capture in issue order.
   std::vector<int64_t> launch_of;   // node index -> launch index (-1: not a kernel)
   std::vector<std::pair<hipGraphNode_t, int64_t>> index;
+  std::vector<char> taken(lfunc.size(), 0);
+  std::vector<size_t> lentry;       // launch index -> entry index (argument bytes)
+  for (size_t i = 0; i < p->entries.size(); ++i)
+    if (p->entries[i].func) lentry.push_back(i);
   int64_t k = 0;
   for (size_t i = 0; i < n; ++i) {
     hipGraphNodeType t;
     r = hipGraphNodeGetType(nodes[i], &t);
     if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphNodeGetType");
+    index.emplace_back(nodes[i], (int64_t)i);
     if (t != hipGraphNodeTypeKernel) {
       launch_of.push_back(-1);
-      index.emplace_back(nodes[i], (int64_t)i);
       continue;
-    }
-    if (k >= (int64_t)lfunc.size()) {
-      set_error("plan_check_deps: the graph holds more kernel nodes than the plan has launches");
-      return ALIGNN_E_BAD_SHAPE;
     }
     hipKernelNodeParams kp{};
     r = hipGraphKernelNodeGetParams(nodes[i], &kp);
     if (r != hipSuccess) return hip_status(r, "plan_check_deps: hipGraphKernelNodeGetParams");
-    if (kp.func != lfunc[k] || kp.gridDim.x != lgrid[k].x || kp.gridDim.y != lgrid[k].y ||
-        kp.gridDim.z != lgrid[k].z || kp.blockDim.x != lblock[k].x || kp.blockDim.y != lblock[k].y ||
-        kp.blockDim.z != lblock[k].z) {
-      set_error("plan_check_deps: kernel node %lld does not match launch %lld of the plan (func %p vs %p)",
-                (long long)k, (long long)k, kp.func, lfunc[k]);
+    int64_t hit = -1;
+    for (size_t a = 0; a < lfunc.size() && hit < 0; ++a) {
+      if (taken[a] || kp.func != lfunc[a] || kp.gridDim.x != lgrid[a].x || kp.gridDim.y != lgrid[a].y ||
+          kp.gridDim.z != lgrid[a].z || kp.blockDim.x != lblock[a].x || kp.blockDim.y != lblock[a].y ||
+          kp.blockDim.z != lblock[a].z)
+        continue;
+      const PlanEntry& e = p->entries[lentry[a]];
+      bool same = true;
+      if (kp.kernelParams) {
+        for (size_t j = 0; j < e.nargs && same; ++j) {
+          const size_t q = e.arg0 + j;
+          same = kp.kernelParams[j] && std::memcmp(kp.kernelParams[j], p->args.data() + p->arg_off[q], p->arg_size[q]) == 0;
+        }
+      }
+      if (same) hit = (int64_t)a;
+    }
+    if (hit < 0) {
+      set_error("plan_check_deps: kernel node %zu (func %p) matches no launch of the plan", i, kp.func);
       return ALIGNN_E_BAD_SHAPE;
     }
-    launch_of.push_back(k++);
-    index.emplace_back(nodes[i], (int64_t)i);
+    taken[hit] = 1;
+    launch_of.push_back(hit);
+    ++k;
   }
   if (k != (int64_t)lfunc.size()) {
     set_error("plan_check_deps: the graph holds %lld kernel nodes, the plan %zu launches", (long long)k, lfunc.size());

@@ -292,6 +292,14 @@ int alignn_lg_bwd_dst_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int
                            float* dz_e, float* alpha_e, float drop_p, uint64_t seed, void* stream);
 /* dst (bf16, RNE) = src (fp32) for a [rows, cols] block; cols and both leading dimensions multiples
  * of 4, src rows 16-byte aligned. */
+/* The matrix-core form of alignn_lg_fwd_bf16 (lgmma.hip; D = 256, H = 4, same arguments and outputs;
+ * rows 16-byte aligned): per 16-edge tile the scores [F | K] . [U^T ; blockdiag(q)] as bf16 16x16x32
+ * MFMA products and the weighted sums of F and V as bf16 4x4x4 products (q, u and alpha rounded to
+ * bf16 as the reference's autocast holds them, train.py:632-636; softmax and sums in fp32). */
+int alignn_lg_fwd_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
+                       const AlignnSchedule* sched, const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv,
+                       const float* U, const float* wbar, const uint16_t* F16, int64_t ldf, float* aggV, float* S,
+                       float* sumA, float* mstat, float* den, float drop_p, uint64_t seed, void* stream);
 int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, uint16_t* dst, int64_t ldd,
                          void* stream);
 

@@ -231,8 +231,8 @@ def test_c3_size_fp32_forward_vs_oracle():
     cpu_batch = mp_like_batch(256, lg_offset="num_nodes")
     assert cpu_batch.lg_edge_index.size(1) == 2027520
     model.to(DEV).eval()
-    with torch.no_grad():
-        mean, logvar = model(cpu_batch.to(DEV))
+    with torch.no_grad():   # (Batch.to moves in place: a separate copy for the device)
+        mean, logvar = model(mp_like_batch(256, lg_offset="num_nodes").to(DEV))
     torch.cuda.synchronize()
     mean, logvar = mean.cpu(), logvar.cpu()
     rb = RefData(**{k: getattr(cpu_batch, k) for k in cpu_batch.keys()})

@@ -2,7 +2,7 @@
 # Round-4 GPU job: named steps in order, each under its own time limit; stops at the first step that
 # crashed or timed out (exit codes other than 0 = ok and 1 = test failures).
 #   usage: bash tools/job_r4.sh OUTDIR STEP...
-#   STEP: new | tests | smoke | bench | quick | c3 | probes | rocprof-c2 | rocprof-c3 | pmc-c2 | pmc-c3
+#   STEP: new | lgm | tests | smoke | bench | quick | c3 | probes | rocprof-c2 | rocprof-c3 | pmc-c2 | pmc-c3
 O=${1:?outdir}; shift
 mkdir -p "$O"
 PT=(python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider)
@@ -28,7 +28,8 @@ pmc() {   # pmc NAME COUNTERS BENCHARGS...
 }
 for st in "$@"; do
   case "$st" in
-    new) run new 600 "${PT[@]}" -x tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py ;;
+    new) run new 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py tests/test_gpu_x_lgmma.py ;;
+    lgm) run lgm 300 python tools/lgm_bench.py --reps 20 ;;
     tests) run tests 1000 "${PT[@]}" tests ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
