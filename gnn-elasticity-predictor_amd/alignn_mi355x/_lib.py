@@ -83,6 +83,9 @@ _SIGNATURES = {
                             c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_lg_fwd_mfma": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_lg_bwd_dst_mfma": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                c_u64, c_vp], c_i32),
     "alignn_lg_bwd_dst_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                 c_u64, c_vp], c_i32),

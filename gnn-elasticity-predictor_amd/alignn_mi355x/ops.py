@@ -907,6 +907,24 @@ def lg_bwd_dst_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, do
                          "alignn_lg_bwd_dst_bf16"))
 
 
+def lg_bwd_dst_mfma(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz,
+                    sigz, dz_e, alpha_e, drop_p: float, seed: int):
+    """alignn_lg_bwd_dst_mfma: lg_bwd_dst_bf16 on the matrix cores (D = 256, H = 4)."""
+    _check_lg_bf16(g, D, H, QKV, KV16, F16)
+    if (U.numel() < g.n * H * D or Vd.numel() < g.n * H * D or Sz.numel() < g.n * H * D or dq.size(0) < g.n
+            or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H or dout.numel() < g.n * D
+            or outp.numel() < g.n * D):
+        raise ValueError("lg_bwd_dst_mfma: U, Vd, Sz [n, H, D], dq [n, >= D], dz_e/alpha_e [m, H] required")
+    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m} bf16", 0.0, _lg_bf16_bytes(g.n, g.m, D, H, "bwd_dst"),
+                     lambda: check(_lib.lib().alignn_lg_bwd_dst_mfma(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
+                         QKV.data_ptr(), QKV.stride(0), KV16.data_ptr(), KV16.stride(0), U.data_ptr(), Vd.data_ptr(),
+                         _p(wbar), F16.data_ptr(), F16.stride(0), dout.data_ptr(), outp.data_ptr(), mstat.data_ptr(),
+                         den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
+                         dz_e.data_ptr(), alpha_e.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+                         "alignn_lg_bwd_dst_mfma"))
+
+
 def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out (bf16, round to nearest even) = src (fp32 [rows, cols], cols % 4 == 0)."""
     if out is None:

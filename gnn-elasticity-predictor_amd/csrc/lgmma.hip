@@ -20,9 +20,9 @@
 // against the VALU kernels and the oracle within bf16 tolerances (tests/test_gpu_x_lgmma.py).
 //
 // Schedule: one single-wave workgroup per target segment (the lgconv.hip work list: descending
-// in-degree, XCD-contiguous ranges); the next tile's F, K, V rows are loaded into registers while the
-// current one is computed; edge positions past the segment end are clamped to its last edge (valid
-// rows, masked out of the softmax), so every tile issues the same loads.
+// in-degree, XCD-contiguous ranges), two waves per SIMD; the F, K, V rows of the next tile are in
+// flight while one is computed; edge positions past the segment end are clamped to its last edge
+// (valid rows, masked out of the softmax), so every tile issues the same loads.
 #include "common.h"
 #include "vec.h"
 
@@ -39,6 +39,9 @@ constexpr int D = 256, H = 4, TE = 16;   // C = D / H = 64 features per head
 // LDS row pitch of a tile image, bf16 elements: 272 (544 B) puts rows 8 dwords apart modulo the 64
 // banks, so a transposed read's eight rows per 32-lane half hit distinct banks
 constexpr int LP = 272;
+#ifndef LGM_WPE
+#define LGM_WPE 2   // waves per SIMD the register budget is cut for (256 VGPR + AGPR per wave)
+#endif
 
 struct Params {
   int64_t n, m;
@@ -52,6 +55,10 @@ struct Params {
   const uint16_t* KV16; int64_t ldkv; // bf16 K | V rows
   const uint16_t* F16; int64_t ldf;   // bf16 edge-feature rows (target-sorted)
   float* aggV; float* S; float* sumA; float* mstat; float* den;
+  // backward (target side)
+  const float* Vd;                    // [n, H, D]
+  const float* dout; const float* outp; const float* mstat_in; const float* den_in;
+  float* dq; int64_t lddq; float* Sz; float* sigz; float* dz_e; float* alpha_e;
   DropParams drop;
 };
 
@@ -68,7 +75,15 @@ struct Tile {
 
 __device__ __forceinline__ void load_tile(Tile& T, const Params& p, int32_t t0, int32_t last, int r, int g) {
   const int32_t t = min(t0 + r, last);
-  const int64_t s = (int64_t)p.src_at[t];
+  // the tile's 16 source ids as scalar loads (lgkmcnt): a vector index load would make the K/V loads
+  // wait on vmcnt, which counts every load issued before it — the tiles already in flight
+  int32_t sid[TE];
+#pragma unroll
+  for (int j = 0; j < TE; ++j) sid[j] = uni(sld(p.src_at, (int64_t)min(t0 + j, last)));
+  int32_t sv = sid[0];
+#pragma unroll
+  for (int j = 1; j < TE; ++j) sv = (r == j) ? sid[j] : sv;
+  const int64_t s = (int64_t)sv;
   const uint16_t* fr = p.F16 + (int64_t)t * p.ldf + 8 * g;
   const uint16_t* kr = p.KV16 + s * p.ldkv + 8 * g;
 #pragma unroll
@@ -92,7 +107,7 @@ __device__ __forceinline__ s4v tr_read(const uint16_t* img, int G, int c0, int l
 }
 
 template <bool DROP>
-__global__ __launch_bounds__(64) void lgm_fwd_kernel(Params p) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LGM_WPE, LGM_WPE))) void lgm_fwd_kernel(Params p) {
   if constexpr (DROP) resolve_drop(p.drop);
   __shared__ __attribute__((aligned(16))) uint16_t Fs[TE * LP];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[TE * LP];
@@ -141,10 +156,10 @@ __global__ __launch_bounds__(64) void lgm_fwd_kernel(Params p) {
       cb = __shfl(part, 16 * (r & 3), 64);
     }
     const int32_t last = end - 1;
-    Tile T;
-    load_tile(T, p, beg, last, r, g);
-    for (int32_t t0 = beg;; t0 += TE) {
-      // tile image for the transposed reads (the previous tile's reads completed before its MFMAs)
+    // one tile: image for the transposed reads, scores, (the register set is free: `refill` issues the
+    // loads of a later tile into it), online softmax, weighted sums
+    auto tile = [&](Tile& T, int32_t t0, int32_t t_next) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the previous tile's transposed reads are done
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         *reinterpret_cast<u4v*>(Fs + r * LP + 32 * c + 8 * g) = T.f[c];
@@ -157,8 +172,7 @@ __global__ __launch_bounds__(64) void lgm_fwd_kernel(Params p) {
         z4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(T.f[c]), Bu[c], z4, 0, 0, 0);
         z4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(T.k[c]), Bq[c], z4, 0, 0, 0);
       }
-      const bool more = t0 + TE < end;
-      if (more) load_tile(T, p, t0 + TE, last, r, g);   // next tile's rows while this one finishes
+      load_tile(T, p, t_next, last, r, g);
       // online softmax (edges 4g + i of head r)
       float z[4], tmax = -INFINITY;
 #pragma unroll
@@ -198,21 +212,43 @@ __global__ __launch_bounds__(64) void lgm_fwd_kernel(Params p) {
       }
       // alpha of edge group G for the 4x4x4 blocks: lane (b, i) takes the row of head i from lane 16G + i
       const uint32_t e01 = pack_bf16(ed[0], ed[1]), e23 = pack_bf16(ed[2], ed[3]);
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the tile image is written (one wave)
+      s4v A[4];
 #pragma unroll
       for (int G = 0; G < 4; ++G) {
         const int src = 16 * G + (lane & 3);
         const u2v a2 = {(uint32_t)__shfl((int)e01, src, 64), (uint32_t)__shfl((int)e23, src, 64)};
-        const s4v A = __builtin_bit_cast(s4v, a2);
+        A[G] = __builtin_bit_cast(s4v, a2);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the tile image is written (one wave)
+      // transposed reads in batches of eight (one edge group: 4 chunks of F and of V), the next
+      // group's batch issued before this group's products, so no product waits on a single read
+      s4v rb[2][8];
+      auto reads = [&](s4v (&b)[8], int G) {
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
-          accS[c4] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(A, tr_read(Fs, G, 64 * c4, lane), accS[c4], 0, 0, 0);
-          accV[c4] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(A, tr_read(Vs, G, 64 * c4, lane), accV[c4], 0, 0, 0);
+          b[c4] = tr_read(Fs, G, 64 * c4, lane);
+          b[4 + c4] = tr_read(Vs, G, 64 * c4, lane);
+        }
+      };
+      reads(rb[0], 0);
+#pragma unroll
+      for (int G = 0; G < 4; ++G) {
+        if (G + 1 < 4) reads(rb[(G + 1) & 1], G + 1);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          accS[c4] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(A[G], rb[G & 1][c4], accS[c4], 0, 0, 0);
+          accV[c4] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(A[G], rb[G & 1][4 + c4], accV[c4], 0, 0, 0);
         }
       }
-      if (!more) break;
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // the transposed reads are done before the image is rewritten
-    }
+    };
+    // one register set, refilled with the next tile's rows as soon as this tile's scores have consumed
+    // it (the loads land during the softmax and the weighted sums; a second wave per SIMD covers the
+    // rest: the kernel is held to 2 waves per SIMD, amdgpu_waves_per_eu).  Loads are unconditional,
+    // clamped to the last edge: a conditional load leaves the compiler's wait counters unable to tell
+    // which loads are outstanding, and it drains them all.
+    Tile T;
+    load_tile(T, p, beg, last, r, g);
+    for (int32_t t0 = beg; t0 < end; t0 += TE) tile(T, t0, t0 + TE);
   }
   // per-head totals over the four lane groups
   float s = s_p + __shfl_xor(s_p, 16, 64);
@@ -237,7 +273,163 @@ __global__ __launch_bounds__(64) void lgm_fwd_kernel(Params p) {
   }
 }
 
+// =============================================================================================
+// Backward, target side (lgconv.hip lg3_bwd_dst's contract): per edge dz = alpha (dalpha' - c3) / sqrt(C)
+// and alpha' = alpha x dropout; per target dq = sum dz k, Sz = sum dz f, sigz = sum dz.  Scores as in
+// the forward plus P = [F | V] . [Vd^T ; blockdiag(dout)] (dalpha' numerators), the sums of dz as
+// 4x4x4 products against the F and K tile images.
+// =============================================================================================
+#ifndef LGM_WPE_BWD
+#define LGM_WPE_BWD 1
+#endif
+template <bool DROP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LGM_WPE_BWD, LGM_WPE_BWD)))
+void lgm_bwd_dst_kernel(Params p) {
+  if constexpr (DROP) resolve_drop(p.drop);
+  __shared__ __attribute__((aligned(16))) uint16_t Fs[TE * LP];
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[TE * LP];
+  const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
+  const float scale = 0.125f;   // 1 / sqrt(C)
+  const int64_t d = (int64_t)uni(sld(p.items, (int64_t)blockIdx.x));
+  const int32_t beg = uni(sld(p.off, d)), end = uni(sld(p.off, d + 1));
+  const bool hl = r < H;
+
+  float sgz_p = 0.f;
+  f4v accSz[4], accDq[4];   // 4x4x4 block layout: acc[c4][h] = value of head h at feature 64 c4 + lane
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    accSz[c] = f4v{0.f, 0.f, 0.f, 0.f};
+    accDq[c] = f4v{0.f, 0.f, 0.f, 0.f};
+  }
+
+  if (beg < end) {
+    bf16x8 Bu[8], Bq[8], Bvd[8], Bgo[8];
+    const float* Qd = p.Q + d * p.ldq;
+    const float* God = p.dout + d * D;
+    const float* Ud = p.U + (d * H + (r & 3)) * D;
+    const float* Vdd = p.Vd + (d * H + (r & 3)) * D;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int k0 = 32 * c + 8 * g;
+      float u[8], q[8], vd[8], go[8];
+      vload<8>(Ud + k0, u);
+      vload<8>(Qd + k0, q);
+      vload<8>(Vdd + k0, vd);
+      vload<8>(God + k0, go);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Bu[c][j] = (__bf16)(hl ? u[j] : 0.f);
+        Bq[c][j] = (__bf16)(r == (c >> 1) ? q[j] : 0.f);
+        Bvd[c][j] = (__bf16)(hl ? vd[j] : 0.f);
+        Bgo[c][j] = (__bf16)(r == (c >> 1) ? go[j] : 0.f);
+      }
+    }
+    // per-head offsets (fp32): cb = wbar.q, c2 = wbar.dout, c3 = dout.outp (row sums of head g's 16 lanes)
+    float cb = 0.f, c2 = 0.f, c3;
+    {
+      float q4[4], go4[4], op4[4];
+      vload<4>(Qd + 4 * lane, q4);
+      vload<4>(God + 4 * lane, go4);
+      vload<4>(p.outp + d * D + 4 * lane, op4);
+      if (p.wbar) {
+        float wb[4];
+        vload<4>(p.wbar + 4 * lane, wb);
+        cb = __shfl(row_sum16(vdot(wb, q4)), 16 * (r & 3), 64);
+        c2 = __shfl(row_sum16(vdot(wb, go4)), 16 * (r & 3), 64);
+      }
+      c3 = __shfl(row_sum16(vdot(go4, op4)), 16 * (r & 3), 64);
+    }
+    const float mst = hl ? p.mstat_in[d * H + r] : 0.f;
+    const float inv_den = hl ? 1.0f / p.den_in[d * H + r] : 0.f;
+    const int32_t last = end - 1;
+    auto tile = [&](Tile& T, int32_t t0, int32_t t_next) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the previous tile's transposed reads are done
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        *reinterpret_cast<u4v*>(Fs + r * LP + 32 * c + 8 * g) = T.f[c];
+        *reinterpret_cast<u4v*>(Ks + r * LP + 32 * c + 8 * g) = T.k[c];
+      }
+      f4v z4 = {0.f, 0.f, 0.f, 0.f}, p4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        z4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(T.f[c]), Bu[c], z4, 0, 0, 0);
+        p4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(T.f[c]), Bvd[c], p4, 0, 0, 0);
+        z4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(T.k[c]), Bq[c], z4, 0, 0, 0);
+        p4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(T.v[c]), Bgo[c], p4, 0, 0, 0);
+      }
+      load_tile(T, p, t_next, last, r, g);
+      float dz[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t e = t0 + 4 * g + i;
+        const bool ok = hl && e < end;
+        const float z = (z4[i] + cb) * scale;
+        const float alpha = __expf(z - mst) * inv_den;
+        float mul = 1.0f;
+        if constexpr (DROP) {
+          if (hl) mul = dropout_mul(p.drop.seed, (uint64_t)e * H + r, p.drop.thresh, p.drop.inv_keep);
+        }
+        const float al = alpha * mul;
+        const float dal = (p4[i] + c2) * mul;
+        dz[i] = ok ? alpha * (dal - c3) * scale : 0.f;
+        if (ok) {
+          p.dz_e[(int64_t)e * H + r] = dz[i];
+          p.alpha_e[(int64_t)e * H + r] = al;
+        }
+        sgz_p += dz[i];
+      }
+      const uint32_t e01 = pack_bf16(dz[0], dz[1]), e23 = pack_bf16(dz[2], dz[3]);
+      s4v A[4];
+#pragma unroll
+      for (int G = 0; G < 4; ++G) {
+        const int src = 16 * G + (lane & 3);
+        const u2v a2 = {(uint32_t)__shfl((int)e01, src, 64), (uint32_t)__shfl((int)e23, src, 64)};
+        A[G] = __builtin_bit_cast(s4v, a2);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the tile images are written (one wave)
+      s4v rb[2][8];
+      auto reads = [&](s4v (&b)[8], int G) {
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          b[c4] = tr_read(Fs, G, 64 * c4, lane);
+          b[4 + c4] = tr_read(Ks, G, 64 * c4, lane);
+        }
+      };
+      reads(rb[0], 0);
+#pragma unroll
+      for (int G = 0; G < 4; ++G) {
+        if (G + 1 < 4) reads(rb[(G + 1) & 1], G + 1);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          accSz[c4] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(A[G], rb[G & 1][c4], accSz[c4], 0, 0, 0);
+          accDq[c4] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(A[G], rb[G & 1][4 + c4], accDq[c4], 0, 0, 0);
+        }
+      }
+    };
+    Tile T;
+    load_tile(T, p, beg, last, r, g);
+    for (int32_t t0 = beg; t0 < end; t0 += TE) tile(T, t0, t0 + TE);
+  }
+  float sg = sgz_p + __shfl_xor(sgz_p, 16, 64);
+  sg += __shfl_xor(sg, 32, 64);
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) p.Sz[(d * H + h) * D + 64 * c4 + lane] = accSz[c4][h];
+    p.dq[d * p.lddq + 64 * c4 + lane] = accDq[c4][c4];
+  }
+  if (lane < H) p.sigz[d * H + lane] = sg;
+}
+
 }  // namespace lgm
+
+int lgm_bwd_dst(const lgm::Params& p, hipStream_t s) {
+  if (p.n_items <= 0) return ALIGNN_OK;
+  if (p.drop.active) launch(lgm::lgm_bwd_dst_kernel<true>, dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+  else launch(lgm::lgm_bwd_dst_kernel<false>, dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+  ALIGNN_LAUNCH_CHECK("lgm_bwd_dst_kernel");
+  return ALIGNN_OK;
+}
 
 int lgm_fwd(const lgm::Params& p, hipStream_t s) {
   if (p.n_items <= 0) return ALIGNN_OK;
@@ -251,12 +443,8 @@ int lgm_fwd(const lgm::Params& p, hipStream_t s) {
 
 using namespace alignn;
 
-// Matrix-core form of alignn_lg_fwd_bf16 (D = 256, H = 4; same arguments and outputs).
-extern "C" int alignn_lg_fwd_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
-                                  const int32_t* src_at, const AlignnSchedule* sched, const float* Q, int64_t ldq,
-                                  const uint16_t* KV16, int64_t ldkv, const float* U, const float* wbar,
-                                  const uint16_t* F16, int64_t ldf, float* aggV, float* S, float* sumA, float* mstat,
-                                  float* den, float drop_p, uint64_t seed, void* stream) {
+static int lgm_check(int64_t n, int32_t D, int32_t H, const AlignnSchedule* sched, const float* Q, int64_t ldq,
+                     const uint16_t* KV16, int64_t ldkv, const float* U, const uint16_t* F16, int64_t ldf) {
   if (D != lgm::D || H != lgm::H) {
     set_error("lg mfma: needs hidden 256 and 4 heads (got %d, %d)", (int)D, (int)H);
     return ALIGNN_E_UNSUPPORTED;
@@ -271,6 +459,42 @@ extern "C" int alignn_lg_fwd_mfma(int64_t n, int64_t m, int32_t D, int32_t H, co
     set_error("lg mfma: Q (ldq >= 3D), K|V bf16 rows (ldkv >= 2D) and F bf16 rows (ldf >= D), 16-byte aligned rows");
     return ALIGNN_E_BAD_SHAPE;
   }
+  return ALIGNN_OK;
+}
+
+// Matrix-core form of alignn_lg_bwd_dst_bf16 (D = 256, H = 4; same arguments and outputs).
+extern "C" int alignn_lg_bwd_dst_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                                      const int32_t* src_at, const AlignnSchedule* sched, const float* Q, int64_t ldq,
+                                      const uint16_t* KV16, int64_t ldkv, const float* U, const float* Vd,
+                                      const float* wbar, const uint16_t* F16, int64_t ldf, const float* dout,
+                                      const float* outp, const float* mstat, const float* den, float* dq,
+                                      int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e, float drop_p,
+                                      uint64_t seed, void* stream) {
+  int rc = lgm_check(n, D, H, sched, Q, ldq, KV16, ldkv, U, F16, ldf);
+  if (rc || n == 0) return rc;
+  if (!Vd || !dout || !outp || !mstat || !den || !dq || !Sz || !sigz || !dz_e || !alpha_e ||
+      (reinterpret_cast<uintptr_t>(Vd) & 15) || (reinterpret_cast<uintptr_t>(dout) & 15) ||
+      (reinterpret_cast<uintptr_t>(outp) & 15)) {
+    set_error("lg mfma bwd: Vd, dout, outp (16-byte aligned rows) and every output are required");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  lgm::Params p{};
+  p.n = n; p.m = m; p.off = off_dst; p.src_at = src_at; p.items = sched->light; p.n_items = sched->n_light;
+  p.Q = Q; p.ldq = ldq; p.U = U; p.wbar = wbar; p.KV16 = KV16; p.ldkv = ldkv; p.F16 = F16; p.ldf = ldf;
+  p.Vd = Vd; p.dout = dout; p.outp = outp; p.mstat_in = mstat; p.den_in = den;
+  p.dq = dq; p.lddq = lddq; p.Sz = Sz; p.sigz = sigz; p.dz_e = dz_e; p.alpha_e = alpha_e;
+  p.drop = make_drop(drop_p, seed);
+  return lgm_bwd_dst(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+// Matrix-core form of alignn_lg_fwd_bf16 (D = 256, H = 4; same arguments and outputs).
+extern "C" int alignn_lg_fwd_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                                  const int32_t* src_at, const AlignnSchedule* sched, const float* Q, int64_t ldq,
+                                  const uint16_t* KV16, int64_t ldkv, const float* U, const float* wbar,
+                                  const uint16_t* F16, int64_t ldf, float* aggV, float* S, float* sumA, float* mstat,
+                                  float* den, float drop_p, uint64_t seed, void* stream) {
+  int rc = lgm_check(n, D, H, sched, Q, ldq, KV16, ldkv, U, F16, ldf);
+  if (rc) return rc;
   if (n == 0) return ALIGNN_OK;
   lgm::Params p{};
   p.n = n; p.m = m; p.off = off_dst; p.src_at = src_at; p.items = sched->light; p.n_items = sched->n_light;

@@ -300,6 +300,16 @@ int alignn_lg_fwd_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t
                        const AlignnSchedule* sched, const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv,
                        const float* U, const float* wbar, const uint16_t* F16, int64_t ldf, float* aggV, float* S,
                        float* sumA, float* mstat, float* den, float drop_p, uint64_t seed, void* stream);
+/* The matrix-core form of alignn_lg_bwd_dst_bf16 (same arguments and outputs): the scores and the
+ * dalpha numerators [F | V] . [Vd^T ; blockdiag(dout)] as bf16 16x16x32 MFMA products, dq and Sz as
+ * bf16 4x4x4 products of dz (rounded to bf16) with the tile's K and F rows; per-edge dz / alpha and
+ * sigz in fp32. */
+int alignn_lg_bwd_dst_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
+                           const AlignnSchedule* sched, const float* Q, int64_t ldq, const uint16_t* KV16,
+                           int64_t ldkv, const float* U, const float* Vd, const float* wbar, const uint16_t* F16,
+                           int64_t ldf, const float* dout, const float* outp, const float* mstat, const float* den,
+                           float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e, float drop_p,
+                           uint64_t seed, void* stream);
 int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, uint16_t* dst, int64_t ldd,
                          void* stream);
 

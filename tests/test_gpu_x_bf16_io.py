@@ -91,6 +91,7 @@ def test_bf16_gemm_output_refuses_beta():
 @pytest.mark.parametrize("compact", [False, True])
 def test_gate_ln_bf16_io_bitwise(compact):
     from alignn_mi355x import ops
+    ops.set_step_seed(None)   # host seeds only: the dropout masks must not read a step seed another test left
     n, D = 3000, 256
     R16 = _rand(n, D, seed=9).bfloat16()
     X = _rand(n, D, seed=10)

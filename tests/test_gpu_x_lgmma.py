@@ -60,7 +60,8 @@ def test_mfma_forward_matches_valu_bf16_kernel(degs, drop):
             assert _nrel(a[k], b[k]) < 2e-2, (k, _nrel(a[k], b[k]))
         fin = torch.isfinite(b["mstat"])
         assert torch.equal(fin, torch.isfinite(a["mstat"]))
-        assert float((a["mstat"][fin] - b["mstat"][fin]).abs().max(initial=0.0)) < 5e-2
+        if fin.any():
+            assert float((a["mstat"][fin] - b["mstat"][fin]).abs().max()) < 5e-2
         assert _nrel(a["den"], b["den"]) < 5e-2
 
 
@@ -71,3 +72,35 @@ def test_mfma_forward_is_deterministic():
     b = _fwd(ops.lg_fwd_mfma, csr, t, 0.15)
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def _bwd(fn, csr, m, t, fo, drop, D=256, H=4):
+    n = csr.n
+    g = torch.Generator().manual_seed(99)
+    Vd = (torch.randn(n, H, D, generator=g) * 0.5).to(DEV)
+    dout = (torch.randn(n, D, generator=g) * 0.5).to(DEV)
+    outs = dict(dq=torch.full((n, D), float("nan"), device=DEV), Sz=torch.empty(n, H, D, device=DEV),
+                sigz=torch.empty(n, H, device=DEV), dz=torch.zeros(max(m, 1), H, device=DEV),
+                al=torch.zeros(max(m, 1), H, device=DEV))
+    fn(csr, D, H, t["QKV"], t["KV16"], t["U"], Vd, t["wbar"], t["F16"], dout, fo["aggV"], fo["mstat"], fo["den"],
+       outs["dq"], outs["Sz"], outs["sigz"], outs["dz"], outs["al"], drop, 77)
+    torch.cuda.synchronize()
+    return outs
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.15])
+@pytest.mark.parametrize("degs", list(DEGREES))
+def test_mfma_backward_matches_valu_bf16_kernel(degs, drop):
+    """Both backwards on the SAME forward statistics (the VALU forward's), so the comparison isolates
+    the backward's own bf16 rounding (q, u, Vd, dout in the products, dz in the sums)."""
+    from alignn_mi355x import ops
+    for seed, with_wbar in enumerate((True, False)):
+        csr, m, t = _case(DEGREES[degs], 80 + seed, with_wbar)
+        fo = _fwd(ops.lg_fwd_bf16, csr, t, drop)
+        a = _bwd(ops.lg_bwd_dst_mfma, csr, m, t, fo, drop)
+        b = _bwd(ops.lg_bwd_dst_bf16, csr, m, t, fo, drop)
+        for k in ("dq", "Sz", "sigz", "dz", "al"):
+            assert torch.isfinite(a[k]).all(), k
+            if m == 0 and k in ("dz", "al"):
+                continue
+            assert _nrel(a[k], b[k]) < 3e-2, (k, _nrel(a[k], b[k]))

@@ -30,6 +30,10 @@ for st in "$@"; do
   case "$st" in
     new) run new 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py tests/test_gpu_x_lgmma.py ;;
     lgm) run lgm 300 python tools/lgm_bench.py --reps 20 ;;
+    lgmv) for v in gnn-elasticity-predictor_amd/alignn_mi355x/variants/*.so; do
+            ALIGNN_HIP_LIB=$v run "lgm_$(basename $v .so)" 300 python tools/lgm_bench.py --reps 20
+          done ;;
+    lgmt) run lgmt 300 "${PT[@]}" tests/test_gpu_x_lgmma.py tests/test_gpu_x_bf16_io.py ;;
     tests) run tests 1000 "${PT[@]}" tests ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
