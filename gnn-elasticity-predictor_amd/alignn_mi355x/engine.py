@@ -413,13 +413,15 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
                   skip_early: bool = False, bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
-                  want_X16: bool = False):
+                  want_X16: bool = False, mfma: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     bf16_io (bf16 storage, config C3 — the tensor dtypes of the reference's autocast, train.py:632-636):
     on a compacted graph the skip projection's output R and, in the backward, its gradient dR are
     bf16 (Linear outputs and their gradients); X16: a bf16 copy of X (the Linear's input as autocast
     casts it: bitwise the operand the bf16 matrix cores round X to) read by the skip projection and its
     weight gradient; want_X16: the gate kernel also writes a bf16 copy of the new state (c.Xn16).
+    mfma: the bf16-storage attention on the matrix cores (lgmma.hip: D = 256, H = 4), forward and
+    target-side backward.
     skip_early: on a compacted graph with a side stream, the skip projection is queued there before
     the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
@@ -468,8 +470,9 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     if F is not None and F.dtype == torch.bfloat16:
         # bf16 storage (config C3): the attention gathers K|V from a bf16 copy and streams bf16 F rows
         c.KV16 = ops.cast_bf16(c.QKV[:, D:3 * D])
-        ops.lg_fwd_bf16(g, D, H, c.QKV, c.KV16, c.U, c.wbar, F, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
-                        seed_att)
+        c.mfma = mfma and D == 256 and H == 4
+        fwd = ops.lg_fwd_mfma if c.mfma else ops.lg_fwd_bf16
+        fwd(g, D, H, c.QKV, c.KV16, c.U, c.wbar, F, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att)
     else:
         ops.tconv_fwd(g, D, H, c.QKV, c.U, c.wbar, F, feat_row, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
                       seed_att)
@@ -550,8 +553,9 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     if c.KV16 is not None:
         if dF is not None:
             raise ValueError("bf16 edge-feature storage needs the deferred angle-encoder backward (no dF)")
-        ops.lg_bwd_dst_bf16(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, c.F, dout_a, c.outp_a, c.mstat, c.den,
-                            dQKV[:, :D], Sz, sigz, dz_e, al_e, c.p, c.seed_att)
+        bwd = ops.lg_bwd_dst_mfma if getattr(c, "mfma", False) else ops.lg_bwd_dst_bf16
+        bwd(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, c.F, dout_a, c.outp_a, c.mstat, c.den, dQKV[:, :D], Sz, sigz,
+            dz_e, al_e, c.p, c.seed_att)
     else:
         ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
                           dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att)
@@ -712,6 +716,9 @@ class AlignnEngine:
         # fp32: the backward's dX products read transposed (K-contiguous) copies of the projection
         # weights, made beside the encoders at the start of the forward
         self.wt_copies = False
+        # bf16 storage: the line-graph attention (forward, target-side backward) on the matrix cores
+        # (lgmma.hip; D = 256, H = 4) instead of the VALU kernels (lgconv.hip)
+        self.attn_mfma = False
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
@@ -861,7 +868,7 @@ class AlignnEngine:
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
                                      skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
-                                     want_X16=bf16_io and l + 1 < L)
+                                     want_X16=bf16_io and l + 1 < L, mfma=self.attn_mfma)
                 e16 = c.Xn16
             else:
                 c = None

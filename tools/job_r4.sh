@@ -39,6 +39,7 @@ for st in "$@"; do
     bench) run bench 600 python bench.py ;;
     quick) run quick 300 python "${Q[@]}" --steps 20 --warmup 5 --dump-probes "$O/probes_c2.json" ;;
     c3) run c3 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_c3.json" ;;
+    c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
     rocprof-c3) run rocprof-c3 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c3" -o run --output-format csv -- \
