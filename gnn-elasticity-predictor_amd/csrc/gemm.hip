@@ -27,16 +27,6 @@
 
 #include "common.h"
 
-// XCD-contiguous tile order (below): same-box A/B +1.5 % step (profiles/r01/v30_ab_gemm_xcd.log)
-#ifndef ALIGNN_GEMM_SPLIT_FLOOR
-#define ALIGNN_GEMM_SPLIT_FLOOR 0  // within noise in the step (8,046 vs 8,042; v39_ab_gemm_split_floor_neutral.log)
-#endif
-#ifndef ALIGNN_GEMM_BK128
-#define ALIGNN_GEMM_BK128 0  // measured -4 % (1 workgroup/CU hides less latency; v32_ab_gemm_bk128_rejected.log)
-#endif
-#ifndef ALIGNN_GEMM_XCD
-#define ALIGNN_GEMM_XCD 1
-#endif
 
 namespace alignn {
 
@@ -344,21 +334,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
-#ifndef ALIGNN_GEMM_XCD_SPLIT
-#define ALIGNN_GEMM_XCD_SPLIT 1  // also for split-K grids: 8,003 vs 7,969 without (v33_ab_gemm_xcd_nosplit.log)
-#endif
-#if ALIGNN_GEMM_XCD
-  // XCD-contiguous work order: workgroups are dispatched round-robin over the 8 XCDs, so the
-  // linear id lin lands on XCD lin % 8.  Give XCD x the contiguous range of (z, tile) items
+  // XCD-contiguous work order (same-box A/B +1.5 % step, profiles/r01/v30_ab_gemm_xcd.log; split-K
+  // grids too: v33_ab_gemm_xcd_nosplit.log): workgroups are dispatched round-robin over the 8 XCDs,
+  // so the linear id lin lands on XCD lin % 8.  Give XCD x the contiguous range of (z, tile) items
   // [x*q + min(x, r), ...) so the column tiles of one A row band share that XCD's L2.
   const int64_t nlin = (int64_t)gridDim.x * gridDim.z;
   const int64_t lin = (int64_t)blockIdx.z * gridDim.x + blockIdx.x;
   const int64_t xq = nlin / 8, xr = nlin % 8, xcd = lin % 8;
-  const int64_t item = (ALIGNN_GEMM_XCD_SPLIT || p.split_k == 1) ? xcd * xq + min(xcd, xr) + lin / 8 : lin;
+  const int64_t item = xcd * xq + min(xcd, xr) + lin / 8;
   const int64_t tile = item % gridDim.x, zid = item / gridDim.x;
-#else
-  const int64_t tile = blockIdx.x, zid = blockIdx.z;
-#endif
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   const int64_t b = RB ? 0 : zid / p.split_k;
   const int sidx = zid % p.split_k;
@@ -423,7 +407,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
 }
 
-// Pipelined variant (ALIGNN_GEMM_PIPE): two register sets of global loads in flight, so a stage's
+// Pipelined variant: two register sets of global loads in flight, so a stage's
 // loads are covered by two stages of MFMAs instead of one (a 16-deep stage is 512 cycles of MFMA per
 // wave against a loaded global round trip of several thousand: the one-stage loop above is latency
 // bound).  Used when every stage of every workgroup is full and both operands take the vector fast
@@ -440,15 +424,11 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
-#if ALIGNN_GEMM_XCD
-  const int64_t nlin = (int64_t)gridDim.x * gridDim.z;
+  const int64_t nlin = (int64_t)gridDim.x * gridDim.z;   // XCD-contiguous order, as gemm_f32_kernel
   const int64_t lin = (int64_t)blockIdx.z * gridDim.x + blockIdx.x;
   const int64_t xq = nlin / 8, xr = nlin % 8, xcd = lin % 8;
-  const int64_t item = (ALIGNN_GEMM_XCD_SPLIT || p.split_k == 1) ? xcd * xq + min(xcd, xr) + lin / 8 : lin;
+  const int64_t item = xcd * xq + min(xcd, xr) + lin / 8;
   const int64_t tile = item % gridDim.x, zid = item / gridDim.x;
-#else
-  const int64_t tile = blockIdx.x, zid = blockIdx.z;
-#endif
   const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   const int64_t b = zid / p.split_k;
   const int sidx = zid % p.split_k;
@@ -531,9 +511,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
-#ifndef ALIGNN_GEMM_PIPE
-#define ALIGNN_GEMM_PIPE 1
-#endif
 template <int BM, int BN, bool A_KC, bool B_KC>
 static void launch_pipe(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
   if (bf) {
@@ -554,14 +531,6 @@ static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream
     else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true, RB>), grid, dim3(256), 0, s, p);
     else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true, RB>), grid, dim3(256), 0, s, p);
   } else {
-#if ALIGNN_GEMM_BK128
-    if constexpr (BM == 64 && BN == 64 && !RB) {
-      if (bk == 128) {
-        launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 128, false, RB>), grid, dim3(256), 0, s, p);
-        return;
-      }
-    }
-#endif
     if (bk >= 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false, RB>), grid, dim3(256), 0, s, p);
     else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false, RB>), grid, dim3(256), 0, s, p);
     else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false, RB>), grid, dim3(256), 0, s, p);
@@ -571,7 +540,7 @@ static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream
 // Every workgroup of the pipelined kernel must have only full stages and fast-path operands.
 template <int BM, int BN, bool A_KC, bool B_KC>
 static bool gemm_pipe_ok(const GemmParams& p, int bk) {
-  if (!ALIGNN_GEMM_PIPE || p.reduce_batch || !p.vecA || !p.vecB || bk > 64 || p.K <= 0) return false;
+  if (p.reduce_batch || !p.vecA || !p.vecB || bk > 64 || p.K <= 0) return false;
   if (p.kchunk % bk != 0 || p.K % bk != 0) return false;   // every split chunk a whole number of stages
   if (!A_KC && p.M % BM != 0) return false;                 // row-contiguous operands: interior tiles only
   if (!B_KC && p.N % BN != 0) return false;
@@ -582,10 +551,7 @@ static bool gemm_pipe_ok(const GemmParams& p, int bk) {
 
 template <int BM, int BN, bool A_KC, bool B_KC>
 static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe, hipStream_t s) {
-#ifndef ALIGNN_GEMM_PIPE_TILES
-#define ALIGNN_GEMM_PIPE_TILES 1  // 0: the pipelined loop for 64x64 tiles only (round-2 behaviour)
-#endif
-  if (!nopipe && (ALIGNN_GEMM_PIPE_TILES || (BM == 64 && BN == 64)) && gemm_pipe_ok<BM, BN, A_KC, B_KC>(p, bk)) {
+  if (!nopipe && gemm_pipe_ok<BM, BN, A_KC, B_KC>(p, bk)) {
     launch_pipe<BM, BN, A_KC, B_KC>(p, grid, bk, bf, s);
     return;
   }
@@ -643,10 +609,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   // bf16 long-K products (weight gradients over every row, M >= 128): 128 x 64 tiles, 32-deep
   // stages, two workgroups per CU (B = 256 bf16 sweep, profiles/r02/v20_gemm_sweep_b256_bf16.json:
   // M768 N256 K16020 38.7 vs 64.6 us, M256 N256 K184320 115 vs 129 us)
-#ifndef ALIGNN_GEMM_BF_LONG
-#define ALIGNN_GEMM_BF_LONG 1
-#endif
-  const bool bf_long = ALIGNN_GEMM_BF_LONG && (tile & ALIGNN_GEMM_BF16) && shape == 0 && !(tile & (ALIGNN_GEMM_BK16 | ALIGNN_GEMM_BK32 |
+  const bool bf_long = (tile & ALIGNN_GEMM_BF16) && shape == 0 && !(tile & (ALIGNN_GEMM_BK16 | ALIGNN_GEMM_BK32 |
                        ALIGNN_GEMM_BK64)) && Ktot >= 4096 && M >= 128 && requested <= 0;
   if (bf_long) {
     pl.bm = 128;
@@ -663,26 +626,12 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
     // of >= 160 tiles is not split (M2580 N256 K768: 25.8 vs 29.9 us in two); long-K splits keep
     // >= 240-deep chunks (M64 N256 K1920 b4: 8 splits, not 16) and go to two workgroups per CU when
     // the chunks would be >= 1024 deep (M256 N256 K23040: 32 splits, 40 vs 51 us)
-#ifndef ALIGNN_GEMM_PLAN_V1
-#define ALIGNN_GEMM_PLAN_V1 0  // 1: round-1 rules (A/B builds)
-#endif
-#if ALIGNN_GEMM_PLAN_V1
-    if (Ktot >= 512 || tiles < 32) {
-      const int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
-      split = (int)std::min(want, std::max<int64_t>(1, Ktot / 32));
-    }
-#else
     if ((Ktot >= 512 && tiles < 160) || tiles < 32) {
-#if ALIGNN_GEMM_SPLIT_FLOOR
-      int64_t want = std::max<int64_t>(1, cus / std::max<int64_t>(tiles, 1));
-#else
       int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
-#endif
       if (Ktot >= 512 && Ktot / want >= 1024) want *= 2;
       const int64_t maxs = std::max<int64_t>(1, Ktot / (Ktot >= 512 ? 240 : 32));
       split = (int)std::min(want, maxs);
     }
-#endif
   }
   if (Ktot == 0) split = 1;
   int64_t kchunk = (Ktot + split - 1) / split;
@@ -698,15 +647,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;
   // 64-deep stages only for long chunks on at most one workgroup per CU (short-K products and
   // two-per-CU splits run faster 16-deep: M2580 N768 K256 18.3 vs 20.6 us, M1024 N256 K1920 23.3 vs 26.0)
-  else if (ALIGNN_GEMM_PLAN_V1) pl.bk = (kchunk >= 128 && tiles * split <= 2 * (int64_t)cus) ? 64 : 16;
   else pl.bk = (kchunk >= 512 && tiles * split <= (int64_t)cus) ? 64 : 16;
-#if ALIGNN_GEMM_BK128
-  // 128-deep stages (half the round trips of 64) for a long split on at most one workgroup per CU
-  // (the 139 KB double-buffered stage allows one per CU); fp32 64x64 only
-  if (!(tile & (ALIGNN_GEMM_BK64 | ALIGNN_GEMM_BK32 | ALIGNN_GEMM_BK16)) && !(tile & ALIGNN_GEMM_BF16) &&
-      pl.bm == 64 && pl.bn == 64 && kchunk >= 256 && tiles * split <= (int64_t)cus)
-    pl.bk = 128;
-#endif
   return pl;
 }
 
