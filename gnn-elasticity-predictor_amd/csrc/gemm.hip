@@ -238,9 +238,24 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, 
   return v;
 }
 
+// x = hi + mid + lo, three bf16 words (RNE each; x - hi and (x - hi) - mid are exact in fp32).  A
+// non-finite hi keeps mid = lo = 0, so inf and NaN propagate as through the f32 MFMA (inf - inf
+// would turn an inf operand into NaN).
+__device__ __forceinline__ void split3(const float (&f)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const __bf16 a = (__bf16)f[s];
+    const float r1 = __builtin_isfinite((float)a) ? f[s] - (float)a : 0.f;
+    const __bf16 b = (__bf16)r1;
+    h[s] = a;
+    m[s] = b;
+    l[s] = (__bf16)(r1 - (float)b);
+  }
+}
+
 // One LDS stage of MFMAs: BKT/16 slices of the wave's (BM/2) x (BN/2) subtile, from an LDS image of
 // depth LD (>= BKT: the wave-group K-split kernel reads its group's slices `sub0..` of a deeper stage).
-template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF, int LD = BKT>
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int BF, int LD = BKT>
 __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], const float* __restrict__ As,
                                           const float* __restrict__ Bs, int wm, int wn, int h, int l32,
                                           int sub0 = 0) {
@@ -253,7 +268,27 @@ __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], con
     for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, LD>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
 #pragma unroll
     for (int j = 0; j < NI; ++j) read_frag<BN, B_KC, LD>(Bs, wn * (BN / 2) + j * 32 + l32, h, sub, fb[j]);
-    if constexpr (BF) {
+    if constexpr (BF == 2) {
+      // fp32 as three bf16 words (x = hi + mid + lo exactly: each word is the RNE of what the
+      // previous ones leave, and the residuals are exact in fp32); the six products down to
+      // 2^-16 relative of hi*hi, smallest first — every dropped term is below 2^-24 |a b|.
+      bf16x8 ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) split3(fa[i], ah[i], am[i], al[i]);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) split3(fb[j], bh[j], bm[j], bl[j]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    } else if constexpr (BF == 1) {
       bf16x8 ha[MI], hb[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -327,7 +362,7 @@ __device__ __forceinline__ float splitk_sum(const GemmParams& p, int64_t b, int6
   return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF, bool RB>
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int BF, bool RB>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
   constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
@@ -416,7 +451,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 // for it); the loop covers pairs of stages with one exit, the odd last stage's MFMAs under a
 // wave-uniform branch.  Same MFMA order and epilogue as gemm_f32_kernel: bitwise equal results.
 typedef float gf4 __attribute__((ext_vector_type(4)));
-template <int BM, int BN, bool A_KC, bool B_KC, int BKT, bool BF>
+template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int BF>
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
   constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
@@ -511,30 +546,33 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   }
 }
 
+template <int BM, int BN, bool A_KC, bool B_KC, int PR>
+static void launch_pipe_p(const GemmParams& p, dim3 grid, int bk, hipStream_t s) {
+  if (bk >= 64) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 64, PR>), grid, dim3(256), 0, s, p);
+  else if (bk == 32) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 32, PR>), grid, dim3(256), 0, s, p);
+  else launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 16, PR>), grid, dim3(256), 0, s, p);
+}
+
+// prec: 0 exact fp32 (v_mfma_f32_32x32x2_f32), 1 bf16 inputs, 2 fp32 as three bf16 words
 template <int BM, int BN, bool A_KC, bool B_KC>
-static void launch_pipe(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
-  if (bf) {
-    if (bk >= 64) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 64, true>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 32, true>), grid, dim3(256), 0, s, p);
-    else launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 16, true>), grid, dim3(256), 0, s, p);
-  } else {
-    if (bk >= 64) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 64, false>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 32, false>), grid, dim3(256), 0, s, p);
-    else launch((gemm_pipe_kernel<BM, BN, A_KC, B_KC, 16, false>), grid, dim3(256), 0, s, p);
-  }
+static void launch_pipe(const GemmParams& p, dim3 grid, int bk, int prec, hipStream_t s) {
+  if (prec == 1) launch_pipe_p<BM, BN, A_KC, B_KC, 1>(p, grid, bk, s);
+  else if (prec == 2) launch_pipe_p<BM, BN, A_KC, B_KC, 2>(p, grid, bk, s);
+  else launch_pipe_p<BM, BN, A_KC, B_KC, 0>(p, grid, bk, s);
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC, bool RB, int PR>
+static void launch_rb_p(const GemmParams& p, dim3 grid, int bk, hipStream_t s) {
+  if (bk >= 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, PR, RB>), grid, dim3(256), 0, s, p);
+  else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, PR, RB>), grid, dim3(256), 0, s, p);
+  else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, PR, RB>), grid, dim3(256), 0, s, p);
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC, bool RB>
-static void launch_rb(const GemmParams& p, dim3 grid, int bk, bool bf, hipStream_t s) {
-  if (bf) {
-    if (bk >= 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, true, RB>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, true, RB>), grid, dim3(256), 0, s, p);
-    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, true, RB>), grid, dim3(256), 0, s, p);
-  } else {
-    if (bk >= 64) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 64, false, RB>), grid, dim3(256), 0, s, p);
-    else if (bk == 32) launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 32, false, RB>), grid, dim3(256), 0, s, p);
-    else launch((gemm_f32_kernel<BM, BN, A_KC, B_KC, 16, false, RB>), grid, dim3(256), 0, s, p);
-  }
+static void launch_rb(const GemmParams& p, dim3 grid, int bk, int prec, hipStream_t s) {
+  if (prec == 1) launch_rb_p<BM, BN, A_KC, B_KC, RB, 1>(p, grid, bk, s);
+  else if (prec == 2) launch_rb_p<BM, BN, A_KC, B_KC, RB, 2>(p, grid, bk, s);
+  else launch_rb_p<BM, BN, A_KC, B_KC, RB, 0>(p, grid, bk, s);
 }
 
 // Every workgroup of the pipelined kernel must have only full stages and fast-path operands.
@@ -550,7 +588,7 @@ static bool gemm_pipe_ok(const GemmParams& p, int bk) {
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC>
-static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe, hipStream_t s) {
+static void launch(const GemmParams& p, dim3 grid, int bk, int bf, bool nopipe, hipStream_t s) {
   if (!nopipe && gemm_pipe_ok<BM, BN, A_KC, B_KC>(p, bk)) {
     launch_pipe<BM, BN, A_KC, B_KC>(p, grid, bk, bf, s);
     return;
@@ -560,7 +598,7 @@ static void launch(const GemmParams& p, dim3 grid, int bk, bool bf, bool nopipe,
 }
 
 template <int BM, int BN>
-static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, bool bf, bool nopipe,
+static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, int bk, int bf, bool nopipe,
                             hipStream_t s) {
   if (akc && bkc) launch<BM, BN, true, true>(p, grid, bk, bf, nopipe, s);
   else if (akc && !bkc) launch<BM, BN, true, false>(p, grid, bk, bf, nopipe, s);
@@ -986,7 +1024,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   }
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
-  const bool bf = (a->tile & ALIGNN_GEMM_BF16) != 0;
+  const int bf = (a->tile & ALIGNN_GEMM_BF16) ? 1 : (a->tile & ALIGNN_GEMM_F32X3) ? 2 : 0;
   const bool np = (a->tile & ALIGNN_GEMM_NOPIPE) != 0;
   if (pl.bm == 128 && pl.bn == 128) dispatch_layout<128, 128>(p, akc, bkc, grid, pl.bk, bf, np, s);
   else if (pl.bm == 128) dispatch_layout<128, 64>(p, akc, bkc, grid, pl.bk, bf, np, s);

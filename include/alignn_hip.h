@@ -93,6 +93,11 @@ typedef struct AlignnGemmArgs {
 #define ALIGNN_GEMM_A_BF16 1024
 #define ALIGNN_GEMM_B_BF16 2048
 #define ALIGNN_GEMM_C_BF16 4096
+/* fp32 inputs as three bf16 words each (x = hi + mid + lo exactly) on v_mfma_f32_32x32x16_bf16: the
+ * six cross products down to 2^-16 of hi*hi (every dropped term below 2^-24 |a b|), fp32 accumulation
+ * — fp32-class accuracy (not the f32 MFMA's bits) at 6 x 32 instead of 8 x 64 MFMA cycles per
+ * 16-deep slice.  Ignored with ALIGNN_GEMM_BF16. */
+#define ALIGNN_GEMM_F32X3 8192
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 

@@ -39,6 +39,11 @@ for st in "$@"; do
     bench) run bench 600 python bench.py ;;
     quick) run quick 300 python "${Q[@]}" --steps 20 --warmup 5 --dump-probes "$O/probes_c2.json" ;;
     c3) run c3 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_c3.json" ;;
+    hostprof) run hostprof 300 python -u tools/host_prep_profile.py --graphs 2000 --steps 30 ;;
+    gemmbf) run gemmbf 300 python -u tools/gemm_bench.py --quick --reps 10 --flag 64 ;;
+    gemmx3) run gemmx3 300 python -u tools/gemm_bench.py --quick --reps 10 --flag 8192 ;;
+    x3t) run x3t 600 "${PT[@]}" tests/test_gpu_x_gemm_x3.py "tests/test_gpu_parity.py::test_c2_batch32_fused_step_vs_oracle" ;;
+    qx3) run qx3 300 python "${Q[@]}" --steps 20 --warmup 5 --set engine.gemm_x3=1 --dump-probes "$O/probes_qx3.json" ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
