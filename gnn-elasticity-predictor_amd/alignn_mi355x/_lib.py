@@ -74,6 +74,7 @@ _SIGNATURES = {
     "alignn_wcolsum2_f32": ([c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
                              c_vp], c_i32),
     "alignn_graph_prep": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "alignn_schedule_build": ([c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp], c_i32),
     "alignn_gather_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "alignn_scatter_rows_f32": ([c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp], c_i32),
     "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,

@@ -131,15 +131,20 @@ class BatchCache:
         self.N = int(x.size(0))
         self.E = int(batch.edge_index.size(1))
         self.T = int(batch.lg_edge_index.size(1))
+        # host facts of a batch collated from a GraphStore (store.collate): in-degree bounds (the
+        # attention schedules are then built on the device) and the compacted line graph's size
+        hints = getattr(batch, "_alignn_hints", None) or {}
         self.ag = ops.GraphCSR(batch.edge_index, self.N)
         self.ag.xcd_chunk = self.ATOM_XCD_CHUNK
+        self.ag.deg_bound = hints.get("ag")
         if validate:
             self.ag.check_indices("edge_index")
         # a batch padded to a store.BatchCapacity: the ghost graph fills the compacted line graph up
         # to the capacity's size (and the loss covers the real graphs only, trainer)
         self.pad = getattr(batch, "_alignn_pad", None)
         self.real_graphs = getattr(batch, "num_real_graphs", None)
-        self.lg = self._line_graph(batch.lg_edge_index, self.E, validate, self.pad)
+        self.lg = self._line_graph(batch.lg_edge_index, self.E, validate, self.pad, hints.get("lg_active"))
+        self.lg.deg_bound = hints.get("lg")
         la = batch.lg_edge_attr
         self.angle_dim = int(la.size(-1)) if la.dim() == 2 else 0
         if self.T > 0 and la.numel() > 0:
@@ -174,8 +179,12 @@ class BatchCache:
     # flags) can be copied into the captured batch's buffers and the plan replayed unchanged.
     # -------------------------------------------------------------------------------------------
     def schedules(self) -> None:
-        """Builds the atom and line graphs' schedules with ONE device->host copy (their in-degrees
-        are needed on the host to order the work items) instead of one per graph."""
+        """Builds the atom and line graphs' schedules: on the device when the batch's in-degrees are
+        bounded on the host (store batches, GraphCSR.device_schedule_ok), else with ONE device->host
+        copy of both graphs' offsets (the in-degrees order the work items) instead of one per graph."""
+        for g in (self.ag, self.lg):   # host-bounded in-degrees: built on the device, no copy
+            if g._sched is None and g.device_schedule_ok():
+                g.schedule()
         gs = [g for g in (self.ag, self.lg) if g._sched is None]
         if len(gs) == 2:
             off = torch.cat([g.off_dst for g in gs]).cpu().numpy().astype(np.int64)
@@ -230,12 +239,15 @@ class BatchCache:
     COMPACT_FRACTION = 0.75
 
     @classmethod
-    def _line_graph(cls, edge_index: torch.Tensor, n: int, validate: bool, pad=None) -> ops.GraphCSR:
+    def _line_graph(cls, edge_index: torch.Tensor, n: int, validate: bool, pad=None,
+                    active_bound: Optional[int] = None) -> ops.GraphCSR:
         """CSR of the line graph, compacted when few bonds are active.  The active set is marked from
         the edge endpoints directly (no CSR of all n bonds is built first): one CSR build per batch.
         pad (a padded batch): compaction as its capacity says; with a compacted capacity, ghost bonds
         past the first pad['kg'] (those the ghost triplets use) join the active set until it has
-        pad['active'] members — device arithmetic, no host round trip."""
+        pad['active'] members — device arithmetic, no host round trip.  active_bound (a host bound
+        of the active count, store batches): the same filling up to that many, so the size needs no
+        device->host copy either (a bond without line-graph edges is inert in the compacted graph)."""
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError("edge_index must be int64 [2, m]")
         m = edge_index.size(1)
@@ -250,13 +262,20 @@ class BatchCache:
                 raise IndexError(f"lg_edge_index: edge index out of range [0, {n})")
         if pad is not None and pad["active"] is None:
             return ops.GraphCSR(edge_index, n)
+        if pad is None and active_bound is not None and not (0 < active_bound <= cls.COMPACT_FRACTION * n):
+            return ops.GraphCSR(edge_index, n)
         active = torch.zeros(n, dtype=torch.bool, device=edge_index.device)
         active[edge_index[0]] = True
         active[edge_index[1]] = True
         if pad is not None:
             active = cls._fill_active(active, pad["edges"] + pad["kg"], int(pad["active"]))
-        return cls._compact(active, edge_index, n, force=pad is not None,
-                            na=None if pad is None else int(pad["active"]))
+            na = int(pad["active"])
+        elif active_bound is not None:
+            active = cls._fill_active(active, n, int(active_bound))
+            na = int(active_bound)
+        else:
+            na = None
+        return cls._compact(active, edge_index, n, force=na is not None, na=na)
 
     @staticmethod
     def _fill_active(active: torch.Tensor, first: int, na: int) -> torch.Tensor:

@@ -612,7 +612,7 @@ class GraphCSR:
     """Target- and source-sorted CSR of one edge_index (see include/alignn_hip.h)."""
 
     __slots__ = ("n", "m", "off_dst", "perm_dst", "src_at", "dst_at", "off_src", "pos_src", "err", "_sched", "rows",
-                 "n_full", "cmap", "_dst_src", "xcd_chunk", "policy")
+                 "n_full", "cmap", "_dst_src", "xcd_chunk", "policy", "deg_bound")
 
     # in-degree above which a target node gets a 4-wave workgroup (LDS merge of the waves); below it
     # one wave walks the node's edges.  256: every node of the MP-like line graph (in-degree <= 132
@@ -640,6 +640,7 @@ class GraphCSR:
         self.rows = None     # compacted graph: int32 ids of its nodes in the full node set
         self.n_full = n
         self.cmap = None     # compacted graph: int32 [n_full] full row -> node id, -1 if inactive
+        self.deg_bound = None   # host bound of every in-degree (store batches): device-built schedule
         ws = WS.get("graph", 2 * n + 64, dev, torch.int32)
         check(_lib.lib().alignn_graph_prep(ei.data_ptr(), m, n, self.off_dst.data_ptr(), self.perm_dst.data_ptr(),
                                            self.src_at.data_ptr(), self.dst_at.data_ptr(), self.off_src.data_ptr(),
@@ -658,6 +659,8 @@ class GraphCSR:
         """Light/heavy target-node lists for the attention kernels (host-built once per graph:
         one small device->host copy of the offsets — or the in-degrees ``deg`` the caller fetched —
         numpy ordering, one upload)."""
+        if self._sched is None and deg is None and self.device_schedule_ok():
+            self._sched = self._schedule_on_device()
         if self._sched is None:
             if deg is None:
                 off = self.off_dst.cpu().numpy().astype(np.int64)
@@ -674,6 +677,28 @@ class GraphCSR:
             self._sched = (sc, light, heavy)
         return self._sched[0]
 
+    def device_schedule_ok(self) -> bool:
+        """The work list can be built on the device (alignn_schedule_build, no host round trip): the
+        caller bounded every in-degree on the host (deg_bound) below the heavy threshold — so there is
+        no heavy list and the light list holds all n targets — and the policy orders by degree."""
+        po = self.policy
+        return (self.deg_bound is not None and po.wave_items and 0 <= self.deg_bound <= po.heavy_threshold
+                and po.heavy_threshold <= 512 and po.xcds <= 8)
+
+    def _schedule_on_device(self):
+        po = self.policy
+        light = torch.empty(max(self.n, 1), dtype=torch.int32, device=self.off_dst.device)[:self.n]
+        check(_lib.lib().alignn_schedule_build(self.off_dst.data_ptr(), self.n, po.heavy_threshold,
+                                               po.xcds if po.xcd_items else 1, max(1, int(self.xcd_chunk)),
+                                               light.data_ptr() if self.n else None, self.err.data_ptr(),
+                                               stream_ptr()), "alignn_schedule_build")
+        heavy = light[:0]
+        sc = _lib.Schedule()
+        sc.light, sc.n_light = (light.data_ptr() if self.n else None), self.n
+        sc.heavy, sc.n_heavy = None, 0
+        sc.flags = _lib.SCHED_WAVE_ITEMS if po.wave_items else 0
+        return (sc, light, heavy)
+
     def family(self, D: int, H: int, F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor] = None) -> int:
         """Attention kernel family the library runs for this graph and operands (3: single-wave
         items, lgconv.hip; 2: light/heavy workgroups, tconv.hip); alignn_tconv_family."""
@@ -682,8 +707,11 @@ class GraphCSR:
 
     def check_indices(self, what: str) -> None:
         """Host check of the device error flag (one sync).  PyG raises IndexError here."""
-        if int(self.err.item()) != 0:
+        err = int(self.err.item())
+        if err & 1:
             raise IndexError(f"{what}: edge index out of range [0, {self.n})")
+        if err & 2:
+            raise RuntimeError(f"{what}: an in-degree exceeds the host bound the device schedule was built for")
 
 
 @dataclass(frozen=True)

@@ -244,6 +244,51 @@ class GraphStore:
         hi = (_excl_cumsum(n) + self._lg_spans()[gids][:, 1])[has]
         return int(hi.max()) < int(e.sum())
 
+    def _deg_max(self) -> Dict[str, np.ndarray]:
+        """Per stored graph: the largest in-degree of its atom graph ("ag": over its atoms) and of its
+        line graph ("lg": over its local bond ids), once, on the device."""
+        if getattr(self, "_degmax", None) is None:
+            out = {}
+            for f, rows in (("edge_index", "x"), ("lg_edge_index", "edge_index")):
+                if f not in self.arrays or rows not in self.counts:
+                    continue
+                a = self.arrays[f]
+                dev = a.device
+                cnt = torch.from_numpy(self.counts[f]).to(dev)
+                base = torch.repeat_interleave(torch.from_numpy(self.starts[rows]).to(dev), cnt,
+                                               output_size=a.size(1))
+                total = int(self.counts[rows].sum())
+                deg = torch.bincount(a[1] + base, minlength=total)[:total]
+                lens = torch.from_numpy(self.counts[rows]).to(dev)
+                mx = torch.segment_reduce(deg.double(), "max", lengths=lens, unsafe=True) if total else deg.double()
+                mx = torch.nan_to_num(mx, neginf=0.0).clamp(min=0.0)
+                out["ag" if f == "edge_index" else "lg"] = mx.cpu().numpy().astype(np.int64)
+            self._degmax = out
+        return self._degmax
+
+    def degree_bounds(self, gids: np.ndarray, lg_offset: str) -> Dict[str, int]:
+        """Host bounds of every in-degree of a batch of stored graphs ``gids`` (collate order): the
+        atom graph's is its graphs' largest; a line-graph bond's in-edges come from every graph whose
+        shifted window [increment, increment + bonds) holds it — disjoint windows under
+        lg_offset='num_edges', overlapping under PyG's 'num_nodes' rule — so its bound is the largest
+        sum of window maxima over any point (a sweep over the window ends)."""
+        dm = self._deg_max()
+        out = {}
+        if "ag" in dm:
+            out["ag"] = int(dm["ag"][gids].max()) if len(gids) else 0
+        if "lg" in dm:
+            m = dm["lg"][gids]
+            e = self.counts["edge_index"][gids].astype(np.int64)
+            if lg_offset == "num_edges" or len(gids) == 0:
+                out["lg"] = int(m.max()) if len(gids) else 0
+            else:
+                inc = _excl_cumsum(self.counts["x"][gids].astype(np.int64))
+                pos = np.concatenate([inc, inc + e])
+                val = np.concatenate([m, -m])
+                order = np.lexsort((val, pos))        # at one point, window ends (-) before starts (+)
+                out["lg"] = int(max(0, np.cumsum(val[order]).max()))
+        return out
+
     def batch_sizes(self, indices, lg_offset: str = "num_nodes") -> Dict[str, int]:
         """Host sizes of a batch: atoms, bonds, triplets, and an upper bound of the line graph's active
         bonds (union of each graph's touched-bond span shifted by its PyG increment)."""
@@ -506,6 +551,7 @@ class GraphStore:
         to it by one ghost graph (``num_real_graphs`` = the real graph count); a batch that does not
         fit is returned unpadded."""
         pl = self.plan(indices, lg_offset)
+        sample_index_np = pl.sample_index
         G = len(pl.idx)
         dev = next(iter(self.arrays.values())).device
         gh = None
@@ -590,6 +636,16 @@ class GraphStore:
         # batch's bond count, which lg_offset='num_nodes' does not imply (a graph with fewer bonds than
         # atoms): checked here on the host from the per-graph spans
         b._alignn_trusted = self.indices_checked and self._lg_bound_ok(pl.idx, lg_offset)
+        if b._alignn_trusted:
+            # host facts that let engine.BatchCache prepare the batch without a device->host copy: in-degree
+            # bounds (device-built attention schedules) and, unpadded under PyG's offset rule, the size of
+            # the compacted line graph (the span bound of batch_sizes; inert bonds fill it up)
+            hints = self.degree_bounds(pl.idx, lg_offset)
+            if gh is not None:
+                hints = {k: max(v, capacity.max_in_degree) for k, v in hints.items()}
+            elif lg_offset == "num_nodes" and "lg_edge_index" in pl.fields:
+                hints["lg_active"] = self.batch_sizes(sample_index_np, lg_offset)["active"]
+            b._alignn_hints = hints
         b.ptr = ptr.clone()
         b.sample_index = sample_index.clone()   # train.py:171 (dataset indices of the batch's graphs)
         b.num_graphs = G

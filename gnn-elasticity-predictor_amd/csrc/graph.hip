@@ -195,6 +195,112 @@ static int build_csr(const K* keys, int64_t m, int64_t n, int32_t* off, int32_t*
   return ALIGNN_OK;
 }
 
+
+// -------------------------------------------------------------------------------------------
+// Attention work lists on the device (ops.schedule_lists restated without the host round trip of
+// the in-degrees): every target with in-edges, longest in-edge list first within each of `xcds`
+// contiguous id ranges holding equal numbers of edges, the ranges interleaved in chunks of `chunk`
+// items, then the targets without in-edges.  One workgroup: pass 1 histograms (range, degree) in
+// LDS, pass 2 places each target at its rank.  Within one (range, degree) bucket the order is the
+// order of LDS atomics — every target is one work item whose outputs do not depend on where it
+// runs, so only the launch order (not a result bit) differs from the host lists.  Needs every
+// in-degree <= thr (the caller's host bound: no heavy list); a larger one sets *err.
+// -------------------------------------------------------------------------------------------
+constexpr int SCHED_MAX_THR = 512;
+constexpr int SCHED_MAX_XCDS = 8;
+
+__global__ __launch_bounds__(1024) void schedule_build_kernel(const int32_t* __restrict__ off, int64_t n, int thr,
+                                                              int xcds, int chunk, int32_t* __restrict__ light,
+                                                              int32_t* __restrict__ err) {
+  __shared__ int32_t cur[SCHED_MAX_XCDS][SCHED_MAX_THR + 1];   // histogram, then bucket cursors
+  __shared__ int64_t bounds[SCHED_MAX_XCDS + 1];
+  __shared__ int32_t cnt[SCHED_MAX_XCDS];
+  __shared__ int32_t nlit_s, zero_cur;
+  const int t = threadIdx.x;
+  for (int i = t; i < SCHED_MAX_XCDS * (SCHED_MAX_THR + 1); i += blockDim.x) (&cur[0][0])[i] = 0;
+  const int64_t tot = off[n];
+  // range x covers ids [bounds[x], bounds[x+1]): bounds[x] = first id whose inclusive edge count
+  // exceeds tot * x / xcds (numpy searchsorted(cumsum(deg), tot * x // xcds, 'right'))
+  if (t <= xcds) {
+    int64_t b;
+    if (t == 0) b = 0;
+    else if (t == xcds) b = n;
+    else {
+      const int64_t target = tot * t / xcds;
+      int64_t lo = 0, hi = n;        // first i in [0, n) with off[i + 1] > target
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if ((int64_t)off[mid + 1] > target) hi = mid;
+        else lo = mid + 1;
+      }
+      b = lo;
+    }
+    bounds[t] = b;
+  }
+  if (t == 0) { nlit_s = 0; zero_cur = 0; }
+  __syncthreads();
+  auto range_of = [&](int64_t i) {
+    int r = 0;
+    for (int x = 1; x < xcds; ++x) r += bounds[x] <= i;
+    return r;
+  };
+  int mylit = 0;
+  for (int64_t i = t; i < n; i += blockDim.x) {
+    const int d = off[i + 1] - off[i];
+    if (d > thr) {
+      atomicOr(err, 2);
+      continue;
+    }
+    if (d > 0) {
+      atomicAdd(&cur[range_of(i)][d], 1);
+      ++mylit;
+    }
+  }
+  atomicAdd(&nlit_s, mylit);
+  __syncthreads();
+  const int64_t nlit = nlit_s;
+  // fewer targets with in-edges than ranges: one range (the host rule: len(lit) > xcds)
+  const bool ranged = nlit > xcds;
+  if (!ranged) {
+    for (int d = t; d <= thr; d += blockDim.x) {
+      int32_t s = 0;
+      for (int x = 0; x < xcds; ++x) s += cur[x][d];
+      for (int x = 1; x < xcds; ++x) cur[x][d] = 0;
+      cur[0][d] = s;
+    }
+    __syncthreads();
+  }
+  // per range: exclusive starts over degrees in descending order
+  if (t < xcds) {
+    int32_t run = 0;
+    for (int d = thr; d >= 1; --d) {
+      const int32_t c = cur[t][d];
+      cur[t][d] = run;
+      run += c;
+    }
+    cnt[t] = run;
+  }
+  __syncthreads();
+  const int c = chunk < 1 ? 1 : chunk;
+  for (int64_t i = t; i < n; i += blockDim.x) {
+    const int d = off[i + 1] - off[i];
+    if (d > thr) continue;
+    if (d == 0) {
+      light[nlit + atomicAdd(&zero_cur, 1)] = (int32_t)i;
+      continue;
+    }
+    const int r = ranged ? range_of(i) : 0;
+    const int64_t k = atomicAdd(&cur[r][d], 1);   // rank within range r
+    const int64_t j = k / c;                        // round
+    int64_t pos = k % c;
+    for (int x = 0; x < xcds; ++x) {
+      const int64_t cx = cnt[x];
+      pos += min(cx, j * c);                        // every range's items of earlier rounds
+      if (x < r) pos += min((int64_t)c, max((int64_t)0, cx - j * c));   // earlier ranges, this round
+    }
+    light[pos] = (int32_t)i;
+  }
+}
 }  // namespace alignn
 
 using namespace alignn;
@@ -238,5 +344,21 @@ extern "C" int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int
   launch(scatter_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
                      out, ld_out, accumulate);
   ALIGNN_LAUNCH_CHECK("scatter_rows_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_schedule_build(const int32_t* off_dst, int64_t n, int32_t heavy_threshold, int32_t xcds,
+                                     int32_t chunk, int32_t* light, int32_t* err_flag, void* stream) {
+  if (n < 0 || n > 0x7ffffffeLL || heavy_threshold < 1 || heavy_threshold > SCHED_MAX_THR || xcds < 1 ||
+      xcds > SCHED_MAX_XCDS || chunk < 1) {
+    set_error("schedule_build: bad arguments n=%lld threshold=%d xcds=%d chunk=%d", (long long)n, heavy_threshold,
+              xcds, chunk);
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (n == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  launch(schedule_build_kernel, dim3(1), dim3(1024), 0, s, off_dst, n, (int)heavy_threshold, (int)xcds, (int)chunk,
+         light, err_flag);
+  ALIGNN_LAUNCH_CHECK("schedule_build_kernel");
   return ALIGNN_OK;
 }

@@ -208,6 +208,16 @@ int alignn_graph_prep(const int64_t* edge_index, int64_t m, int64_t n,
                       int32_t* off_src, int32_t* pos_src,
                       int32_t* workspace, int32_t* err_flag, void* stream);
 
+/* The attention work list (AlignnSchedule.light, every one of the n targets) built on the device
+ * from alignn_graph_prep's off_dst, without copying the in-degrees to the host: targets with
+ * in-edges, longest in-edge list first within each of `xcds` contiguous id ranges of equal edge
+ * count, interleaved range by range in chunks of `chunk` items, then the targets without in-edges
+ * (ops.schedule_lists' order up to ties; every target is one work item, so no result depends on
+ * it).  For callers that bound every in-degree by heavy_threshold on the host (no heavy list: a
+ * larger in-degree ORs 2 into *err_flag).  heavy_threshold <= 512, xcds <= 8.  One workgroup. */
+int alignn_schedule_build(const int32_t* off_dst, int64_t n, int32_t heavy_threshold, int32_t xcds,
+                          int32_t chunk, int32_t* light, int32_t* err_flag, void* stream);
+
 /* rows_out[i, :] = rows_in[idx[i], :] (float, ld in elements).  Used to lay per-edge inputs out
  * in target-sorted order (lg_edge_attr, train.py:553-554) once per batch. */
 int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int32_t* idx, int64_t rows,

@@ -241,3 +241,82 @@ def test_c3_size_fp32_forward_vs_oracle():
         rmean, rlogvar = model_ref.hetero_forward(st, rb, 4)
     assert rel_err(mean, rmean) < 1e-4
     assert rel_err(logvar, rlogvar) < 1e-4
+
+
+# ------------------------------------------------------------------------------------------------
+# Store batches prepared without device->host copies (device-built schedules, host-sized compaction)
+# ------------------------------------------------------------------------------------------------
+def _host_and_device_lists(g):
+    import numpy as np
+    from alignn_mi355x import ops
+    off = g.off_dst.cpu().numpy().astype(np.int64)
+    deg = off[1:] - off[:-1]
+    po = g.policy
+    light, heavy = ops.schedule_lists(deg, po.heavy_threshold, po.wave_items, po.xcd_items and po.wave_items,
+                                      po.xcds, g.xcd_chunk)
+    g._sched = None
+    g.deg_bound = int(deg.max()) if len(deg) else 0
+    sc = g.schedule()
+    dev = g._sched[1].cpu().numpy().astype(np.int64)
+    assert sc.n_heavy == 0 and len(heavy) == 0 and sc.n_light == g.n
+    return deg, off, light, dev
+
+
+@pytest.mark.parametrize("which,B,lg_offset,chunk", [("lg", 32, "num_nodes", 1), ("ag", 32, "num_nodes", 4),
+                                                     ("lg", 4, "num_edges", 1), ("lg", 1, "num_nodes", 1),
+                                                     ("ag", 256, "num_nodes", 4), ("lg", 256, "num_nodes", 1)])
+def test_device_schedule_matches_host_lists_up_to_ties(which, B, lg_offset, chunk):
+    """alignn_schedule_build against ops.schedule_lists: the same targets, and at every position a
+    target of the same in-degree from the same XCD id range (only ties are ordered differently)."""
+    import numpy as np
+    from alignn_mi355x.engine import batch_cache
+    from alignn_mi355x.synthetic import mp_like_batch
+    b = mp_like_batch(B, lg_offset=lg_offset).to(DEV)
+    bc = batch_cache(b)
+    g = bc.lg if which == "lg" else bc.ag
+    g.xcd_chunk = chunk
+    deg, off, host, dev = _host_and_device_lists(g)
+    assert sorted(dev.tolist()) == list(range(g.n))
+    assert np.array_equal(deg[dev], deg[host])
+    tot = int(off[-1])
+    bounds = np.asarray([0] + [int(np.searchsorted(off[1:], tot * x // 8, side="right")) for x in range(1, 8)]
+                        + [g.n])
+    rng_of = lambda ids: np.searchsorted(bounds, ids, side="right") - 1   # noqa: E731
+    lit = deg[host] > 0
+    if int(lit.sum()) > 8:
+        assert np.array_equal(rng_of(dev[lit]), rng_of(host[lit]))
+
+
+def test_store_batch_prepares_without_a_host_sync_and_trains_bitwise_equal():
+    """A store-collated batch carries host bounds (in-degrees, compacted line-graph size): collate +
+    prepare_batch then run under torch's sync debug mode set to error (no .item / .cpu / nonzero), and
+    the training step on it equals the step on the same batch prepared the synchronous way."""
+    import numpy as np
+    import alignn_mi355x as A
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_graph
+    st = GraphStore.from_data_list([mp_like_graph(g) for g in range(40)], DEV)
+    sel = np.random.default_rng(3).choice(40, size=32, replace=False)
+    st.collate(sel)                      # first use: the store's one-time per-graph statistics
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        b_fast = st.collate(sel)
+        prepare_batch(b_fast)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert b_fast._alignn_cache.lg.device_schedule_ok() and b_fast._alignn_cache.ag.device_schedule_ok()
+    b_slow = st.collate(sel)
+    del b_slow._alignn_hints
+    prepare_batch(b_slow)
+    assert b_slow._alignn_cache.lg.n == b_fast._alignn_cache.lg.n == 2580
+    grads = []
+    for b in (b_fast, b_slow):
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(DEV)
+        tr = A.FusedTrainer(model)
+        tr.forward_backward(b, 5)
+        grads.append(tr.st.grad.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(grads[0], grads[1])

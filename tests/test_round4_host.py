@@ -89,3 +89,34 @@ def test_replay_refuses_exchange_changed_after_capture(monkeypatch):
     tr.grad_hook = lambda g: calls.append(2)   # a different hook object is a different exchange
     with pytest.raises(RuntimeError, match="exchange changed after capture"):
         tr.step(batch, seed=3)
+
+
+@pytest.mark.parametrize("lg_offset", ["num_nodes", "num_edges"])
+def test_store_degree_and_active_bounds_cover_the_collated_batch(lg_offset):
+    """GraphStore.degree_bounds / batch_sizes['active'] (the host facts behind a store batch's device-
+    built schedules and sync-free compaction): every in-degree of the collated atom and line graphs and
+    the line graph's active-bond count lie within them, on graphs of mixed sizes (overlapping PyG
+    windows of different widths) — and on MP-like graphs they are exact."""
+    from alignn_mi355x.data import Batch
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_graph
+    sizes = [(60, 6), (24, 3), (40, 5), (13, 2), (60, 6), (31, 4), (9, 1)]
+    mixed = [mp_like_graph(g, n_atoms=sizes[g % 7][0], half_degree=sizes[g % 7][1]) for g in range(14)]
+    mp = [mp_like_graph(g) for g in range(12)]
+    rng = np.random.default_rng(7)
+    for gs, exact in ((mixed, False), (mp, True)):
+        st = GraphStore.from_data_list(gs, "cpu")
+        for _ in range(6):
+            sel = rng.choice(len(gs), size=int(rng.integers(1, len(gs))), replace=False)
+            b = Batch.from_data_list([gs[i] for i in sel], lg_offset=lg_offset)
+            hb = st.degree_bounds(st.ids[sel], lg_offset)
+            E = b.edge_index.size(1)
+            ag = int(torch.bincount(b.edge_index[1], minlength=b.x.size(0)).max())
+            lg = int(torch.bincount(b.lg_edge_index[1], minlength=E).max())
+            act = torch.zeros(E, dtype=torch.bool)
+            act[b.lg_edge_index[0]] = True
+            act[b.lg_edge_index[1]] = True
+            bound_act = st.batch_sizes(sel, lg_offset)["active"]
+            assert ag <= hb["ag"] and lg <= hb["lg"] and int(act.sum()) <= bound_act, (list(sel), hb)
+            if exact:
+                assert (ag, lg, int(act.sum())) == (hb["ag"], hb["lg"], bound_act)
