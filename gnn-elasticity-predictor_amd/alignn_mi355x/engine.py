@@ -265,8 +265,8 @@ class BatchCache:
         if pad is None and active_bound is not None and not (0 < active_bound <= cls.COMPACT_FRACTION * n):
             return ops.GraphCSR(edge_index, n)
         active = torch.zeros(n, dtype=torch.bool, device=edge_index.device)
-        active[edge_index[0]] = True
-        active[edge_index[1]] = True
+        active.index_fill_(0, edge_index[0], True)    # (index_fill_: no host sync, unlike index_put_)
+        active.index_fill_(0, edge_index[1], True)
         if pad is not None:
             active = cls._fill_active(active, pad["edges"] + pad["kg"], int(pad["active"]))
             na = int(pad["active"])
@@ -738,13 +738,6 @@ class AlignnEngine:
         # bf16 storage: the line-graph attention (forward, target-side backward) on the matrix cores
         # (lgmma.hip; D = 256, H = 4) instead of the VALU kernels (lgconv.hip)
         self.attn_mfma = False
-        # precision "fp32": the GEMMs' fp32 operands as three exact bf16 words on the bf16 matrix cores
-        # (ALIGNN_GEMM_F32X3: fp32-class accuracy, 6 x 32 instead of 8 x 64 MFMA cycles per 16-deep
-        # slice) instead of the f32 MFMA
-        self.gemm_x3 = False
-
-    def _gemm_precision(self) -> str:
-        return "fp32x3" if self.precision == "fp32" and self.gemm_x3 else self.precision
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
@@ -799,7 +792,7 @@ class AlignnEngine:
 
     def forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
                 x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
-        with ops.using(self.ctx), ops.gemm_precision(self._gemm_precision()):
+        with ops.using(self.ctx), ops.gemm_precision(self.precision):
             return self._forward(P, batch, bc, training, seed, x, global_x, mode)
 
     def backward(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor, between=None) -> None:
@@ -814,14 +807,14 @@ class AlignnEngine:
 
     def backward_layers(self, P: FlatViews, G: FlatViews, ctx, dout: torch.Tensor):
         """Heads, readout and the L x (node block, edge block) backward; returns the tail's state."""
-        with ops.using(self.ctx), ops.gemm_precision(self._gemm_precision()):
+        with ops.using(self.ctx), ops.gemm_precision(self.precision):
             self.ctx.new_pass()
             return self._backward_layers(P, G, ctx, dout)
 
     def backward_tail(self, t) -> None:
         """The edge-projection chain rules, the deferred angle-encoder backward and the encoder MLPs'
         backward, then the join of every stream into the current one."""
-        with ops.using(self.ctx), ops.gemm_precision(self._gemm_precision()):
+        with ops.using(self.ctx), ops.gemm_precision(self.precision):
             self._backward_tail(t)
 
     def _forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,

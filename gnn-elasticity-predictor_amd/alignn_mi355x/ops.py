@@ -342,21 +342,17 @@ GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
 GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
 GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an operand / the output
-GEMM_F32X3 = 8192     # ALIGNN_GEMM_F32X3: fp32 operands as three bf16 words on the bf16 matrix cores
 
 
 @contextmanager
 def gemm_precision(precision: str):
-    """GEMMs issued inside run with "fp32" (exact fp32 MFMA), "fp32x3" (fp32 operands split
-    exactly into three bf16 words, six cross products on the bf16 matrix cores, fp32 accumulation:
-    fp32-class accuracy, ALIGNN_GEMM_F32X3) or "bf16" arithmetic (bf16-rounded inputs on
-    v_mfma_f32_32x32x16_bf16, fp32 accumulation and output: ALIGNN_GEMM_BF16)."""
+    """GEMMs issued inside run with "fp32" (exact fp32 MFMA) or "bf16" arithmetic (bf16-rounded
+    inputs on v_mfma_f32_32x32x16_bf16, fp32 accumulation and output: ALIGNN_GEMM_BF16)."""
     global _GEMM_FLAGS
-    flags = {"fp32": 0, "fp32x3": GEMM_F32X3, "bf16": GEMM_BF16}
-    if precision not in flags:
-        raise ValueError(f"precision must be 'fp32', 'fp32x3' or 'bf16', got {precision!r}")
+    if precision not in ("fp32", "bf16"):
+        raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
     prev = _GEMM_FLAGS
-    _GEMM_FLAGS = flags[precision]
+    _GEMM_FLAGS = GEMM_BF16 if precision == "bf16" else 0
     try:
         yield
     finally:

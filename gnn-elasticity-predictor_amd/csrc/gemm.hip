@@ -1,6 +1,6 @@
 // gemm.hip — GEMM entry points (alignn_gemm_f32 / _workspace / _path): plan, split-K reduce, the bf16
 // streaming kernel and the column sums.  The tiled kernels live in gemm_tile.h, instantiated per
-// arithmetic in gemm_tile_p0/1/2.hip.
+// arithmetic in gemm_tile_p0/1.hip.
 #include <cstring>
 
 #include "gemm_tile.h"
@@ -439,7 +439,6 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
   const bool np = (a->tile & ALIGNN_GEMM_NOPIPE) != 0;
   if (a->tile & ALIGNN_GEMM_BF16) gemm_tiled_launch<1>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
-  else if (a->tile & ALIGNN_GEMM_F32X3) gemm_tiled_launch<2>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   else gemm_tiled_launch<0>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {

@@ -238,21 +238,6 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int64_t b, 
   return v;
 }
 
-// x = hi + mid + lo, three bf16 words (RNE each; x - hi and (x - hi) - mid are exact in fp32).  A
-// non-finite hi keeps mid = lo = 0, so inf and NaN propagate as through the f32 MFMA (inf - inf
-// would turn an inf operand into NaN).
-__device__ __forceinline__ void split3(const float (&f)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const __bf16 a = (__bf16)f[s];
-    const float r1 = __builtin_isfinite((float)a) ? f[s] - (float)a : 0.f;
-    const __bf16 b = (__bf16)r1;
-    h[s] = a;
-    m[s] = b;
-    l[s] = (__bf16)(r1 - (float)b);
-  }
-}
-
 // One LDS stage of MFMAs: BKT/16 slices of the wave's (BM/2) x (BN/2) subtile, from an LDS image of
 // depth LD (>= BKT: the wave-group K-split kernel reads its group's slices `sub0..` of a deeper stage).
 template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int BF, int LD = BKT>
@@ -268,27 +253,7 @@ __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], con
     for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, LD>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
 #pragma unroll
     for (int j = 0; j < NI; ++j) read_frag<BN, B_KC, LD>(Bs, wn * (BN / 2) + j * 32 + l32, h, sub, fb[j]);
-    if constexpr (BF == 2) {
-      // fp32 as three bf16 words (x = hi + mid + lo exactly: each word is the RNE of what the
-      // previous ones leave, and the residuals are exact in fp32); the six products down to
-      // 2^-16 relative of hi*hi, smallest first — every dropped term is below 2^-24 |a b|.
-      bf16x8 ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) split3(fa[i], ah[i], am[i], al[i]);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) split3(fb[j], bh[j], bm[j], bl[j]);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    } else if constexpr (BF == 1) {
+    if constexpr (BF == 1) {
       bf16x8 ha[MI], hb[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -581,8 +546,8 @@ static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, 
   else launch_tile<BM, BN, false, false, PR>(p, grid, bk, nopipe, s);
 }
 
-// The tiled kernels of one arithmetic (PR: 0 exact fp32 on v_mfma_f32_32x32x2_f32, 1 bf16 inputs,
-// 2 fp32 as three bf16 words), instantiated in gemm_tile_p<PR>.hip (one translation unit each).
+// The tiled kernels of one arithmetic (PR: 0 exact fp32 on v_mfma_f32_32x32x2_f32, 1 bf16 inputs),
+// instantiated in gemm_tile_p<PR>.hip (one translation unit each).
 template <int PR>
 void gemm_tiled_launch(const GemmParams& p, int bm, int bn, bool akc, bool bkc, dim3 grid, int bk, bool nopipe,
                        hipStream_t s) {
@@ -594,6 +559,5 @@ void gemm_tiled_launch(const GemmParams& p, int bm, int bn, bool akc, bool bkc, 
 
 extern template void gemm_tiled_launch<0>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
 extern template void gemm_tiled_launch<1>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
-extern template void gemm_tiled_launch<2>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
 
 }  // namespace alignn

@@ -199,24 +199,29 @@ static int build_csr(const K* keys, int64_t m, int64_t n, int32_t* off, int32_t*
 // -------------------------------------------------------------------------------------------
 // Attention work lists on the device (ops.schedule_lists restated without the host round trip of
 // the in-degrees): every target with in-edges, longest in-edge list first within each of `xcds`
-// contiguous id ranges holding equal numbers of edges, the ranges interleaved in chunks of `chunk`
-// items, then the targets without in-edges.  One workgroup: pass 1 histograms (range, degree) in
-// LDS, pass 2 places each target at its rank.  Within one (range, degree) bucket the order is the
-// order of LDS atomics — every target is one work item whose outputs do not depend on where it
-// runs, so only the launch order (not a result bit) differs from the host lists.  Needs every
-// in-degree <= thr (the caller's host bound: no heavy list); a larger one sets *err.
+// contiguous id ranges holding equal numbers of edges (ties in ascending id), the ranges interleaved
+// in chunks of `chunk` items, then the targets without in-edges in ascending id — the host lists
+// exactly.  One workgroup of 16 waves: pass 1 histograms (range, degree) in LDS; pass 2 walks each
+// range in id order, 1024 targets at a time, and places each at its stable rank (rank among equal
+// in-degrees within its wave from a ballot per distinct degree, plus the counts of the earlier waves
+// of the block and of the earlier blocks).  The order matters for speed, not results: targets of one
+// degree adjacent in id share their sources' rows in L2.  Needs every in-degree <= thr (the caller's
+// host bound: no heavy list); a larger one sets bit 2 of *err.
 // -------------------------------------------------------------------------------------------
 constexpr int SCHED_MAX_THR = 512;
 constexpr int SCHED_MAX_XCDS = 8;
+constexpr int SCHED_WAVES = 16;
 
 __global__ __launch_bounds__(1024) void schedule_build_kernel(const int32_t* __restrict__ off, int64_t n, int thr,
                                                               int xcds, int chunk, int32_t* __restrict__ light,
                                                               int32_t* __restrict__ err) {
   __shared__ int32_t cur[SCHED_MAX_XCDS][SCHED_MAX_THR + 1];   // histogram, then bucket cursors
+  __shared__ int32_t wcnt[SCHED_WAVES][SCHED_MAX_THR + 1];     // one block of 1024: per-wave counts by degree
   __shared__ int64_t bounds[SCHED_MAX_XCDS + 1];
   __shared__ int32_t cnt[SCHED_MAX_XCDS];
-  __shared__ int32_t nlit_s, zero_cur;
-  const int t = threadIdx.x;
+  __shared__ int32_t nlit_s, zbase;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint64_t below = (1ull << lane) - 1;
   for (int i = t; i < SCHED_MAX_XCDS * (SCHED_MAX_THR + 1); i += blockDim.x) (&cur[0][0])[i] = 0;
   const int64_t tot = off[n];
   // range x covers ids [bounds[x], bounds[x+1]): bounds[x] = first id whose inclusive edge count
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(1024) void schedule_build_kernel(const int32_t* __r
     }
     bounds[t] = b;
   }
-  if (t == 0) { nlit_s = 0; zero_cur = 0; }
+  if (t == 0) { nlit_s = 0; zbase = 0; }
   __syncthreads();
   auto range_of = [&](int64_t i) {
     int r = 0;
@@ -259,7 +264,7 @@ __global__ __launch_bounds__(1024) void schedule_build_kernel(const int32_t* __r
   atomicAdd(&nlit_s, mylit);
   __syncthreads();
   const int64_t nlit = nlit_s;
-  // fewer targets with in-edges than ranges: one range (the host rule: len(lit) > xcds)
+  // fewer targets with in-edges than ranges: one range over all ids (the host rule: len(lit) > xcds)
   const bool ranged = nlit > xcds;
   if (!ranged) {
     for (int d = t; d <= thr; d += blockDim.x) {
@@ -282,23 +287,66 @@ __global__ __launch_bounds__(1024) void schedule_build_kernel(const int32_t* __r
   }
   __syncthreads();
   const int c = chunk < 1 ? 1 : chunk;
-  for (int64_t i = t; i < n; i += blockDim.x) {
-    const int d = off[i + 1] - off[i];
-    if (d > thr) continue;
-    if (d == 0) {
-      light[nlit + atomicAdd(&zero_cur, 1)] = (int32_t)i;
-      continue;
+  const int nr = ranged ? xcds : 1;
+  for (int r = 0; r < nr; ++r) {
+    const int64_t b0 = ranged ? bounds[r] : 0, b1 = ranged ? bounds[r + 1] : n;
+    for (int64_t c0 = b0; c0 < b1; c0 += blockDim.x) {
+      for (int i = t; i < SCHED_WAVES * (thr + 1); i += blockDim.x) wcnt[i / (thr + 1)][i % (thr + 1)] = 0;
+      __syncthreads();
+      const int64_t i = c0 + t;
+      int d = 0;
+      if (i < b1) {
+        d = off[i + 1] - off[i];
+        if (d > thr) d = 0;
+      }
+      int rank = 0;
+      if (d > 0) {
+        const uint64_t same = key_group(d);
+        rank = __popcll(same & below);
+        if (lane == __ffsll((unsigned long long)same) - 1) wcnt[w][d] = __popcll(same);
+      }
+      __syncthreads();
+      if (d > 0) {
+        int32_t pre = 0;
+        for (int w2 = 0; w2 < w; ++w2) pre += wcnt[w2][d];
+        const int64_t k = (int64_t)cur[r][d] + pre + rank;   // stable rank within range r
+        const int64_t j = k / c;                              // round
+        int64_t pos = k % c;
+        for (int x = 0; x < xcds; ++x) {
+          const int64_t cx = cnt[x];
+          pos += min(cx, j * c);                              // every range's items of earlier rounds
+          if (x < r) pos += min((int64_t)c, max((int64_t)0, cx - j * c));   // earlier ranges, this round
+        }
+        light[pos] = (int32_t)i;
+      }
+      __syncthreads();
+      for (int dd = t + 1; dd <= thr; dd += blockDim.x) {
+        int32_t s = 0;
+        for (int w2 = 0; w2 < SCHED_WAVES; ++w2) s += wcnt[w2][dd];
+        cur[r][dd] += s;
+      }
+      __syncthreads();
     }
-    const int r = ranged ? range_of(i) : 0;
-    const int64_t k = atomicAdd(&cur[r][d], 1);   // rank within range r
-    const int64_t j = k / c;                        // round
-    int64_t pos = k % c;
-    for (int x = 0; x < xcds; ++x) {
-      const int64_t cx = cnt[x];
-      pos += min(cx, j * c);                        // every range's items of earlier rounds
-      if (x < r) pos += min((int64_t)c, max((int64_t)0, cx - j * c));   // earlier ranges, this round
+  }
+  // targets without in-edges, ascending id, after every listed target
+  for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
+    const int64_t i = c0 + t;
+    const bool z = i < n && off[i + 1] == off[i];
+    const uint64_t zm = __ballot(z);
+    if (lane == 0) wcnt[w][0] = __popcll(zm);
+    __syncthreads();
+    if (z) {
+      int32_t pre = zbase;
+      for (int w2 = 0; w2 < w; ++w2) pre += wcnt[w2][0];
+      light[nlit + pre + __popcll(zm & below)] = (int32_t)i;
     }
-    light[pos] = (int32_t)i;
+    __syncthreads();
+    if (t == 0) {
+      int32_t s = 0;
+      for (int w2 = 0; w2 < SCHED_WAVES; ++w2) s += wcnt[w2][0];
+      zbase += s;
+    }
+    __syncthreads();
   }
 }
 }  // namespace alignn

@@ -93,11 +93,6 @@ typedef struct AlignnGemmArgs {
 #define ALIGNN_GEMM_A_BF16 1024
 #define ALIGNN_GEMM_B_BF16 2048
 #define ALIGNN_GEMM_C_BF16 4096
-/* fp32 inputs as three bf16 words each (x = hi + mid + lo exactly) on v_mfma_f32_32x32x16_bf16: the
- * six cross products down to 2^-16 of hi*hi (every dropped term below 2^-24 |a b|), fp32 accumulation
- * — fp32-class accuracy (not the f32 MFMA's bits) at 6 x 32 instead of 8 x 64 MFMA cycles per
- * 16-deep slice.  Ignored with ALIGNN_GEMM_BF16. */
-#define ALIGNN_GEMM_F32X3 8192
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
@@ -212,8 +207,8 @@ int alignn_graph_prep(const int64_t* edge_index, int64_t m, int64_t n,
  * from alignn_graph_prep's off_dst, without copying the in-degrees to the host: targets with
  * in-edges, longest in-edge list first within each of `xcds` contiguous id ranges of equal edge
  * count, interleaved range by range in chunks of `chunk` items, then the targets without in-edges
- * (ops.schedule_lists' order up to ties; every target is one work item, so no result depends on
- * it).  For callers that bound every in-degree by heavy_threshold on the host (no heavy list: a
+ * (ops.schedule_lists' lists exactly; every target is one work item, so no result depends on the
+ * order, only the L2 reuse of the sources' rows).  For callers that bound every in-degree by heavy_threshold on the host (no heavy list: a
  * larger in-degree ORs 2 into *err_flag).  heavy_threshold <= 512, xcds <= 8.  One workgroup. */
 int alignn_schedule_build(const int32_t* off_dst, int64_t n, int32_t heavy_threshold, int32_t xcds,
                           int32_t chunk, int32_t* light, int32_t* err_flag, void* stream);

@@ -222,13 +222,11 @@ def test_c2_batch32_autograd_vs_oracle():
     _check_grads(((k, p.grad) for k, p in model.named_parameters()), rgrads, c["tols"])
 
 
-@pytest.mark.parametrize("mode", ["plan", "eager", "plan_x3"])
+@pytest.mark.parametrize("mode", ["plan", "eager"])
 def test_c2_batch32_fused_step_vs_oracle(mode):
     """The bench's own step (FusedTrainer, native launch plan replay at B = 32, the timed path of
     bench.py) against the fp64 oracle: the loss and every parameter gradient of the replayed step
-    (the flat gradient buffer, read before the next step), then the AdamW update itself.  plan_x3:
-    the GEMMs' fp32 operands as three bf16 words (engine option gemm_x3, ALIGNN_GEMM_F32X3) under
-    the same tolerances."""
+    (the flat gradient buffer, read before the next step), then the AdamW update itself."""
     import alignn_mi355x as A
     from alignn_mi355x import FusedTrainer
     from alignn_mi355x.layout import offsets
@@ -237,12 +235,11 @@ def test_c2_batch32_fused_step_vs_oracle(mode):
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.0), 2)
     model.load_state_dict(c["st"])
     model.to(DEV).train()
-    model._engine.gemm_x3 = mode.endswith("_x3")
     b = c["batch"].to(DEV)
     tr = FusedTrainer(model, feature_jitter_std=0.0, target_log_means=(4.3228, 3.5567),
                       target_log_stds=(0.9051, 0.9405))
     before = tr.st.flat.clone()
-    if mode.startswith("plan"):
+    if mode == "plan":
         tr.capture(b, mode="plan")
         assert torch.equal(tr.st.flat, before)  # capture leaves the state as it was
     loss = tr.step(b, seed=7)

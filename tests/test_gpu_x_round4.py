@@ -265,9 +265,10 @@ def _host_and_device_lists(g):
 @pytest.mark.parametrize("which,B,lg_offset,chunk", [("lg", 32, "num_nodes", 1), ("ag", 32, "num_nodes", 4),
                                                      ("lg", 4, "num_edges", 1), ("lg", 1, "num_nodes", 1),
                                                      ("ag", 256, "num_nodes", 4), ("lg", 256, "num_nodes", 1)])
-def test_device_schedule_matches_host_lists_up_to_ties(which, B, lg_offset, chunk):
-    """alignn_schedule_build against ops.schedule_lists: the same targets, and at every position a
-    target of the same in-degree from the same XCD id range (only ties are ordered differently)."""
+def test_device_schedule_equals_host_lists(which, B, lg_offset, chunk):
+    """alignn_schedule_build against ops.schedule_lists: the same list, element for element (a stable
+    order: ties in ascending id), and so at every position a target of the same in-degree from the
+    same XCD id range."""
     import numpy as np
     from alignn_mi355x.engine import batch_cache
     from alignn_mi355x.synthetic import mp_like_batch
@@ -277,6 +278,7 @@ def test_device_schedule_matches_host_lists_up_to_ties(which, B, lg_offset, chun
     g.xcd_chunk = chunk
     deg, off, host, dev = _host_and_device_lists(g)
     assert sorted(dev.tolist()) == list(range(g.n))
+    assert np.array_equal(dev, host)
     assert np.array_equal(deg[dev], deg[host])
     tot = int(off[-1])
     bounds = np.asarray([0] + [int(np.searchsorted(off[1:], tot * x // 8, side="right")) for x in range(1, 8)]

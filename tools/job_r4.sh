@@ -29,6 +29,7 @@ pmc() {   # pmc NAME COUNTERS BENCHARGS...
 for st in "$@"; do
   case "$st" in
     new) run new 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py tests/test_gpu_x_lgmma.py ;;
+    sched) run sched 600 "${PT[@]}" tests/test_gpu_x_round4.py -k "schedule or sync" tests/test_gpu_x_store.py tests/test_gpu_x_capacity.py ;;
     lgm) run lgm 300 python tools/lgm_bench.py --reps 20 ;;
     lgmv) for v in gnn-elasticity-predictor_amd/alignn_mi355x/variants/*.so; do
             ALIGNN_HIP_LIB=$v run "lgm_$(basename $v .so)" 300 python tools/lgm_bench.py --reps 20
@@ -41,9 +42,6 @@ for st in "$@"; do
     c3) run c3 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_c3.json" ;;
     hostprof) run hostprof 300 python -u tools/host_prep_profile.py --graphs 2000 --steps 30 ;;
     gemmbf) run gemmbf 300 python -u tools/gemm_bench.py --quick --reps 10 --flag 64 ;;
-    gemmx3) run gemmx3 300 python -u tools/gemm_bench.py --quick --reps 10 --flag 8192 ;;
-    x3t) run x3t 600 "${PT[@]}" tests/test_gpu_x_gemm_x3.py "tests/test_gpu_parity.py::test_c2_batch32_fused_step_vs_oracle" ;;
-    qx3) run qx3 300 python "${Q[@]}" --steps 20 --warmup 5 --set engine.gemm_x3=1 --dump-probes "$O/probes_qx3.json" ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
