@@ -486,8 +486,9 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.mstat = torch.empty(na, H, device=dev)
     c.den = torch.empty(na, H, device=dev)
     c.KV16 = None
-    if F is not None and F.dtype == torch.bfloat16:
-        # bf16 storage (config C3): the attention gathers K|V from a bf16 copy and streams bf16 F rows
+    if F is not None and F.dtype == torch.bfloat16 and feat_row is None:
+        # bf16 storage (config C3), the line graph: the attention gathers K|V from a bf16 copy and streams
+        # the bf16 angle hidden layer (the atom graph's bf16 bond-state rows go through tconv_fwd)
         c.KV16 = ops.cast_bf16(c.QKV[:, D:3 * D])
         c.mfma = mfma and D == 256 and H == 4
         fwd = ops.lg_fwd_mfma if c.mfma else ops.lg_fwd_bf16
@@ -738,6 +739,9 @@ class AlignnEngine:
         # bf16 storage: the line-graph attention (forward, target-side backward) on the matrix cores
         # (lgmma.hip; D = 256, H = 4) instead of the VALU kernels (lgconv.hip)
         self.attn_mfma = False
+        # bf16 storage: the atom-graph attention reads the bond state's bf16 copy (the gate kernel's
+        # Xn16; autocast casts the bond state to bf16 for edge_proj) as its edge-feature rows
+        self.atom_bf16 = True
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
@@ -887,15 +891,17 @@ class AlignnEngine:
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
                                      skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
-                                     want_X16=bf16_io and l + 1 < L, mfma=self.attn_mfma)
+                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16), mfma=self.attn_mfma)
                 e16 = c.Xn16
             else:
                 c = None
             ctx.edge.append(c)
             # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
             if E > 0:
-                with _side_work(aux, (e, h, ctx.M_all, ctx.wbar_all)):
-                    h, c = block_forward(P.node[l], h, bc.ag, e, bc.ag.perm_dst, ctx.M_all[l], ctx.wbar_all[l], H,
+                # bf16 storage: the bond-state rows as autocast hands them to edge_proj (bf16)
+                ef = e16 if (bf16_io and self.atom_bf16 and e16 is not None) else e
+                with _side_work(aux, (e, ef, h, ctx.M_all, ctx.wbar_all)):
+                    h, c = block_forward(P.node[l], h, bc.ag, ef, bc.ag.perm_dst, ctx.M_all[l], ctx.wbar_all[l], H,
                                          p_drop, site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
             else:
                 c = None

@@ -697,7 +697,10 @@ class GraphCSR:
 
     def family(self, D: int, H: int, F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor] = None) -> int:
         """Attention kernel family the library runs for this graph and operands (3: single-wave
-        items, lgconv.hip; 2: light/heavy workgroups, tconv.hip); alignn_tconv_family."""
+        items, lgconv.hip; 2: light/heavy workgroups, tconv.hip); alignn_tconv_family.  bf16 feature
+        rows (alignn_tconv_fwd_ex) always take family 2."""
+        if F is not None and F.dtype == torch.bfloat16:
+            return 2
         return int(_lib.lib().alignn_tconv_family(D, H, None if feat_row is None else feat_row.data_ptr(),
                                                    None if F is None else F.data_ptr(), ctypes.byref(self.schedule())))
 
@@ -794,11 +797,12 @@ def scatter_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, accumu
     return out
 
 
-def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, dF_rw: int = 1) -> float:
+def _tconv_bytes(n: int, m: int, D: int, H: int, kind: str, dF_rw: int = 1, f_elem: int = 4) -> float:
     """Compulsory HBM bytes of one launch (every operand touched once, ideal caching).
-    dF_rw: [m, D] edge-feature gradient rows moved by bwd_dst (0 none, 1 written, 2 read + written)."""
+    dF_rw: [m, D] edge-feature gradient rows moved by bwd_dst (0 none, 1 written, 2 read + written).
+    f_elem: bytes per edge-feature element read (2: bf16 rows)."""
     f = 4.0
-    feat = m * D
+    feat = m * D * f_elem / 4.0
     if kind == "fwd":   # Q,K,V + U + edge features + CSR in; aggV + S + 3 stats out
         return f * (3 * n * D + n * H * D + feat + 2 * m + n + n * D + n * H * D + 3 * n * H)
     if kind == "bwd_dst":  # Q,K,V,U,Vd,dout,outp,features,stats in; dQ,Sz,sigz,dz,alpha(,dF) out
@@ -833,15 +837,19 @@ def _check_tconv(g: GraphCSR, D: int, H: int, QKVR, F, feat_row, node_out=(), no
 def tconv_fwd(g: GraphCSR, D: int, H: int, QKVR: torch.Tensor, U: torch.Tensor, wbar: Optional[torch.Tensor],
               F: Optional[torch.Tensor], feat_row: Optional[torch.Tensor], aggV, S, sumA, mstat, den, drop_p: float,
               seed: int):
+    """F: fp32 edge-feature rows, or bf16 (config C3: the atom graph's bond state as autocast casts it)."""
     _check_tconv(g, D, H, QKVR, F, feat_row, node_out=(aggV,), node_heads=(sumA, mstat, den))
     if U.numel() < g.n * H * D or S.numel() < g.n * H * D:
         raise ValueError("tconv_fwd: U and S must be [n, H, D]")
-    profiling.launch(f"tconv_fwd n{g.n} m{g.m}", 0.0, _tconv_bytes(g.n, g.m, D, H, "fwd"),
-                     lambda: check(_lib.lib().alignn_tconv_fwd(
+    fbf = F is not None and F.dtype == torch.bfloat16
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m}" + (" F16" if fbf else ""), 0.0,
+                     _tconv_bytes(g.n, g.m, D, H, "fwd", f_elem=2 if fbf else 4),
+                     lambda: check(_lib.lib().alignn_tconv_fwd_ex(
                          g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
                          ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0), U.data_ptr(), _p(wbar),
-                         _p(F), 0 if F is None else F.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(), den.data_ptr(),
-                         float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_tconv_fwd"))
+                         _p(F), 0 if F is None else F.stride(0), int(fbf), aggV.data_ptr(), S.data_ptr(),
+                         sumA.data_ptr(), mstat.data_ptr(), den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1),
+                         stream_ptr()), "alignn_tconv_fwd"))
 
 
 def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, dout, outp, mstat, den,
@@ -854,12 +862,14 @@ def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, d
         raise ValueError("tconv_bwd_dst: U, Vd, Sz must be [n, H, D] and dq [n, >= D]")
     if dF is not None and dF.size(0) < F.size(0):
         raise ValueError("tconv_bwd_dst: dF must cover the rows of F")
-    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}", 0.0,
-                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", 0 if dF is None else (2 if accumulate_dF & 1 else 1)),
-                     lambda: check(_lib.lib().alignn_tconv_bwd_dst(
+    fbf = F is not None and F.dtype == torch.bfloat16
+    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}" + (" F16" if fbf else ""), 0.0,
+                     _tconv_bytes(g.n, g.m, D, H, "bwd_dst", 0 if dF is None else (2 if accumulate_dF & 1 else 1),
+                                  f_elem=2 if fbf else 4),
+                     lambda: check(_lib.lib().alignn_tconv_bwd_dst_ex(
                          g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), _p(feat_row),
                          ctypes.byref(g.schedule()), QKVR.data_ptr(), QKVR.stride(0),
-                         U.data_ptr(), Vd.data_ptr(), _p(wbar), _p(F), 0 if F is None else F.stride(0),
+                         U.data_ptr(), Vd.data_ptr(), _p(wbar), _p(F), 0 if F is None else F.stride(0), int(fbf),
                          dout.data_ptr(), outp.data_ptr(),
                          mstat.data_ptr(), den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(),
                          sigz.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), _p(dF),

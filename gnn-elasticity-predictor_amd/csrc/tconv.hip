@@ -46,14 +46,17 @@ struct EdgeSlot {
   float k[VPL], v[VPL], f[VPL];
 };
 
+// fbf: the feature rows hold bf16 (config C3: the atom graph's edge features are the bond state as
+// autocast casts it for edge_proj, train.py:325/:333 under :632-636), widened exactly at the load
 template <int VPL>
 __device__ __forceinline__ void load_edge(EdgeSlot<VPL>& e, const float* __restrict__ QKVR, int64_t ldq, int D,
-                                          const float* __restrict__ F, int64_t ldf, int64_t src, int64_t row, int j0,
-                                          bool act, int lane) {
+                                          const float* __restrict__ F, int64_t ldf, int fbf, int64_t src, int64_t row,
+                                          int j0, bool act, int lane) {
   if (act) {
     vload(QKVR + src * ldq + D + j0, e.k);
     vload(QKVR + src * ldq + 2 * D + j0, e.v);
-    vload(F + row * ldf + j0, e.f);
+    if (fbf) vload_bf(reinterpret_cast<const uint16_t*>(F) + row * ldf + j0, e.f);
+    else vload(F + row * ldf + j0, e.f);
   }
 }
 
@@ -93,6 +96,7 @@ struct FwdParams {
   const float* F; int64_t ldf;
   float* aggV; float* S; float* sumA; float* mstat; float* den;
   DropParams drop;
+  int fbf, pad3_;   // F holds bf16 elements (ldf in elements)
 };
 
 template <int VPL, int H>
@@ -121,6 +125,7 @@ struct BwdDstParams {
   float* dz_e; float* alpha_e;
   float* dF; int64_t lddf; int acc_dF, pad2_;
   DropParams drop;
+  int fbf, pad3_;   // F holds bf16 elements (ldf in elements)
 };
 
 template <int VPL, int H>
@@ -246,7 +251,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
       vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
       const int32_t t = first + j;
       if (t < end)
-        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)uni(sld(p.src_at, t)),
+        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, t)),
                           p.feat_row ? (int64_t)uni(sld(p.feat_row, t)) : t, j0, act, lane);
     }
     for (int32_t tb = first; tb < end; tb += stride) {
@@ -305,7 +310,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
         if (tn < end)
-          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)uni(sld(p.src_at, tn)),
+          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, tn)),
                             p.feat_row ? (int64_t)uni(sld(p.feat_row, tn)) : tn, j0, act, lane);
       }
     }
@@ -485,7 +490,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
       rows_[j] = 0;
       if (t < end) {
         rows_[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
-        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)uni(sld(p.src_at, t)), rows_[j], j0, act,
+        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, t)), rows_[j], j0, act,
                           lane);
         if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
       }
@@ -583,7 +588,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
         vzero(old[j]);
         if (tn < end) {
           rows_[j] = p.feat_row ? uni(sld(p.feat_row, tn)) : tn;
-          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)uni(sld(p.src_at, tn)), rows_[j], j0,
+          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, tn)), rows_[j], j0,
                             act, lane);
           if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
         }
@@ -866,11 +871,20 @@ int lg3_bwd_dst(int64_t n, int64_t m, int H, const int32_t* off, const int32_t* 
 
 using namespace alignn;
 
-extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
-                                const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
-                                const float* QKVR, int64_t ldq, const float* U, const float* wbar, const float* F,
-                                int64_t ldf, float* aggV, float* S, float* sumA, float* mstat, float* den,
-                                float drop_p, uint64_t seed, void* stream) {
+// bf16 feature rows: the light/heavy kernels only, rows 8-byte aligned for the 4-wide bf16 loads
+static int check_fbf(const void* F, int64_t ldf, int32_t D, const char* what) {
+  if ((D % 4) || (ldf % 4) || (reinterpret_cast<uintptr_t>(F) & 7)) {
+    set_error("%s: bf16 edge-feature rows need D %% 4 == 0, ldf %% 4 == 0 and 8-byte alignment", what);
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_tconv_fwd_ex(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                                   const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
+                                   const float* QKVR, int64_t ldq, const float* U, const float* wbar, const void* F,
+                                   int64_t ldf, int32_t f_bf16, float* aggV, float* S, float* sumA, float* mstat,
+                                   float* den, float drop_p, uint64_t seed, void* stream) {
   int rc = check_dims(D, H);
   if (rc) return rc;
   if (n == 0) return ALIGNN_OK;
@@ -878,22 +892,64 @@ extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, cons
     set_error("tconv_fwd: edge features F are required");
     return ALIGNN_E_BAD_SHAPE;
   }
+  if (f_bf16 && (rc = check_fbf(F, ldf, D, "tconv_fwd"))) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (lg3_supported(D, H, feat_row, F, sched))
-    return lg3_fwd(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
+  const float* Ff = reinterpret_cast<const float*>(F);
+  if (!f_bf16 && lg3_supported(D, H, feat_row, Ff, sched))
+    return lg3_fwd(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, wbar, Ff, ldf, aggV, S, sumA, mstat, den,
                    make_drop(drop_p, seed), s);
-  FwdParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, wbar, F, ldf, aggV, S, sumA, mstat, den,
+  FwdParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, wbar, Ff, ldf, aggV, S, sumA, mstat, den,
               make_drop(drop_p, seed)};
+  p.fbf = f_bf16 ? 1 : 0;
   const Sched sc = make_sched(sched, n);
   ALIGNN_DISPATCH_VH(vpl_for(D), H, launch_fwd, p, sc, s);
   ALIGNN_LAUNCH_CHECK("tconv_fwd2_kernel");
   return ALIGNN_OK;
 }
 
+extern "C" int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                                const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
+                                const float* QKVR, int64_t ldq, const float* U, const float* wbar, const float* F,
+                                int64_t ldf, float* aggV, float* S, float* sumA, float* mstat, float* den,
+                                float drop_p, uint64_t seed, void* stream) {
+  return alignn_tconv_fwd_ex(n, m, D, H, off_dst, src_at, feat_row, sched, QKVR, ldq, U, wbar, F, ldf, 0, aggV, S,
+                             sumA, mstat, den, drop_p, seed, stream);
+}
+
 extern "C" int alignn_tconv_family(int32_t D, int32_t H, const int32_t* feat_row, const float* F,
                                    const AlignnSchedule* sched) {
   if (check_dims(D, H)) return 0;
   return lg3_supported(D, H, feat_row, F, sched) ? 3 : 2;
+}
+
+extern "C" int alignn_tconv_bwd_dst_ex(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                                       const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
+                                       const float* QKVR, int64_t ldq, const float* U, const float* Vd,
+                                       const float* wbar, const void* F, int64_t ldf, int32_t f_bf16,
+                                       const float* dout, const float* outp, const float* mstat, const float* den,
+                                       float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
+                                       float* dF, int64_t lddf, int32_t accumulate_dF, float drop_p, uint64_t seed,
+                                       void* stream) {
+  int rc = check_dims(D, H);
+  if (rc) return rc;
+  if (n == 0) return ALIGNN_OK;
+  if (F == nullptr) {
+    set_error("tconv_bwd_dst: edge features F are required");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (f_bf16 && (rc = check_fbf(F, ldf, D, "tconv_bwd_dst"))) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float* Ff = reinterpret_cast<const float*>(F);
+  if (!f_bf16 && dF == nullptr && lg3_supported(D, H, feat_row, Ff, sched))
+    return lg3_bwd_dst(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, Vd, wbar, Ff, ldf, dout, outp, mstat, den, dq,
+                       lddq, Sz, sigz, dz_e, alpha_e, make_drop(drop_p, seed), s);
+  BwdDstParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, Ff, ldf, dout, outp, mstat, den,
+                 dq, lddq, Sz, sigz, dz_e, alpha_e, dF, lddf, accumulate_dF, 0, make_drop(drop_p, seed)};
+  p.fbf = f_bf16 ? 1 : 0;
+  const Sched sc = make_sched(sched, n);
+  ALIGNN_DISPATCH_VH(vpl_for(D), H, launch_bwd_dst, p, sc, s);
+  ALIGNN_LAUNCH_CHECK("tconv_bwd_dst2_kernel");
+  return ALIGNN_OK;
 }
 
 extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
@@ -903,23 +959,9 @@ extern "C" int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H, 
                                     const float* outp, const float* mstat, const float* den, float* dq, int64_t lddq,
                                     float* Sz, float* sigz, float* dz_e, float* alpha_e, float* dF, int64_t lddf,
                                     int32_t accumulate_dF, float drop_p, uint64_t seed, void* stream) {
-  int rc = check_dims(D, H);
-  if (rc) return rc;
-  if (n == 0) return ALIGNN_OK;
-  if (F == nullptr) {
-    set_error("tconv_bwd_dst: edge features F are required");
-    return ALIGNN_E_BAD_SHAPE;
-  }
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (dF == nullptr && lg3_supported(D, H, feat_row, F, sched))
-    return lg3_bwd_dst(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den, dq,
-                       lddq, Sz, sigz, dz_e, alpha_e, make_drop(drop_p, seed), s);
-  BwdDstParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, F, ldf, dout, outp, mstat, den,
-                 dq, lddq, Sz, sigz, dz_e, alpha_e, dF, lddf, accumulate_dF, 0, make_drop(drop_p, seed)};
-  const Sched sc = make_sched(sched, n);
-  ALIGNN_DISPATCH_VH(vpl_for(D), H, launch_bwd_dst, p, sc, s);
-  ALIGNN_LAUNCH_CHECK("tconv_bwd_dst2_kernel");
-  return ALIGNN_OK;
+  return alignn_tconv_bwd_dst_ex(n, m, D, H, off_dst, src_at, feat_row, sched, QKVR, ldq, U, Vd, wbar, F, ldf, 0, dout,
+                                 outp, mstat, den, dq, lddq, Sz, sigz, dz_e, alpha_e, dF, lddf, accumulate_dF, drop_p,
+                                 seed, stream);
 }
 
 extern "C" int alignn_tconv_bwd_src(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_src,

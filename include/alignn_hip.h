@@ -282,6 +282,22 @@ int alignn_tconv_bwd_dst(int64_t n, int64_t m, int32_t D, int32_t H,
                          float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e,
                          float* dF, int64_t lddf, int32_t accumulate_dF,
                          float drop_p, uint64_t seed, void* stream);
+/* The same two kernels with the edge-feature rows F in bf16 when f_bf16 = 1 (config C3: the atom
+ * graph's edge features are the bond state as the reference's autocast casts it for edge_proj,
+ * train.py:325/:333 under :632-636; widened exactly at the load, all arithmetic and every output
+ * fp32; D % 4 == 0, ldf % 4 == 0, rows 8-byte aligned).  f_bf16 = 0: alignn_tconv_fwd /
+ * alignn_tconv_bwd_dst. */
+int alignn_tconv_fwd_ex(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
+                        const int32_t* feat_row, const AlignnSchedule* sched, const float* QKVR, int64_t ldq,
+                        const float* U, const float* wbar, const void* F, int64_t ldf, int32_t f_bf16, float* aggV,
+                        float* S, float* sumA, float* mstat, float* den, float drop_p, uint64_t seed, void* stream);
+int alignn_tconv_bwd_dst_ex(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                            const int32_t* src_at, const int32_t* feat_row, const AlignnSchedule* sched,
+                            const float* QKVR, int64_t ldq, const float* U, const float* Vd, const float* wbar,
+                            const void* F, int64_t ldf, int32_t f_bf16, const float* dout, const float* outp,
+                            const float* mstat, const float* den, float* dq, int64_t lddq, float* Sz, float* sigz,
+                            float* dz_e, float* alpha_e, float* dF, int64_t lddf, int32_t accumulate_dF,
+                            float drop_p, uint64_t seed, void* stream);
 
 /* bf16 storage variant of the line-graph attention (config C3, the reference's autocast precision:
  * the Linear outputs K, V and the angle encoder's hidden layer are bf16, train.py:632-636): the

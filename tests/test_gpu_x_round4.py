@@ -322,3 +322,41 @@ def test_store_batch_prepares_without_a_host_sync_and_trains_bitwise_equal():
         grads.append(tr.st.grad.clone())
     torch.cuda.synchronize()
     assert torch.equal(grads[0], grads[1])
+
+
+# ------------------------------------------------------------------------------------------------
+# bf16 edge-feature rows in the atom-graph attention (alignn_tconv_fwd_ex / _bwd_dst_ex)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("drop", [0.0, 0.15])
+def test_atom_attention_bf16_feature_rows_bitwise_vs_fp32_on_rounded_rows(drop):
+    """The bond-state rows read as bf16 (config C3: autocast casts the bond state for edge_proj) give
+    bit for bit what the fp32 kernels give on the same rows widened to fp32 (bf16 -> fp32 is exact,
+    the arithmetic is unchanged): forward outputs, and the target-side backward including the
+    edge-feature gradient written through feat_row."""
+    from alignn_mi355x import ops
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.synthetic import mp_like_batch
+    ops.set_step_seed(None)
+    b = mp_like_batch(8).to(DEV)
+    g = prepare_batch(b).ag
+    n, m, D, H = g.n, g.m, 256, 4
+    gen = torch.Generator(device="cpu").manual_seed(21)
+    r = lambda *s: torch.randn(*s, generator=gen).to(DEV)   # noqa: E731
+    QKVR, U, wbar, Vd = r(n, 4 * D), r(n, H, D) * 0.1, r(D) * 0.1, r(n, H, D) * 0.1
+    F16 = r(m, D).bfloat16()
+    dout, outs = r(n, D), []
+    for F in (F16, F16.float()):
+        aggV, S = torch.empty(n, D, device=DEV), torch.empty(n, H, D, device=DEV)
+        sumA, mstat, den = (torch.empty(n, H, device=DEV) for _ in range(3))
+        ops.tconv_fwd(g, D, H, QKVR, U, wbar, F, g.perm_dst, aggV, S, sumA, mstat, den, drop, 99)
+        dq = torch.empty(n, D, device=DEV)
+        Sz = torch.empty(n, H, D, device=DEV)
+        sigz = torch.empty(n, H, device=DEV)
+        dz_e, al_e = torch.empty(m, H, device=DEV), torch.empty(m, H, device=DEV)
+        dF = torch.zeros(m, D, device=DEV)
+        ops.tconv_bwd_dst(g, D, H, QKVR, U, Vd, wbar, F, g.perm_dst, dout, aggV, mstat, den, dq, Sz, sigz, dz_e,
+                          al_e, dF, 1, drop, 99)
+        outs.append((aggV, S, sumA, mstat, den, dq, Sz, sigz, dz_e, al_e, dF))
+    torch.cuda.synchronize()
+    for i, (x, y) in enumerate(zip(*outs)):
+        assert torch.equal(x, y), i

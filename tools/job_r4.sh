@@ -29,7 +29,7 @@ pmc() {   # pmc NAME COUNTERS BENCHARGS...
 for st in "$@"; do
   case "$st" in
     new) run new 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py tests/test_gpu_x_lgmma.py ;;
-    sched) run sched 600 "${PT[@]}" tests/test_gpu_x_round4.py -k "schedule or sync" tests/test_gpu_x_store.py tests/test_gpu_x_capacity.py ;;
+    sched) run sched 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_store.py tests/test_gpu_x_capacity.py tests/test_gpu_x_configs.py ;;
     lgm) run lgm 300 python tools/lgm_bench.py --reps 20 ;;
     lgmv) for v in gnn-elasticity-predictor_amd/alignn_mi355x/variants/*.so; do
             ALIGNN_HIP_LIB=$v run "lgm_$(basename $v .so)" 300 python tools/lgm_bench.py --reps 20
@@ -42,6 +42,13 @@ for st in "$@"; do
     c3) run c3 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_c3.json" ;;
     hostprof) run hostprof 300 python -u tools/host_prep_profile.py --graphs 2000 --steps 30 ;;
     gemmbf) run gemmbf 300 python -u tools/gemm_bench.py --quick --reps 10 --flag 64 ;;
+    ab) for i in 1 2; do
+          run "ab_r3_$i" 300 bash -c "cd _r3ab && python bench.py --no-secondary --no-cpu-baseline --e2e 0 --steps 20 --warmup 5"
+          run "ab_r4_$i" 300 python "${Q[@]}" --steps 20 --warmup 5
+        done ;;
+    ab3) run ab3_r3 300 bash -c "cd _r3ab && python bench.py --no-secondary --no-cpu-baseline --e2e 0 --batch 256 --precision bf16 --steps 10 --warmup 3"
+         run ab3_r4 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    tcb) run tcb 300 python -u tools/tconv_bench.py --batch 256 --reps 10 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
