@@ -14,7 +14,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
     const int64_t row = (i / p.N) % p.M;
     const int64_t b = i / (p.N * p.M);
     // eight independent chains (partial k goes to chain k % 8), combined in a fixed tree
-    store_c(p, b, row, col, epilogue_value(p, b, row, col, splitk_sum(p, b, row, col)));
+    store_c(p, b, row, col, epilogue_value(p, b, row, col, splitk_sum(p, b, row, col)), p.cbf != 0);
   }
 }
 

@@ -280,16 +280,18 @@ __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], con
   }
 }
 
-__device__ __forceinline__ void store_c(const GemmParams& p, int64_t b, int64_t row, int64_t col, float v) {
+// cbf: C holds bf16 (the caller passes a compile-time false for the fp32-arithmetic kernels, whose
+// operands and output are always fp32, so their loops carry no storage-type branches)
+__device__ __forceinline__ void store_c(const GemmParams& p, int64_t b, int64_t row, int64_t col, float v, bool cbf) {
   const int64_t i = b * p.scb + c_row(p, row) * p.scm + col * p.scn;
-  if (p.cbf) reinterpret_cast<uint16_t*>(p.C)[i] = bf_rne(v);
+  if (cbf) reinterpret_cast<uint16_t*>(p.C)[i] = bf_rne(v);
   else p.C[i] = v;
 }
 
 // Epilogue. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
 template <int BM, int BN>
 __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (&acc)[BM / 64][BN / 64], int64_t m0,
-                                           int64_t n0, int64_t b, int sidx, int wm, int wn, int h, int l32) {
+                                           int64_t n0, int64_t b, int sidx, int wm, int wn, int h, int l32, bool cbf) {
   constexpr int MI = BM / 64, NI = BN / 64;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -304,7 +306,7 @@ __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (
         if (p.split_k > 1) {
           p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
         } else {
-          store_c(p, b, row, col, epilogue_value(p, b, row, col, acc[i][j][r]));
+          store_c(p, b, row, col, epilogue_value(p, b, row, col, acc[i][j][r]), cbf);
         }
       }
     }
@@ -350,11 +352,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int64_t kb = (int64_t)sidx * p.kchunk;
   const int64_t ke = min(Ktot, kb + p.kchunk);
 
-  const float* A = eoff(p.A, b * p.sab, p.abf);
-  const float* B = eoff(p.B, b * p.sbb, p.bbf);
+  // bf16 storage exists only with bf16 arithmetic (host check): compile-time fp32 otherwise
+  const int abf = BF == 1 ? p.abf : 0, bbf = BF == 1 ? p.bbf : 0;
+  const float* A = eoff(p.A, b * p.sab, abf);
+  const float* B = eoff(p.B, b * p.sbb, bbf);
   // (batch, local k) of a global k index; identity unless the batch is reduced (RB)
-  auto tileA = [&](int64_t k0) { return RB ? eoff(p.A, (k0 / p.K) * p.sab, p.abf) : A; };
-  auto tileB = [&](int64_t k0) { return RB ? eoff(p.B, (k0 / p.K) * p.sbb, p.bbf) : B; };
+  auto tileA = [&](int64_t k0) { return RB ? eoff(p.A, (k0 / p.K) * p.sab, abf) : A; };
+  auto tileB = [&](int64_t k0) { return RB ? eoff(p.B, (k0 / p.K) * p.sbb, bbf) : B; };
   auto kloc = [&](int64_t k0) { return RB ? k0 % p.K : k0; };
   auto kend = [&](int64_t k0) { return RB ? p.K : ke; };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -374,15 +378,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   // row-contiguous operand; then every full stage [k0, k0 + BKT) <= ke takes them
   const bool fastA = !RB && p.vecA && (A_KC || m0 + BM <= p.M);
   const bool fastB = !RB && p.vecB && (B_KC || n0 + BN <= p.N);
-  if (fastA) la.setup_fast(A, p.sam, p.sak, m0, p.M, kb, p.abf);
-  if (fastB) lb.setup_fast(B, p.sbn, p.sbk, n0, p.N, kb, p.bbf);
+  if (fastA) la.setup_fast(A, p.sam, p.sak, m0, p.M, kb, abf);
+  if (fastB) lb.setup_fast(B, p.sbn, p.sbk, n0, p.N, kb, bbf);
   auto load_stage = [&](int64_t k0) {
     const bool full = k0 + BKT <= ke;
     // A(m,k): rows along m. For A_KC srow = sam, sk = sak; for !A_KC the loader uses (sk = sak).
-    if (fastA && full) la.load_fast(k0 - kb, p.sak, p.abf);
-    else la.load(tileA(k0), p.sam, p.sak, m0, p.M, kloc(k0), kend(k0), p.vecA, p.abf);
-    if (fastB && full) lb.load_fast(k0 - kb, p.sbk, p.bbf);
-    else lb.load(tileB(k0), p.sbn, p.sbk, n0, p.N, kloc(k0), kend(k0), p.vecB, p.bbf);
+    if (fastA && full) la.load_fast(k0 - kb, p.sak, abf);
+    else la.load(tileA(k0), p.sam, p.sak, m0, p.M, kloc(k0), kend(k0), p.vecA, abf);
+    if (fastB && full) lb.load_fast(k0 - kb, p.sbk, bbf);
+    else lb.load(tileB(k0), p.sbn, p.sbk, n0, p.N, kloc(k0), kend(k0), p.vecB, bbf);
   };
   load_stage(kb);
   la.store(smem);
@@ -404,7 +408,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     cur ^= 1;
   }
 
-  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
+  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF == 1 && p.cbf);
 }
 
 // Pipelined variant: two register sets of global loads in flight, so a stage's
@@ -448,9 +452,9 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
 
   TileLoader<BM, A_KC, BKT> la;
   TileLoader<BN, B_KC, BKT> lb;
-  la.setup_fast(eoff(p.A, b * p.sab, p.abf), p.sam, p.sak, m0, p.M, kb, p.abf);
-  lb.setup_fast(eoff(p.B, b * p.sbb, p.bbf), p.sbn, p.sbk, n0, p.N, kb, p.bbf);
-  const bool abf = p.abf != 0, bbf = p.bbf != 0;
+  const bool abf = BF == 1 && p.abf != 0, bbf = BF == 1 && p.bbf != 0;   // compile-time false for fp32
+  la.setup_fast(eoff(p.A, b * p.sab, abf), p.sam, p.sak, m0, p.M, kb, abf);
+  lb.setup_fast(eoff(p.B, b * p.sbb, bbf), p.sbn, p.sbk, n0, p.N, kb, bbf);
   gf4 pa[FA], pb[FB], qa[FA], qb[FB];
   // bf16 operands: 8-byte loads into the first two words, widened when the stage is stored
   auto ld = [](const float* ptr, bool bf) -> gf4 {
@@ -497,7 +501,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
     load(qa, qb, s0 + 4);
     __syncthreads();
   }
-  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32);
+  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF == 1 && p.cbf);
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC, int PR>

@@ -52,7 +52,8 @@ struct GateFwdParams {
   uint16_t* Xn16; int64_t ldxn16;
 };
 
-template <int VPL>
+// IO: some operand is bf16 (bf16 storage); the fp32 instantiation carries no storage-type branches
+template <int VPL, bool IO>
 __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
   if (act) {
     if (orow >= 0) vload(p.outp + orow * D + j0, o);
-    if (p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
+    if (IO && p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
     else vload(p.R + row * p.ldr + j0, r);
     vload(p.wbeta + j0, w1);
     vload(p.wbeta + D + j0, w2);
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
       out[i] = x[i] + a;
     }
     vstore(p.Xn + row * p.ldxn + j0, out);
-    if (p.Xn16) vstore_bf(p.Xn16 + row * p.ldxn16 + j0, out);
+    if (IO && p.Xn16) vstore_bf(p.Xn16 + row * p.ldxn16 + j0, out);
   }
   if (lane == 0) {
     p.beta[row] = b;
@@ -129,7 +130,7 @@ struct GateBwdParams {
   int rbf, drbf;        // bf16 storage: R read as bf16, dR written as bf16 (autocast: grad of a bf16 output)
 };
 
-template <int VPL>
+template <int VPL, bool IO>
 __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
   resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
     const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
     if (act) {
       if (orow >= 0) vload(p.outp + orow * D + j0, o);
-      if (p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
+      if (IO && p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
       else vload(p.R + row * p.ldr + j0, r);
       vload(p.dXn + row * p.lddx + j0, gx);
       if (p.dX2) {   // one add per element, the sum kept as the residual's gradient
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
         a_w3[i] = fmaf(dl, o[i] - r[i], a_w3[i]);
       }
       if (orow >= 0) vstore(p.dout + orow * D + j0, dov);
-      if (p.drbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dR) + row * p.lddr + j0, drv);
+      if (IO && p.drbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dR) + row * p.lddr + j0, drv);
       else vstore(p.dR + row * p.lddr + j0, drv);
     }
   }
@@ -389,11 +390,16 @@ extern "C" int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, co
                   mu, rstd, make_drop(drop_p, seed), outp_rows, r_bf16 ? 1 : 0, 0, Xnew16, ldxn16};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((n + 3) / 4));
+  const bool io = r_bf16 || Xnew16;
   switch (vpl) {
-    case 1: launch(gate_ln_fwd_kernel<1>, g, dim3(256), 0, s, p); break;
-    case 2: launch(gate_ln_fwd_kernel<2>, g, dim3(256), 0, s, p); break;
-    case 4: launch(gate_ln_fwd_kernel<4>, g, dim3(256), 0, s, p); break;
-    default: launch(gate_ln_fwd_kernel<8>, g, dim3(256), 0, s, p); break;
+    case 1: if (io) launch(gate_ln_fwd_kernel<1, true>, g, dim3(256), 0, s, p);
+            else launch(gate_ln_fwd_kernel<1, false>, g, dim3(256), 0, s, p); break;
+    case 2: if (io) launch(gate_ln_fwd_kernel<2, true>, g, dim3(256), 0, s, p);
+            else launch(gate_ln_fwd_kernel<2, false>, g, dim3(256), 0, s, p); break;
+    case 4: if (io) launch(gate_ln_fwd_kernel<4, true>, g, dim3(256), 0, s, p);
+            else launch(gate_ln_fwd_kernel<4, false>, g, dim3(256), 0, s, p); break;
+    default: if (io) launch(gate_ln_fwd_kernel<8, true>, g, dim3(256), 0, s, p);
+             else launch(gate_ln_fwd_kernel<8, false>, g, dim3(256), 0, s, p); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_fwd_kernel");
   return ALIGNN_OK;
@@ -449,11 +455,16 @@ extern "C" int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew
                   dX_add, r_bf16 ? 1 : 0, dr_bf16 ? 1 : 0};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
+  const bool io = r_bf16 || dr_bf16;
   switch (vpl) {
-    case 1: launch(gate_ln_bwd_kernel<1>, g, dim3(256), 0, s, p); break;
-    case 2: launch(gate_ln_bwd_kernel<2>, g, dim3(256), 0, s, p); break;
-    case 4: launch(gate_ln_bwd_kernel<4>, g, dim3(256), 0, s, p); break;
-    default: launch(gate_ln_bwd_kernel<8>, g, dim3(256), 0, s, p); break;
+    case 1: if (io) launch(gate_ln_bwd_kernel<1, true>, g, dim3(256), 0, s, p);
+            else launch(gate_ln_bwd_kernel<1, false>, g, dim3(256), 0, s, p); break;
+    case 2: if (io) launch(gate_ln_bwd_kernel<2, true>, g, dim3(256), 0, s, p);
+            else launch(gate_ln_bwd_kernel<2, false>, g, dim3(256), 0, s, p); break;
+    case 4: if (io) launch(gate_ln_bwd_kernel<4, true>, g, dim3(256), 0, s, p);
+            else launch(gate_ln_bwd_kernel<4, false>, g, dim3(256), 0, s, p); break;
+    default: if (io) launch(gate_ln_bwd_kernel<8, true>, g, dim3(256), 0, s, p);
+             else launch(gate_ln_bwd_kernel<8, false>, g, dim3(256), 0, s, p); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
   return ALIGNN_OK;

@@ -186,7 +186,7 @@ __device__ __forceinline__ float rows_max(float x) {
 template <int VPL, int H>
 constexpr int fwd2_lds_floats() { return cmax(fwd_merge_floats<VPL, H>(), 4 * H * 64 * VPL); }
 
-template <int VPL, int H>
+template <int VPL, int H, bool FBF>
 __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64_t d, int wsub, int nw, bool heavy) {
   static_assert(PF == 4, "row-distributed layout assumes one edge per row");
   constexpr int NS = 3 * H + H * VPL + VPL;
@@ -251,7 +251,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
       vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
       const int32_t t = first + j;
       if (t < end)
-        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, t)),
+        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, t)),
                           p.feat_row ? (int64_t)uni(sld(p.feat_row, t)) : t, j0, act, lane);
     }
     for (int32_t tb = first; tb < end; tb += stride) {
@@ -310,7 +310,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
         const int32_t tn = tb + stride + j;
         if (tn < end)
-          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, tn)),
+          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, tn)),
                             p.feat_row ? (int64_t)uni(sld(p.feat_row, tn)) : tn, j0, act, lane);
       }
     }
@@ -391,7 +391,8 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
   if (heavy) __syncthreads();  // merge buffer / u copies free for the next item
 }
 
-template <int VPL, int H>
+// FBF: bf16 edge-feature rows (a compile-time switch: the fp32 instantiation is unchanged)
+template <int VPL, int H, bool FBF>
 __global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
   resolve_drop(p.drop);
   __shared__ float smem[fwd2_lds_floats<VPL, H>()];
@@ -399,10 +400,10 @@ __global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      fwd2_node<VPL, H>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
+      fwd2_node<VPL, H, FBF>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) fwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
+      if (i < sc.n_light) fwd2_node<VPL, H, FBF>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
     }
   }
 }
@@ -410,7 +411,7 @@ __global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
 template <int VPL, int H>
 constexpr int bwd2_lds_floats() { return cmax(bwd_merge_floats<VPL, H>(), 4 * 2 * H * 64 * VPL); }
 
-template <int VPL, int H>
+template <int VPL, int H, bool FBF>
 __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, int64_t d, int wsub, int nw, bool heavy) {
   static_assert(PF == 4, "row-distributed layout assumes one edge per row");
   constexpr int NS = H + H * VPL + VPL;
@@ -490,7 +491,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
       rows_[j] = 0;
       if (t < end) {
         rows_[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
-        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, t)), rows_[j], j0, act,
+        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, t)), rows_[j], j0, act,
                           lane);
         if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
       }
@@ -588,7 +589,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
         vzero(old[j]);
         if (tn < end) {
           rows_[j] = p.feat_row ? uni(sld(p.feat_row, tn)) : tn;
-          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, p.fbf, (int64_t)uni(sld(p.src_at, tn)), rows_[j], j0,
+          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, tn)), rows_[j], j0,
                             act, lane);
           if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
         }
@@ -632,7 +633,7 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
   if (heavy) __syncthreads();
 }
 
-template <int VPL, int H>
+template <int VPL, int H, bool FBF>
 __global__ TCONV_ATTR void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
   resolve_drop(p.drop);
   __shared__ float smem[bwd2_lds_floats<VPL, H>()];
@@ -640,10 +641,10 @@ __global__ TCONV_ATTR void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      bwd2_node<VPL, H>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
+      bwd2_node<VPL, H, FBF>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) bwd2_node<VPL, H>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
+      if (i < sc.n_light) bwd2_node<VPL, H, FBF>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
     }
   }
 }
@@ -810,13 +811,17 @@ static int vpl_for(int D) {
 template <int VPL, int H>
 static void launch_fwd(const FwdParams& p, const Sched& sc, hipStream_t s) {
   const int64_t items = sc.items();
-  if (items > 0) launch((tconv_fwd2_kernel<VPL, H>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  if (items <= 0) return;
+  if (p.fbf) launch((tconv_fwd2_kernel<VPL, H, true>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  else launch((tconv_fwd2_kernel<VPL, H, false>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
 }
 
 template <int VPL, int H>
 static void launch_bwd_dst(const BwdDstParams& p, const Sched& sc, hipStream_t s) {
   const int64_t items = sc.items();
-  if (items > 0) launch((tconv_bwd_dst2_kernel<VPL, H>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  if (items <= 0) return;
+  if (p.fbf) launch((tconv_bwd_dst2_kernel<VPL, H, true>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  else launch((tconv_bwd_dst2_kernel<VPL, H, false>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
 }
 
 template <int VPL, int H>

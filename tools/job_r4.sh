@@ -49,6 +49,10 @@ for st in "$@"; do
     ab3) run ab3_r3 300 bash -c "cd _r3ab && python bench.py --no-secondary --no-cpu-baseline --e2e 0 --batch 256 --precision bf16 --steps 10 --warmup 3"
          run ab3_r4 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
     tcb) run tcb 300 python -u tools/tconv_bench.py --batch 256 --reps 10 ;;
+    rpab) run rpab_r3 400 rocprofv3 --kernel-trace --stats -d "$O/rp_ab_r3" -o run --output-format csv -- \
+            python _r3ab/bench.py --no-secondary --no-cpu-baseline --e2e 0 --steps 10 --warmup 3 --no-roofline
+          run rpab_r4 400 rocprofv3 --kernel-trace --stats -d "$O/rp_ab_r4" -o run --output-format csv -- \
+            python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
