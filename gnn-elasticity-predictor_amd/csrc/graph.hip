@@ -201,8 +201,9 @@ static int build_csr(const K* keys, int64_t m, int64_t n, int32_t* off, int32_t*
 // the in-degrees): every target with in-edges, longest in-edge list first within each of `xcds`
 // contiguous id ranges holding equal numbers of edges (ties in ascending id), the ranges interleaved
 // in chunks of `chunk` items, then the targets without in-edges in ascending id — the host lists
-// exactly.  One workgroup of 16 waves: pass 1 histograms (range, degree) in LDS; pass 2 walks each
-// range in id order, 1024 targets at a time, and places each at its stable rank (rank among equal
+// exactly.  One workgroup of four waves (it runs on the loader stream beside a step, where a small
+// workgroup is easier to place than a 16-wave one): pass 1 histograms (range, degree) in LDS;
+// pass 2 walks each range in id order, 256 targets at a time, and places each at its stable rank (rank among equal
 // in-degrees within its wave from a ballot per distinct degree, plus the counts of the earlier waves
 // of the block and of the earlier blocks).  The order matters for speed, not results: targets of one
 // degree adjacent in id share their sources' rows in L2.  Needs every in-degree <= thr (the caller's
@@ -210,13 +211,13 @@ static int build_csr(const K* keys, int64_t m, int64_t n, int32_t* off, int32_t*
 // -------------------------------------------------------------------------------------------
 constexpr int SCHED_MAX_THR = 512;
 constexpr int SCHED_MAX_XCDS = 8;
-constexpr int SCHED_WAVES = 16;
+constexpr int SCHED_WAVES = 4;
 
-__global__ __launch_bounds__(1024) void schedule_build_kernel(const int32_t* __restrict__ off, int64_t n, int thr,
+__global__ __launch_bounds__(256) void schedule_build_kernel(const int32_t* __restrict__ off, int64_t n, int thr,
                                                               int xcds, int chunk, int32_t* __restrict__ light,
                                                               int32_t* __restrict__ err) {
   __shared__ int32_t cur[SCHED_MAX_XCDS][SCHED_MAX_THR + 1];   // histogram, then bucket cursors
-  __shared__ int32_t wcnt[SCHED_WAVES][SCHED_MAX_THR + 1];     // one block of 1024: per-wave counts by degree
+  __shared__ int32_t wcnt[SCHED_WAVES][SCHED_MAX_THR + 1];     // one block of 256: per-wave counts by degree
   __shared__ int64_t bounds[SCHED_MAX_XCDS + 1];
   __shared__ int32_t cnt[SCHED_MAX_XCDS];
   __shared__ int32_t nlit_s, zbase;
@@ -405,7 +406,7 @@ extern "C" int alignn_schedule_build(const int32_t* off_dst, int64_t n, int32_t 
   }
   if (n == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  launch(schedule_build_kernel, dim3(1), dim3(1024), 0, s, off_dst, n, (int)heavy_threshold, (int)xcds, (int)chunk,
+  launch(schedule_build_kernel, dim3(1), dim3(64 * SCHED_WAVES), 0, s, off_dst, n, (int)heavy_threshold, (int)xcds, (int)chunk,
          light, err_flag);
   ALIGNN_LAUNCH_CHECK("schedule_build_kernel");
   return ALIGNN_OK;

@@ -53,6 +53,10 @@ for st in "$@"; do
             python _r3ab/bench.py --no-secondary --no-cpu-baseline --e2e 0 --steps 10 --warmup 3 --no-roofline
           run rpab_r4 400 rocprofv3 --kernel-trace --stats -d "$O/rp_ab_r4" -o run --output-format csv -- \
             python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
+    rpe2e) run rpe2e 400 rocprofv3 --kernel-trace --stats -d "$O/rp_e2e" -o run --output-format csv -- \
+             python bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 10 --warmup 3 --no-roofline ;;
+    e2eab) run e2eab_r3 400 python _r3ab/bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 20 --warmup 5 --no-roofline
+           run e2eab_r4 400 python bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 20 --warmup 5 --no-roofline ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
