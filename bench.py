@@ -107,6 +107,11 @@ def apply_settings(args, model):
             args.loader_priority = int(v)
         elif k == "main_priority":
             args.main_priority = int(v)
+        elif k == "stream_priority":   # the engine's side / aux streams (ops.STREAM_PRIORITY)
+            from alignn_mi355x import ops
+            ops.STREAM_PRIORITY = int(v)
+        elif k == "prefetch":          # e2e loops: batches prepared ahead on the loader stream
+            args.prefetch = int(v)
         else:
             raise ValueError(f"unknown --set key {k}")
     return kw
@@ -217,22 +222,23 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
         return b
 
     r0, m0 = trainer.rebinds, trainer.rebind_misses
-    nxt = make()
+    depth = max(1, int(getattr(args, "prefetch", 1) or 1))   # batches prepared ahead
+    ahead = [make() for _ in range(depth)]
     for i in range(args.warmup):
-        cur = nxt
+        cur = ahead.pop(0)
         trainer.step(cur, seed=7919 * rank + i)
-        nxt = make()
+        ahead.append(make())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     host_step = host_make = 0.0
     t0 = time.perf_counter()
     for i in range(args.steps):
-        cur = nxt
+        cur = ahead.pop(0)
         ta = time.perf_counter()
         trainer.step(cur, seed=7919 * rank + args.warmup + i)
         tb = time.perf_counter()
-        nxt = make()
+        ahead.append(make())
         host_step += tb - ta
         host_make += time.perf_counter() - tb
     torch.cuda.synchronize()

@@ -42,7 +42,10 @@ def _dkey(device) -> str:
     return str(d)
 
 
-_FREE_STREAMS: dict = {}   # device -> library streams no live context holds
+_FREE_STREAMS: dict = {}   # (device, priority) -> library streams no live context holds
+# HIP priority of the side / aux streams contexts create from now on (0 normal, -1 high): with the
+# caller's step stream also at -1, a loader stream at 0 only takes what the step leaves idle
+STREAM_PRIORITY = 0
 
 
 class ExecContext:
@@ -97,14 +100,15 @@ class ExecContext:
         would then mistake for its side / aux stream.  Held by one live context at a time; a released
         one is reused, never destroyed (tensors recorded on it may outlive the context)."""
         key = _dkey(device)
-        free = _FREE_STREAMS.setdefault(key, [])
+        prio = int(STREAM_PRIORITY)
+        free = _FREE_STREAMS.setdefault((key, prio), [])
         if free:
             h = free.pop()
         else:
             hv = ctypes.c_void_p()
-            check(_lib.lib().alignn_stream_create(0, ctypes.byref(hv)), "alignn_stream_create")
+            check(_lib.lib().alignn_stream_create(prio, ctypes.byref(hv)), "alignn_stream_create")
             h = hv.value
-        self._owned_streams.append((key, h))
+        self._owned_streams.append(((key, prio), h))
         return torch.cuda.ExternalStream(h, device=torch.device(key))
 
     def side(self, device) -> torch.cuda.Stream:
@@ -123,8 +127,8 @@ class ExecContext:
 
     def __del__(self):
         try:
-            for key, h in self._owned_streams:
-                _FREE_STREAMS.setdefault(key, []).append(h)
+            for kp, h in self._owned_streams:
+                _FREE_STREAMS.setdefault(kp, []).append(h)
             self._owned_streams = []
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass

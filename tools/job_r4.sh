@@ -57,6 +57,13 @@ for st in "$@"; do
              python bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 10 --warmup 3 --no-roofline ;;
     e2eab) run e2eab_r3 400 python _r3ab/bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 20 --warmup 5 --no-roofline
            run e2eab_r4 400 python bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 20 --warmup 5 --no-roofline ;;
+    e2ep) P=(--set stream_priority=-1 --set main_priority=-1 --set loader_priority=0)
+          E=(bench.py --no-secondary --no-cpu-baseline --e2e 2000 --no-roofline)
+          run e2ep_b32_base 400 python "${E[@]}" --steps 20 --warmup 5
+          run e2ep_b32_prio 400 python "${E[@]}" --steps 20 --warmup 5 "${P[@]}"
+          run e2ep_b32_prio_pf2 400 python "${E[@]}" --steps 20 --warmup 5 "${P[@]}" --set prefetch=2
+          run e2ep_c5_base 400 python "${E[@]}" --batch 256 --precision bf16 --steps 10 --warmup 3
+          run e2ep_c5_prio_pf2 400 python "${E[@]}" --batch 256 --precision bf16 --steps 10 --warmup 3 "${P[@]}" --set prefetch=2 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
