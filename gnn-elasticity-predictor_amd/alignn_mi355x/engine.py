@@ -742,6 +742,10 @@ class AlignnEngine:
         # bf16 storage: the atom-graph attention reads the bond state's bf16 copy (the gate kernel's
         # Xn16; autocast casts the bond state to bf16 for edge_proj) as its edge-feature rows
         self.atom_bf16 = True
+        # forward preamble on the aux stream: the line convs' folded projections (weights only), then the
+        # atom encoder and the atom convs' projections — only the first atom block needs them, so they
+        # overlap the bond encoder and the first line block instead of preceding them
+        self.preamble_aux = True
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
@@ -774,6 +778,11 @@ class AlignnEngine:
             ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
         else:
             ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
+
+    def _line_proj(self, P: FlatViews, ctx, L: int, D: int) -> None:
+        """The line convs' edge projections with the angle encoder's second Linear folded in."""
+        W2, b2 = P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias")
+        ctx.Ml_all, ctx.wl_all = proj_weights(P.edge_We, W2.expand(L, D, D), b2.expand(L, D))
 
     def _mlp_fwd(self, x, W1, b1, W2, b2):
         D = self.cfg.hidden
@@ -860,9 +869,16 @@ class AlignnEngine:
         elif wt:
             ops.transpose_(ctx.Wt_edge, P.edge_Wqkvr)
             ops.transpose_(ctx.Wt_node, P.node_Wqkvr)
+        main = torch.cuda.current_stream(dev)
+        pre = ops.aux_stream(dev) if (self.preamble_aux and side is not None and E > 0 and L > 0) else None
+        line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
+        if pre is not None and line_proj:
+            with _side_work(pre, (x,)):    # forks from the main stream (after the jitter)
+                self._line_proj(P, ctx, L, D)
         # encoders (train.py:547-556)
-        ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
-                                   P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
+        if pre is None:
+            ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
+                                       P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
         if edge_attr.numel() > 0:
             ctx.h1e, e = self._mlp_fwd(edge_attr, P.enc("edge", 0, "weight"), P.enc("edge", 0, "bias"),
                                        P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
@@ -874,11 +890,20 @@ class AlignnEngine:
             self._angle_hidden(P, bc, D, dev, a)
         ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
-        if T > 0 and E > 0 and L > 0 and ctx.has_angle:
-            W2, b2 = P.enc("angle", 2, "weight"), P.enc("angle", 2, "bias")
-            ctx.Ml_all, ctx.wl_all = proj_weights(P.edge_We, W2.expand(L, D, D), b2.expand(L, D))
-        if E > 0 and L > 0:
-            ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
+        if pre is not None:
+            if line_proj:
+                ops.stream_wait(main, pre)   # the line projections
+            # beside the first line block (already forked when the line projections went first)
+            with _side_work(pre, (x,), wait=not line_proj):
+                ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
+                                           P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
+                ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
+        else:
+            if line_proj:
+                self._line_proj(P, ctx, L, D)
+            if E > 0 and L > 0:
+                ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
+        pre_pending = pre is not None
         # atom blocks on the aux stream: atom block l waits for line block l, line block l+1 does not
         # wait for it (it reads only the bond states); the readout joins the aux stream
         aux = ops.aux_stream(dev) if (self._atom_mode(T, E) == 2 and side is not None) else None
@@ -897,6 +922,9 @@ class AlignnEngine:
                 c = None
             ctx.edge.append(c)
             # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
+            if E > 0 and pre_pending and aux is None:
+                ops.stream_wait(main, pre)   # the atom encoder and projections (inline atom blocks)
+                pre_pending = False
             if E > 0:
                 # bf16 storage: the bond-state rows as autocast hands them to edge_proj (bf16)
                 ef = e16 if (bf16_io and self.atom_bf16 and e16 is not None) else e
@@ -906,8 +934,8 @@ class AlignnEngine:
             else:
                 c = None
             ctx.node.append(c)
-        if aux is not None:
-            ops.stream_wait(torch.cuda.current_stream(dev), aux)
+        if aux is not None or pre_pending:
+            ops.stream_wait(torch.cuda.current_stream(dev), aux if aux is not None else pre)
         ctx.h = h
         # readout (train.py:562-574)
         gdim = global_x.numel() // max(B, 1)

@@ -64,6 +64,11 @@ for st in "$@"; do
           run e2ep_b32_prio_pf2 400 python "${E[@]}" --steps 20 --warmup 5 "${P[@]}" --set prefetch=2
           run e2ep_c5_base 400 python "${E[@]}" --batch 256 --precision bf16 --steps 10 --warmup 3
           run e2ep_c5_prio_pf2 400 python "${E[@]}" --batch 256 --precision bf16 --steps 10 --warmup 3 "${P[@]}" --set prefetch=2 ;;
+    pre) run pre_off 300 python "${Q[@]}" --steps 20 --warmup 5 --set engine.preamble_aux=0
+         run pre_on 300 python "${Q[@]}" --steps 20 --warmup 5
+         run pre_off3 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.preamble_aux=0
+         run pre_on3 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    ptest) run ptest 600 "${PT[@]}" tests/test_gpu_x_pending.py tests/test_gpu_x_round4.py -k "neutral or aux or validator or capture" ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
