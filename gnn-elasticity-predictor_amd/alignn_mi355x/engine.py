@@ -978,28 +978,32 @@ class AlignnEngine:
         g = G.named
         ops.zero_(G.flat)
         dout = dout.contiguous()
-        # heads (train.py:582-585)
+        side = ops.side_stream(dev) if self.overlap else None
+        # heads (train.py:582-585); their weight gradients on the side stream (off the dh chain)
         if ctx.mode == "embed":
             dshared = dout
         else:
             dshared = torch.empty(B, D, device=dev)
             if ctx.mode == "hetero":
-                ops.gemm(dout[:, :Tt].t(), ctx.shared, G.Wmean)
-                ops.colsum(dout[:, :Tt], G.bmean)
-                ops.gemm(dout[:, Tt:].t(), ctx.shared, G.Wlogvar)
-                ops.colsum(dout[:, Tt:], G.blogvar)
+                with _side_work(side, (dout, ctx.shared)):
+                    ops.gemm(dout[:, :Tt].t(), ctx.shared, G.Wmean)
+                    ops.colsum(dout[:, :Tt], G.bmean)
+                    ops.gemm(dout[:, Tt:].t(), ctx.shared, G.Wlogvar)
+                    ops.colsum(dout[:, Tt:], G.blogvar)
                 ops.gemm(dout[:, :Tt], P.Wmean, dshared)
                 ops.gemm(dout[:, Tt:], P.Wlogvar, dshared, beta=1.0)
             else:
-                ops.gemm(dout.t(), ctx.shared, G.Wout)
-                ops.colsum(dout, G.bout)
+                with _side_work(side, (dout, ctx.shared)):
+                    ops.gemm(dout.t(), ctx.shared, G.Wout)
+                    ops.colsum(dout, G.bout)
                 ops.gemm(dout, P.Wout, dshared)
         # feat_proj + readout (train.py:562-573)
         dpre = torch.empty(B, D, device=dev)
         ops.dropout(dshared, dpre, ctx.pre, p_drop, site_seed(seed, 4 * L + 1))
         Wf = P.named[pre + "feat_proj.0.weight"]
-        ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"])
-        ops.colsum(dpre, g[pre + "feat_proj.0.bias"])
+        with _side_work(side, (dpre, ctx.feats)):
+            ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"])
+            ops.colsum(dpre, g[pre + "feat_proj.0.bias"])
         Wfeat = ctx.feats.size(1)
         dfeats = ops.zeros(B, Wfeat, device=dev)
         ops.gemm(dpre, Wf[:, :D], dfeats[:, :D])
@@ -1014,7 +1018,6 @@ class AlignnEngine:
             dM_all = torch.empty(L, D, D, device=dev)
             dwbar_all = torch.empty(L, D, device=dev)
         line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
-        side = ops.side_stream(dev) if self.overlap else None
         wgrad = self.wgrad_early if self.wgrad_early >= 0 else (2 if T < self.WGRAD_SPLIT_MAX_T else 1)
         if line_proj:
             dMl_all = torch.empty(L, D, D, device=dev)
