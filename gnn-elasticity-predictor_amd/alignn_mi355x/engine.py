@@ -744,8 +744,9 @@ class AlignnEngine:
         self.atom_bf16 = True
         # forward preamble on the aux stream: the line convs' folded projections (weights only), then the
         # atom encoder and the atom convs' projections — only the first atom block needs them, so they
-        # overlap the bond encoder and the first line block instead of preceding them
-        self.preamble_aux = True
+        # could overlap the bond encoder and the first line block.  Measured within noise, slightly
+        # negative (B = 32: 9,117 -> 9,034 graphs/s; C3: 19,531 -> 19,436; gpurun_out r4f pre_*): off
+        self.preamble_aux = False
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy

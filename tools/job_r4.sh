@@ -70,6 +70,9 @@ for st in "$@"; do
          run pre_on3 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
     ptest) run ptest 600 "${PT[@]}" tests/test_gpu_x_pending.py tests/test_gpu_x_round4.py -k "neutral or aux or validator or capture" ;;
     gsweep) run gsweep 600 python -u tools/gemm_bench.py --reps 8 --json "$O/gemm_sweep_c2.json" ;;
+    rpvar) run rpvar 500 rocprofv3 --kernel-trace --stats -d "$O/rp_var" -o run --output-format csv -- \
+             python bench.py --no-secondary --no-cpu-baseline --e2e 2000 --steps 10 --warmup 3 --no-roofline \
+             --set stream_priority=-1 --set main_priority=-1 --set loader_priority=0 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
