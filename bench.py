@@ -205,13 +205,17 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     from alignn_mi355x.engine import prepare_batch
 
     rng = np.random.default_rng(1234 + rank)
-    # B >= 128: a high-priority loader stream, so the small collate/CSR kernels (and the host syncs of
-    # batch preparation that wait for them) are dispatched ahead of the running step's queued kernels
-    # (B = 256 bf16: 12,160-12,240 -> 16,110-16,150 graphs/s); at B = 32 the same costs 22-35 %
-    # (8,027-8,077 -> 5,226-6,286; profiles/r02/v43_ab_loader_priority_*.log)
+    # The step's streams run at high priority (main()).  A fixed-signature loop prepares on a normal-
+    # priority loader stream, which then fills the step's idle time instead of slowing it (round 4,
+    # batch preparation without host syncs: B = 32 7,880 -> 8,497 graphs/s, C5 17,115 -> 18,733 = 96 % of
+    # the bare step; gpurun_out r4f e2ep_*).  Padded batches (capacity) need more preparation work than
+    # those gaps hold — starved, it serialised with the step (5.1 vs 3.6 ms, r4g rp_var) — so their
+    # loader shares the step's priority.  (Round 2, with host syncs in the preparation and the step at
+    # normal priority: a high-priority loader from B = 128 on, profiles/r02/v43_ab_loader_priority_*.log
+    # — kept for --set main_priority=0.)
     prio = getattr(args, "loader_priority", None)
     if prio is None:
-        prio = -1 if B >= 128 else 0
+        prio = (0 if capacity is None else -1) if args.main_priority else (-1 if B >= 128 else 0)
     loader = torch.cuda.Stream(device=dev, priority=prio)
 
     def make():
@@ -254,6 +258,7 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
            "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
                                 "collate_and_prepare": round(host_make / args.steps * 1e3, 3)},
            "eager_steps": trainer.rebind_misses - m0,
+           "stream_priorities": {"step": args.main_priority, "loader": prio, "prefetch": depth},
            "signature": ("every batch padded to one capacity (store.BatchCapacity)" if capacity is not None else
                          "fixed: every synthetic graph has 60 atoms, so every batch has the captured signature "
                          "(best case; see e2e_variable for variable-size graphs)"),
@@ -628,11 +633,15 @@ def main():
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    args.main_priority = int(dict(x.split("=", 1) for x in args.set).get("main_priority", 0))
+    # every stream of the step at high priority (-1, the highest torch exposes; equal among themselves,
+    # so the bare step is unchanged), so that a batch-preparation stream at normal priority takes only
+    # what the step leaves idle (end_to_end).  --set main_priority=0 / stream_priority=0: all normal
+    settings = dict(x.split("=", 1) for x in args.set)
+    args.main_priority = int(settings.get("main_priority", -1))
+    from alignn_mi355x import ops as _ops
+    _ops.STREAM_PRIORITY = int(settings.get("stream_priority", args.main_priority))
     if args.main_priority:
-        # the step's critical-path stream at a higher HIP priority than the weight-gradient side
-        # stream (A/B option; priority -1 is the highest torch exposes)
-        hi = torch.cuda.Stream(device=dev, priority=-1)
+        hi = torch.cuda.Stream(device=dev, priority=args.main_priority)
         hi.wait_stream(torch.cuda.current_stream(dev))
         torch.cuda.set_stream(hi)
 
