@@ -80,7 +80,9 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
     if ((Ktot >= 512 && tiles < 160) || tiles < 32) {
       int64_t want = std::max<int64_t>(1, (cus + tiles / 2) / std::max<int64_t>(tiles, 1));
       if (Ktot >= 512 && Ktot / want >= 1024) want *= 2;
-      const int64_t maxs = std::max<int64_t>(1, Ktot / (Ktot >= 512 ? 240 : 32));
+      // a grid of at most 4 tiles splits down to 16-deep chunks (round-4 sweep, gpurun_out r4g
+      // gemm_sweep_c2.json: the heads' M32 N256 K545 24.6 -> 10.6 us in 32, M256 N36 K23040 30.9 -> 27.3)
+      const int64_t maxs = std::max<int64_t>(1, Ktot / (tiles <= 4 ? 16 : (Ktot >= 512 ? 240 : 32)));
       split = (int)std::min(want, maxs);
     }
   }
@@ -98,7 +100,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;
   // 64-deep stages only for long chunks on at most one workgroup per CU (short-K products and
   // two-per-CU splits run faster 16-deep: M2580 N768 K256 18.3 vs 20.6 us, M1024 N256 K1920 23.3 vs 26.0)
-  else pl.bk = (kchunk >= 512 && tiles * split <= (int64_t)cus) ? 64 : 16;
+  else pl.bk = ((kchunk >= 512 || (tiles <= 4 && kchunk >= 128)) && tiles * split <= (int64_t)cus) ? 64 : 16;
   return pl;
 }
 
