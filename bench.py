@@ -697,10 +697,15 @@ def main():
     e2e, store = None, None
     if args.e2e > 0:
         store, t_build = build_store(args, dev, rank)
-        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
         if c3 is not None:
-            # config C5 at N = 1: the B = 256 bf16 step over the ~10k-graph HBM dataset
+            # config C5 at N = 1: the B = 256 bf16 step over the ~10k-graph HBM dataset; then the C3
+            # trainer is released, so the B = 32 loop runs with one captured trainer alive
             secondary["c5_e2e_b256_bf16"] = end_to_end(args, store, t_build, c3["trainer"], 256, dev, rank, world)
+            _release(c3)
+            c3 = None
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
     _release(r)
     if c3 is not None:
         _release(c3)
