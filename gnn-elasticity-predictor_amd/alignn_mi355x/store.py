@@ -157,6 +157,8 @@ class GraphStore:
         self.extras = extras or {}    # non-tensor per-graph attributes (e.g. material ids)
         self.num_stored = len(next(iter(counts.values())))
         self._staging = None
+        self._stage_ring = []   # pinned host staging slots for collate's offset upload: [tensor, event]
+        self._stage_next = 0
         # dataset index -> stored graph (graphs with NaN / inf dropped, as PtGraphDataset's file list)
         self.ids = self._valid_ids() if drop_invalid else np.arange(self.num_stored, dtype=np.int64)
         self.num_graphs = len(self.ids)
@@ -545,6 +547,24 @@ class GraphStore:
         pl.sample_index = idx
         return pl
 
+    STAGE_SLOTS = 8
+
+    def _stage_slot(self, src: torch.Tensor):
+        """``src`` copied into the next pinned staging slot (grown, never shrunk): a ring of pinned host
+        buffers reused batch after batch, so collate allocates no pinned memory per batch (a pinned
+        allocation can wait for the device).  A slot is reused after the upload that read it ran."""
+        n = src.numel()
+        if len(self._stage_ring) < self.STAGE_SLOTS:
+            self._stage_ring.append([torch.empty(0, dtype=torch.int64).pin_memory(), torch.cuda.Event()])
+        slot = self._stage_ring[self._stage_next % len(self._stage_ring)]
+        self._stage_next += 1
+        slot[1].synchronize()   # the upload that last read this slot (long done but for 8 batches in flight)
+        if slot[0].numel() < n:
+            slot[0] = torch.empty(max(n, 2 * slot[0].numel()), dtype=torch.int64).pin_memory()
+        buf = slot[0][:n]
+        buf.copy_(src)
+        return buf, slot[1]
+
     def collate(self, indices, lg_offset: str = "num_nodes", capacity: Optional[BatchCapacity] = None) -> Batch:
         """Batch of the given graphs, assembled on the device (same tensors as
         ``Batch.from_data_list([graphs...], lg_offset)``).  With a ``capacity`` the batch is padded
@@ -572,8 +592,11 @@ class GraphStore:
         flat = np.concatenate(host).astype(np.int64)
         staged = torch.from_numpy(flat)
         if dev.type == "cuda":
-            staged = staged.pin_memory()
-        offs = staged.to(dev, non_blocking=True)
+            staged, ev = self._stage_slot(staged)
+            offs = staged.to(dev, non_blocking=True)
+            ev.record(torch.cuda.current_stream(dev))   # the slot is free again once the copy has read it
+        else:
+            offs = staged.to(dev)
         views, o = [], 0
         for h in host:
             views.append(offs[o:o + len(h)])
