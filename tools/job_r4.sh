@@ -77,6 +77,9 @@ for st in "$@"; do
         run lp_def 500 python bench.py --no-cpu-baseline ;;
     lp2) run lp2_a 500 python bench.py --no-cpu-baseline
          run lp2_b 500 python bench.py --no-cpu-baseline --set prefetch=2 ;;
+    hwq) run hwq4 500 python bench.py --no-cpu-baseline
+         GPU_MAX_HW_QUEUES=8 run hwq8 500 python bench.py --no-cpu-baseline
+         GPU_MAX_HW_QUEUES=8 run hwq8b 500 python bench.py --no-cpu-baseline ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
