@@ -80,6 +80,8 @@ _SIGNATURES = {
     "alignn_tconv_fwd": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                           c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_family": ([c_i32, c_i32, c_vp, c_vp, c_vp], c_i32),
+    "alignn_tconv_bwd_src_by_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                      c_vp, c_i64, c_vp], c_i32),
     "alignn_tconv_fwd_ex": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                              c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_tconv_bwd_dst_ex": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,

@@ -485,11 +485,13 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.sumA = torch.empty(na, H, device=dev)
     c.mstat = torch.empty(na, H, device=dev)
     c.den = torch.empty(na, H, device=dev)
-    c.KV16 = None
+    c.KV16 = c.QKV16 = None
     if F is not None and F.dtype == torch.bfloat16 and feat_row is None:
         # bf16 storage (config C3), the line graph: the attention gathers K|V from a bf16 copy and streams
         # the bf16 angle hidden layer (the atom graph's bf16 bond-state rows go through tconv_fwd)
-        c.KV16 = ops.cast_bf16(c.QKV[:, D:3 * D])
+        # one bf16 copy of Q|K|V: K|V gathered by the attention, Q by the source-side backward
+        c.QKV16 = ops.cast_bf16(c.QKV)
+        c.KV16 = c.QKV16[:, D:3 * D]
         c.mfma = mfma and D == 256 and H == 4
         fwd = ops.lg_fwd_mfma if c.mfma else ops.lg_fwd_bf16
         fwd(g, D, H, c.QKV, c.KV16, c.U, c.wbar, F, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att)
@@ -585,7 +587,12 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     early = wgrad_early if side is not None else 0
     if early >= 2:
         _weight_grads(*wg, part="a")     # final once the target-side kernel is done
-    ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
+    if c.QKV16 is not None:
+        # bf16 storage: the gathered target rows (Q, dout) from bf16 copies — half the traffic
+        ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D], Q16=c.QKV16[:, :D],
+                          dout16=ops.cast_bf16(dout_a))
+    else:
+        ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D])
     if keep_edge_scalars:
         c.edge_scalars = (Vd, dz_e, al_e)
     dQv = dQKV[:, :D].view(na, H, C).transpose(0, 1)

@@ -979,12 +979,31 @@ def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Te
     return out
 
 
-def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV, by_source: bool = True):
+def tconv_bwd_src(g: GraphCSR, D: int, H: int, QKVR, dout, dz_e, alpha_e, dKV, by_source: bool = True,
+                  Q16: Optional[torch.Tensor] = None, dout16: Optional[torch.Tensor] = None):
     """Source-side attention backward.  by_source: over the by-source target list
-    (alignn_tconv_bwd_src_by, the default); False: the plain entry (alignn_tconv_bwd_src), same bits."""
+    (alignn_tconv_bwd_src_by, the default); False: the plain entry (alignn_tconv_bwd_src), same bits.
+    Q16 / dout16 (bf16 storage, both or neither): the gathered target rows from bf16 copies
+    (alignn_tconv_bwd_src_by_bf16; QKVR and dout are then not read)."""
     if (QKVR.size(0) < g.n or dout.numel() < g.n * D or dKV.size(0) < g.n or dKV.size(1) < 2 * D
             or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H):
         raise ValueError("tconv_bwd_src: operands do not cover the graph's n nodes / m edges")
+    if (Q16 is None) != (dout16 is None):
+        raise ValueError("tconv_bwd_src: Q16 and dout16 go together")
+    if Q16 is not None and g.m > 0:
+        for t, what in ((Q16, "Q16"), (dout16, "dout16")):
+            if t.dtype != torch.bfloat16 or t.size(0) < g.n or t.size(1) < D or t.stride(1) != 1:
+                raise ValueError(f"tconv_bwd_src: {what} must be bf16 [n, >= D] row-major")
+        if not dout16.is_contiguous() or dout16.size(1) != D:
+            raise ValueError("tconv_bwd_src: dout16 must be a contiguous [n, D] tensor")
+        ds = g.dst_src()
+        fn = lambda: check(_lib.lib().alignn_tconv_bwd_src_by_bf16(  # noqa: E731
+            g.n, g.m, D, H, g.off_src.data_ptr(), g.pos_src.data_ptr(), ds.data_ptr(), Q16.data_ptr(),
+            Q16.stride(0), dout16.data_ptr(), dz_e.data_ptr(), alpha_e.data_ptr(), dKV.data_ptr(), dKV.stride(0),
+            stream_ptr()), "alignn_tconv_bwd_src_by_bf16")
+        nbytes = _tconv_bytes(g.n, g.m, D, H, "bwd_src") - 4.0 * g.n * D   # Q and dout rows at 2 bytes
+        profiling.launch(f"tconv_bwd_src n{g.n} m{g.m} Q16", 0.0, nbytes, fn)
+        return
     if by_source and g.m > 0:
         ds = g.dst_src()
         fn = lambda: check(_lib.lib().alignn_tconv_bwd_src_by(  # noqa: E731

@@ -664,6 +664,9 @@ struct BwdSrcParams {
   const float* alpha_e;
   float* dKV; int64_t lddkv;
   const int32_t* dst_src;  // optional: dst_at[pos_src[i]] in by-source order (one index level less)
+  // bf16 storage (tconv_bwd_src2_kernel<.., true>): the gathered target rows Q (ld ldq16) and dout
+  // as bf16 copies, widened exactly at the load (autocast: Q is a bf16 Linear output)
+  const uint16_t* Q16; int64_t ldq16; const uint16_t* dout16;
 };
 
 #ifndef ALIGNN_SRC_PF
@@ -722,8 +725,8 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
 // position are two independent scalar loads instead of a dependent pair, the next group's indices are
 // loaded while this group's rows are in flight, and tail edges are clamped to the source's last
 // edge with their scalars zeroed (unconditional loads).  Bitwise equal to tconv_bwd_src_kernel.
-template <int VPL, int H>
-__global__ __launch_bounds__(256) void tconv_bwd_src2_kernel(BwdSrcParams p) {
+template <int VPL, int H, bool QBF>
+__device__ __forceinline__ void tconv_bwd_src2_body(const BwdSrcParams& p) {
   constexpr int PF = SRC_PF;
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
@@ -756,8 +759,13 @@ __global__ __launch_bounds__(256) void tconv_bwd_src2_kernel(BwdSrcParams p) {
         const int64_t po = pos[cur][j], d = dd[cur][j];
         dz[j] = p.dz_e[po * H + hl];
         al[j] = p.alpha_e[po * H + hl];
-        vload(p.QKVR + d * p.ldq + j0, qv[j]);
-        vload(p.dout + d * D + j0, gv[j]);
+        if constexpr (QBF) {
+          vload_bf(p.Q16 + d * p.ldq16 + j0, qv[j]);
+          vload_bf(p.dout16 + d * D + j0, gv[j]);
+        } else {
+          vload(p.QKVR + d * p.ldq + j0, qv[j]);
+          vload(p.dout + d * D + j0, gv[j]);
+        }
       }
       if (ib + PF < end) indices(pos[cur ^ 1], dd[cur ^ 1], ib + PF);
 #pragma unroll
@@ -779,6 +787,16 @@ __global__ __launch_bounds__(256) void tconv_bwd_src2_kernel(BwdSrcParams p) {
   }
 }
 
+template <int VPL, int H>
+__global__ __launch_bounds__(256) void tconv_bwd_src2_kernel(BwdSrcParams p) {
+  tconv_bwd_src2_body<VPL, H, false>(p);
+}
+
+// bf16 target rows (the gathered Q and dout rows are the kernel's traffic: half the bytes)
+template <int VPL, int H>
+__global__ __launch_bounds__(256) void tconv_bwd_src2_bf16_kernel(BwdSrcParams p) {
+  tconv_bwd_src2_body<VPL, H, true>(p);
+}
 // ---------------------------------------------------------------------------------------------
 // Dispatch on (VPL, H)
 // ---------------------------------------------------------------------------------------------
@@ -826,7 +844,8 @@ static void launch_bwd_dst(const BwdDstParams& p, const Sched& sc, hipStream_t s
 
 template <int VPL, int H>
 static void launch_bwd_src(const BwdSrcParams& p, hipStream_t s) {
-  if (p.dst_src) launch((tconv_bwd_src2_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  if (p.Q16) launch((tconv_bwd_src2_bf16_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  else if (p.dst_src) launch((tconv_bwd_src2_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
   else launch((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
 }
 
@@ -1000,5 +1019,29 @@ extern "C" int alignn_tconv_bwd_src_by(int64_t n, int64_t m, int32_t D, int32_t 
   const int vpl = vpl_for(D);
   ALIGNN_DISPATCH_VH(vpl, H, launch_bwd_src, p, s);
   ALIGNN_LAUNCH_CHECK("tconv_bwd_src2_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_tconv_bwd_src_by_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_src,
+                                            const int32_t* pos_src, const int32_t* dst_src, const uint16_t* Q16,
+                                            int64_t ldq16, const uint16_t* dout16, const float* dz_e,
+                                            const float* alpha_e, float* dKV, int64_t lddkv, void* stream) {
+  int rc = check_dims(D, H);
+  if (rc) return rc;
+  if (!dst_src || !Q16 || !dout16) {
+    set_error("tconv_bwd_src_by_bf16: dst_src, Q16 and dout16 are required");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if ((D % 4) || (ldq16 % 4) || (reinterpret_cast<uintptr_t>(Q16) & 7) || (reinterpret_cast<uintptr_t>(dout16) & 7)) {
+    set_error("tconv_bwd_src_by_bf16: bf16 rows need D %% 4 == 0, ldq16 %% 4 == 0 and 8-byte alignment");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (n == 0) return ALIGNN_OK;
+  BwdSrcParams p{n, m, D, 0, off_src, pos_src, nullptr, nullptr, 0, nullptr, dz_e, alpha_e, dKV, lddkv, dst_src,
+                 Q16, ldq16, dout16};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int vpl = vpl_for(D);
+  ALIGNN_DISPATCH_VH(vpl, H, launch_bwd_src, p, s);
+  ALIGNN_LAUNCH_CHECK("tconv_bwd_src2_bf16_kernel");
   return ALIGNN_OK;
 }

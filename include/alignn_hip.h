@@ -359,6 +359,14 @@ int alignn_tconv_bwd_src_by(int64_t n, int64_t m, int32_t D, int32_t H, const in
                             const int32_t* pos_src, const int32_t* dst_src, const float* QKVR, int64_t ldq,
                             const float* dout, const float* dz_e, const float* alpha_e, float* dKV, int64_t lddkv,
                             void* stream);
+/* bf16 storage (config C3: Q is a bf16 Linear output under the reference's autocast, train.py:632-636):
+ * the same sums with the gathered target rows read from bf16 copies — Q16 [n, ldq16] and dout16
+ * [n, D] — widened exactly at the load (the fp32 entry on the widened rows gives the same bits);
+ * these rows are the kernel's traffic, so it halves.  D % 4 == 0, ldq16 % 4 == 0, 8-byte aligned. */
+int alignn_tconv_bwd_src_by_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_src,
+                                 const int32_t* pos_src, const int32_t* dst_src, const uint16_t* Q16, int64_t ldq16,
+                                 const uint16_t* dout16, const float* dz_e, const float* alpha_e, float* dKV,
+                                 int64_t lddkv, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Gate + LayerNorm + ReLU + dropout + residual, fused row kernel.  Replaces TransformerConv's

@@ -360,3 +360,28 @@ def test_atom_attention_bf16_feature_rows_bitwise_vs_fp32_on_rounded_rows(drop):
     torch.cuda.synchronize()
     for i, (x, y) in enumerate(zip(*outs)):
         assert torch.equal(x, y), i
+
+
+def test_source_side_backward_bf16_rows_bitwise_vs_fp32_on_rounded_rows():
+    """alignn_tconv_bwd_src_by_bf16 (the line graph's source-side backward at bf16 storage: Q and dout
+    gathered from bf16 copies) equals the fp32 kernel on the same rows widened to fp32, bit for bit."""
+    from alignn_mi355x import ops
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.synthetic import mp_like_batch
+    b = mp_like_batch(8).to(DEV)
+    g = prepare_batch(b).lg
+    n, m, D, H = g.n, g.m, 256, 4
+    gen = torch.Generator(device="cpu").manual_seed(31)
+    QKV16 = torch.randn(n, 3 * D, generator=gen).to(DEV).bfloat16()
+    dout16 = torch.randn(n, D, generator=gen).to(DEV).bfloat16()
+    dz, al = torch.randn(m, H, generator=gen).to(DEV), torch.rand(m, H, generator=gen).to(DEV)
+    out = []
+    for bf in (True, False):
+        dKV = torch.empty(n, 2 * D, device=DEV)
+        if bf:
+            ops.tconv_bwd_src(g, D, H, QKV16.float(), dout16.float(), dz, al, dKV, Q16=QKV16[:, :D], dout16=dout16)
+        else:
+            ops.tconv_bwd_src(g, D, H, QKV16.float(), dout16.float(), dz, al, dKV)
+        out.append(dKV)
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], out[1])
