@@ -530,7 +530,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
                    wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None,
-                   Wt: Optional[torch.Tensor] = None) -> None:
+                   Wt: Optional[torch.Tensor] = None, bf16_src: bool = True) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -587,7 +587,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     early = wgrad_early if side is not None else 0
     if early >= 2:
         _weight_grads(*wg, part="a")     # final once the target-side kernel is done
-    if c.QKV16 is not None:
+    if c.QKV16 is not None and bf16_src:
         # bf16 storage: the gathered target rows (Q, dout) from bf16 copies — half the traffic
         ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D], Q16=c.QKV16[:, :D],
                           dout16=ops.cast_bf16(dout_a))
@@ -754,6 +754,8 @@ class AlignnEngine:
         # could overlap the bond encoder and the first line block.  Measured within noise, slightly
         # negative (B = 32: 9,117 -> 9,034 graphs/s; C3: 19,531 -> 19,436; gpurun_out r4f pre_*): off
         self.preamble_aux = False
+        # bf16 storage: the line graph's source-side backward gathers Q and dout as bf16 copies
+        self.bf16_src = True
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
@@ -1078,12 +1080,12 @@ class AlignnEngine:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
                                    wgrad_early=wgrad, dX_add=add,
-                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l])
+                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
                                    wgrad_early=wgrad, dX_add=add,
-                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l])
+                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

@@ -80,6 +80,10 @@ for st in "$@"; do
     hwq) run hwq4 500 python bench.py --no-cpu-baseline
          GPU_MAX_HW_QUEUES=8 run hwq8 500 python bench.py --no-cpu-baseline
          GPU_MAX_HW_QUEUES=8 run hwq8b 500 python bench.py --no-cpu-baseline ;;
+    src) run src_off 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.bf16_src=0
+         run src_on 300 python "${C3[@]}" --steps 10 --warmup 3
+         run src_off2 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.bf16_src=0
+         run src_on2 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
