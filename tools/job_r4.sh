@@ -84,6 +84,7 @@ for st in "$@"; do
          run src_on 300 python "${C3[@]}" --steps 10 --warmup 3
          run src_off2 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.bf16_src=0
          run src_on2 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    gbst) run gbst 600 python -u tools/gemm_bench.py --quick --reps 5 --batch 256 --precision bf16 --flag 512 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
                   python "${Q[@]}" --steps 10 --warmup 3 --no-roofline ;;
