@@ -346,6 +346,7 @@ GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
 GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
 GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an operand / the output
+GEMM_STREAM = 8192    # ALIGNN_GEMM_STREAM: the streaming kernel's row floor 32768 -> 4096 (tests / A/B)
 
 
 @contextmanager

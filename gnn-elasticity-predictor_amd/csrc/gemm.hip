@@ -196,11 +196,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_
 // alpha acc (column layout) -> LDS tile -> rows: fma(beta, C, .), + bias, ReLU, mask, 16-byte stores
 // (epilogue_value's order).  Rows past M fall outside the store descriptor and are dropped; beta == 0
 // reads an empty descriptor.
-template <bool BETA, bool MASK, bool CBF>
+// The C values band_store's beta term reads, loaded ahead (CPRE: issued before the band's MFMAs, so
+// the read is in flight while they run instead of exposed in the epilogue)
+__device__ __forceinline__ void load_c(gf4 (&c)[16], const GemmParams& p, __amdgpu_buffer_rsrc_t cld, int64_t row0,
+                                       int lane) {
+  const int rr = lane >> 1, cc = (lane & 1) * 16;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * 4);
+      c[4 * j + i] = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
+    }
+  asm volatile("" ::: "memory");
+}
+
+template <bool BETA, bool MASK, bool CBF, bool CPRE = false>
 __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], const float* __restrict__ bptr,
                                            float* __restrict__ Ls, __amdgpu_buffer_rsrc_t cst,
                                            __amdgpu_buffer_rsrc_t cld, __amdgpu_buffer_rsrc_t cmk, int64_t row0,
-                                           int l32, int h, int lane) {
+                                           int l32, int h, int lane, const gf4* cpre = nullptr) {
   const int rr = lane >> 1, cc = (lane & 1) * 16;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -212,7 +227,7 @@ __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (
       gf4 v = *reinterpret_cast<const gf4*>(Ls + rr * EPI_LD + cc + 4 * i);
       const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * (CBF ? 2 : 4));
       if constexpr (BETA) {   // the tiled epilogue's order: fma(beta, C, alpha acc), then + bias
-        const gf4 c = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
+        const gf4 c = CPRE ? cpre[4 * j + i] : __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
         v = gf4{fmaf(p.beta, c.x, v.x), fmaf(p.beta, c.y, v.y), fmaf(p.beta, c.z, v.z), fmaf(p.beta, c.w, v.w)};
       }
       if (bptr) {
@@ -293,17 +308,27 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
   floatx16 acc[4];
   int64_t band = q;
   if (band >= nbands) return;
+  // bf16 A with a beta term (dX += dR W at C3): the band's C rows are loaded with the band's A rows,
+  // one band ahead, into two more register sets (the bf16 A sets are half as wide: room for them)
+  constexpr bool CPRE = BETA && ABF && !MASK;
+  gf4 c0[CPRE ? 16 : 1], c1[CPRE ? 16 : 1];
+  auto lc = [&](gf4 (&c)[CPRE ? 16 : 1], int64_t b) {
+    if constexpr (CPRE) load_c(c, p, cld, min(b, nbands - 1) * ROWS + wr * 32, lane);
+  };
   lband(a0, arow(band));
+  lc(c0, band);
   while (true) {  // two bands per iteration: the register sets keep fixed names
     const int64_t b1 = band + Q;
     lband(a1, arow(min(b1, nbands - 1)));
+    lc(c1, b1);
     band_mma<KT, ABF>(acc, a0, Bs, col0, l32, h);
-    band_store<BETA, MASK, CBF>(p, acc, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane);
+    band_store<BETA, MASK, CBF, CPRE>(p, acc, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane, c0);
     if (b1 >= nbands) break;
     const int64_t b2 = b1 + Q;
     lband(a0, arow(min(b2, nbands - 1)));
+    lc(c0, b2);
     band_mma<KT, ABF>(acc, a1, Bs, col0, l32, h);
-    band_store<BETA, MASK, CBF>(p, acc, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane);
+    band_store<BETA, MASK, CBF, CPRE>(p, acc, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane, c1);
     if (b2 >= nbands) break;
     band = b2;
   }
@@ -312,13 +337,26 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
 }  // namespace bst
 
 // The streaming kernel's shapes (host check): bf16 arithmetic, K in {64, 128, 256}, N a multiple of
-// 256, M >= 4096, A k-contiguous 16-byte rows, no batch / split / batch reduction, epilogue alpha /
+// 256, M >= stream_min_m(), A k-contiguous 16-byte rows, no batch / split / batch reduction, epilogue alpha /
 // beta / bias / ReLU into a row-major C with 32-bit byte offsets.
+// Below this many rows the tiled kernels take the product. In isolation the streaming kernel still
+// wins near M = 16k (N = 768: 55 vs 60 us), but it holds one workgroup per CU for the whole product,
+// and inside the C3 plan, with the other streams' kernels resident, a 16k-row product took 235 us
+// where the tiled one fills in around them (profiles/r04). ALIGNN_GEMM_STREAM_MIN_M overrides it for
+// the A/B (read once).
+static int64_t stream_min_m() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("ALIGNN_GEMM_STREAM_MIN_M");
+    return e ? std::max<int64_t>(4096, std::atoll(e)) : int64_t(32768);
+  }();
+  return v;
+}
+
 static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
   if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOSTREAM) || (a->tile & 15) != 0) return false;
   if (a->batch != 1 || a->reduce_batch || split != 1) return false;
   if (a->K != 64 && a->K != 128 && a->K != 256) return false;
-  if (a->N % bst::NB != 0 || a->M < 4096) return false;
+  if (a->N % bst::NB != 0 || a->M < ((a->tile & ALIGNN_GEMM_STREAM) ? 4096 : stream_min_m())) return false;
   const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, cbf = (a->tile & ALIGNN_GEMM_C_BF16) != 0;
   if (a->tile & ALIGNN_GEMM_B_BF16) return false;
   // bf16 A or C: K = 256 instantiations only, no mask; bf16 C without beta (write-only)

@@ -84,7 +84,7 @@ typedef struct AlignnGemmArgs {
  * give bitwise the same result).  For A/B tests. */
 #define ALIGNN_GEMM_NOPIPE 256
 /* bf16 only: never the streaming kernel (the large-M products K in {64, 128, 256}, N % 256 == 0,
- * M >= 4096 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
+ * M >= 32768 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
 #define ALIGNN_GEMM_NOSTREAM 512
 /* bf16 storage (config C3, autocast's tensor dtypes, train.py:632-636): the A / B pointer holds bf16
  * elements (widened exactly as they are staged; strides stay in elements, vector loads need 8-byte
@@ -93,6 +93,9 @@ typedef struct AlignnGemmArgs {
 #define ALIGNN_GEMM_A_BF16 1024
 #define ALIGNN_GEMM_B_BF16 2048
 #define ALIGNN_GEMM_C_BF16 4096
+/* bf16 only: the streaming kernel's row floor drops from 32768 (the C3-plan-measured crossover; the
+ * environment variable ALIGNN_GEMM_STREAM_MIN_M moves it) to 4096.  For tests and A/B. */
+#define ALIGNN_GEMM_STREAM 8192
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 

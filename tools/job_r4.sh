@@ -28,7 +28,7 @@ pmc() {   # pmc NAME COUNTERS BENCHARGS...
 }
 for st in "$@"; do
   case "$st" in
-    new) run new 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py tests/test_gpu_x_lgmma.py ;;
+    new) run new 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_bf16_io.py tests/test_gpu_x_lgmma.py tests/test_gpu_x_bf16_stream.py ;;
     sched) run sched 600 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_store.py tests/test_gpu_x_capacity.py tests/test_gpu_x_configs.py ;;
     lgm) run lgm 300 python tools/lgm_bench.py --reps 20 ;;
     lgmv) for v in gnn-elasticity-predictor_amd/alignn_mi355x/variants/*.so; do
@@ -84,6 +84,11 @@ for st in "$@"; do
          run src_on 300 python "${C3[@]}" --steps 10 --warmup 3
          run src_off2 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.bf16_src=0
          run src_on2 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    smm) ALIGNN_GEMM_STREAM_MIN_M=4096 run smm_4k 300 python "${C3[@]}" --steps 10 --warmup 3
+         run smm_32k 300 python "${C3[@]}" --steps 10 --warmup 3
+         ALIGNN_GEMM_STREAM_MIN_M=4096 run smm_4k2 300 python "${C3[@]}" --steps 10 --warmup 3
+         run smm_32k2 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    bst) run bst 300 "${PT[@]}" tests/test_gpu_x_bf16_stream.py ;;
     gbst) run gbst 600 python -u tools/gemm_bench.py --quick --reps 5 --batch 256 --precision bf16 --flag 512 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
     rocprof-c2) run rocprof-c2 400 rocprofv3 --kernel-trace --stats -d "$O/rp_c2" -o run --output-format csv -- \
