@@ -132,14 +132,31 @@ struct Params {
   DropParams drop;
 };
 
+// The group's four source ids.  One scalar load of src_at[t0..t0+3] when that lies inside the array:
+// entries past the segment's last edge are the next segment's sources — valid rows, and those edges
+// are masked out of the arithmetic.  Loading them one by one, clamped, compiled to four dependent
+// s_load / s_waitcnt round trips per group on the wave's critical path.
+typedef int i4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void group_src(const Params& p, int32_t t0, int32_t last, int32_t (&s)[G]) {
+  if ((int64_t)t0 + G <= p.m) {
+    const i4u v = *((const __attribute__((address_space(4))) i4u*)(p.src_at + t0));
+    s[0] = v.x; s[1] = v.y; s[2] = v.z; s[3] = v.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < G; ++j) s[j] = sld(p.src_at, min(t0 + j, last));
+  }
+}
+
 // Loads of one group: edges t0..t0+3, clamped to `last` (the segment's last edge position).
 template <bool BF>
 __device__ __forceinline__ void load_group(typename RingT<BF>::type (&r)[G], const Params& p, int32_t t0, int32_t last,
                                            int j0) {
+  int32_t sg[G];
+  group_src(p, t0, last, sg);
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const int32_t t = min(t0 + j, last);
-    const int64_t s = (int64_t)uni(sld(p.src_at, t));
+    const int64_t s = (int64_t)uni(sg[j]);
     if constexpr (BF) {
       const uint16_t* kv = p.KV16 + s * p.ldkv + j0;
       r[j].k = *reinterpret_cast<const u2v*>(kv);
@@ -263,8 +280,21 @@ __device__ __forceinline__ void store_edge_heads(float* __restrict__ out, int64_
 #ifndef ALIGNN_LG3_WPE2
 #define ALIGNN_LG3_WPE2 2
 #endif
-template <int NR>
-struct Occ { static constexpr int wpe = NR == 1 ? ALIGNN_LG3_WPE1 : ALIGNN_LG3_WPE2; };
+// bf16 rows at C3 size (2,027,520 edges over 16,020 targets; tools/lgm_bench.py, variants built
+// with these macros): one group in flight and more waves beat the four-group ring — forward
+// 438 -> 391 us at 3 waves/SIMD, 377 us at 4; target-side backward 497 -> 478 us at 3 (at 4 its
+// registers spill: 635 us).  The fp32 kernels keep two groups at 2 waves/SIMD (B = 32 sweeps).
+#ifndef ALIGNN_LG3_WPE_BF_FWD
+#define ALIGNN_LG3_WPE_BF_FWD 4
+#endif
+#ifndef ALIGNN_LG3_WPE_BF_BWD
+#define ALIGNN_LG3_WPE_BF_BWD 3
+#endif
+template <int NR, bool BF = false, bool FWD = true>
+struct Occ {
+  static constexpr int wpe = BF && NR == 1 ? (FWD ? ALIGNN_LG3_WPE_BF_FWD : ALIGNN_LG3_WPE_BF_BWD)
+                                           : (NR == 1 ? ALIGNN_LG3_WPE1 : ALIGNN_LG3_WPE2);
+};
 
 // Four groups in flight (bf16 rows: a group's loads take half the registers of fp32, so four cost
 // what two do in fp32): fixed register names r0..r3, each refilled four groups ahead right after it
@@ -409,7 +439,7 @@ __device__ __forceinline__ void fwd_group(const Params& p, const Edge (&r)[G], c
 }
 
 template <int H, int NR, bool DROP, bool BF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR>::wpe, Occ<NR>::wpe)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR, BF, true>::wpe, Occ<NR, BF, true>::wpe)))
 void lg3_fwd_kernel(Params p) {
   if constexpr (DROP) resolve_drop(p.drop);
   constexpr int C = D / H;
@@ -621,7 +651,7 @@ __device__ __forceinline__ void bwd_group(const Params& p, const Edge (&r)[G], c
 }
 
 template <int H, int NR, bool DROP, bool BF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR>::wpe, Occ<NR>::wpe)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR, BF, false>::wpe, Occ<NR, BF, false>::wpe)))
 void lg3_bwd_dst_kernel(Params p) {
   if constexpr (DROP) resolve_drop(p.drop);
   constexpr int C = D / H;
@@ -736,9 +766,9 @@ void lg3_bwd_dst_kernel(Params p) {
 #define ALIGNN_LG3_NR_BWD 2
 #endif
 
-// bf16 rows: groups in flight (4: the ring above; 2: as fp32)
+// bf16 rows: groups in flight (1: measured best at C3 with Occ's wave counts; 4: the ring above)
 #ifndef ALIGNN_LG3_NR_BF
-#define ALIGNN_LG3_NR_BF 4
+#define ALIGNN_LG3_NR_BF 1
 #endif
 template <int H, bool DROP, bool BF>
 static void launch_fwd_h(const Params& p, hipStream_t s) {

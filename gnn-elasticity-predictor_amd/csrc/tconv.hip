@@ -669,6 +669,9 @@ struct BwdSrcParams {
   const uint16_t* Q16; int64_t ldq16; const uint16_t* dout16;
 };
 
+#ifndef ALIGNN_SRC_XCD
+#define ALIGNN_SRC_XCD 1
+#endif
 #ifndef ALIGNN_SRC_PF
 #define ALIGNN_SRC_PF 16  // 4 -> 16: +1.2 % same-box (8: +0.6 %; 12, 3 waves/SIMD: -0.4 % vs 16; 24 drops to 1 wave/SIMD; v36, v41)
 #endif
@@ -725,11 +728,21 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
 // position are two independent scalar loads instead of a dependent pair, the next group's indices are
 // loaded while this group's rows are in flight, and tail edges are clamped to the source's last
 // edge with their scalars zeroed (unconditional loads).  Bitwise equal to tconv_bwd_src_kernel.
+// Source of this wave in XCD-contiguous order: workgroups are dispatched round-robin over the 8 XCDs
+// (linear id b lands on XCD b % 8), so XCD x is given the contiguous workgroup range
+// [x*q + min(x, r), ...): a source range's edges reach targets near it (the graphs are banded), and
+// their gathered target rows stay in that XCD's L2 instead of every XCD pulling every row.
+__device__ __forceinline__ int64_t xcd_source(int wave) {
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x * q + min(x, r) + b / 8) * 4 + wave;
+}
+
 template <int VPL, int H, bool QBF>
 __device__ __forceinline__ void tconv_bwd_src2_body(const BwdSrcParams& p) {
   constexpr int PF = SRC_PF;
   const int lane = threadIdx.x & 63;
-  const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
+  const int64_t s = ALIGNN_SRC_XCD ? xcd_source(wave_id()) : (int64_t)blockIdx.x * 4 + wave_id();
   if (s >= p.n) return;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
@@ -797,6 +810,103 @@ template <int VPL, int H>
 __global__ __launch_bounds__(256) void tconv_bwd_src2_bf16_kernel(BwdSrcParams p) {
   tconv_bwd_src2_body<VPL, H, true>(p);
 }
+// bf16 target rows through buffer loads (the C3 line graph: 2,027,520 edges over 16,020 sources).
+// Each edge's offsets are scalars (the instruction's SGPR offset) and the lane's part is one fixed
+// VGPR offset, so a group holds nothing but its data: src2's flat loads formed a 64-bit VGPR address
+// per load (240 VGPRs, 2 waves/SIMD).  Rows stay bf16 in registers until their FMAs; the sums run in
+// src2's order (bitwise equal).  Offsets are 32-bit: the host takes this kernel only when every
+// operand spans < 2 GB.
+#ifndef ALIGNN_SRC3
+#define ALIGNN_SRC3 1
+#endif
+#ifndef ALIGNN_SRC3_PF
+#define ALIGNN_SRC3_PF 8   // C3 step: 8 edges per group (95 VGPRs, 5 waves/SIMD) 20,381-20,431 graphs/s, 16 (2 waves) 19,784-19,850
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n, 0x00020000);
+}
+
+#ifndef ALIGNN_SRC3_WPE
+#define ALIGNN_SRC3_WPE 1  // minimum waves per SIMD asked of the register allocator (1: its own choice)
+#endif
+template <int VPL, int H>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VPL == 4 ? ALIGNN_SRC3_WPE : 1, 8)))
+void tconv_bwd_src3_bf16_kernel(BwdSrcParams p) {
+  static_assert(VPL % 4 == 0, "bwd_src3: four bf16 features per 8-byte load");
+  constexpr int PF = ALIGNN_SRC3_PF;
+  constexpr int NQ = VPL / 4;
+  typedef unsigned u2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int64_t s = ALIGNN_SRC_XCD ? xcd_source(wave_id()) : (int64_t)blockIdx.x * 4 + wave_id();
+  if (s >= p.n) return;
+  const int D = p.D, C = D / H;
+  const int j0 = lane * VPL;
+  const bool act = j0 < D;
+  const int hl = act ? j0 / C : 0;
+  float dk[VPL], dv[VPL];
+  vzero(dk);
+  vzero(dv);
+  const int32_t beg = uni(sld(p.off_src, s)), end = uni(sld(p.off_src, s + 1));
+  if (act && beg < end) {
+    const __amdgpu_buffer_rsrc_t rq = buf_rsrc(p.Q16, p.n * p.ldq16 * 2), rg = buf_rsrc(p.dout16, p.n * D * 2);
+    const __amdgpu_buffer_rsrc_t rz = buf_rsrc(p.dz_e, p.m * H * 4), ra = buf_rsrc(p.alpha_e, p.m * H * 4);
+    const int vrow = j0 * 2, vh = hl * 4;
+    const int32_t last = end - 1;
+    int32_t pos[2][PF], dd[2][PF];
+    auto indices = [&](int32_t (&po)[PF], int32_t (&d)[PF], int32_t ib) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int32_t i = min(ib + j, last);
+        po[j] = uni(sld(p.pos_src, i));
+        d[j] = uni(sld(p.dst_src, i));
+      }
+    };
+    indices(pos[0], dd[0], beg);
+    int cur = 0;
+    for (int32_t ib = beg; ib < end; ib += PF) {
+      u2 qr[PF][NQ], gr[PF][NQ];
+      float dz[PF], al[PF];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int po = pos[cur][j] * H * 4, d = dd[cur][j];
+        dz[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rz, vh, po, 0));
+        al[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, vh, po, 0));
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          qr[j][q] = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(rq, vrow + 8 * q, (int)(d * p.ldq16 * 2), 0));
+          gr[j][q] = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(rg, vrow + 8 * q, d * D * 2, 0));
+        }
+      }
+      if (ib + PF < end) indices(pos[cur ^ 1], dd[cur ^ 1], ib + PF);
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const bool valid = ib + j < end;  // wave-uniform
+        const float zj = valid ? dz[j] : 0.f, aj = valid ? al[j] : 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const float qv[4] = {__builtin_bit_cast(float, qr[j][q].x << 16), __builtin_bit_cast(float, qr[j][q].x & 0xffff0000u),
+                               __builtin_bit_cast(float, qr[j][q].y << 16), __builtin_bit_cast(float, qr[j][q].y & 0xffff0000u)};
+          const float gv[4] = {__builtin_bit_cast(float, gr[j][q].x << 16), __builtin_bit_cast(float, gr[j][q].x & 0xffff0000u),
+                               __builtin_bit_cast(float, gr[j][q].y << 16), __builtin_bit_cast(float, gr[j][q].y & 0xffff0000u)};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            dk[4 * q + k] = fmaf(zj, valid ? qv[k] : 0.f, dk[4 * q + k]);
+            dv[4 * q + k] = fmaf(aj, valid ? gv[k] : 0.f, dv[4 * q + k]);
+          }
+        }
+      }
+      cur ^= 1;
+    }
+  }
+  if (act) {
+    vstore(p.dKV + s * p.lddkv + j0, dk);
+    vstore(p.dKV + s * p.lddkv + D + j0, dv);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Dispatch on (VPL, H)
 // ---------------------------------------------------------------------------------------------
@@ -844,7 +954,16 @@ static void launch_bwd_dst(const BwdDstParams& p, const Sched& sc, hipStream_t s
 
 template <int VPL, int H>
 static void launch_bwd_src(const BwdSrcParams& p, hipStream_t s) {
-  if (p.Q16) launch((tconv_bwd_src2_bf16_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  if (p.Q16) {
+    constexpr int64_t lim = int64_t(1) << 31;
+    if constexpr (VPL % 4 == 0 && ALIGNN_SRC3) {
+      if (p.n * p.ldq16 * 2 < lim && p.n * p.D * 2 < lim && p.m * H * 4 < lim) {
+        launch((tconv_bwd_src3_bf16_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+        return;
+      }
+    }
+    launch((tconv_bwd_src2_bf16_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  }
   else if (p.dst_src) launch((tconv_bwd_src2_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
   else launch((tconv_bwd_src_kernel<VPL, H>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
 }

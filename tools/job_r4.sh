@@ -88,6 +88,34 @@ for st in "$@"; do
          run smm_32k 300 python "${C3[@]}" --steps 10 --warmup 3
          ALIGNN_GEMM_STREAM_MIN_M=4096 run smm_4k2 300 python "${C3[@]}" --steps 10 --warmup 3
          run smm_32k2 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    lgx) run lgx_tests 300 "${PT[@]}" tests/test_gpu_x_lg3.py tests/test_gpu_x_bf16.py
+         ALIGNN_HIP_LIB=$PWD/gnn-elasticity-predictor_amd/alignn_mi355x/variants/base.so run lgx_lgm_base 300 python tools/lgm_bench.py --reps 20
+         run lgx_lgm_new 300 python tools/lgm_bench.py --reps 20
+         ALIGNN_HIP_LIB=$PWD/gnn-elasticity-predictor_amd/alignn_mi355x/variants/base.so run lgx_c2_base 300 python "${Q[@]}" --steps 20 --warmup 5
+         run lgx_c2_new 300 python "${Q[@]}" --steps 20 --warmup 5
+         ALIGNN_HIP_LIB=$PWD/gnn-elasticity-predictor_amd/alignn_mi355x/variants/base.so run lgx_c3_base 300 python "${C3[@]}" --steps 10 --warmup 3
+         run lgx_c3_new 300 python "${C3[@]}" --steps 10 --warmup 3 ;;
+    lgy) VD=$PWD/gnn-elasticity-predictor_amd/alignn_mi355x/variants
+         run lgy_tests 300 "${PT[@]}" tests/test_gpu_x_lg3.py tests/test_gpu_x_bf16.py tests/test_gpu_x_round4.py
+         run lgy_lgm_new 300 python tools/lgm_bench.py --reps 20
+         ALIGNN_HIP_LIB=$VD/base.so run lgy_lgm_base 300 python tools/lgm_bench.py --reps 20
+         for r in 1 2; do
+           for v in base nosrc3 s3pf8; do
+             ALIGNN_HIP_LIB=$VD/$v.so run lgy_c3_${v}_$r 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_${v}_$r.json"
+           done
+           run lgy_c3_new_$r 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_new_$r.json"
+         done ;;
+    lgz) VD=$PWD/gnn-elasticity-predictor_amd/alignn_mi355x/variants
+         run lgz_diff 200 python tools/lg_diff.py
+         run lgz_tests 300 "${PT[@]}" tests/test_gpu_x_round4.py tests/test_gpu_x_lg3.py tests/test_gpu_parity.py
+         for r in 1 2; do
+           for v in noxcd_nosrc3 src3pf8; do
+             ALIGNN_HIP_LIB=$VD/$v.so run lgz_c3_${v}_$r 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_${v}_$r.json"
+           done
+           run lgz_c3_new_$r 300 python "${C3[@]}" --steps 10 --warmup 3 --dump-probes "$O/probes_new_$r.json"
+           ALIGNN_HIP_LIB=$VD/noxcd_nosrc3.so run lgz_c2_noxcd_$r 300 python "${Q[@]}" --steps 20 --warmup 5
+           run lgz_c2_new_$r 300 python "${Q[@]}" --steps 20 --warmup 5
+         done ;;
     bst) run bst 300 "${PT[@]}" tests/test_gpu_x_bf16_stream.py ;;
     gbst) run gbst 600 python -u tools/gemm_bench.py --quick --reps 5 --batch 256 --precision bf16 --flag 512 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
