@@ -669,9 +669,6 @@ struct BwdSrcParams {
   const uint16_t* Q16; int64_t ldq16; const uint16_t* dout16;
 };
 
-#ifndef ALIGNN_SRC_XCD
-#define ALIGNN_SRC_XCD 1
-#endif
 #ifndef ALIGNN_SRC_PF
 #define ALIGNN_SRC_PF 16  // 4 -> 16: +1.2 % same-box (8: +0.6 %; 12, 3 waves/SIMD: -0.4 % vs 16; 24 drops to 1 wave/SIMD; v36, v41)
 #endif
@@ -728,21 +725,11 @@ __global__ __launch_bounds__(256) void tconv_bwd_src_kernel(BwdSrcParams p) {
 // position are two independent scalar loads instead of a dependent pair, the next group's indices are
 // loaded while this group's rows are in flight, and tail edges are clamped to the source's last
 // edge with their scalars zeroed (unconditional loads).  Bitwise equal to tconv_bwd_src_kernel.
-// Source of this wave in XCD-contiguous order: workgroups are dispatched round-robin over the 8 XCDs
-// (linear id b lands on XCD b % 8), so XCD x is given the contiguous workgroup range
-// [x*q + min(x, r), ...): a source range's edges reach targets near it (the graphs are banded), and
-// their gathered target rows stay in that XCD's L2 instead of every XCD pulling every row.
-__device__ __forceinline__ int64_t xcd_source(int wave) {
-  const int64_t nb = gridDim.x, b = blockIdx.x;
-  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
-  return (x * q + min(x, r) + b / 8) * 4 + wave;
-}
-
 template <int VPL, int H, bool QBF>
 __device__ __forceinline__ void tconv_bwd_src2_body(const BwdSrcParams& p) {
   constexpr int PF = SRC_PF;
   const int lane = threadIdx.x & 63;
-  const int64_t s = ALIGNN_SRC_XCD ? xcd_source(wave_id()) : (int64_t)blockIdx.x * 4 + wave_id();
+  const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
   if (s >= p.n) return;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
@@ -840,7 +827,7 @@ void tconv_bwd_src3_bf16_kernel(BwdSrcParams p) {
   constexpr int NQ = VPL / 4;
   typedef unsigned u2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
-  const int64_t s = ALIGNN_SRC_XCD ? xcd_source(wave_id()) : (int64_t)blockIdx.x * 4 + wave_id();
+  const int64_t s = (int64_t)blockIdx.x * 4 + wave_id();
   if (s >= p.n) return;
   const int D = p.D, C = D / H;
   const int j0 = lane * VPL;
