@@ -84,7 +84,7 @@ def parse():
     p.add_argument("--seed", type=int, default=42, help="base seed of the ensemble members (train.py --seed)")
     p.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
                    help="engine option of this run's model (engine.<attr>=0/1|N), trainer optimizer (optimizer=hip) "
-                        "or stream priorities (loader_priority / main_priority); repeatable — for measuring "
+                        "or stream priorities (loader_priority / main_priority / loader_dedicated); repeatable — for measuring "
                         "opt-in paths")
     return p.parse_args()
 
@@ -105,6 +105,8 @@ def apply_settings(args, model):
             kw["optimizer"] = v
         elif k == "loader_priority":
             args.loader_priority = int(v)
+        elif k == "loader_dedicated":
+            args.loader_dedicated = int(v)
         elif k == "main_priority":
             args.main_priority = int(v)
         elif k == "stream_priority":   # the engine's side / aux streams (ops.STREAM_PRIORITY)
@@ -201,6 +203,7 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     the captured plan to it (FusedTrainer._rebind: copies into the captured batch's buffers) and
     replays.  Timed like the headline: barrier + synchronize on both sides, max over ranks."""
     import numpy as np
+    from alignn_mi355x import ops as _ops
     from alignn_mi355x.dp import max_over_ranks
     from alignn_mi355x.engine import prepare_batch
 
@@ -216,7 +219,11 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     prio = getattr(args, "loader_priority", None)
     if prio is None:
         prio = (0 if capacity is None else -1) if args.main_priority else (-1 if B >= 128 else 0)
-    loader = torch.cuda.Stream(device=dev, priority=prio)
+    # A normal-priority loader gets a hardware queue of its own (ops.dedicated_stream): from the pool
+    # of four it could land on a step stream's queue, and which loop ran first decided that (B = 32:
+    # 5,760-5,800 first vs 8,450-8,610 second, gpurun_out r4h-r4k).
+    dedicated = prio == 0 and bool(int(getattr(args, "loader_dedicated", 1)))
+    loader = _ops.dedicated_stream(dev) if dedicated else torch.cuda.Stream(device=dev, priority=prio)
 
     def make():
         with torch.cuda.stream(loader):
@@ -259,7 +266,8 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
            "host_ms_per_step": {"rebind_and_replay": round(host_step / args.steps * 1e3, 3),
                                 "collate_and_prepare": round(host_make / args.steps * 1e3, 3)},
            "eager_steps": trainer.rebind_misses - m0,
-           "stream_priorities": {"step": args.main_priority, "loader": prio, "prefetch": depth},
+           "stream_priorities": {"step": args.main_priority, "loader": prio, "prefetch": depth,
+                                 "loader_queue": "dedicated" if dedicated else "pooled"},
            "signature": ("every batch padded to one capacity (store.BatchCapacity)" if capacity is not None else
                          "fixed: every synthetic graph has 60 atoms, so every batch has the captured signature "
                          "(best case; see e2e_variable for variable-size graphs)"),

@@ -169,6 +169,7 @@ _SIGNATURES = {
     "alignn_graph_census": ([c_vp, c_vp, c_vp], c_i32),
     "alignn_plan_check_deps": ([c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_stream_create": ([c_i32, ctypes.POINTER(c_vp)], c_i32),
+    "alignn_stream_create_dedicated": ([ctypes.POINTER(c_vp)], c_i32),
     "alignn_stream_destroy": ([c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
     "alignn_add_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),

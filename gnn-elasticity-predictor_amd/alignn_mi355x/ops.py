@@ -35,6 +35,24 @@ def _require(t: torch.Tensor, name: str, dtype=torch.float32):
 # ------------------------------------------------------------------------------------------------
 # Execution context: scratch workspaces, auxiliary streams and the device step seed of one engine
 # ------------------------------------------------------------------------------------------------
+_DEDICATED: dict = {}
+
+
+def dedicated_stream(device) -> torch.cuda.Stream:
+    """A stream on a hardware queue of its own (alignn_stream_create_dedicated), one per device, kept
+    for the process: for a batch-preparation stream beside a replayed step.  With the process's
+    pooled queues (GPU_MAX_HW_QUEUES = 4) a loader stream could share a queue with one of the step's
+    streams, and its kernels then wait behind the step's in queue order."""
+    key = _dkey(device)
+    h = _DEDICATED.get(key)
+    if h is None:
+        hv = ctypes.c_void_p()
+        with torch.cuda.device(torch.device(key)):
+            check(_lib.lib().alignn_stream_create_dedicated(ctypes.byref(hv)), "alignn_stream_create_dedicated")
+        h = _DEDICATED[key] = hv.value
+    return torch.cuda.ExternalStream(h, device=torch.device(key))
+
+
 def _dkey(device) -> str:
     d = torch.device(device)
     if d.type == "cuda" and d.index is None:

@@ -636,6 +636,30 @@ extern "C" int alignn_stream_create(int32_t priority, void** out) {
   return ALIGNN_OK;
 }
 
+// A stream on a hardware queue of its own: a CU-masked stream (every CU enabled) is given a new queue
+// instead of one from the process's pool of GPU_MAX_HW_QUEUES (4 here), so a batch-preparation stream
+// cannot end up sharing a queue — and its in-order dispatch — with one of the step's streams.
+extern "C" int alignn_stream_create_dedicated(void** out) {
+  if (!out) return ALIGNN_E_BAD_SHAPE;
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess || cus <= 0) {
+    set_error("alignn_stream_create_dedicated: CU count: %s", hipGetErrorString(e));
+    return ALIGNN_E_HIP;
+  }
+  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+  if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+  hipStream_t s = nullptr;
+  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+  if (e != hipSuccess) {
+    set_error("hipExtStreamCreateWithCUMask: %s", hipGetErrorString(e));
+    return ALIGNN_E_HIP;
+  }
+  *out = reinterpret_cast<void*>(s);
+  return ALIGNN_OK;
+}
+
 extern "C" int alignn_stream_destroy(void* stream) {
   if (!stream) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -658,6 +658,9 @@ int alignn_plan_check_deps(const void* plan, void* graph, int64_t* bad_from, int
  * streams: never one of torch's pooled streams, which may coincide with a capture or loader stream);
  * destroy synchronises it first. */
 int alignn_stream_create(int32_t priority, void** out);
+/* A stream on a hardware queue of its own (CU-masked stream, every CU enabled; normal priority): for
+ * a batch-preparation (loader) stream that must not share in-order dispatch with the step's streams. */
+int alignn_stream_create_dedicated(void** out);
 int alignn_stream_destroy(void* stream);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);

@@ -134,8 +134,11 @@ def test_bf16_storage_attention_vs_fp32_kernels_on_rounded_inputs():
                                   dz=dz[:m], al=al[:m])
             for k in outs["fp32"]:
                 a, r = outs["bf16"][k].double(), outs["fp32"][k].double()
-                assert torch.isfinite(a).all(), (k, H, drop)
-                assert float((a - r).abs().max()) <= 1e-5 * max(float(r.abs().max()), 1e-30), (k, H, drop)
+                fin = torch.isfinite(r)   # mstat is -inf on targets without in-edges
+                assert torch.equal(torch.isfinite(a), fin) and torch.equal(a[~fin], r[~fin]), (k, H, drop)
+                a, r = a[fin], r[fin]
+                if r.numel():
+                    assert float((a - r).abs().max()) <= 1e-5 * max(float(r.abs().max()), 1e-30), (k, H, drop)
 
 
 def test_cast_and_skinny_bf16_outputs_bitwise():
