@@ -223,7 +223,15 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     # of four it could land on a step stream's queue, and which loop ran first decided that (B = 32:
     # 5,760-5,800 first vs 8,450-8,610 second, gpurun_out r4h-r4k).
     dedicated = prio == 0 and bool(int(getattr(args, "loader_dedicated", 1)))
-    loader = _ops.dedicated_stream(dev) if dedicated else torch.cuda.Stream(device=dev, priority=prio)
+    loader = None
+    if dedicated:
+        try:
+            loader = _ops.dedicated_stream(dev)
+        except RuntimeError as e:   # reported in the line; the loop still runs on a pooled stream
+            print(f"[bench] dedicated loader queue unavailable ({e}); pooled stream", file=sys.stderr)
+            dedicated = False
+    if loader is None:
+        loader = torch.cuda.Stream(device=dev, priority=prio)
 
     def make():
         with torch.cuda.stream(loader):
