@@ -324,6 +324,34 @@ def test_store_batch_prepares_without_a_host_sync_and_trains_bitwise_equal():
     assert torch.equal(grads[0], grads[1])
 
 
+def test_batch_prepared_on_a_dedicated_queue_stream_equals_the_current_stream():
+    """ops.dedicated_stream (alignn_stream_create_dedicated: a CU-masked stream on a hardware queue of
+    its own, bench's loader): one per device, reused; a store batch collated and prepared on it has the
+    same line-graph CSR and work list as one prepared on the current stream."""
+    import numpy as np
+    from alignn_mi355x import ops
+    from alignn_mi355x.engine import prepare_batch
+    from alignn_mi355x.store import GraphStore
+    from alignn_mi355x.synthetic import mp_like_graph
+    s1 = ops.dedicated_stream(DEV)
+    assert ops.dedicated_stream(DEV).cuda_stream == s1.cuda_stream
+    assert s1.cuda_stream != torch.cuda.current_stream().cuda_stream
+    st = GraphStore.from_data_list([mp_like_graph(g) for g in range(24)], DEV)
+    sel = np.random.default_rng(5).choice(24, size=16, replace=False)
+    ref = st.collate(sel)
+    prepare_batch(ref)
+    with torch.cuda.stream(s1):
+        b = st.collate(sel)
+    prepare_batch(b, s1)
+    torch.cuda.current_stream().wait_stream(s1)
+    torch.cuda.synchronize()
+    for name in ("lg", "ag"):
+        g, r = getattr(b._alignn_cache, name), getattr(ref._alignn_cache, name)
+        assert g.n == r.n and g.m == r.m
+        for f in ("off_dst", "src_at", "off_src", "pos_src"):
+            assert torch.equal(getattr(g, f), getattr(r, f)), (name, f)
+
+
 # ------------------------------------------------------------------------------------------------
 # bf16 edge-feature rows in the atom-graph attention (alignn_tconv_fwd_ex / _bwd_dst_ex)
 # ------------------------------------------------------------------------------------------------

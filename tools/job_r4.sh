@@ -116,7 +116,7 @@ for st in "$@"; do
            ALIGNN_HIP_LIB=$VD/noxcd_nosrc3.so run lgz_c2_noxcd_$r 300 python "${Q[@]}" --steps 20 --warmup 5
            run lgz_c2_new_$r 300 python "${Q[@]}" --steps 20 --warmup 5
          done ;;
-    e2ed) run e2ed_tests 300 "${PT[@]}" tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py
+    e2ed) run e2ed_tests 300 "${PT[@]}" tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round4.py
           run e2ed_on 400 python bench.py --no-cpu-baseline
           run e2ed_off 400 python bench.py --no-cpu-baseline --set loader_dedicated=0
           run e2ed_on2 400 python bench.py --no-cpu-baseline ;;
