@@ -30,6 +30,16 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "graphs/sec fwd+bwd (ALIGNN, ~60-atom MP crystals) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def survey_bytes_per_graph(s: int, D: int = 256, L: int = 4, N: int = 60, E: int = 720, T: int = 7920,
+                           Fn: int = 206, Fe: int = 36, Fa: int = 11) -> float:
+    """SURVEY §8d's compulsory HBM bytes per MP-like graph (ideal fusion, s bytes per activation):
+    inp = 4(N Fn + E Fe + T Fa + 291) + 4(2E + 2T + N); fwd_l = s(TD + 3ED + 2ND);
+    bwd_l = 2 fwd_l + 8TD; bytes = inp + L(fwd_l + bwd_l).  190.8 MB at s = 4, 128.1 MB at s = 2."""
+    inp = 4 * (N * Fn + E * Fe + T * Fa + 291) + 4 * (2 * E + 2 * T + N)
+    fwd_l = s * (T * D + 3 * E * D + 2 * N * D)
+    return float(inp + L * (fwd_l + 2 * fwd_l + 8 * T * D))
 FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
 BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 PROBE_STEPS = 3            # untimed replays the dominant-kernel ranking sums over
@@ -495,7 +505,11 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
         "gemm_gflop_per_graph": round(step_work["gemm_gflop"] / B, 4),
         "mfma_frac": round(step_work["gemm_gflop"] / B * (value / world) / (mfma_peak * 1e3), 4),
         "tconv_mbyte_per_graph": round(step_work["tconv_gbyte"] * 1e3 / B, 2),
-        "hbm_frac": round(step_work["tconv_gbyte"] / B * value / world / HBM_PEAK_GBS, 4)}
+        "hbm_frac": round(step_work["tconv_gbyte"] / B * value / world / HBM_PEAK_GBS, 4),
+        # the north-star figure for bf16: the survey's per-graph bytes at the measured rate
+        "survey_mbyte_per_graph": round(survey_bytes_per_graph(2 if precision == "bf16" else 4) / 1e6, 2),
+        "survey_hbm_frac": round(survey_bytes_per_graph(2 if precision == "bf16" else 4) / 1e9 * value / world
+                                 / HBM_PEAK_GBS, 4)}
     return {"value": value, "dt": dt, "ms_per_step": dt / steps * 1e3, "launch": launch_mode, "roofline": roof,
             "step_roofline": step_roof, "trainer": trainer, "batch": batch}
 
