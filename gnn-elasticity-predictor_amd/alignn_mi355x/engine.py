@@ -530,7 +530,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
                    wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None,
-                   Wt: Optional[torch.Tensor] = None, bf16_src: bool = True) -> None:
+                   Wt: Optional[torch.Tensor] = None, bf16_src: bool = True,
+                   dx_stream: Optional[torch.cuda.Stream] = None) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -547,7 +548,10 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     dX_add: a second part of the incoming gradient (the atom block's edge-feature gradient), added
     to dX by the gate kernel (ops.gate_ln_bwd).
     Wt: [D, 4D] transposed copy of cv.Wqkvr — the dX products then read the weights K-contiguous
-    (bitwise the same products, fewer cycles)."""
+    (bitwise the same products, fewer cycles).
+    dx_stream: on a compacted graph, the skip projection's dX product (every row, reads only dR) runs
+    there right after the gate kernel, beside the attention backward; joined before the Q/K/V
+    projections' dX product, which accumulates into the same rows (bitwise the same sums, same order)."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -565,6 +569,11 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
                     gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None,
                     dX_add=dX_add)
+    Wb = cv.Wqkvr if Wt is None else Wt.t()   # B operand [4D, D]
+    skip_early = dx_stream is not None and rows is not None
+    if skip_early:
+        with _side_work(dx_stream, (dR, dX, Wb)):
+            ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                      # residual + skip projection
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
     Vd = torch.empty(na, H, D, device=dev)
     ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
@@ -604,11 +613,13 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         ops.gemm(Sz.transpose(0, 1), Mt, dQv, beta=1.0)
     if early:
         _weight_grads(*wg, part="b" if early >= 2 else "ab")
-    Wb = cv.Wqkvr if Wt is None else Wt.t()   # B operand [4D, D]
     if rows is None:
         ops.gemm(dQKVR, Wb, dX, beta=1.0)                               # residual + projections
     else:
-        ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                          # residual + skip projection
+        if skip_early:
+            ops.stream_wait(torch.cuda.current_stream(dev), dx_stream)
+        else:
+            ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                      # residual + skip projection
         ops.gemm(dQKV, Wb[:3 * D], dX, beta=1.0, c_rows=rows)           # + Q/K/V projections (active rows)
     if not early:
         _weight_grads(*wg, part="ab")
@@ -754,6 +765,9 @@ class AlignnEngine:
         # could overlap the bond encoder and the first line block.  Measured within noise, slightly
         # negative (B = 32: 9,117 -> 9,034 graphs/s; C3: 19,531 -> 19,436; gpurun_out r4f pre_*): off
         self.preamble_aux = False
+        # line blocks' skip-projection dX product beside the attention backward: 0 in order, 1 on the
+        # aux stream when the atom blocks do not use it, 2 on the side stream
+        self.skip_dx = 0
         # bf16 storage: the line graph's source-side backward gathers Q and dout as bf16 copies
         self.bf16_src = True
 
@@ -1076,16 +1090,23 @@ class AlignnEngine:
                 # dF of the line convs is the gradient of the angle hidden layer, summed over layers;
                 # the last (l = 0) applies the ReLU mask in place
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
+                dxs = None
+                if side is not None and self.skip_dx == 1 and aux is None:
+                    dxs = ops.aux_stream(dev)
+                elif side is not None and self.skip_dx == 2:
+                    dxs = side
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
                                    wgrad_early=wgrad, dX_add=add,
-                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src)
+                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src,
+                                   dx_stream=dxs)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
                                    wgrad_early=wgrad, dX_add=add,
-                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src)
+                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src,
+                                   dx_stream=dxs)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

@@ -120,6 +120,14 @@ for st in "$@"; do
           run e2ed_on 400 python bench.py --no-cpu-baseline
           run e2ed_off 400 python bench.py --no-cpu-baseline --set loader_dedicated=0
           run e2ed_on2 400 python bench.py --no-cpu-baseline ;;
+    sdx) run sdx_tests 300 "${PT[@]}" tests/test_gpu_x_pending.py tests/test_gpu_x_round4.py
+         for r in 1 2; do
+           run sdx_c2_0_$r 300 python "${Q[@]}" --steps 20 --warmup 5
+           run sdx_c2_1_$r 300 python "${Q[@]}" --steps 20 --warmup 5 --set engine.skip_dx=1
+           run sdx_c2_2_$r 300 python "${Q[@]}" --steps 20 --warmup 5 --set engine.skip_dx=2
+           run sdx_c3_0_$r 300 python "${C3[@]}" --steps 10 --warmup 3
+           run sdx_c3_2_$r 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.skip_dx=2
+         done ;;
     bst) run bst 300 "${PT[@]}" tests/test_gpu_x_bf16_stream.py ;;
     gbst) run gbst 600 python -u tools/gemm_bench.py --quick --reps 5 --batch 256 --precision bf16 --flag 512 ;;
     c3m) run c3m 300 python "${C3[@]}" --steps 10 --warmup 3 --set engine.attn_mfma=1 --dump-probes "$O/probes_c3m.json" ;;
