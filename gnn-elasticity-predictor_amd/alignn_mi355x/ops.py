@@ -365,9 +365,6 @@ GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (
 GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
 GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an operand / the output
 GEMM_STREAM = 8192    # ALIGNN_GEMM_STREAM: the streaming kernel's row floor 32768 -> 4096 (tests / A/B)
-GEMM_REG = 16384      # ALIGNN_GEMM_REG: fp32 register-direct kernel, 64x32 per wave (k-contiguous operands)
-GEMM_REG2 = 32768     # ALIGNN_GEMM_REG2: the same, 64x64 per wave (both bits: 32x64)
-GEMM_NOREG = 65536    # ALIGNN_GEMM_NOREG: never the register-direct kernel (A/B tests)
 
 
 @contextmanager

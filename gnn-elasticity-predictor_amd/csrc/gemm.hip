@@ -352,37 +352,6 @@ static int64_t stream_min_m() {
   return v;
 }
 
-// fp32 register-direct kernel (gemm_reg.hip) for k-contiguous x k-contiguous products: forced by the
-// ALIGNN_GEMM_REG* tile bits (A/B, tests), or automatic for M >= ALIGNN_GEMM_REG_MIN_M (default 8192)
-// in the mode ALIGNN_GEMM_REG_MODE names (environment, read once).
-static int reg_env_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("ALIGNN_GEMM_REG_MODE");
-    return e ? std::max(0, std::min(3, std::atoi(e))) : 0;
-  }();
-  return v;
-}
-static int64_t reg_min_m() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("ALIGNN_GEMM_REG_MIN_M");
-    return e ? std::max<int64_t>(64, std::atoll(e)) : int64_t(8192);
-  }();
-  return v;
-}
-static int gemm_reg_mode(const AlignnGemmArgs* a, const GemmParams& p, int split) {
-  if ((a->tile & ALIGNN_GEMM_NOREG) || (a->tile & ALIGNN_GEMM_BF16) || p.abf || p.bbf || p.cbf) return 0;
-  const int forced = ((a->tile & ALIGNN_GEMM_REG) ? 1 : 0) + ((a->tile & ALIGNN_GEMM_REG2) ? 2 : 0);
-  int mode = forced;
-  if (!forced) {
-    if ((a->tile & 15) != 0 || a->M < reg_min_m()) return 0;
-    mode = reg_env_mode();
-  }
-  if (mode == 0 || split != 1 || p.reduce_batch || !p.vecA || !p.vecB) return 0;
-  if (a->sak != 1 || a->sbk != 1) return 0;   // both operands k-contiguous
-  if (a->K < 16 * gemm_reg_depth() || a->K % (16 * gemm_reg_depth()) != 0) return 0;
-  return mode;
-}
-
 static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
   if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOSTREAM) || (a->tile & 15) != 0) return false;
   if (a->batch != 1 || a->reduce_batch || split != 1) return false;
@@ -504,11 +473,6 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (bf16_stream_ok(a, pl.split)) {
     bf16_stream_launch(p, device_cus(), s);
     ALIGNN_LAUNCH_CHECK("gemm_bf16_stream_kernel");
-    return ALIGNN_OK;
-  }
-  if (const int rm = gemm_reg_mode(a, p, pl.split)) {
-    gemm_reg_launch(p, rm, nbatch_out, s);
-    ALIGNN_LAUNCH_CHECK("gemm_reg_kernel");
     return ALIGNN_OK;
   }
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);

@@ -561,11 +561,6 @@ void gemm_tiled_launch(const GemmParams& p, int bm, int bn, bool akc, bool bkc, 
   else dispatch_layout<64, 64, PR>(p, akc, bkc, grid, bk, nopipe, s);
 }
 
-// gemm_reg.hip: the register-direct fp32 kernel (mode 1: 64x32 per wave, 2: 64x64, 3: 32x64) and
-// its K granularity in 16-deep slices
-void gemm_reg_launch(const GemmParams& p, int mode, int64_t nbatch, hipStream_t s);
-int gemm_reg_depth();
-
 extern template void gemm_tiled_launch<0>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
 extern template void gemm_tiled_launch<1>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
 

@@ -96,13 +96,6 @@ typedef struct AlignnGemmArgs {
 /* bf16 only: the streaming kernel's row floor drops from 32768 (the C3-plan-measured crossover; the
  * environment variable ALIGNN_GEMM_STREAM_MIN_M moves it) to 4096.  For tests and A/B. */
 #define ALIGNN_GEMM_STREAM 8192
-/* fp32 only, both operands k-contiguous (sak = sbk = 1, 16-byte rows), no split / batch reduction,
- * K % 64 == 0: the register-direct kernel (one wave per 64x32 (REG), 64x64 (REG2) or 32x64 (both)
- * output tile, fragments loaded straight into VGPRs, no LDS).  Bitwise equal to the tiled kernels.
- * Forced by these bits (A/B, tests); ALIGNN_GEMM_NOREG keeps a product off it. */
-#define ALIGNN_GEMM_REG 16384
-#define ALIGNN_GEMM_REG2 32768
-#define ALIGNN_GEMM_NOREG 65536
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
