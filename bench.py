@@ -581,17 +581,29 @@ def _release(r):
     torch.cuda.empty_cache()
 
 
+def _visible_gpus() -> int:
+    """Number of GPUs a rank would see, counted in a child interpreter so that this (launcher)
+    process never calls into HIP; 0 when the child fails."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else 0
+    except (ValueError, IndexError):
+        return 0
+
+
 def launch_ranks(args) -> int:
     """``--gpus N`` run without a launcher: start N ranks with torch.distributed.run on this node
     (rendezvous on 127.0.0.1, a free port), each running this script with the same arguments, and
     return their exit status (non-zero if any rank failed or fewer than N could start).  Nothing
-    here initialises the GPU (device_count does not on this image), so no process that touched it
-    ever starts another."""
+    here touches the GPU: the devices are counted by a child interpreter (_visible_gpus), so no
+    process that initialised HIP ever starts another."""
     import socket
     import subprocess
     n = args.gpus
     if not args.dry_run and not args.share_device:
-        have = torch.cuda.device_count()
+        have = _visible_gpus()
         if have < n:
             print(f"[bench] --gpus {n}: only {have} GPU(s) visible", file=sys.stderr)
             return 2

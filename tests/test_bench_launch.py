@@ -38,3 +38,17 @@ def test_world_size_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"], cwd=REPO,
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_launcher_counts_gpus_without_touching_hip():
+    """The self-launch path counts devices in a child interpreter: the launching process itself never
+    initialises HIP (a process that did must not start another program on this pool)."""
+    code = ("import sys; sys.argv = ['bench.py']; sys.path.insert(0, %r); import bench, torch; "
+            "n = bench._visible_gpus(); print(n, torch.cuda.is_initialized())" % REPO)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=_env(), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    n, init = r.stdout.split()[-2:]
+    assert init == "False"
+    import torch
+    assert int(n) == (torch.cuda.device_count() if torch.cuda.is_available() else 0)
