@@ -17,7 +17,8 @@ import alignn_mi355x as A  # noqa: E402
 from alignn_mi355x import ops  # noqa: E402
 from alignn_mi355x.synthetic import mp_like_batch  # noqa: E402
 
-TILES = {20: "auto"}
+AUTO = -1
+TILES = {AUTO: "auto"}
 TILES.update({b + k: f"{s}/bk{bk}" for k, s in ((1, "128x128"), (2, "128x64"), (3, "64x128"), (4, "64x64"))
          for b, bk in ((0, "auto"), (16, 32), (32, 16), (128, 64))})
 
@@ -62,7 +63,10 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="bf16: the step's products with bf16 matrix-core inputs (config C3); the library "
                          "reference is then torch.matmul on bf16 copies of the operands")
+    ap.add_argument("--min-m", type=int, default=0, help="only products with at least this many rows")
+    ap.add_argument("--splits", default="1,2,4,8,16,32,64", help="split-K counts the forced plans try")
     a = ap.parse_args()
+    splits = [int(x) for x in a.splits.split(",")]
     dev = "cuda"
     torch.manual_seed(0)
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(dev)
@@ -84,6 +88,8 @@ def main():
     tot_auto = tot_best = tot_lib = 0.0
     for key, cs in groups.items():
         c = cs[0]
+        if c["A"].shape[-2] < a.min_m:
+            continue
         C_save = c["C"].clone()
 
         def run(tile=0, split=None, c=c):
@@ -117,16 +123,16 @@ def main():
             tot_flag[0] += t_flag * len(cs)
         trials = {}
         for tile in ([] if a.quick else sorted(TILES)):
-            if tile < 16 or tile == 20:
+            if tile < 16:
                 continue
-            for split in (1, 2, 4, 8, 16, 32, 64):
+            for split in splits:
                 try:
                     trials[(tile, split)] = timeit(lambda: run(tile, split), a.reps)
                 except Exception as e:  # noqa: BLE001 - workspace or shape limits
                     trials[(tile, split)] = float("inf")
         c["C"].copy_(C_save)
         if not trials:
-            trials[(20, 0)] = t_auto
+            trials[(AUTO, 0)] = t_auto
         best = min(trials, key=trials.get)
         n = len(cs)
         tot_auto += t_auto * n
