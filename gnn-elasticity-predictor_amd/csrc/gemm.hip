@@ -352,6 +352,18 @@ static int64_t stream_min_m() {
   return v;
 }
 
+// bf16 arithmetic through bf16 LDS images (gemm_tile.h arithmetic 2, bitwise equal to 1): forced on /
+// off by ALIGNN_GEMM_LDS16 / ALIGNN_GEMM_NOLDS16, otherwise the environment's ALIGNN_GEMM_LDS16
+// (read once) decides.
+static bool lds16(const AlignnGemmArgs* a) {
+  static const bool env = [] {
+    const char* e = std::getenv("ALIGNN_GEMM_LDS16");
+    return e && std::atoi(e) != 0;
+  }();
+  if (a->tile & ALIGNN_GEMM_NOLDS16) return false;
+  return (a->tile & ALIGNN_GEMM_LDS16) || env;
+}
+
 static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
   if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOSTREAM) || (a->tile & 15) != 0) return false;
   if (a->batch != 1 || a->reduce_batch || split != 1) return false;
@@ -478,7 +490,8 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
   const bool np = (a->tile & ALIGNN_GEMM_NOPIPE) != 0;
-  if (a->tile & ALIGNN_GEMM_BF16) gemm_tiled_launch<1>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
+  if ((a->tile & ALIGNN_GEMM_BF16) && lds16(a)) gemm_tiled_launch<2>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
+  else if (a->tile & ALIGNN_GEMM_BF16) gemm_tiled_launch<1>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   else gemm_tiled_launch<0>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {

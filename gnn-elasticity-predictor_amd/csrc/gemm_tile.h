@@ -71,10 +71,16 @@ __device__ __forceinline__ uint16_t bf_rne(float v) { return __builtin_bit_cast(
 
 // Loads one operand tile (ROWS x BKT) into registers.  KC: load along k (general strides,
 // float4 when stride_k==1 and aligned); !KC: load along rows (stride_row == 1).
-template <int ROWS, bool KC, int BKT, int NT = 256>
+template <int ROWS, bool KC, int BKT, bool L16 = false, int NT = 256>
 struct TileLoader {
   static constexpr int F4 = ROWS * BKT / 4 / NT;   // float4 per thread
   static constexpr int KP = BKT + 4;               // padded k-row of the [row][k] image
+  static constexpr int KP16 = BKT + 8;             // L16: bf16 [row][k] image for both layouts (16-byte rows)
+  // !KC thread -> (k, first of four rows) map.  L16 walks k fastest, so a wave's 2-byte transposing
+  // LDS stores land on consecutive halfwords (rows fastest would put 16 lanes on two banks); global
+  // loads then still read 64-byte row pieces (four lanes per k).
+  __device__ __forceinline__ static int nk(int idx) { return L16 ? idx % BKT : idx / (ROWS / 4); }
+  __device__ __forceinline__ static int nr(int idx) { return L16 ? (idx / BKT) * 4 : (idx % (ROWS / 4)) * 4; }
   float4 r[F4];
   const float* base[F4];                           // fast path: this thread's float4 at k = kb
   bool raw = false;                                // r[] holds 4 bf16 values in .x/.y (widened by store)
@@ -92,7 +98,7 @@ struct TileLoader {
         const int64_t gr = min(row0 + idx / (BKT / 4), rows - 1);
         base[i] = eoff(P, gr * srow + kb + (idx % (BKT / 4)) * 4, bf);
       } else {
-        base[i] = eoff(P, (kb + idx / (ROWS / 4)) * sk + row0 + (idx % (ROWS / 4)) * 4, bf);
+        base[i] = eoff(P, (kb + nk(idx)) * sk + row0 + nr(idx), bf);
       }
     }
   }
@@ -128,8 +134,8 @@ struct TileLoader {
             gr = row0 + (idx / (BKT / 4));
             gk = k0 + (idx % (BKT / 4)) * 4 + j;
           } else {
-            gk = k0 + (idx / (ROWS / 4));
-            gr = row0 + (idx % (ROWS / 4)) * 4 + j;
+            gk = k0 + nk(idx);
+            gr = row0 + nr(idx) + j;
           }
           if (gr < rows && gk < kend) v[j] = bf_at(P, KC ? gr * srow + gk * sk : gk * sk + gr);
         }
@@ -145,8 +151,8 @@ struct TileLoader {
         gr = row0 + (idx / (BKT / 4));
         gk = k0 + (idx % (BKT / 4)) * 4;
       } else {
-        gk = k0 + (idx / (ROWS / 4));
-        gr = row0 + (idx % (ROWS / 4)) * 4;
+        gk = k0 + nk(idx);
+        gr = row0 + nr(idx);
       }
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (KC) {
@@ -177,6 +183,36 @@ struct TileLoader {
   }
 
   __device__ __forceinline__ void store(float* __restrict__ lds) {
+    if constexpr (L16) {
+      // bf16 LDS image [row][KP16] for either global layout: values rounded (RNE) once here instead
+      // of per fragment read, raw bf16 operands stored as they are.  KC: one 8-byte store of four k;
+      // !KC (four rows at one k): four 2-byte stores, transposing into the [row][k] image.
+      uint16_t* L = reinterpret_cast<uint16_t*>(lds);
+#pragma unroll
+      for (int i = 0; i < F4; ++i) {
+        const int idx = threadIdx.x + NT * i;
+        uint32_t w0, w1;
+        if (raw) {
+          w0 = __builtin_bit_cast(uint32_t, r[i].x);
+          w1 = __builtin_bit_cast(uint32_t, r[i].y);
+        } else {
+          w0 = (uint32_t)bf_rne(r[i].x) | ((uint32_t)bf_rne(r[i].y) << 16);
+          w1 = (uint32_t)bf_rne(r[i].z) | ((uint32_t)bf_rne(r[i].w) << 16);
+        }
+        if (KC) {
+          const int rr = idx / (BKT / 4), kk = (idx % (BKT / 4)) * 4;
+          *reinterpret_cast<uint2*>(L + rr * KP16 + kk) = make_uint2(w0, w1);
+        } else {
+          const int kk = nk(idx), rr = nr(idx);
+          L[(rr + 0) * KP16 + kk] = (uint16_t)w0;
+          L[(rr + 1) * KP16 + kk] = (uint16_t)(w0 >> 16);
+          L[(rr + 2) * KP16 + kk] = (uint16_t)w1;
+          L[(rr + 3) * KP16 + kk] = (uint16_t)(w1 >> 16);
+        }
+      }
+      raw = false;
+      return;
+    }
     if (raw) {
 #pragma unroll
       for (int i = 0; i < F4; ++i) {
@@ -199,9 +235,9 @@ struct TileLoader {
   }
 };
 
-template <int ROWS, bool KC, int BKT>
+template <int ROWS, bool KC, int BKT, bool L16 = false>
 constexpr int lds_floats() {
-  return KC ? ROWS * (BKT + 4) : BKT * (ROWS + 4);
+  return L16 ? ROWS * (BKT + 8) / 2 : KC ? ROWS * (BKT + 4) : BKT * (ROWS + 4);
 }
 
 // Reads the 8 k-values of lane half h in 16-deep slice `sub` for subtile row `row`:
@@ -248,6 +284,23 @@ __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], con
 #pragma unroll
   for (int s16 = 0; s16 < BKT / 16; ++s16) {
     const int sub = sub0 + s16;
+    if constexpr (BF == 2) {   // bf16 images [row][LD + 8]: a lane's eight k are one 16-byte read
+      const uint16_t* A16 = reinterpret_cast<const uint16_t*>(As);
+      const uint16_t* B16 = reinterpret_cast<const uint16_t*>(Bs);
+      bf16x8 ha[MI], hb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        ha[i] = *reinterpret_cast<const bf16x8*>(A16 + (wm * (BM / 2) + i * 32 + l32) * (LD + 8) + 16 * sub + 8 * h);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        hb[j] = *reinterpret_cast<const bf16x8*>(B16 + (wn * (BN / 2) + j * 32 + l32) * (LD + 8) + 16 * sub + 8 * h);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], hb[j], acc[i][j], 0, 0, 0);
+      continue;
+    }
     float fa[MI][8], fb[NI][8];
 #pragma unroll
     for (int i = 0; i < MI; ++i) read_frag<BM, A_KC, LD>(As, wm * (BM / 2) + i * 32 + l32, h, sub, fa[i]);
@@ -332,7 +385,8 @@ __device__ __forceinline__ float splitk_sum(const GemmParams& p, int64_t b, int6
 template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int BF, bool RB>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
-  constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
+  constexpr bool L16 = BF == 2;
+  constexpr int LA = lds_floats<BM, A_KC, BKT, L16>(), LB = lds_floats<BN, B_KC, BKT, L16>();
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
@@ -353,7 +407,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int64_t ke = min(Ktot, kb + p.kchunk);
 
   // bf16 storage exists only with bf16 arithmetic (host check): compile-time fp32 otherwise
-  const int abf = BF == 1 ? p.abf : 0, bbf = BF == 1 ? p.bbf : 0;
+  const int abf = BF >= 1 ? p.abf : 0, bbf = BF >= 1 ? p.bbf : 0;
   const float* A = eoff(p.A, b * p.sab, abf);
   const float* B = eoff(p.B, b * p.sbb, bbf);
   // (batch, local k) of a global k index; identity unless the batch is reduced (RB)
@@ -372,8 +426,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  TileLoader<BM, A_KC, BKT> la;
-  TileLoader<BN, B_KC, BKT> lb;
+  TileLoader<BM, A_KC, BKT, L16> la;
+  TileLoader<BN, B_KC, BKT, L16> lb;
   // fast loads (block-uniform): vectorisable operand, not batch-reduced, interior tile for a
   // row-contiguous operand; then every full stage [k0, k0 + BKT) <= ke takes them
   const bool fastA = !RB && p.vecA && (A_KC || m0 + BM <= p.M);
@@ -408,7 +462,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     cur ^= 1;
   }
 
-  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF == 1 && p.cbf);
+  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF >= 1 && p.cbf);
 }
 
 // Pipelined variant: two register sets of global loads in flight, so a stage's
@@ -423,8 +477,9 @@ typedef float gf4 __attribute__((ext_vector_type(4)));
 template <int BM, int BN, bool A_KC, bool B_KC, int BKT, int BF>
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
   constexpr int MI = BM / 64, NI = BN / 64;
-  constexpr int LA = lds_floats<BM, A_KC, BKT>(), LB = lds_floats<BN, B_KC, BKT>();
-  constexpr int FA = TileLoader<BM, A_KC, BKT>::F4, FB = TileLoader<BN, B_KC, BKT>::F4;
+  constexpr bool L16 = BF == 2;
+  constexpr int LA = lds_floats<BM, A_KC, BKT, L16>(), LB = lds_floats<BN, B_KC, BKT, L16>();
+  constexpr int FA = TileLoader<BM, A_KC, BKT, L16>::F4, FB = TileLoader<BN, B_KC, BKT, L16>::F4;
   __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
 
   const int64_t tiles_n = (p.N + BN - 1) / BN;
@@ -450,9 +505,9 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  TileLoader<BM, A_KC, BKT> la;
-  TileLoader<BN, B_KC, BKT> lb;
-  const bool abf = BF == 1 && p.abf != 0, bbf = BF == 1 && p.bbf != 0;   // compile-time false for fp32
+  TileLoader<BM, A_KC, BKT, L16> la;
+  TileLoader<BN, B_KC, BKT, L16> lb;
+  const bool abf = BF >= 1 && p.abf != 0, bbf = BF >= 1 && p.bbf != 0;   // compile-time false for fp32
   la.setup_fast(eoff(p.A, b * p.sab, abf), p.sam, p.sak, m0, p.M, kb, abf);
   lb.setup_fast(eoff(p.B, b * p.sbb, bbf), p.sbn, p.sbk, n0, p.N, kb, bbf);
   gf4 pa[FA], pb[FB], qa[FA], qb[FB];
@@ -501,7 +556,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
     load(qa, qb, s0 + 4);
     __syncthreads();
   }
-  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF == 1 && p.cbf);
+  store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF >= 1 && p.cbf);
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC, int PR>
@@ -550,8 +605,9 @@ static void dispatch_layout(const GemmParams& p, bool akc, bool bkc, dim3 grid, 
   else launch_tile<BM, BN, false, false, PR>(p, grid, bk, nopipe, s);
 }
 
-// The tiled kernels of one arithmetic (PR: 0 exact fp32 on v_mfma_f32_32x32x2_f32, 1 bf16 inputs),
-// instantiated in gemm_tile_p<PR>.hip (one translation unit each).
+// The tiled kernels of one arithmetic (PR: 0 exact fp32 on v_mfma_f32_32x32x2_f32, 1 bf16 inputs,
+// 2 bf16 inputs rounded as they are staged into bf16 LDS images — bitwise equal to 1), instantiated
+// in gemm_tile_p<PR>.hip (one translation unit each).
 template <int PR>
 void gemm_tiled_launch(const GemmParams& p, int bm, int bn, bool akc, bool bkc, dim3 grid, int bk, bool nopipe,
                        hipStream_t s) {
@@ -563,5 +619,6 @@ void gemm_tiled_launch(const GemmParams& p, int bm, int bn, bool akc, bool bkc, 
 
 extern template void gemm_tiled_launch<0>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
 extern template void gemm_tiled_launch<1>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
+extern template void gemm_tiled_launch<2>(const GemmParams&, int, int, bool, bool, dim3, int, bool, hipStream_t);
 
 }  // namespace alignn

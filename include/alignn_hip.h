@@ -96,6 +96,11 @@ typedef struct AlignnGemmArgs {
 /* bf16 only: the streaming kernel's row floor drops from 32768 (the C3-plan-measured crossover; the
  * environment variable ALIGNN_GEMM_STREAM_MIN_M moves it) to 4096.  For tests and A/B. */
 #define ALIGNN_GEMM_STREAM 8192
+/* bf16 only, tiled kernels: operands rounded to bf16 as they are staged and kept as bf16 LDS images
+ * (half the LDS bytes, one 16-byte read per fragment, no per-fragment conversion); bitwise equal to
+ * the fp32 images.  LDS16 forces it on, NOLDS16 off (A/B, tests). */
+#define ALIGNN_GEMM_LDS16 16384
+#define ALIGNN_GEMM_NOLDS16 32768
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
