@@ -365,7 +365,7 @@ GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (
 GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
 GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an operand / the output
 GEMM_STREAM = 8192    # ALIGNN_GEMM_STREAM: the streaming kernel's row floor 32768 -> 4096 (tests / A/B)
-GEMM_LDS16 = 16384    # ALIGNN_GEMM_LDS16: bf16 tiled products through bf16 LDS images (forced on)
+GEMM_LDS16 = 16384    # ALIGNN_GEMM_LDS16: bf16 tiled products through bf16 LDS images (forced on; default: A k-contiguous)
 GEMM_NOLDS16 = 32768  # ALIGNN_GEMM_NOLDS16: ... forced off (A/B tests)
 
 

@@ -353,15 +353,19 @@ static int64_t stream_min_m() {
 }
 
 // bf16 arithmetic through bf16 LDS images (gemm_tile.h arithmetic 2, bitwise equal to 1): forced on /
-// off by ALIGNN_GEMM_LDS16 / ALIGNN_GEMM_NOLDS16, otherwise the environment's ALIGNN_GEMM_LDS16
-// (read once) decides.
-static bool lds16(const AlignnGemmArgs* a) {
-  static const bool env = [] {
+// off by ALIGNN_GEMM_LDS16 / ALIGNN_GEMM_NOLDS16; otherwise taken when A is k-contiguous.  C3 sweep
+// (profiles/r04/v3_lds16_*): the products over rows (X·Wᵀ, dX) run 7-28 % faster, e.g. M 16,020 x 768 x
+// 256 60.6 -> 44.6 us, M 15,360 x 1,024 x 256 70.2 -> 51.6; the weight gradients, whose A is
+// row-contiguous and transposed into the image by 2-byte stores, 15-50 % slower (M 256 x 256 x 184,320
+// 108.7 -> 138.1).  ALIGNN_GEMM_LDS16=0 in the environment (read once) turns the default off (A/B).
+static bool lds16(const AlignnGemmArgs* a, bool akc) {
+  static const bool env_off = [] {
     const char* e = std::getenv("ALIGNN_GEMM_LDS16");
-    return e && std::atoi(e) != 0;
+    return e && std::atoi(e) == 0;
   }();
   if (a->tile & ALIGNN_GEMM_NOLDS16) return false;
-  return (a->tile & ALIGNN_GEMM_LDS16) || env;
+  if (a->tile & ALIGNN_GEMM_LDS16) return true;
+  return akc && !env_off;
 }
 
 static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
@@ -490,7 +494,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);
   dim3 grid((unsigned)tiles, 1, (unsigned)(nbatch_out * pl.split));
   const bool np = (a->tile & ALIGNN_GEMM_NOPIPE) != 0;
-  if ((a->tile & ALIGNN_GEMM_BF16) && lds16(a)) gemm_tiled_launch<2>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
+  if ((a->tile & ALIGNN_GEMM_BF16) && lds16(a, akc)) gemm_tiled_launch<2>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   else if (a->tile & ALIGNN_GEMM_BF16) gemm_tiled_launch<1>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   else gemm_tiled_launch<0>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");

@@ -98,7 +98,8 @@ typedef struct AlignnGemmArgs {
 #define ALIGNN_GEMM_STREAM 8192
 /* bf16 only, tiled kernels: operands rounded to bf16 as they are staged and kept as bf16 LDS images
  * (half the LDS bytes, one 16-byte read per fragment, no per-fragment conversion); bitwise equal to
- * the fp32 images.  LDS16 forces it on, NOLDS16 off (A/B, tests). */
+ * the fp32 images.  Taken by default when A is k-contiguous (the products over rows; the weight
+ * gradients' transposing stores cost more than the images save); LDS16 forces it on, NOLDS16 off. */
 #define ALIGNN_GEMM_LDS16 16384
 #define ALIGNN_GEMM_NOLDS16 32768
 
