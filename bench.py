@@ -43,6 +43,7 @@ def survey_bytes_per_graph(s: int, D: int = 256, L: int = 4, N: int = 60, E: int
 FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
 BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 PROBE_STEPS = 3            # untimed replays the dominant-kernel ranking sums over
+SERIAL_STEPS = 3           # serialised replays after the timed region (the dominant kernel's own duration)
 
 
 def parse():
@@ -404,10 +405,12 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
 
     # pick the dominant kernel: the probed family (GEMM shape / attention launch) with the largest
     # total device time summed over PROBE_STEPS untimed steps.  With native plans the probe is a
-    # separate capture whose every probed launch is bracketed by plan timestamps, so the ranking is
-    # taken on the replayed step itself (the concurrency of the timed region and of a rocprofv3 trace
-    # of it), not on an eager step whose overlap differs (round 3: the eager probe flipped between two
-    # GEMM families from run to run).
+    # separate capture whose every probed launch is bracketed by plan timestamps, replayed SERIALISED
+    # (every launch on one stream, alignn_plan_replay_serial): each kernel's own duration, as a PMC
+    # pass runs it.  In-step timestamps of a multi-stream replay include the time a launch queues
+    # behind the other streams' kernels (round 4, C3: the atom-graph backward at 749 us in-step
+    # against 279 us in a rocprofv3 trace and 202 us under the counters), so ranking on them measured
+    # overlap, not kernels.
     dominant, step_work = None, None
     if roofline:
         totals, summ = {}, {}
@@ -419,6 +422,7 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
         else:
             step(0)
             torch.cuda.synchronize()
+        trainer.serial_replay = plan_probe
         for i in range(PROBE_STEPS):
             if not plan_probe:
                 profiling.enable(None)
@@ -429,6 +433,7 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
                 profiling.disable()
             for k, v in summ.items():
                 totals[k] = totals.get(k, 0.0) + v["total_ms"]
+        trainer.serial_replay = False
         if plan_probe:
             trainer.release_capture()
         profiling.clear()
@@ -498,7 +503,21 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
                  "hip events around each launch, timed region" if launch_mode == "eager" else
                  "hip events, 2 eager steps after the timed region")
     value = B * world * steps / dt
-    roof = _roofline(profiling.summary(), dominant, mfma_peak, probe_src) if dominant is not None else None
+    summ = profiling.summary() if dominant is not None else {}
+    in_step = summ.get(dominant)
+    if probe_in_graph and launch_mode == "native_plan":
+        # the kernel's own duration: the same plan replayed serialised (after the timed region); the
+        # in-step figure (last timed replay) stays beside it
+        trainer.serial_replay = True
+        for i in range(SERIAL_STEPS):
+            step(2 * 10**6 + i)
+        torch.cuda.synchronize()
+        trainer.serial_replay = False
+        summ = profiling.summary()
+        probe_src = f"plan timestamps, plan replayed serialised on one stream (last of {SERIAL_STEPS} replays after the timed region)"
+    roof = _roofline(summ, dominant, mfma_peak, probe_src) if dominant is not None else None
+    if roof is not None and in_step is not None:
+        roof["avg_us_in_step"] = round(in_step["avg_ms"] * 1e3, 2)
     step_roof = None if step_work is None else {
         # whole-step view: this formulation's GEMM flops and attention bytes per graph
         # and the fraction of the MFMA / HBM peaks they imply at the measured rate

@@ -89,11 +89,6 @@ _SIGNATURES = {
                                  c_vp, c_i64, c_i32, c_f32, c_u64, c_vp], c_i32),
     "alignn_lg_fwd_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
-    "alignn_lg_fwd_mfma": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
-                            c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
-    "alignn_lg_bwd_dst_mfma": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
-                                c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
-                                c_u64, c_vp], c_i32),
     "alignn_lg_bwd_dst_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                 c_u64, c_vp], c_i32),
@@ -127,6 +122,8 @@ _SIGNATURES = {
     "alignn_dropout_f32": ([c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_u64, c_vp], c_i32),
     "alignn_hetero_nll": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp],
                           c_i32),
+    "alignn_hetero_nll_amp": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_i64,
+                               c_vp], c_i32),
     "alignn_add_noise_f32": ([c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_ensemble_moments": ([c_i32, c_i64, c_i32, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_vp, c_vp], c_i32),
@@ -160,6 +157,7 @@ _SIGNATURES = {
     "alignn_plan_end": ([], c_vp),
     "alignn_plan_abort": ([], c_i32),
     "alignn_plan_replay": ([c_vp, c_vp], c_i32),
+    "alignn_plan_replay_serial": ([c_vp, c_vp], c_i32),
     "alignn_plan_info": ([c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
     "alignn_plan_destroy": ([c_vp], c_i32),
     "alignn_plan_note_timestamp": ([c_vp], c_i32),
@@ -173,7 +171,6 @@ _SIGNATURES = {
     "alignn_stream_destroy": ([c_vp], c_i32),
     "alignn_fill_f32": ([c_vp, c_i64, c_f32, c_vp], c_i32),
     "alignn_add_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
-    "alignn_transpose_f32": ([c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
     "alignn_set_i64": ([c_vp, c_i64, c_vp], c_i32),
     "alignn_copy_f32": ([c_vp, c_vp, c_i64, c_vp], c_i32),
     "alignn_adamw_f32": ([c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_f32,

@@ -15,6 +15,7 @@ Data layout in HBM (D = hidden, H = heads, C = D/H):
 """
 from __future__ import annotations
 
+from contextlib import contextmanager
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -432,15 +433,13 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
                   skip_early: bool = False, bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
-                  want_X16: bool = False, mfma: bool = False):
+                  want_X16: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     bf16_io (bf16 storage, config C3 — the tensor dtypes of the reference's autocast, train.py:632-636):
     on a compacted graph the skip projection's output R and, in the backward, its gradient dR are
     bf16 (Linear outputs and their gradients); X16: a bf16 copy of X (the Linear's input as autocast
     casts it: bitwise the operand the bf16 matrix cores round X to) read by the skip projection and its
     weight gradient; want_X16: the gate kernel also writes a bf16 copy of the new state (c.Xn16).
-    mfma: the bf16-storage attention on the matrix cores (lgmma.hip: D = 256, H = 4), forward and
-    target-side backward.
     skip_early: on a compacted graph with a side stream, the skip projection is queued there before
     the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
@@ -492,9 +491,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
         # one bf16 copy of Q|K|V: K|V gathered by the attention, Q by the source-side backward
         c.QKV16 = ops.cast_bf16(c.QKV)
         c.KV16 = c.QKV16[:, D:3 * D]
-        c.mfma = mfma and D == 256 and H == 4
-        fwd = ops.lg_fwd_mfma if c.mfma else ops.lg_fwd_bf16
-        fwd(g, D, H, c.QKV, c.KV16, c.U, c.wbar, F, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att)
+        ops.lg_fwd_bf16(g, D, H, c.QKV, c.KV16, c.U, c.wbar, F, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop, seed_att)
     else:
         ops.tconv_fwd(g, D, H, c.QKV, c.U, c.wbar, F, feat_row, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
                       seed_att)
@@ -530,8 +527,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
                    wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None,
-                   Wt: Optional[torch.Tensor] = None, bf16_src: bool = True,
-                   dx_stream: Optional[torch.cuda.Stream] = None) -> None:
+                   bf16_src: bool = True) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -546,12 +542,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     products; 1: once dQ is final, before the dX products; 2: those final after the target-side
     kernel (dM, dw̄, the skip projection's) right after it, the rest once dQ is final.
     dX_add: a second part of the incoming gradient (the atom block's edge-feature gradient), added
-    to dX by the gate kernel (ops.gate_ln_bwd).
-    Wt: [D, 4D] transposed copy of cv.Wqkvr — the dX products then read the weights K-contiguous
-    (bitwise the same products, fewer cycles).
-    dx_stream: on a compacted graph, the skip projection's dX product (every row, reads only dR) runs
-    there right after the gate kernel, beside the attention backward; joined before the Q/K/V
-    projections' dX product, which accumulates into the same rows (bitwise the same sums, same order)."""
+    to dX by the gate kernel (ops.gate_ln_bwd)."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -569,11 +560,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
                     gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None,
                     dX_add=dX_add)
-    Wb = cv.Wqkvr if Wt is None else Wt.t()   # B operand [4D, D]
-    skip_early = dx_stream is not None and rows is not None
-    if skip_early:
-        with _side_work(dx_stream, (dR, dX, Wb)):
-            ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                      # residual + skip projection
+    Wb = cv.Wqkvr   # B operand [4D, D]
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
     Vd = torch.empty(na, H, D, device=dev)
     ops.gemm(dout_a.view(na, H, C).transpose(0, 1), c.M.view(H, C, D), Vd.transpose(0, 1))
@@ -584,9 +571,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     if c.KV16 is not None:
         if dF is not None:
             raise ValueError("bf16 edge-feature storage needs the deferred angle-encoder backward (no dF)")
-        bwd = ops.lg_bwd_dst_mfma if getattr(c, "mfma", False) else ops.lg_bwd_dst_bf16
-        bwd(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, c.F, dout_a, c.outp_a, c.mstat, c.den, dQKV[:, :D], Sz, sigz,
-            dz_e, al_e, c.p, c.seed_att)
+        ops.lg_bwd_dst_bf16(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, c.F, dout_a, c.outp_a, c.mstat, c.den, dQKV[:, :D], Sz, sigz,
+                            dz_e, al_e, c.p, c.seed_att)
     else:
         ops.tconv_bwd_dst(g, D, H, c.QKV, c.U, Vd, c.wbar, c.F, c.feat_row, dout_a, c.outp_a, c.mstat, c.den,
                           dQKV[:, :D], Sz, sigz, dz_e, al_e, dF, dF_accumulate, c.p, c.seed_att)
@@ -616,10 +602,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     if rows is None:
         ops.gemm(dQKVR, Wb, dX, beta=1.0)                               # residual + projections
     else:
-        if skip_early:
-            ops.stream_wait(torch.cuda.current_stream(dev), dx_stream)
-        else:
-            ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                      # residual + skip projection
+        ops.gemm(dR, Wb[3 * D:], dX, beta=1.0)                          # residual + skip projection
         ops.gemm(dQKV, Wb[:3 * D], dX, beta=1.0, c_rows=rows)           # + Q/K/V projections (active rows)
     if not early:
         _weight_grads(*wg, part="ab")
@@ -751,25 +734,23 @@ class AlignnEngine:
         # bf16: 0 -> 2 +2.6 % (18,963 -> 19,458 graphs/s); B = 32: 2 within noise of 0 (-0.5 %),
         # 1 -0.6 % (profiles/r03/v21_ab_atom_stream.log)
         self.atom_stream = -1
-        # fp32: the backward's dX products read transposed (K-contiguous) copies of the projection
-        # weights, made beside the encoders at the start of the forward
-        self.wt_copies = False
-        # bf16 storage: the line-graph attention (forward, target-side backward) on the matrix cores
-        # (lgmma.hip; D = 256, H = 4) instead of the VALU kernels (lgconv.hip)
-        self.attn_mfma = False
         # bf16 storage: the atom-graph attention reads the bond state's bf16 copy (the gate kernel's
         # Xn16; autocast casts the bond state to bf16 for edge_proj) as its edge-feature rows
         self.atom_bf16 = True
-        # forward preamble on the aux stream: the line convs' folded projections (weights only), then the
-        # atom encoder and the atom convs' projections — only the first atom block needs them, so they
-        # could overlap the bond encoder and the first line block.  Measured within noise, slightly
-        # negative (B = 32: 9,117 -> 9,034 graphs/s; C3: 19,531 -> 19,436; gpurun_out r4f pre_*): off
-        self.preamble_aux = False
-        # line blocks' skip-projection dX product beside the attention backward: 0 in order, 1 on the
-        # aux stream when the atom blocks do not use it, 2 on the side stream
-        self.skip_dx = 0
         # bf16 storage: the line graph's source-side backward gathers Q and dout as bf16 copies
         self.bf16_src = True
+
+    @contextmanager
+    def using_precision(self, precision: str):
+        """Runs the enclosed calls at ``precision`` ("fp32" / "bf16"), then restores the engine's own
+        (the module API's per-call autocast precision, model._autocast_dtype)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        prev, self.precision = self.precision, precision
+        try:
+            yield
+        finally:
+            self.precision = prev
 
     def _bf16_io(self, D: int) -> bool:
         """bf16 storage of the line blocks' skip projection (R, dR) and of the bond state's bf16 copy
@@ -879,30 +860,14 @@ class AlignnEngine:
             a = torch.empty(T, D, device=dev, dtype=torch.bfloat16 if self._bf16_angle(bc, D) else torch.float32)
         else:
             a = ops.zeros(T, D, device=dev)
-        # transposed copies of the conv blocks' projection weights for the backward's dX products
-        wt = self.wt_copies and self.precision == "fp32" and L > 0
-        ctx.Wt_edge = torch.empty(L, D, 4 * D, device=dev) if wt else None
-        ctx.Wt_node = torch.empty(L, D, 4 * D, device=dev) if wt else None
         if angle_side:
             # beside the node/edge encoders; the main stream waits for it before the first line block
-            with _side_work(side, (a, ctx.Wt_edge, ctx.Wt_node)):
+            with _side_work(side, (a,)):
                 self._angle_hidden(P, bc, D, dev, a)
-                if wt:
-                    ops.transpose_(ctx.Wt_edge, P.edge_Wqkvr)
-                    ops.transpose_(ctx.Wt_node, P.node_Wqkvr)
-        elif wt:
-            ops.transpose_(ctx.Wt_edge, P.edge_Wqkvr)
-            ops.transpose_(ctx.Wt_node, P.node_Wqkvr)
-        main = torch.cuda.current_stream(dev)
-        pre = ops.aux_stream(dev) if (self.preamble_aux and side is not None and E > 0 and L > 0) else None
         line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
-        if pre is not None and line_proj:
-            with _side_work(pre, (x,)):    # forks from the main stream (after the jitter)
-                self._line_proj(P, ctx, L, D)
         # encoders (train.py:547-556)
-        if pre is None:
-            ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
-                                       P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
+        ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
+                                   P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
         if edge_attr.numel() > 0:
             ctx.h1e, e = self._mlp_fwd(edge_attr, P.enc("edge", 0, "weight"), P.enc("edge", 0, "bias"),
                                        P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
@@ -914,20 +879,10 @@ class AlignnEngine:
             self._angle_hidden(P, bc, D, dev, a)
         ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
-        if pre is not None:
-            if line_proj:
-                ops.stream_wait(main, pre)   # the line projections
-            # beside the first line block (already forked when the line projections went first)
-            with _side_work(pre, (x,), wait=not line_proj):
-                ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
-                                           P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
-                ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
-        else:
-            if line_proj:
-                self._line_proj(P, ctx, L, D)
-            if E > 0 and L > 0:
-                ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
-        pre_pending = pre is not None
+        if line_proj:
+            self._line_proj(P, ctx, L, D)
+        if E > 0 and L > 0:
+            ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
         # atom blocks on the aux stream: atom block l waits for line block l, line block l+1 does not
         # wait for it (it reads only the bond states); the readout joins the aux stream
         aux = ops.aux_stream(dev) if (self._atom_mode(T, E) == 2 and side is not None) else None
@@ -940,15 +895,12 @@ class AlignnEngine:
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
                                      skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
-                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16), mfma=self.attn_mfma)
+                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16))
                 e16 = c.Xn16
             else:
                 c = None
             ctx.edge.append(c)
             # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
-            if E > 0 and pre_pending and aux is None:
-                ops.stream_wait(main, pre)   # the atom encoder and projections (inline atom blocks)
-                pre_pending = False
             if E > 0:
                 # bf16 storage: the bond-state rows as autocast hands them to edge_proj (bf16)
                 ef = e16 if (bf16_io and self.atom_bf16 and e16 is not None) else e
@@ -958,8 +910,8 @@ class AlignnEngine:
             else:
                 c = None
             ctx.node.append(c)
-        if aux is not None or pre_pending:
-            ops.stream_wait(torch.cuda.current_stream(dev), aux if aux is not None else pre)
+        if aux is not None:
+            ops.stream_wait(torch.cuda.current_stream(dev), aux)
         ctx.h = h
         # readout (train.py:562-574)
         gdim = global_x.numel() // max(B, 1)
@@ -1059,12 +1011,10 @@ class AlignnEngine:
                 return
             if atom_mode:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, dF_atom[l], 0, dM_all[l], dwbar_all[l],
-                               side=side, gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad,
-                               Wt=None if ctx.Wt_node is None else ctx.Wt_node[l])
+                               side=side, gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad)
             else:
                 block_backward(P.node[l], G.node[l], c, bc.ag, dh, de, True, dM_all[l], dwbar_all[l], side=side,
-                               gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad,
-                               Wt=None if ctx.Wt_node is None else ctx.Wt_node[l])
+                               gate_reduce_side=self.gate_reduce_side, wgrad_early=wgrad)
 
         if aux is not None and L > 0:
             with _side_work(aux, (dh, dF_atom, dM_all, dwbar_all)):
@@ -1090,23 +1040,14 @@ class AlignnEngine:
                 # dF of the line convs is the gradient of the angle hidden layer, summed over layers;
                 # the last (l = 0) applies the ReLU mask in place
                 flags = (1 if da_written else 0) | (2 if (ctx.has_angle and l == 0) else 0)
-                dxs = None
-                if side is not None and self.skip_dx == 1 and aux is None:
-                    dxs = ops.aux_stream(dev)
-                elif side is not None and self.skip_dx == 2:
-                    dxs = side
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add,
-                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src,
-                                   dx_stream=dxs)
+                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add,
-                                   Wt=None if ctx.Wt_edge is None else ctx.Wt_edge[l], bf16_src=self.bf16_src,
-                                   dx_stream=dxs)
+                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

@@ -106,6 +106,15 @@ class _BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, X, Fe, *ps):
         edge_index, heads, p_drop, seed = meta
+        # under the reference's CUDA autocast the block's Linears take bf16 inputs (fp32 accumulation);
+        # LayerNorm runs in fp32, so the block's output stays fp32 as autocast's layer_norm returns it
+        ctx.precision = "bf16" if _autocast_dtype() is not None else "fp32"
+        with torch.autocast("cuda", enabled=False), ops.gemm_precision(ctx.precision):
+            return _BlockFn._fwd(ctx, meta, X, Fe, *ps)
+
+    @staticmethod
+    def _fwd(ctx, meta, X, Fe, *ps):
+        edge_index, heads, p_drop, seed = meta
         X = X.contiguous().float()
         Fe = Fe.contiguous().float()
         n = X.size(0)
@@ -123,10 +132,15 @@ class _BlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dXn):
+        with ops.gemm_precision(ctx.precision):
+            return _BlockFn._bwd(ctx, dXn)
+
+    @staticmethod
+    def _bwd(ctx, dXn):
         cv, c, g = ctx.cv, ctx.c, ctx.g
         D = cv.We.size(0)
         dev = dXn.device
-        dX = dXn.contiguous().clone()
+        dX = dXn.float().contiguous().clone()
         dF = torch.empty(ctx.F_shape, device=dev)
         gv = _Conv()
         gv.Wqkvr = torch.zeros(4 * D, D, device=dev)
@@ -206,19 +220,35 @@ class FlatState:
         self.names = list(self.P.named.keys())
 
 
+def _autocast_dtype() -> Optional[torch.dtype]:
+    """The reference's CUDA step calls ``model(batch)`` inside ``autocast(device_type="cuda",
+    dtype=bfloat16)`` (train.py:632-636, :653-655).  Under an enabled CUDA autocast the engine runs that
+    call at bf16 precision (bf16 matrix-core inputs, fp32 accumulation; the C3 path) and the outputs
+    come back in the autocast dtype, as autocast's Linear heads return them.  None: no autocast."""
+    if not torch.is_autocast_enabled("cuda"):
+        return None
+    dt = torch.get_autocast_dtype("cuda")
+    if dt != torch.bfloat16:
+        # the reference picks float16 only on GPUs without bf16 (train.py:634-635); MI355X has bf16
+        raise NotImplementedError(f"autocast dtype {dt}: the engine implements the reference's bfloat16 autocast")
+    return dt
+
+
 class _ModelFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, holder, x, global_x, *params):
-        model, batch, bc, mode, seed = holder
+        model, batch, bc, mode, seed, precision = holder
         st = model._flat_state
-        out, ectx = model._engine.forward(st.P, batch, bc, model.training, seed, x, global_x, mode)
-        ctx.model, ctx.ectx = model, ectx
+        with torch.autocast("cuda", enabled=False), model._engine.using_precision(precision):
+            out, ectx = model._engine.forward(st.P, batch, bc, model.training, seed, x, global_x, mode)
+        ctx.model, ctx.ectx, ctx.precision = model, ectx, precision
         return out
 
     @staticmethod
     def backward(ctx, dout):
         st = ctx.model._flat_state
-        ctx.model._engine.backward(st.P, st.G, ctx.ectx, dout)
+        with ctx.model._engine.using_precision(ctx.precision):
+            ctx.model._engine.backward(st.P, st.G, ctx.ectx, dout.float())
         return (None, None, None, *[st.G.named[n] for n in st.names])
 
 
@@ -266,8 +296,12 @@ class _EngineModelMixin:
         _require_device(st.flat, type(self).__name__)
         bc = batch_cache(data)
         params = [dict(self.named_parameters())[n] for n in st.names]
-        holder = (self, data, bc, mode, _next_seed())
-        return _ModelFn.apply(holder, data.x.contiguous().float(), data.global_x.contiguous().float(), *params)
+        amp = _autocast_dtype()
+        holder = (self, data, bc, mode, _next_seed(), "bf16" if amp is not None else self._engine.precision)
+        out = _ModelFn.apply(holder, data.x.contiguous().float(), data.global_x.contiguous().float(), *params)
+        # autocast's Linear outputs (heads / feat_proj) are bf16: the fp32-accumulated outputs rounded
+        # once, their gradient handed back to the engine in fp32
+        return out if amp is None else out.to(amp)
 
 
 class AlignnRegressor(_EngineModelMixin, nn.Module):

@@ -290,20 +290,6 @@ def add_(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def transpose_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
-    """dst [nb, C, R] (contiguous) = src [nb, R, C] transposed (src rows unit-stride, any row and
-    batch strides) by a library kernel (alignn_transpose_f32)."""
-    _require(dst, "transpose_ dst")
-    _require(src, "transpose_ src")
-    if src.dim() != 3 or dst.dim() != 3 or src.stride(2) != 1 or not dst.is_contiguous() or \
-            tuple(dst.shape) != (src.size(0), src.size(2), src.size(1)):
-        raise ValueError("transpose_: dst must be a contiguous [nb, C, R] for a row-major src [nb, R, C]")
-    nb, R, C = src.shape
-    check(_lib.lib().alignn_transpose_f32(dst.data_ptr(), src.data_ptr(), nb, R, C, src.stride(1),
-                                          src.stride(0) if nb > 1 else 0, stream_ptr()), "alignn_transpose_f32")
-    return dst
-
-
 def zeros(*shape, device) -> torch.Tensor:
     return zero_(torch.empty(*shape, device=device))
 
@@ -937,22 +923,6 @@ def lg_fwd_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, wbar, F16, aggV, S, s
                          "alignn_lg_fwd_bf16"))
 
 
-def lg_fwd_mfma(g: GraphCSR, D: int, H: int, QKV, KV16, U, wbar, F16, aggV, S, sumA, mstat, den, drop_p: float,
-                seed: int):
-    """alignn_lg_fwd_mfma: lg_fwd_bf16 on the matrix cores (D = 256, H = 4; scores and weighted sums
-    as bf16 MFMA products, softmax and accumulation in fp32)."""
-    _check_lg_bf16(g, D, H, QKV, KV16, F16)
-    if U.numel() < g.n * H * D or S.numel() < g.n * H * D or aggV.numel() < g.n * D:
-        raise ValueError("lg_fwd_mfma: U and S must be [n, H, D], aggV [n, D]")
-    profiling.launch(f"tconv_fwd n{g.n} m{g.m} bf16", 0.0, _lg_bf16_bytes(g.n, g.m, D, H, "fwd"),
-                     lambda: check(_lib.lib().alignn_lg_fwd_mfma(
-                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
-                         QKV.data_ptr(), QKV.stride(0), KV16.data_ptr(), KV16.stride(0), U.data_ptr(), _p(wbar),
-                         F16.data_ptr(), F16.stride(0), aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(),
-                         mstat.data_ptr(), den.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
-                         "alignn_lg_fwd_mfma"))
-
-
 def lg_bwd_dst_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz,
                     sigz, dz_e, alpha_e, drop_p: float, seed: int):
     """alignn_lg_bwd_dst_bf16: the target-side attention backward with bf16 K|V and feature rows."""
@@ -968,24 +938,6 @@ def lg_bwd_dst_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, do
                          den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
                          dz_e.data_ptr(), alpha_e.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
                          "alignn_lg_bwd_dst_bf16"))
-
-
-def lg_bwd_dst_mfma(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz,
-                    sigz, dz_e, alpha_e, drop_p: float, seed: int):
-    """alignn_lg_bwd_dst_mfma: lg_bwd_dst_bf16 on the matrix cores (D = 256, H = 4)."""
-    _check_lg_bf16(g, D, H, QKV, KV16, F16)
-    if (U.numel() < g.n * H * D or Vd.numel() < g.n * H * D or Sz.numel() < g.n * H * D or dq.size(0) < g.n
-            or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H or dout.numel() < g.n * D
-            or outp.numel() < g.n * D):
-        raise ValueError("lg_bwd_dst_mfma: U, Vd, Sz [n, H, D], dq [n, >= D], dz_e/alpha_e [m, H] required")
-    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m} bf16", 0.0, _lg_bf16_bytes(g.n, g.m, D, H, "bwd_dst"),
-                     lambda: check(_lib.lib().alignn_lg_bwd_dst_mfma(
-                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
-                         QKV.data_ptr(), QKV.stride(0), KV16.data_ptr(), KV16.stride(0), U.data_ptr(), Vd.data_ptr(),
-                         _p(wbar), F16.data_ptr(), F16.stride(0), dout.data_ptr(), outp.data_ptr(), mstat.data_ptr(),
-                         den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
-                         dz_e.data_ptr(), alpha_e.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
-                         "alignn_lg_bwd_dst_mfma"))
 
 
 def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -1180,16 +1132,18 @@ def dropout(x, y, relu_ref=None, drop_p=0.0, seed=0):
     return y
 
 
-def hetero_nll(heads, y, log_means, log_stds, floor, l2, loss, dheads, weights: Optional[torch.Tensor] = None):
-    """weights: per-graph KNN sample weights [B] (train.py:660-674) or None."""
+def hetero_nll(heads, y, log_means, log_stds, floor, l2, loss, dheads, weights: Optional[torch.Tensor] = None,
+               amp: bool = False):
+    """weights: per-graph KNN sample weights [B] (train.py:660-674) or None.  amp: the loss as the
+    reference's CUDA step computes it under autocast(bfloat16) on bf16 heads (alignn_hetero_nll_amp)."""
     B = heads.size(0)
     T = heads.size(1) // 2
     if weights is not None and (weights.numel() != B or weights.dtype != torch.float32 or not weights.is_contiguous()):
         raise ValueError("hetero_nll: weights must be a contiguous float32 [B] tensor")
-    check(_lib.lib().alignn_hetero_nll(B, T, heads.data_ptr(), heads.stride(0), y.data_ptr(), _p(weights),
-                                       log_means.data_ptr(), log_stds.data_ptr(), float(floor), float(l2),
-                                       loss.data_ptr(), dheads.data_ptr(), dheads.stride(0), stream_ptr()),
-          "alignn_hetero_nll")
+    fn = _lib.lib().alignn_hetero_nll_amp if amp else _lib.lib().alignn_hetero_nll
+    check(fn(B, T, heads.data_ptr(), heads.stride(0), y.data_ptr(), _p(weights), log_means.data_ptr(),
+             log_stds.data_ptr(), float(floor), float(l2), loss.data_ptr(), dheads.data_ptr(), dheads.stride(0),
+             stream_ptr()), "alignn_hetero_nll_amp" if amp else "alignn_hetero_nll")
 
 
 def add_noise(x: torch.Tensor, std: float, seed: int):

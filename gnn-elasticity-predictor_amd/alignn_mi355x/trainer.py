@@ -33,7 +33,7 @@ class FusedTrainer:
                  target_log_means: Sequence[float] = TARGET_LOG_MEANS,
                  target_log_stds: Sequence[float] = TARGET_LOG_STDS, fused_adamw: bool = True,
                  optimizer: str = "hip", precision: Optional[str] = None, grad_scaler: Optional[bool] = None,
-                 init_scale: float = 65536.0, growth_interval: int = 2000):
+                 init_scale: float = 65536.0, growth_interval: int = 2000, amp_loss: Optional[bool] = None):
         self.model = model
         if precision is not None:
             model.set_precision(precision)
@@ -63,13 +63,18 @@ class FusedTrainer:
         # GradScaler (train.py:690-695, built at :1475-1476 whenever the reference runs on the GPU,
         # i.e. with autocast: our bf16 precision): a step with non-finite (scaled) gradients is skipped
         # and the scale halves; device state [scale, growth_tracker, found_inf, skipped steps]
+        # (default on for bf16 with the HIP optimizer; torch's optimizer runs without one)
         if grad_scaler is None:
-            grad_scaler = model._engine.precision == "bf16"
+            grad_scaler = model._engine.precision == "bf16" and optimizer == "hip"
         if grad_scaler and optimizer != "hip":
             raise ValueError("grad_scaler needs optimizer='hip'")
         self.growth_interval = int(growth_interval)
         self.scaler = (torch.tensor([float(init_scale), 0.0, 0.0, 0.0], device=st.flat.device) if grad_scaler
                        else None)
+        # bf16: the loss on the heads as autocast returns them (bf16) with autocast's dtypes and
+        # autograd's gradient roundings (train.py:653-681; ops.hetero_nll amp) — the step the module
+        # API runs under the reference's own autocast + GradScaler loop, bit for bit
+        self.amp_loss = (model._engine.precision == "bf16") if amp_loss is None else bool(amp_loss)
         self.max_norm = max_norm
         self.l2 = log_sigma_l2
         self.jitter = feature_jitter_std
@@ -97,6 +102,9 @@ class FusedTrainer:
         self.rebind_copy_all = False
         self.rebinds = 0
         self.rebind_misses = 0
+        # roofline probes (bench.py): replay the plans serialised on one stream (each kernel alone on
+        # the device; alignn_plan_replay_serial) instead of on their recorded streams
+        self.serial_replay = False
         self.replays = 0
         self.lr_dev = None
         self._wbuf = None      # a weighted capture's per-graph weights (device [real graphs])
@@ -159,7 +167,7 @@ class FusedTrainer:
         nr = out.size(0) if bc.real_graphs is None else bc.real_graphs
         y = batch.y.contiguous().float()
         ops.hetero_nll(out[:nr], y[:nr * (out.size(1) // 2)], self.log_means, self.log_stds, self.floor, self.l2,
-                       self.loss, dout[:nr], weights=sample_weights)
+                       self.loss, dout[:nr], weights=sample_weights, amp=self.amp_loss)
         if nr < out.size(0):
             ops.zero_(dout[nr:])
         return model._engine.backward_layers(st.P, st.G, ctx, dout)
@@ -407,7 +415,9 @@ class FusedTrainer:
         n = len(plans) if plans else len(graphs)
 
         def run(i):
-            if plans:
+            if plans and self.serial_replay:
+                check(_lib.lib().alignn_plan_replay_serial(plans[i], ops.stream_ptr()), "alignn_plan_replay_serial")
+            elif plans:
                 check(_lib.lib().alignn_plan_replay(plans[i], ops.stream_ptr()), "alignn_plan_replay")
             else:
                 graphs[i].replay()

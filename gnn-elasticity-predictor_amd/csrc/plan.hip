@@ -125,24 +125,6 @@ __global__ __launch_bounds__(256) void add_f32_kernel(float* __restrict__ x, con
     x[i] += y[i];
 }
 
-// dst[b][c][r] = src[b][r][c] (fp32; src rows ld_src apart, batches sb_src apart; dst contiguous
-// [nb, cols, rows]): 32 x 32 tiles through LDS (padded rows), coalesced on both sides
-__global__ __launch_bounds__(256) void transpose_f32_kernel(float* __restrict__ dst, const float* __restrict__ src,
-                                                            int64_t rows, int64_t cols, int64_t ld_src,
-                                                            int64_t sb_src) {
-  __shared__ float tile[32][33];
-  const int64_t b = blockIdx.z;
-  const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-  const float* s = src + b * sb_src;
-  float* d = dst + b * rows * cols;
-  for (int i = ty; i < 32; i += 8)
-    if (r0 + i < rows && c0 + tx < cols) tile[i][tx] = s[(r0 + i) * ld_src + c0 + tx];
-  __syncthreads();
-  for (int i = ty; i < 32; i += 8)
-    if (c0 + i < cols && r0 + tx < rows) d[(c0 + i) * rows + r0 + tx] = tile[tx][i];
-}
-
 static unsigned blocks_for(int64_t n) { return (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 255) / 256), 8192); }
 
 }  // namespace alignn
@@ -247,6 +229,34 @@ extern "C" int alignn_plan_replay(void* plan, void* stream) {
       hipError_t r = hipEventRecord(p->events[e.event], p->streams[e.src]);
       if (r == hipSuccess) r = hipStreamWaitEvent(p->streams[e.slot], p->events[e.event], 0);
       if (r != hipSuccess) return hip_status(r, "plan_replay: stream edge");
+    }
+  }
+  return ALIGNN_OK;
+}
+
+// Serialised replay (roofline probes): every launch and timestamp in recorded issue order on
+// `stream` alone, the cross-stream edges dropped — issue order already satisfies them (a wait is
+// noted after the work it waits for was issued).  The timestamps then bracket each kernel alone on
+// the device, as a counter-collection pass runs it, instead of including the time it queued behind
+// the other streams' kernels.
+extern "C" int alignn_plan_replay_serial(void* plan, void* stream) {
+  Plan* p = reinterpret_cast<Plan*>(plan);
+  if (!p) return ALIGNN_E_BAD_SHAPE;
+  if (g_recording) {
+    set_error("plan_replay_serial: not allowed while a plan is being recorded");
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  std::vector<void*> ptrs;
+  for (const PlanEntry& e : p->entries) {
+    if (e.func) {
+      ptrs.resize(e.nargs + 1);
+      for (size_t i = 0; i < e.nargs; ++i) ptrs[i] = p->args.data() + p->arg_off[e.arg0 + i];
+      hipError_t r = hipLaunchKernel(e.func, e.grid, e.block, ptrs.data(), e.shmem, s);
+      if (r != hipSuccess) return hip_status(r, "plan_replay_serial: hipLaunchKernel");
+    } else if (e.event < 0) {
+      hipError_t r = hipEventRecord(p->stamps[-1 - e.event], s);
+      if (r != hipSuccess) return hip_status(r, "plan_replay_serial: timestamp");
     }
   }
   return ALIGNN_OK;
@@ -607,17 +617,6 @@ extern "C" int alignn_add_f32(float* x, const float* y, int64_t n, void* stream)
   if (n == 0) return ALIGNN_OK;
   launch(add_f32_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x, y, n);
   ALIGNN_LAUNCH_CHECK("add_f32_kernel");
-  return ALIGNN_OK;
-}
-
-extern "C" int alignn_transpose_f32(float* dst, const float* src, int64_t nb, int64_t rows, int64_t cols,
-                                    int64_t ld_src, int64_t sb_src, void* stream) {
-  if (nb < 0 || rows < 0 || cols < 0 || ld_src < cols || nb > 65535) return ALIGNN_E_BAD_SHAPE;
-  if (nb == 0 || rows == 0 || cols == 0) return ALIGNN_OK;
-  const dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32), (unsigned)nb);
-  launch(transpose_f32_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dst, src, rows, cols, ld_src,
-         sb_src);
-  ALIGNN_LAUNCH_CHECK("transpose_f32_kernel");
   return ALIGNN_OK;
 }
 

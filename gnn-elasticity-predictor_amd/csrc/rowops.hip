@@ -352,6 +352,66 @@ __global__ __launch_bounds__(256) void hetero_nll_kernel(int64_t B, int T, const
   if (threadIdx.x == 0) *loss = red[0] * inv;
 }
 
+// The same loss as the reference's CUDA step computes it under autocast(bfloat16) (train.py:653-681,
+// use_amp): the heads arrive as autocast's bf16 Linear outputs and every op keeps autocast's dtype —
+// clamp, the target cast, ``mean - target`` and ``0.5 * logvar`` in bf16 (fp32 arithmetic rounded to
+// bf16), exp / pow / div / the means in fp32 — and the backward rounds each gradient to the dtype of
+// the tensor it belongs to.  The bf16 logvar receives three gradients (from ``0.5 * logvar``, from the
+// promoted add, from exp), accumulated by autograd in bf16 in that order.  Unscaled (GradScaler's
+// power-of-two scale commutes with every rounding here).  Gradients bitwise those of torch's autograd
+// on the same bf16 heads (tests/test_gpu_x_round5.py).
+__device__ __forceinline__ float bf16r(float x) { return (float)(__bf16)x; }
+
+__global__ __launch_bounds__(256) void hetero_nll_amp_kernel(int64_t B, int T, const float* __restrict__ heads,
+                                                             int64_t ldh, const float* __restrict__ y,
+                                                             const float* __restrict__ w, const float* __restrict__ lm,
+                                                             const float* __restrict__ ls, float floor, float l2,
+                                                             float* __restrict__ loss, float* __restrict__ dh,
+                                                             int64_t lddh) {
+  __shared__ float red[2][256];
+  const int64_t total = B * T;
+  const float floor16 = bf16r(floor);                      // clamp's Scalar min as a bf16 value
+  const float dnll = (1.0f / (float)B) / (float)T;         // mean().backward, then mean(dim=1).backward
+  const float dP = (1.0f * l2) / (float)total;             // (l2 * mean(log_sigma^2)).backward
+  float acc = 0.f, accp = 0.f;
+  for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
+    const int64_t b = i / T;
+    const int t = (int)(i % T);
+    const float mu = bf16r(heads[b * ldh + t]);
+    const float lvr = bf16r(heads[b * ldh + T + t]);
+    const float lc = (lvr != lvr) ? lvr : fmaxf(lvr, floor16);
+    const float yt = bf16r((logf(y[b * T + t]) - lm[t]) / ls[t]);
+    const float d = bf16r(mu - yt);
+    const float p = d * d;
+    const float var = expf(lc);
+    const float q = p / var;
+    float nll = 0.5f * (lc + q);
+    const float ls16 = bf16r(0.5f * lc);
+    if (w) nll = nll * w[b];
+    acc += nll;
+    accp += ls16 * ls16;
+    const float ds = (w ? dnll * w[b] : dnll) * 0.5f;
+    const float g1 = bf16r(ds);
+    const float dp = ds / var;
+    const float dvar = -ds * ((p / var) / var);
+    const float g2 = bf16r(dvar * var);
+    const float g3 = bf16r(bf16r(dP * (2.0f * ls16)) * 0.5f);
+    dh[b * lddh + t] = bf16r(dp * (2.0f * d));
+    dh[b * lddh + T + t] = lvr >= floor16 ? bf16r(bf16r(g3 + g1) + g2) : 0.f;
+  }
+  red[0][threadIdx.x] = acc;
+  red[1][threadIdx.x] = accp;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0][0] / (float)total + l2 * (red[1][0] / (float)total);
+}
+
 __global__ void add_noise_kernel(int64_t n, float* __restrict__ x, float stdv, uint64_t seed, const uint64_t* sptr) {
   seed = mix_seed(seed, sptr);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -576,6 +636,17 @@ extern "C" int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64
   launch(hetero_nll_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, weights, log_means, log_stds,
                      floor, l2, loss, dheads, lddh);
   ALIGNN_LAUNCH_CHECK("hetero_nll_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_hetero_nll_amp(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
+                                     const float* weights, const float* log_means, const float* log_stds,
+                                     float floor, float l2, float* loss, float* dheads, int64_t lddh, void* stream) {
+  if (B <= 0 || T <= 0) return ALIGNN_E_BAD_SHAPE;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  launch(hetero_nll_amp_kernel, dim3(1), dim3(256), 0, s, B, T, heads, ldh, y, weights, log_means, log_stds,
+         floor, l2, loss, dheads, lddh);
+  ALIGNN_LAUNCH_CHECK("hetero_nll_amp_kernel");
   return ALIGNN_OK;
 }
 

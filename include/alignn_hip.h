@@ -327,24 +327,6 @@ int alignn_lg_bwd_dst_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int
                            float* dz_e, float* alpha_e, float drop_p, uint64_t seed, void* stream);
 /* dst (bf16, RNE) = src (fp32) for a [rows, cols] block; cols and both leading dimensions multiples
  * of 4, src rows 16-byte aligned. */
-/* The matrix-core form of alignn_lg_fwd_bf16 (lgmma.hip; D = 256, H = 4, same arguments and outputs;
- * rows 16-byte aligned): per 16-edge tile the scores [F | K] . [U^T ; blockdiag(q)] as bf16 16x16x32
- * MFMA products and the weighted sums of F and V as bf16 4x4x4 products (q, u and alpha rounded to
- * bf16 as the reference's autocast holds them, train.py:632-636; softmax and sums in fp32). */
-int alignn_lg_fwd_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
-                       const AlignnSchedule* sched, const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv,
-                       const float* U, const float* wbar, const uint16_t* F16, int64_t ldf, float* aggV, float* S,
-                       float* sumA, float* mstat, float* den, float drop_p, uint64_t seed, void* stream);
-/* The matrix-core form of alignn_lg_bwd_dst_bf16 (same arguments and outputs): the scores and the
- * dalpha numerators [F | V] . [Vd^T ; blockdiag(dout)] as bf16 16x16x32 MFMA products, dq and Sz as
- * bf16 4x4x4 products of dz (rounded to bf16) with the tile's K and F rows; per-edge dz / alpha and
- * sigz in fp32. */
-int alignn_lg_bwd_dst_mfma(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
-                           const AlignnSchedule* sched, const float* Q, int64_t ldq, const uint16_t* KV16,
-                           int64_t ldkv, const float* U, const float* Vd, const float* wbar, const uint16_t* F16,
-                           int64_t ldf, const float* dout, const float* outp, const float* mstat, const float* den,
-                           float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e, float* alpha_e, float drop_p,
-                           uint64_t seed, void* stream);
 int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, uint16_t* dst, int64_t ldd,
                          void* stream);
 
@@ -473,6 +455,15 @@ int alignn_dropout_f32(int64_t rows, int64_t cols, const float* x, int64_t ldx, 
 int alignn_hetero_nll(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
                       const float* weights, const float* log_means, const float* log_stds, float floor, float l2,
                       float* loss, float* dheads, int64_t lddh, void* stream);
+
+/* The same loss as the reference's CUDA step computes it under autocast(bfloat16) (train.py:632-636,
+ * :653-681 with use_amp): mean/logvar rounded to bf16 as autocast's Linear returns them, clamp, the
+ * target cast, mean - target and 0.5*logvar in bf16, exp/pow/div/means in fp32; dheads = autograd's
+ * gradient of those ops (each rounded to its tensor's dtype; logvar's three bf16 gradients summed in
+ * autograd's order), unscaled.  Same arguments as alignn_hetero_nll. */
+int alignn_hetero_nll_amp(int64_t B, int32_t T, const float* heads, int64_t ldh, const float* y,
+                          const float* weights, const float* log_means, const float* log_stds, float floor,
+                          float l2, float* loss, float* dheads, int64_t lddh, void* stream);
 
 /* Feature jitter (train.py:641-646): x += std * N(0,1) from a counter-based generator. */
 int alignn_add_noise_f32(int64_t n, float* x, float std, uint64_t seed, void* stream);
@@ -635,6 +626,10 @@ int alignn_plan_note_wait(void* dst_stream, void* src_stream);
 void* alignn_plan_end(void);
 int alignn_plan_abort(void);
 int alignn_plan_replay(void* plan, void* stream);
+/* alignn_plan_replay_serial(plan, stream): the same launches and timestamps in recorded issue order,
+ * all on `stream`, cross-stream edges dropped (issue order satisfies them): each kernel alone on the
+ * device, so the plan timestamps give its isolated duration (the bench's roofline probes). */
+int alignn_plan_replay_serial(void* plan, void* stream);
 int alignn_plan_info(const void* plan, int64_t* launches, int64_t* waits, int64_t* streams, int64_t* arg_bytes);
 int alignn_plan_destroy(void* plan);
 int alignn_plan_note_timestamp(void* stream);
@@ -671,11 +666,6 @@ int alignn_stream_destroy(void* stream);
 int alignn_fill_f32(float* x, int64_t n, float value, void* stream);
 int alignn_copy_f32(float* dst, const float* src, int64_t n, void* stream);
 int alignn_add_f32(float* x, const float* y, int64_t n, void* stream);
-/* alignn_transpose_f32: dst[b][c][r] = src[b][r][c] for b < nb (src rows ld_src apart, batches sb_src
- * apart; dst contiguous [nb, cols, rows]) — the transposed copies of the conv blocks' projection
- * weights the backward's dX products read K-contiguous (bitwise the same products). */
-int alignn_transpose_f32(float* dst, const float* src, int64_t nb, int64_t rows, int64_t cols, int64_t ld_src,
-                         int64_t sb_src, void* stream);
 int alignn_set_i64(int64_t* x, int64_t value, void* stream);
 
 #ifdef __cplusplus

@@ -73,15 +73,12 @@ def test_forward_side_stream_is_bitwise_neutral():
 
 
 @pytest.mark.parametrize("flag,value", [("enc_bwd_aux", 1), ("gate_reduce_side", True), ("skip_early", True),
-                                        ("angle_side", True), ("wgrad_early", 1), ("wgrad_early", 2),
-                                        ("wt_copies", True), ("preamble_aux", True), ("skip_dx", 1),
-                                        ("skip_dx", 2)])
+                                        ("angle_side", True), ("wgrad_early", 1), ("wgrad_early", 2)])
 def test_backward_third_stream_is_bitwise_neutral(flag, value):
     """Branches off the main stream (the deferred angle-encoder backward on the third stream, the
     gate/LayerNorm parameter reduction on the side stream, the skip projection queued before Q/K/V,
-    the angle encoder beside the node/edge encoders, the weight gradients queued before dX, the atom
-    encoder and the conv projections on the aux stream, the line blocks' skip-projection dX product
-    beside the attention backward) change no bits."""
+    the angle encoder beside the node/edge encoders, the weight gradients queued before dX) change no
+    bits."""
     _, tr1, b1 = _setup()
     _, tr2, b2 = _setup()
     setattr(tr1.model._engine, flag, type(value)(0))

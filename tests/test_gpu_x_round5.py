@@ -1,0 +1,186 @@
+"""Round-5 GPU checks: the drop-in module under the reference's own CUDA autocast (train.py:632-636,
+:653-681, :690-695).
+
+* ``alignn_hetero_nll_amp`` against torch's autograd of the reference's loss lines under
+  ``torch.autocast("cuda", bfloat16)`` on the same bf16 heads: gradients bit for bit, loss to fp32
+  summation order.
+* A restatement of ``train_epoch_hetero``'s amp branch (autocast + ``torch.amp.GradScaler`` +
+  ``clip_grad_norm_`` + AdamW) through the module API against ``FusedTrainer(precision="bf16")``:
+  heads bitwise, every parameter gradient bitwise, the post-step parameters to the optimizer
+  tolerance of test_hip_clip_adamw_matches_torch (torch's AdamW vs the library's), and a skipped
+  (non-finite) step skipped by both with the same scale back-off.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+FLOOR = -2.9          # MIN_LOGVAR_FLOOR (train.py)
+LOG_MEANS = (4.3228, 3.5567)   # alignn_mi355x.synthetic.TARGET_LOG_* (the trainer's LogTransformer state)
+LOG_STDS = (0.9051, 0.9405)
+
+
+def _ref_loss(mean, logvar, y, lm, ls, l2, w=None):
+    """train.py:648-681 (with transformer.transform_tensor, train.py:268-279), as written; the caller
+    holds the autocast context."""
+    target_trans = (torch.log(y) - lm) / ls
+    logvar = torch.clamp(logvar, min=FLOOR)
+    logvar_loss = logvar
+    var = torch.exp(logvar_loss)
+    diff = mean - target_trans.to(mean.dtype)
+    nll = 0.5 * (logvar_loss + diff.pow(2) / var)
+    if w is not None:
+        nll = nll * w.view(-1, 1)
+    sample_loss = nll.mean(dim=1)
+    loss = sample_loss.mean()
+    if l2 > 0.0:
+        log_sigma = 0.5 * logvar_loss
+        loss = loss + float(l2) * log_sigma.pow(2).mean()
+    return loss
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("B", [32, 7, 256])
+def test_amp_loss_kernel_matches_autocast_autograd(weighted, B):
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(B + weighted)
+    T = 2
+    heads = (torch.randn(B, 2 * T, generator=g) * 2.0).to(DEV)
+    heads[0, T] = -7.0                         # below the floor: clamp's zero gradient
+    heads[1, T + 1] = -2.9                     # rounds to the bf16 floor itself (subgradient 1)
+    y = (torch.rand(B, T, generator=g) * 299 + 1).to(DEV)
+    w = (torch.rand(B, generator=g) + 0.5).to(DEV) if weighted else None
+    lm = torch.tensor(LOG_MEANS, device=DEV)
+    ls = torch.tensor(LOG_STDS, device=DEV)
+    S = 65536.0
+    h16 = heads.to(torch.bfloat16).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = _ref_loss(h16[:, :T], h16[:, T:], y, lm, ls, 0.1, w)
+    (loss * torch.tensor(S, device=DEV)).backward()
+    ref = h16.grad.float() / S
+    out_loss = torch.zeros(1, device=DEV)
+    dh = torch.empty_like(heads)
+    ops.hetero_nll(heads, y, lm, ls, FLOOR, 0.1, out_loss, dh, weights=w, amp=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dh, ref), float((dh - ref).abs().max())
+    assert abs(float(out_loss) - float(loss)) <= 2e-6 * abs(float(loss))
+
+
+def _model(seed, dropout=0.15):
+    import alignn_mi355x as A
+    torch.manual_seed(seed)
+    return A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, dropout), 2).to(DEV)
+
+
+def _reference_amp_step(model, opt, scaler, batch, draw_seed):
+    """One iteration of train_epoch_hetero's loop body with use_amp (train.py:647-699), jitter off."""
+    opt.zero_grad(set_to_none=True)
+    target = batch.y.view(batch.num_graphs, -1)
+    lm = torch.tensor(LOG_MEANS, device=DEV)
+    ls = torch.tensor(LOG_STDS, device=DEV)
+    torch.manual_seed(draw_seed)                 # the module draws its dropout seed from torch's generator
+    with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        mean, logvar = model(batch)
+        heads = torch.cat([mean, logvar], 1).detach().clone()
+        loss = _ref_loss(mean, logvar, target, lm, ls, 0.1)
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+    norm = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0)
+    scaler.step(opt)
+    scaler.update()
+    return loss.detach(), heads, grads, float(norm)
+
+
+def _torch_adamw(model):
+    """The reference's two parameter groups (train.py:1516-1542) on torch's single-tensor AdamW (the
+    arithmetic the library's optimizer restates)."""
+    base = list(model.base.parameters()) + list(model.mean_heads.parameters())
+    sigma = list(model.logvar_heads.parameters())
+    return torch.optim.AdamW([{"params": base, "lr": 3e-4}, {"params": sigma, "lr": 3e-4}], lr=3e-4,
+                             weight_decay=1e-4, foreach=False, fused=False)
+
+
+def test_module_api_under_autocast_matches_fused_bf16_step():
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_batch
+    batch = mp_like_batch(4).to(DEV)
+    mod = _model(0).train()
+    fus = _model(0).train()
+    assert mod._engine.precision == "fp32"                  # autocast, not set_precision, picks bf16
+    tr = A.FusedTrainer(fus, precision="bf16", feature_jitter_std=0.0, lr=3e-4, sigma_lr=3e-4)
+    assert tr.amp_loss and tr.scaler is not None
+    opt = _torch_adamw(mod)
+    scaler = torch.amp.GradScaler("cuda")
+    names = tr.st.names
+    for it, draw in enumerate((11, 12, 13)):
+        p_before = {n: p.detach().clone() for n, p in mod.named_parameters()}
+        loss_m, heads_m, grads_m, norm_m = _reference_amp_step(mod, opt, scaler, batch, draw)
+        assert heads_m.dtype == torch.bfloat16
+        torch.manual_seed(draw)
+        seed = int(torch.randint(0, 2**62, (1,)).item())   # the same draw model._run makes
+        tr.forward_backward(batch, seed)
+        torch.cuda.synchronize()
+        assert abs(float(tr.loss) - float(loss_m)) <= 2e-6 * abs(float(loss_m)), it
+        assert set(grads_m) == set(names)          # base.output_heads: unused by the hetero forward
+        for n in names:
+            assert torch.equal(tr.st.G.named[n], grads_m[n]), (it, n)
+        tr._clip_and_update()
+        torch.cuda.synchronize()
+        assert float(tr.gnorm) == pytest.approx(norm_m, rel=1e-5)
+        assert tr.scaler.tolist()[0] == scaler.get_scale() == 65536.0
+        # the optimizers: torch's single-tensor AdamW vs the library's restatement (2 ulp of |p| on top
+        # of 1e-4 of the update, as test_hip_clip_adamw_matches_torch)
+        for n in names:
+            pt, pf = dict(mod.named_parameters())[n].detach(), tr.st.P.named[n]
+            tol = 1e-4 * (pt - p_before[n]).abs().max() + 2 * torch.finfo(torch.float32).eps * pt.abs()
+            assert bool(((pt - pf).abs() <= tol).all()), (it, n, float((pt - pf).abs().max()))
+        # re-synchronise the parameters so the next step's forward starts from identical weights
+        with torch.no_grad():
+            for n in names:
+                dict(mod.named_parameters())[n].copy_(tr.st.P.named[n])
+
+
+def test_module_api_under_autocast_skips_a_nonfinite_step_like_the_fused_step():
+    """An infinite target makes the loss and every gradient non-finite: GradScaler skips the update and
+    halves the scale in both paths."""
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_batch
+    batch = mp_like_batch(4).to(DEV)
+    batch.y = batch.y.clone()
+    batch.y[1] = float("inf")
+    mod = _model(1).train()
+    fus = _model(1).train()
+    tr = A.FusedTrainer(fus, precision="bf16", feature_jitter_std=0.0)
+    opt = _torch_adamw(mod)
+    scaler = torch.amp.GradScaler("cuda")
+    p0 = {n: p.detach().clone() for n, p in mod.named_parameters()}
+    f0 = tr.st.flat.clone()
+    _reference_amp_step(mod, opt, scaler, batch, 5)
+    torch.manual_seed(5)
+    tr.step(batch, seed=int(torch.randint(0, 2**62, (1,)).item()))
+    torch.cuda.synchronize()
+    assert all(torch.equal(p.detach(), p0[n]) for n, p in mod.named_parameters())
+    assert torch.equal(tr.st.flat, f0)
+    assert scaler.get_scale() == 32768.0 and tr.scaler.tolist()[0] == 32768.0 and tr.scaler.tolist()[3] == 1.0
+
+
+def test_module_api_autocast_outputs_and_embed_dtype():
+    """Under autocast the heads and the embedding come back in bf16 (autocast's Linear outputs), the
+    engine's own precision is untouched afterwards, and outside autocast everything is fp32."""
+    from alignn_mi355x.synthetic import mp_like_batch
+    batch = mp_like_batch(2).to(DEV)
+    m = _model(2, dropout=0.0).eval()
+    with torch.no_grad():
+        m32, l32 = m(batch)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            m16, l16 = m(batch)
+            e16 = m.embed(batch)
+        e32 = m.embed(batch)
+    assert m16.dtype == l16.dtype == e16.dtype == torch.bfloat16
+    assert m32.dtype == l32.dtype == e32.dtype == torch.float32
+    assert m._engine.precision == "fp32"
+    assert float((m16.float() - m32).abs().max()) <= 3e-2 * float(m32.abs().max())
+    with pytest.raises(NotImplementedError):
+        with torch.autocast("cuda", dtype=torch.float16):
+            m(batch)

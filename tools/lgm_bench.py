@@ -79,32 +79,12 @@ def main():
         outs[mode] = dict(outp=outp.clone(), S=S.clone(), sumA=sumA.clone(), mstat=mstat.clone(), den=den.clone(),
                           dq=dq.clone(), Sz=Sz.clone(), sigz=sigz.clone(), dz=dz.clone(), al=al.clone())
         times[mode] = {"fwd_us": round(timeit(fwd, a.reps), 1), "bwd_dst_us": round(timeit(bwd, a.reps), 1)}
-    if H == 4:   # the matrix-core forward (lgmma.hip)
-        outp, S = torch.empty(n, D, device="cuda"), torch.empty(n, H, D, device="cuda")
-        sumA, mstat, den = (torch.empty(n, H, device="cuda") for _ in range(3))
-        fwd = lambda: ops.lg_fwd_mfma(g, D, H, QKV, KV16, U, wbar, F16, outp, S, sumA, mstat, den, a.drop, 9)  # noqa: E731
-        fwd()
-        torch.cuda.synchronize()
-        dq, Sz = torch.empty(n, D, device="cuda"), torch.empty(n, H, D, device="cuda")
-        sigz = torch.empty(n, H, device="cuda")
-        dz, al = torch.empty(m, H, device="cuda"), torch.empty(m, H, device="cuda")
-        bwd = lambda: ops.lg_bwd_dst_mfma(g, D, H, QKV, KV16, U, Vd, wbar, F16, dout, outp, mstat, den, dq, Sz,  # noqa: E731
-                                          sigz, dz, al, a.drop, 9)
-        bwd()
-        torch.cuda.synchronize()
-        outs["mfma"] = dict(outp=outp.clone(), S=S.clone(), sumA=sumA.clone(), mstat=mstat.clone(), den=den.clone(),
-                            dq=dq.clone(), Sz=Sz.clone(), sigz=sigz.clone(), dz=dz.clone(), al=al.clone())
-        times["mfma"] = {"fwd_us": round(timeit(fwd, a.reps), 1), "bwd_dst_us": round(timeit(bwd, a.reps), 1)}
     fb = ops._lg_bf16_bytes(n, m, D, H, "fwd")
     bb = ops._lg_bf16_bytes(n, m, D, H, "bwd_dst")
     res = {"n": n, "m": m, "H": H, "lib": os.environ.get("ALIGNN_HIP_LIB", "in-tree"), "times": times,
            "bf16_fwd_TBps": round(fb / times["bf16"]["fwd_us"] * 1e-6, 3),
            "bf16_bwd_TBps": round(bb / times["bf16"]["bwd_dst_us"] * 1e-6, 3),
            "rel_diff_vs_fp32": {k: rel(outs["bf16"][k], outs["fp32"][k]) for k in outs["fp32"]}}
-    if "mfma" in outs:
-        res["mfma_fwd_TBps"] = round(fb / times["mfma"]["fwd_us"] * 1e-6, 3)
-        res["mfma_bwd_TBps"] = round(bb / times["mfma"]["bwd_dst_us"] * 1e-6, 3)
-        res["mfma_rel_diff_vs_bf16"] = {k: rel(outs["mfma"][k], outs["bf16"][k]) for k in outs["mfma"]}
     print(json.dumps(res))
 
 
