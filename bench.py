@@ -43,6 +43,7 @@ def survey_bytes_per_graph(s: int, D: int = 256, L: int = 4, N: int = 60, E: int
 FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
 BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 PROBE_STEPS = 3            # untimed replays the dominant-kernel ranking sums over
+C1_WARM, C1_REPS = 10, 50   # config C1 forward timing (median of 50 after 10)
 SERIAL_STEPS = 3           # serialised replays after the timed region (the dominant kernel's own duration)
 
 
@@ -185,6 +186,76 @@ def cpu_baseline(args, B):
             "sample": f"median of {args.cpu_steps} steps x {B} graphs (fp32 fwd+NLL+bwd+clip+AdamW, dropout 0) after "
                       f"1 warm-up, torch.set_num_threads({threads}) (the job's CPU share; os.cpu_count() = "
                       f"{os.cpu_count()}); {cpu_model}"}
+
+
+def c1_forward(args, dev):
+    """Config C1: one graph, forward only, fp32 — (1a) the reference's smoke shape
+    (tests/smoke.py:106-145: node/edge/angle dims 6/8/7, hidden 32, 1 layer, 1 head) and (1b) one
+    MP-like graph at L = 1 (D = 256, H = 4).  The reference's CPU path (the oracle, all of the job's
+    host threads) and the engine on the GPU (model(batch) in eval mode, synchronised per call: the
+    latency of one forward), each the median of C1_REPS calls after C1_WARM warm-up calls."""
+    from oracle import model_ref
+    from oracle.pyg_ref import RefData, collate
+
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_graph, si2_smoke_graph
+
+    threads = _cpu_threads()
+    prev = torch.get_num_threads()
+    out = {}
+    shapes = {"c1a_smoke_shape": ((6, 8, 7, 289, 2, 32, 1, 1, 0.0), lambda: si2_smoke_graph(0), 1),
+              "c1b_mp_like_L1": ((206, 36, 11, 289, 2, args.hidden, 1, args.heads, 0.0), lambda: mp_like_graph(0),
+                                 args.heads)}
+    for name, (cfg, graph, heads) in shapes.items():
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(*cfg), 2).eval()
+        st = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        g = graph()
+        ref = collate([RefData(**{k: getattr(g, k) for k in g.keys()})], lg_offset=args.lg_offset)
+
+        def cpu_fwd():
+            with torch.no_grad():
+                model_ref.hetero_forward(st, ref, heads)
+
+        torch.set_num_threads(threads)
+        try:
+            t_cpu = _median_time(cpu_fwd, C1_WARM, C1_REPS, sync=False)
+        finally:
+            torch.set_num_threads(prev)
+        model.to(dev)
+        b = A.Batch.from_data_list([g]).to(dev)
+
+        def gpu_fwd():
+            with torch.no_grad():
+                model(b)
+
+        t_gpu = _median_time(gpu_fwd, C1_WARM, C1_REPS, sync=True)
+        out[name] = {"graph": {"atoms": int(g.x.size(0)), "bonds": int(g.edge_index.size(1)),
+                               "triplets": int(g.lg_edge_index.size(1))},
+                     "model": dict(zip(("node_dim", "edge_dim", "angle_dim", "global_dim", "targets", "hidden",
+                                        "layers", "heads"), cfg[:8])),
+                     "cpu_ms": round(t_cpu * 1e3, 3), "cpu_threads": threads,
+                     "gpu_ms": round(t_gpu * 1e3, 3), "speedup": round(t_cpu / t_gpu, 1)}
+        del model, b
+    out["protocol"] = (f"forward only, fp32, eval mode; median of {C1_REPS} calls after {C1_WARM} warm-up; the GPU "
+                       f"figure is one model(batch) call synchronised (host launch latency included, eager)")
+    return out
+
+
+def _median_time(fn, warm, reps, sync):
+    for _ in range(warm):
+        fn()
+    if sync:
+        torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        if sync:
+            torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
 def build_store(args, dev, rank):
@@ -748,6 +819,8 @@ def main():
                 "value": round(w["value"], 2), "unit": "graphs/s", "ms_per_step": round(w["ms_per_step"], 3),
                 "steps": sec_steps, "roofline": w["roofline"]}
             _release(w)
+        if not args.no_cpu_baseline:
+            secondary["c1_forward"] = c1_forward(args, dev)
         if (B, args.precision) != (256, "bf16"):
             c3 = measure(args, dev, rank, world, 256, args.lg_offset, "bf16", sec_steps, sec_warm, roofline=True)
             secondary["c3_b256_bf16"] = {

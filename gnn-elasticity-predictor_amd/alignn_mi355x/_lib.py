@@ -92,6 +92,11 @@ _SIGNATURES = {
     "alignn_lg_bwd_dst_bf16": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                 c_u64, c_vp], c_i32),
+    "alignn_lg_fwd_x": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
+                         c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_lg_bwd_dst_x": ([c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
+                             c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                             c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_cast_bf16_f32": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "alignn_linear_smallk_bf16out": ([c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp],
                                      c_i32),

@@ -433,13 +433,16 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
                   skip_early: bool = False, bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
-                  want_X16: bool = False):
+                  want_X16: bool = False, angle_x=None):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     bf16_io (bf16 storage, config C3 — the tensor dtypes of the reference's autocast, train.py:632-636):
     on a compacted graph the skip projection's output R and, in the backward, its gradient dR are
     bf16 (Linear outputs and their gradients); X16: a bf16 copy of X (the Linear's input as autocast
     casts it: bitwise the operand the bf16 matrix cores round X to) read by the skip projection and its
     weight gradient; want_X16: the gate kernel also writes a bf16 copy of the new state (c.Xn16).
+    angle_x (the line graph, F None): (X, W1, b1, bf16) — the edge features are the angle encoder's
+    hidden layer relu(X W1^T + b1), recomputed inside the attention kernels from the raw inputs X
+    (ops.lg_fwd_x) instead of read; bf16: the bf16-storage form (K|V and f in bf16, config C3).
     skip_early: on a compacted graph with a side stream, the skip projection is queued there before
     the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
@@ -485,7 +488,15 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.mstat = torch.empty(na, H, device=dev)
     c.den = torch.empty(na, H, device=dev)
     c.KV16 = c.QKV16 = None
-    if F is not None and F.dtype == torch.bfloat16 and feat_row is None:
+    c.angle_x = angle_x
+    if angle_x is not None:
+        Xa, W1, b1, bf = angle_x
+        if bf:   # one bf16 copy of Q|K|V: K|V gathered by the attention, Q by the source-side backward
+            c.QKV16 = ops.cast_bf16(c.QKV)
+            c.KV16 = c.QKV16[:, D:3 * D]
+        ops.lg_fwd_x(g, D, H, c.QKV, c.KV16, c.U, c.wbar, Xa, W1, b1, c.outp_a, c.S, c.sumA, c.mstat, c.den, p_drop,
+                     seed_att)
+    elif F is not None and F.dtype == torch.bfloat16 and feat_row is None:
         # bf16 storage (config C3), the line graph: the attention gathers K|V from a bf16 copy and streams
         # the bf16 angle hidden layer (the atom graph's bf16 bond-state rows go through tconv_fwd)
         # one bf16 copy of Q|K|V: K|V gathered by the attention, Q by the source-side backward
@@ -568,7 +579,13 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     sigz = torch.empty(na, H, device=dev)
     dz_e = torch.empty(max(m, 1), H, device=dev)
     al_e = torch.empty(max(m, 1), H, device=dev)
-    if c.KV16 is not None:
+    if c.angle_x is not None:
+        if dF is not None:
+            raise ValueError("recomputed edge features need the deferred angle-encoder backward (no dF)")
+        Xa, W1, b1, _ = c.angle_x
+        ops.lg_bwd_dst_x(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, Xa, W1, b1, dout_a, c.outp_a, c.mstat, c.den,
+                         dQKV[:, :D], Sz, sigz, dz_e, al_e, c.p, c.seed_att)
+    elif c.KV16 is not None:
         if dF is not None:
             raise ValueError("bf16 edge-feature storage needs the deferred angle-encoder backward (no dF)")
         ops.lg_bwd_dst_bf16(g, D, H, c.QKV, c.KV16, c.U, Vd, c.wbar, c.F, dout_a, c.outp_a, c.mstat, c.den, dQKV[:, :D], Sz, sigz,
@@ -739,6 +756,14 @@ class AlignnEngine:
         self.atom_bf16 = True
         # bf16 storage: the line graph's source-side backward gathers Q and dout as bf16 copies
         self.bf16_src = True
+        # the line convs' edge features (the angle encoder's hidden layer, [T, 256]) recomputed inside
+        # the attention kernels from the 11 raw inputs instead of materialised and re-read 8 times
+        # (ops.lg_fwd_x / lg_bwd_dst_x; the deferred encoder backward recomputes its ReLU mask)
+        self.recompute_angle = True
+        # ... and at bf16 storage (config C3): the recompute kernels hold W1 in 44 registers, which
+        # halves the occupancy the bf16 kernels run at (4 / 3 -> 2 waves per SIMD; C3 20,416 ->
+        # 18,394 graphs/s, gpurun_out r5b): off until the bf16 form is restructured
+        self.recompute_angle_bf16 = False
 
     @contextmanager
     def using_precision(self, precision: str):
@@ -766,6 +791,15 @@ class AlignnEngine:
                 and ops.enc_bwd_ok(D, self.cfg.heads, self.cfg.layers, bc.xa.size(1))):
             return False
         return bc.lg.schedule().n_heavy == 0
+
+    def _angle_xf(self, bc, D: int) -> bool:
+        """The line convs recompute their edge features (recompute_angle): D = 256, H = 4, 11 raw
+        angle inputs, the deferred encoder backward, a single-wave-item line-graph schedule."""
+        if self.precision == "bf16" and self.bf16_storage and not self.recompute_angle_bf16:
+            return False
+        return bool(self.recompute_angle and self.defer_angle_bwd and bc.xa is not None and bc.lg is not None
+                    and ops.lg_x_ok(bc.lg, D, self.cfg.heads, bc.xa)
+                    and ops.enc_bwd_ok(D, self.cfg.heads, self.cfg.layers, bc.xa.size(1)))
 
     def _angle_hidden(self, P: FlatViews, bc: BatchCache, D: int, dev, a: torch.Tensor) -> None:
         """a = relu(x_angle W1^T + b1), the angle encoder's hidden layer (its 2nd Linear is folded).
@@ -855,8 +889,16 @@ class AlignnEngine:
         # backward GEMMs never run.
         ctx.has_angle = cfg.angle_dim > 0 and bc.xa is not None
         side = ops.side_stream(dev) if (self.overlap and self.overlap_forward) else None
-        angle_side = self.angle_side and side is not None and ctx.has_angle
-        if ctx.has_angle:
+        # the line convs recompute the angle hidden layer from the raw inputs (no [T, D] array)
+        xf = ctx.has_angle and T > 0 and E > 0 and L > 0 and self._angle_xf(bc, D)
+        angle_x = None
+        if xf:
+            angle_x = (bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"), self._bf16_angle(bc, D))
+        ctx.angle_x = angle_x
+        angle_side = self.angle_side and side is not None and ctx.has_angle and not xf
+        if xf:
+            a = None
+        elif ctx.has_angle:
             a = torch.empty(T, D, device=dev, dtype=torch.bfloat16 if self._bf16_angle(bc, D) else torch.float32)
         else:
             a = ops.zeros(T, D, device=dev)
@@ -875,7 +917,7 @@ class AlignnEngine:
             ctx.h1e, e = None, ops.zeros(E, D, device=dev)
         if angle_side:
             ops.stream_wait(torch.cuda.current_stream(dev), side)
-        elif ctx.has_angle:
+        elif ctx.has_angle and not xf:
             self._angle_hidden(P, bc, D, dev, a)
         ctx.h1a = ctx.a = a
         ctx.edge, ctx.node = [], []
@@ -895,7 +937,7 @@ class AlignnEngine:
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
                                      skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
-                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16))
+                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16), angle_x=angle_x)
                 e16 = c.Xn16
             else:
                 c = None
@@ -1080,6 +1122,8 @@ class AlignnEngine:
         # the VALU kernel: exact fp32 MFMA runs at the VALU rate and measured slower (v15_*)
         f_rows = (ctx.a if (defer and ctx.a is not None and ctx.a.dtype == torch.bfloat16 and ctx.a.dim() == 2
                             and ctx.a.size(1) == 256 and cfg.heads % 2 == 0) else None)
+        # recomputed edge features: the bf16 form recomputes its ReLU mask from the raw inputs too
+        enc16 = defer and ctx.angle_x is not None and ctx.angle_x[3]
         if f_rows is not None:
             kept.append(f_rows)
         # the deferred angle-encoder backward (the longest branch of the tail) on a third stream,
@@ -1091,7 +1135,7 @@ class AlignnEngine:
                 ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
                             [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                             [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
-                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F=f_rows)
+                            G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F=f_rows, bf16=enc16)
         with _side_work(side, (da, *kept)):
             if E > 0 and L > 0:
                 proj_grads(P.node_We, P.node_Wp, P.node_bp, dM_all, dwbar_all, G.node_We, G.node_Wp, G.node_bp)
@@ -1103,7 +1147,7 @@ class AlignnEngine:
                     ops.enc_bwd(bc.lg, bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"),
                                 [c.U for c in ctx.edge], [c.edge_scalars[0] for c in ctx.edge],
                                 [c.edge_scalars[1] for c in ctx.edge], [c.edge_scalars[2] for c in ctx.edge],
-                                G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F=f_rows)
+                                G.enc("angle", 0, "weight"), G.enc("angle", 0, "bias"), F=f_rows, bf16=enc16)
             elif ctx.has_angle and da_written:
                 # da is the masked hidden-layer gradient
                 if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLN_MAX:

@@ -563,12 +563,13 @@ def enc_bwd_ok(D: int, H: int, L: int, kin: int) -> bool:
 
 def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, Us, Vds, dzs, alphas,
             dW1: torch.Tensor, db1: torch.Tensor, accumulate: bool = False,
-            F: Optional[torch.Tensor] = None) -> None:
+            F: Optional[torch.Tensor] = None, bf16: bool = False) -> None:
     """Deferred backward of the angle encoder's first Linear + ReLU over the line graph ``g``:
     dW1/db1 (+)= sum_t dpre_t x_t^T / dpre_t with dpre_t = relu'(W1 x_t + b1) * sum_l,h
     (dz_l u_l + alpha_l Vd_l) — see include/alignn_hip.h (alignn_enc_bwd_f32).  F: the forward's bf16
     hidden layer [T, 256] (bf16 storage, config C3) — the two products then run on the matrix cores in
-    bf16 with the ReLU mask read from F (alignn_enc_bwd_bf16)."""
+    bf16 with the ReLU mask read from F (alignn_enc_bwd_bf16).  bf16 without F: the same products with
+    the mask recomputed from x (the line convs' recompute path, alignn_lg_fwd_x)."""
     L = len(Us)
     T, kin = x.shape
     D = W1.size(0)
@@ -598,6 +599,13 @@ def enc_bwd(g: "GraphCSR", x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, 
     a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
     # compulsory bytes: x rows, targets, 2LH scalars per edge; U/Vd rows once per target
     nbytes = 4.0 * (T * (kin + 1 + 2 * L * H) + 2 * L * g.n * H * D)
+    if bf16 and F is None:
+        if D != 256 or H % 2 or kin < 1 or kin > 12:
+            raise ValueError("enc_bwd: the bf16 recompute form needs D = 256, H even, 1 <= kin <= 12")
+        profiling.launch(f"enc_bwd_bf16 T{T} L{L} x", 0.0, nbytes,
+                         lambda: check(lib.alignn_enc_bwd_bf16(ctypes.byref(a), None, 0, stream_ptr()),
+                                       "alignn_enc_bwd_bf16"))
+        return
     if F is not None:
         if (F.dtype != torch.bfloat16 or F.dim() != 2 or F.size(0) < T or F.size(1) != D or F.stride(1) != 1
                 or F.stride(0) % 8 or F.data_ptr() % 16 or D != 256 or H % 2 or kin < 1):
@@ -938,6 +946,82 @@ def lg_bwd_dst_bf16(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, F16, do
                          den.data_ptr(), dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(),
                          dz_e.data_ptr(), alpha_e.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
                          "alignn_lg_bwd_dst_bf16"))
+
+
+LGX_KIN = 11   # alignn_lg_fwd_x / _bwd_dst_x: raw angle inputs per triplet (rows of 12 floats)
+
+
+def lg_x_ok(g: GraphCSR, D: int, H: int, X: Optional[torch.Tensor]) -> bool:
+    """The recompute (XF) kernels' domain: D = 256, H = 4, 11 raw angle inputs in 16-byte aligned rows
+    of 12 floats, a single-wave-item schedule without heavy targets."""
+    return (D == 256 and H == 4 and X is not None and X.dim() == 2 and X.size(1) == LGX_KIN
+            and X.stride(1) == 1 and X.stride(0) == 12 and X.data_ptr() % 16 == 0 and g.policy.wave_items
+            and g.schedule().n_heavy == 0)
+
+
+def _lg_x_bytes(n: int, m: int, D: int, H: int, kind: str, kv_elem: int) -> float:
+    """Compulsory HBM bytes of one recompute (XF) launch: as _lg_bf16_bytes / _tconv_bytes with the
+    [m, D] edge-feature rows replaced by the raw inputs (48 B per triplet) and W1 / b1."""
+    xb = 48.0 * m + 4.0 * (D * LGX_KIN + D)
+    if kind == "fwd":   # Q + U + CSR in (4), K|V (kv_elem), x; aggV + S + 3 stats out
+        return 4.0 * (n * D + n * H * D + 2 * m + n + n * D + n * H * D + 3 * n * H) + kv_elem * 2.0 * n * D + xb
+    # bwd_dst: Q,U,Vd,dout,outp,stats,CSR in; K|V; x; dQ,Sz,sigz,dz,alpha out
+    return (4.0 * (n * D + 2 * n * H * D + 2 * n * D + 2 * n * H + 2 * m + n + n * D + n * H * D + n * H + 2 * m * H)
+            + kv_elem * 2.0 * n * D + xb)
+
+
+def _check_lg_x(g: GraphCSR, D: int, H: int, QKV, KV16, X, W1, b1):
+    n, m = g.n, g.m
+    if QKV.size(0) < n or QKV.size(1) < 3 * D or QKV.stride(1) != 1:
+        raise ValueError(f"lg x: QKV {tuple(QKV.shape)} must cover [{n}, >= {3 * D}] row-major")
+    if KV16 is not None and (KV16.dtype != torch.bfloat16 or KV16.size(0) < n or KV16.size(1) < 2 * D
+                             or KV16.stride(1) != 1):
+        raise ValueError(f"lg x: KV16 must be bf16 [{n}, >= {2 * D}] row-major")
+    if not lg_x_ok(g, D, H, X) or (m > 0 and X.size(0) < m):
+        raise ValueError(f"lg x: X must be [{m}, {LGX_KIN}] rows of 12 floats, 16-byte aligned (D = 256, H = 4, "
+                         f"single-wave-item schedule)")
+    if (tuple(W1.shape) != (D, LGX_KIN) or not W1.is_contiguous() or b1.numel() != D or not b1.is_contiguous()
+            or W1.dtype != torch.float32 or b1.dtype != torch.float32):
+        raise ValueError("lg x: W1 [256, 11] and b1 [256] contiguous fp32 required")
+
+
+def lg_fwd_x(g: GraphCSR, D: int, H: int, QKV, KV16, U, wbar, X, W1, b1, aggV, S, sumA, mstat, den, drop_p: float,
+             seed: int):
+    """alignn_lg_fwd_x: the line-graph attention forward with the edge features recomputed from the raw
+    angle inputs (f = relu(X W1^T + b1), bitwise linear_smallk; rounded to bf16 when KV16 is given —
+    the bf16-storage path) instead of read from a materialised [m, D] hidden layer."""
+    _check_lg_x(g, D, H, QKV, KV16, X, W1, b1)
+    if U.numel() < g.n * H * D or S.numel() < g.n * H * D or aggV.numel() < g.n * D:
+        raise ValueError("lg_fwd_x: U and S must be [n, H, D], aggV [n, D]")
+    tag = " bf16" if KV16 is not None else ""
+    profiling.launch(f"tconv_fwd n{g.n} m{g.m} x{tag}", 0.0,
+                     _lg_x_bytes(g.n, g.m, D, H, "fwd", 2 if KV16 is not None else 4),
+                     lambda: check(_lib.lib().alignn_lg_fwd_x(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
+                         QKV.data_ptr(), QKV.stride(0), _p(KV16), 0 if KV16 is None else KV16.stride(0),
+                         U.data_ptr(), _p(wbar), X.data_ptr(), X.stride(0), X.size(1), W1.data_ptr(), b1.data_ptr(),
+                         aggV.data_ptr(), S.data_ptr(), sumA.data_ptr(), mstat.data_ptr(), den.data_ptr(),
+                         float(drop_p), int(seed) & (2**64 - 1), stream_ptr()), "alignn_lg_fwd_x"))
+
+
+def lg_bwd_dst_x(g: GraphCSR, D: int, H: int, QKV, KV16, U, Vd, wbar, X, W1, b1, dout, outp, mstat, den, dq, Sz,
+                 sigz, dz_e, alpha_e, drop_p: float, seed: int):
+    """alignn_lg_bwd_dst_x: the target-side attention backward with the edge features recomputed."""
+    _check_lg_x(g, D, H, QKV, KV16, X, W1, b1)
+    if (U.numel() < g.n * H * D or Vd.numel() < g.n * H * D or Sz.numel() < g.n * H * D or dq.size(0) < g.n
+            or dz_e.numel() < g.m * H or alpha_e.numel() < g.m * H):
+        raise ValueError("lg_bwd_dst_x: U, Vd, Sz [n, H, D], dq [n, >= D], dz_e/alpha_e [m, H] required")
+    tag = " bf16" if KV16 is not None else ""
+    profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m} x{tag}", 0.0,
+                     _lg_x_bytes(g.n, g.m, D, H, "bwd_dst", 2 if KV16 is not None else 4),
+                     lambda: check(_lib.lib().alignn_lg_bwd_dst_x(
+                         g.n, g.m, D, H, g.off_dst.data_ptr(), g.src_at.data_ptr(), ctypes.byref(g.schedule()),
+                         QKV.data_ptr(), QKV.stride(0), _p(KV16), 0 if KV16 is None else KV16.stride(0),
+                         U.data_ptr(), Vd.data_ptr(), _p(wbar), X.data_ptr(), X.stride(0), X.size(1), W1.data_ptr(),
+                         b1.data_ptr(), dout.data_ptr(), outp.data_ptr(), mstat.data_ptr(), den.data_ptr(),
+                         dq.data_ptr(), dq.stride(0), Sz.data_ptr(), sigz.data_ptr(), dz_e.data_ptr(),
+                         alpha_e.data_ptr(), float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+                         "alignn_lg_bwd_dst_x"))
 
 
 def cast_bf16(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

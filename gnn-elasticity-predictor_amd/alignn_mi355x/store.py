@@ -284,8 +284,17 @@ class GraphStore:
             if lg_offset == "num_edges" or len(gids) == 0:
                 out["lg"] = int(m.max()) if len(gids) else 0
             else:
+                # each graph's in-edges land inside its touched-bond span [inc + lo, inc + hi] (the span
+                # batch_sizes uses), not its whole window [inc, inc + bonds): tighter where windows overlap
                 inc = _excl_cumsum(self.counts["x"][gids].astype(np.int64))
-                pos = np.concatenate([inc, inc + e])
+                t = self.counts["lg_edge_index"][gids].astype(np.int64)
+                sp = self._lg_spans()[gids]
+                has = t > 0
+                inc, m, sp = inc[has], m[has], sp[has]
+                if not has.any():
+                    out["lg"] = 0
+                    return out
+                pos = np.concatenate([inc + sp[:, 0], inc + sp[:, 1] + 1])
                 val = np.concatenate([m, -m])
                 order = np.lexsort((val, pos))        # at one point, window ends (-) before starts (+)
                 out["lg"] = int(max(0, np.cumsum(val[order]).max()))

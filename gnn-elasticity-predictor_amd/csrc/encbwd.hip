@@ -242,15 +242,34 @@ struct EbSlot {
   static __device__ __forceinline__ int head(int hh, int j) { return hh * JPL + j % JPL; }
 };
 
-template <int H>
+// XF: no hidden-layer rows (the line convs recompute them, lgconv.hip): the ReLU mask comes from the
+// pre-activation W1 x + b1 recomputed here with the forward's arithmetic — a k-ordered chain of
+// v_mfma_f32_4x4x1f32 (bitwise linear_smallk's fmaf chain, tools/probe/mfma441.hip) laid out as the G
+// tile: lane L's column 64 w + 32 ct + (L & 31) is the B operand, and the A operand of MFMA q from
+// lane l is x[edge (l & 3) + 8 q + 4 (l >> 5)][k] — register rr of MFMA q then holds G register
+// 4 q + rr's edge.  kin <= EB_XF_KMAX inputs.
+constexpr int EB_XF_KMAX = 12;
+constexpr int EBF_BLOCKS_XF = EBF_BLOCKS * 2 / 3;   // 197 VGPRs: two workgroups per CU resident
+template <int H, bool XF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))  // 166 VGPRs: 3 waves/SIMD
 void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64_t ldf) {
   constexpr int D = 256;
-  __shared__ __attribute__((aligned(16))) uint16_t fs[32 * EBF_FP];   // the chunk's f rows
-  __shared__ float xs[32 * EBF_XP];                                     // the chunk's raw inputs
+  __shared__ __attribute__((aligned(16))) uint16_t fs[XF ? 8 : 32 * EBF_FP];   // the chunk's f rows
+  __shared__ float xs[32 * EBF_XP];                                            // the chunk's raw inputs
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int kin = p.kin;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  float w1[2][EB_XF_KMAX], b1[2];   // XF: W1 / b1 of this lane's two columns
+  if constexpr (XF) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int col = 64 * w + 32 * ct + r;
+#pragma unroll
+      for (int k = 0; k < EB_XF_KMAX; ++k) w1[ct][k] = k < kin ? p.w1[col * kin + k] : 0.f;
+      b1[ct] = p.b1[col];
+    }
+  }
   ebx16 Z[2];
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct)
@@ -279,10 +298,12 @@ void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64
       // stage the chunk's f rows (32 x 256 bf16: four 16-byte loads per thread, rows past the chunk
       // read a valid row and are never used) and raw inputs
       ebu4 fv[4];
+      if constexpr (!XF) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = threadIdx.x + 256 * u, e = i >> 5, c8 = (i & 31) * 8;
-        fv[u] = *reinterpret_cast<const ebu4*>(F16 + (tc + min(e, ne - 1)) * ldf + c8);
+        for (int u = 0; u < 4; ++u) {
+          const int i = threadIdx.x + 256 * u, e = i >> 5, c8 = (i & 31) * 8;
+          fv[u] = *reinterpret_cast<const ebu4*>(F16 + (tc + min(e, ne - 1)) * ldf + c8);
+        }
       }
       float xv[2];
 #pragma unroll
@@ -303,10 +324,12 @@ void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64
           sv[s][j] = (s ? p.al : p.dz)[l < EB_LMAX ? l : 0][te * H + EbSlot<H>::head(hh, j)];
         }
       __syncthreads();   // the previous chunk's LDS readers are done
+      if constexpr (!XF) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = threadIdx.x + 256 * u, e = i >> 5, c8 = (i & 31) * 8;
-        *reinterpret_cast<ebu4*>(fs + e * EBF_FP + c8) = fv[u];
+        for (int u = 0; u < 4; ++u) {
+          const int i = threadIdx.x + 256 * u, e = i >> 5, c8 = (i & 31) * 8;
+          *reinterpret_cast<ebu4*>(fs + e * EBF_FP + c8) = fv[u];
+        }
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -341,11 +364,30 @@ void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64
         // (edges past the chunk's end have zero G rows: their [dz | alpha'] rows are zero)
         const int col = 64 * w + 32 * ct + r;
         ebh8 GA[2];
+        if constexpr (XF) {
+          v4f pre[4];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int e = (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const uint32_t fb = fs[e * EBF_FP + col];
-          GA[i >> 3][i & 7] = (__bf16)(__builtin_bit_cast(float, fb << 16) > 0.f ? G[i] : 0.f);
+          for (int q = 0; q < 4; ++q) pre[q] = v4f{0.f, 0.f, 0.f, 0.f};
+          const int ea = (lane & 3) + 4 * hh;   // A operand's edge (+ 8 q)
+#pragma unroll
+          for (int k = 0; k < EB_XF_KMAX; ++k) {
+            if (k >= kin) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              pre[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(xs[(ea + 8 * q) * EBF_XP + k], w1[ct][k], pre[q], 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float f = (float)(__bf16)fmaxf(pre[i >> 2][i & 3] + b1[ct], 0.f);   // the forward's bf16 f
+            GA[i >> 3][i & 7] = (__bf16)(f > 0.f ? G[i] : 0.f);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int e = (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const uint32_t fb = fs[e * EBF_FP + col];
+            GA[i >> 3][i & 7] = (__bf16)(__builtin_bit_cast(float, fb << 16) > 0.f ? G[i] : 0.f);
+          }
         }
         Z[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(GA[0], XB[0], Z[ct], 0, 0, 0);
         Z[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(GA[1], XB[1], Z[ct], 0, 0, 0);
@@ -378,24 +420,33 @@ extern "C" int alignn_enc_bwd_bf16(const AlignnEncBwdArgs* a, const uint16_t* F1
   EncBwdParams p;
   const int rc = enc_bwd_params(a, p);
   if (rc != ALIGNN_OK) return rc;
-  if (a->D != 256 || a->kin < 1 || a->H < 2 || (a->T > 0 && (!F16 || ldf < a->D || ldf % 8 != 0 || (reinterpret_cast<uintptr_t>(F16) & 15)))) {
+  if (a->D != 256 || a->kin < 1 || a->H < 2 || (!F16 && a->kin > EB_XF_KMAX) ||
+      (a->T > 0 && F16 && (ldf < a->D || ldf % 8 != 0 || (reinterpret_cast<uintptr_t>(F16) & 15)))) {
     set_error("enc_bwd_bf16: needs D = 256, H >= 2, kin >= 1 and 16-byte aligned bf16 hidden-layer rows (ldf >= D, "
-              "ldf %% 8 == 0; D=%d kin=%d ldf=%lld)", a->D, a->kin, (long long)ldf);
+              "ldf %% 8 == 0) or none (kin <= %d; D=%d kin=%d ldf=%lld)", EB_XF_KMAX, a->D, a->kin, (long long)ldf);
     return ALIGNN_E_UNSUPPORTED;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->T > 0) {
-    switch (a->H) {
-      case 2: launch(enc_bwd_bf16_kernel<2>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
-      case 4: launch(enc_bwd_bf16_kernel<4>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
-      default: launch(enc_bwd_bf16_kernel<8>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+    if (F16) {
+      switch (a->H) {
+        case 2: launch(enc_bwd_bf16_kernel<2, false>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+        case 4: launch(enc_bwd_bf16_kernel<4, false>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+        default: launch(enc_bwd_bf16_kernel<8, false>, dim3(EBF_BLOCKS), dim3(256), 0, s, p, F16, ldf); break;
+      }
+    } else {   // the hidden layer recomputed (the line convs' XF path)
+      switch (a->H) {
+        case 2: launch(enc_bwd_bf16_kernel<2, true>, dim3(EBF_BLOCKS_XF), dim3(256), 0, s, p, F16, ldf); break;
+        case 4: launch(enc_bwd_bf16_kernel<4, true>, dim3(EBF_BLOCKS_XF), dim3(256), 0, s, p, F16, ldf); break;
+        default: launch(enc_bwd_bf16_kernel<8, true>, dim3(EBF_BLOCKS_XF), dim3(256), 0, s, p, F16, ldf); break;
+      }
     }
     ALIGNN_LAUNCH_CHECK("enc_bwd_bf16_kernel");
   } else {
     const int rc2 = alignn_fill_f32(a->workspace, (int64_t)EBF_BLOCKS * (a->kin + 1) * a->D, 0.f, stream);
     if (rc2 != ALIGNN_OK) return rc2;
   }
-  return enc_bwd_stage2_launch(a, s, EBF_BLOCKS);
+  return enc_bwd_stage2_launch(a, s, F16 ? EBF_BLOCKS : EBF_BLOCKS_XF);
 }
 
 static int enc_bwd_params(const AlignnEncBwdArgs* a, EncBwdParams& p) {

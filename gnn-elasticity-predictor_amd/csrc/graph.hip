@@ -329,10 +329,13 @@ __global__ __launch_bounds__(256) void schedule_build_kernel(const int32_t* __re
       __syncthreads();
     }
   }
-  // targets without in-edges, ascending id, after every listed target
+  // targets without in-edges, ascending id, after every listed target — and any target whose
+  // in-degree exceeds the threshold the caller promised (err bit 2): it still gets its place (the
+  // single-wave kernels walk a segment of any length), so the list stays a permutation of the n
+  // targets and no entry is left unwritten for the attention kernels to read as a node id
   for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
     const int64_t i = c0 + t;
-    const bool z = i < n && off[i + 1] == off[i];
+    const bool z = i < n && (off[i + 1] == off[i] || off[i + 1] - off[i] > thr);
     const uint64_t zm = __ballot(z);
     if (lane == 0) wcnt[w][0] = __popcll(zm);
     __syncthreads();

@@ -21,6 +21,16 @@
 //    uniform per-target values (score offsets, softmax stats) are kept row-replicated in VGPRs.
 //  * Per-(edge, head) dropout multipliers: lanes < G*H hash (t, h) with the same counter hash as
 //    fwd2/bwd2 (bitwise the same masks), every lane fetches its row's H values by ds_bpermute.
+//  * XF (the line graph's edge features recomputed, not streamed): the edge features of the line
+//    convs are the angle encoder's hidden layer f_t = relu(W1 x_t + b1) of 11 raw inputs
+//    (train.py:358-364, :553-556).  Instead of reading the [T, 256] rows the angle encoder's first
+//    Linear wrote (82-86 % of these kernels' HBM bytes), each group loads its 4 edges' raw inputs (48 B
+//    each) and recomputes its lanes' 4 x 4 features on the matrix cores: v_mfma_f32_4x4x1f32 with
+//    A = x[edge lane & 3][k] and B = W1[4 lane + m][k] leaves h[edge r][4 lane + m] in register r —
+//    a k-ordered chain of fused multiply-adds, bitwise linear_smallk's fmaf chain (skinny.hip;
+//    tools/probe/mfma441.hip: 0 mismatches in 204,800), then + b1, ReLU (and the bf16 rounding of
+//    the bf16-storage path), exactly as linear_smallk stores them.  W1 stays in registers (44 per
+//    lane); the matrix cores are otherwise idle in these kernels.
 #include "common.h"
 #include "vec.h"
 
@@ -97,17 +107,64 @@ __device__ __forceinline__ f4 widen(u2v u) {  // bf16 -> fp32 is exact: the bf16
 template <bool BF> struct RingT { using type = Edge; };
 template <> struct RingT<true> { using type = EdgeH; };
 // A group's rows as fp32 where it is consumed (widening at the consumer keeps the loads' wait there)
-template <bool BF>
+template <bool BF, bool XF = false>
 __device__ __forceinline__ void to_f32(const typename RingT<BF>::type (&r)[G], Edge (&e)[G]) {
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     if constexpr (BF) {
       e[j].k = widen(r[j].k);
       e[j].v = widen(r[j].v);
-      e[j].f = widen(r[j].f);
+      if constexpr (!XF) e[j].f = widen(r[j].f);
+    } else if constexpr (XF) {
+      e[j].k = r[j].k;
+      e[j].v = r[j].v;
     } else {
       e[j] = r[j];
     }
+  }
+}
+
+// XF: the raw angle inputs of the lane's edge (group edge lane & 3), 12 floats (11 used + pad)
+constexpr int KX = 11;    // raw angle inputs per triplet (lg_edge_attr width, SURVEY §8: F_a = 11)
+constexpr int KXP = 12;   // row of the cache's padded copy (48 B: three 16-byte loads)
+struct XRow {
+  f4 a, b, c;
+};
+// The angle encoder's weights of this lane's four features (registers for the whole kernel)
+struct W1Regs {
+  float w[VPL][KX];
+  float b[VPL];
+};
+__device__ __forceinline__ void load_w1(const float* __restrict__ W1, const float* __restrict__ b1, int j0, W1Regs& W) {
+#pragma unroll
+  for (int m = 0; m < VPL; ++m) {
+#pragma unroll
+    for (int k = 0; k < KX; ++k) W.w[m][k] = W1[(j0 + m) * KX + k];
+    W.b[m] = b1[j0 + m];
+  }
+}
+// f rows of the group's four edges for this lane's four features: relu(W1 x + b1) on the matrix
+// cores (see the header), rounded to bf16 and widened back on the bf16-storage path (BF)
+typedef float v4f __attribute__((ext_vector_type(4)));
+template <bool BF>
+__device__ __forceinline__ void angle_rows(const XRow& xr, const W1Regs& W, Edge (&e)[G]) {
+  const float xs[KXP] = {xr.a.x, xr.a.y, xr.a.z, xr.a.w, xr.b.x, xr.b.y, xr.b.z, xr.b.w, xr.c.x, xr.c.y, xr.c.z, xr.c.w};
+  v4f acc[VPL];
+#pragma unroll
+  for (int m = 0; m < VPL; ++m) {
+    acc[m] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KX; ++k) acc[m] = __builtin_amdgcn_mfma_f32_4x4x1f32(xs[k], W.w[m][k], acc[m], 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    float f[VPL];
+#pragma unroll
+    for (int m = 0; m < VPL; ++m) {
+      f[m] = fmaxf(acc[m][j] + W.b[m], 0.f);
+      if constexpr (BF) f[m] = (float)(__bf16)f[m];
+    }
+    e[j].f = f4{f[0], f[1], f[2], f[3]};
   }
 }
 
@@ -124,6 +181,8 @@ struct Params {
   const float* F; int64_t ldf;    // edge-feature rows, row of edge position t is t
   // bf16 storage (BF kernels): K|V rows [n, ldkv] (K at col 0, V at D) and edge-feature rows (ldf)
   const uint16_t* KV16; int64_t ldkv; const uint16_t* F16;
+  // XF: raw angle inputs [m, ldx = 12] (target-sorted, 11 used), W1 [256, 11], b1 [256]
+  const float* X; int64_t ldx; const float* W1; const float* b1;
   // forward outputs
   float* aggV; float* S; float* sumA; float* mstat; float* den;
   // backward inputs / outputs
@@ -148,9 +207,9 @@ __device__ __forceinline__ void group_src(const Params& p, int32_t t0, int32_t l
 }
 
 // Loads of one group: edges t0..t0+3, clamped to `last` (the segment's last edge position).
-template <bool BF>
-__device__ __forceinline__ void load_group(typename RingT<BF>::type (&r)[G], const Params& p, int32_t t0, int32_t last,
-                                           int j0) {
+template <bool BF, bool XF = false>
+__device__ __forceinline__ void load_group(typename RingT<BF>::type (&r)[G], XRow& xr, const Params& p, int32_t t0,
+                                           int32_t last, int j0) {
   int32_t sg[G];
   group_src(p, t0, last, sg);
 #pragma unroll
@@ -161,13 +220,19 @@ __device__ __forceinline__ void load_group(typename RingT<BF>::type (&r)[G], con
       const uint16_t* kv = p.KV16 + s * p.ldkv + j0;
       r[j].k = *reinterpret_cast<const u2v*>(kv);
       r[j].v = *reinterpret_cast<const u2v*>(kv + D);
-      r[j].f = *reinterpret_cast<const u2v*>(p.F16 + (int64_t)t * p.ldf + j0);
+      if constexpr (!XF) r[j].f = *reinterpret_cast<const u2v*>(p.F16 + (int64_t)t * p.ldf + j0);
     } else {
       const float* kv = p.QKV + s * p.ldq + D + j0;
       r[j].k = ld4(kv);
       r[j].v = ld4(kv + D);
-      r[j].f = ld4(p.F + (int64_t)t * p.ldf + j0);
+      if constexpr (!XF) r[j].f = ld4(p.F + (int64_t)t * p.ldf + j0);
     }
+  }
+  if constexpr (XF) {   // the raw inputs of edge t0 + (lane & 3) (clamped like the rows above)
+    const float* row = p.X + (int64_t)min(t0 + (int32_t)(threadIdx.x & 3), last) * p.ldx;
+    xr.a = ld4(row);
+    xr.b = ld4(row + 4);
+    xr.c = ld4(row + 8);
   }
   // Pin the loads here: without this the compiler sinks them to their first use (one iteration
   // later, right behind their wait), which removes the prefetch (seen in the ISA of the 2-group loop:
@@ -290,10 +355,15 @@ __device__ __forceinline__ void store_edge_heads(float* __restrict__ out, int64_
 #ifndef ALIGNN_LG3_WPE_BF_BWD
 #define ALIGNN_LG3_WPE_BF_BWD 3
 #endif
-template <int NR, bool BF = false, bool FWD = true>
+// XF with bf16 K|V: the 44 W1 registers do not fit the 4 / 3 waves of the streamed-row kernels
+#ifndef ALIGNN_LG3_WPE_BF_XF
+#define ALIGNN_LG3_WPE_BF_XF 2
+#endif
+template <int NR, bool BF = false, bool FWD = true, bool XF = false>
 struct Occ {
-  static constexpr int wpe = BF && NR == 1 ? (FWD ? ALIGNN_LG3_WPE_BF_FWD : ALIGNN_LG3_WPE_BF_BWD)
-                                           : (NR == 1 ? ALIGNN_LG3_WPE1 : ALIGNN_LG3_WPE2);
+  static constexpr int wpe = XF ? (BF ? ALIGNN_LG3_WPE_BF_XF : 2)
+                                : (BF && NR == 1 ? (FWD ? ALIGNN_LG3_WPE_BF_FWD : ALIGNN_LG3_WPE_BF_BWD)
+                                                 : (NR == 1 ? ALIGNN_LG3_WPE1 : ALIGNN_LG3_WPE2));
 };
 
 // Four groups in flight (bf16 rows: a group's loads take half the registers of fp32, so four cost
@@ -438,8 +508,9 @@ __device__ __forceinline__ void fwd_group(const Params& p, const Edge (&r)[G], c
   }
 }
 
-template <int H, int NR, bool DROP, bool BF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR, BF, true>::wpe, Occ<NR, BF, true>::wpe)))
+template <int H, int NR, bool DROP, bool BF, bool XF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR, BF, true, XF>::wpe,
+                                                                    Occ<NR, BF, true, XF>::wpe)))
 void lg3_fwd_kernel(Params p) {
   if constexpr (DROP) resolve_drop(p.drop);
   constexpr int C = D / H;
@@ -489,38 +560,45 @@ void lg3_fwd_kernel(Params p) {
       for (int h = 0; h < H; ++h) c[h] = (h == hl) ? part : 0.f;
       reduce_bcast<H>(c, lane);
     }
+    W1Regs W;
+    if constexpr (XF) load_w1(p.W1, p.b1, j0, W);
     __syncthreads();  // one wave: orders the LDS stores before the loop's reads
     // Loads are issued unconditionally (indices past the segment clamp to its last edge): a load
     // under a condition becomes a phi whose register copy waits for it at the join.
     const int32_t last = end - 1;
     using R = typename RingT<BF>::type;
     R ra[G];
-    load_group<BF>(ra, p, beg, last, j0);
-    auto grp = [&](const R (&r)[G], int32_t t) {
+    XRow xa;
+    load_group<BF, XF>(ra, xa, p, beg, last, j0);
+    auto grp = [&](const R (&r)[G], const XRow& xr, int32_t t) {
       Edge e[G];
-      to_f32<BF>(r, e);
+      to_f32<BF, XF>(r, e);
+      if constexpr (XF) angle_rows<BF>(xr, W, e);
       fwd_group<H, NR, DROP>(p, e, uv, t, end, lane, hl, j0, scale, q, mk, c, m, s_row, sa_row, accS, accV);
     };
     if constexpr (NR == 1) {
       for (int32_t tb = beg;; tb += G) {
-        grp(ra, tb);
+        grp(ra, xa, tb);
         if (tb + G >= end) break;
-        load_group<BF>(ra, p, tb + G, last, j0);
+        load_group<BF, XF>(ra, xa, p, tb + G, last, j0);
       }
     } else if constexpr (NR == 4) {
-      auto ld = [&](R (&r)[G], int32_t t) { load_group<BF>(r, p, t, last, j0); };
-      ALIGNN_LG3_RING4_BODY(ld, grp);
+      static_assert(!XF, "the four-group ring streams the edge-feature rows");
+      auto ld = [&](R (&r)[G], int32_t t) { load_group<BF>(r, xa, p, t, last, j0); };
+      auto g4 = [&](const R (&r)[G], int32_t t) { grp(r, xa, t); };
+      ALIGNN_LG3_RING4_BODY(ld, g4);
     } else {
       // one exit: pairs of groups (an odd count ends with a fully masked group, exactly 0)
       R rb[G];
-      load_group<BF>(rb, p, beg + G, last, j0);
+      XRow xb;
+      load_group<BF, XF>(rb, xb, p, beg + G, last, j0);
       const int32_t pairs = (end - beg + 2 * G - 1) / (2 * G);
       int32_t tb = beg;
       for (int32_t it = 0; it < pairs; ++it, tb += 2 * G) {
-        grp(ra, tb);
-        load_group<BF>(ra, p, tb + 2 * G, last, j0);
-        grp(rb, tb + G);
-        load_group<BF>(rb, p, tb + 3 * G, last, j0);
+        grp(ra, xa, tb);
+        load_group<BF, XF>(ra, xa, p, tb + 2 * G, last, j0);
+        grp(rb, xb, tb + G);
+        load_group<BF, XF>(rb, xb, p, tb + 3 * G, last, j0);
       }
     }
   }
@@ -650,8 +728,9 @@ __device__ __forceinline__ void bwd_group(const Params& p, const Edge (&r)[G], c
   }
 }
 
-template <int H, int NR, bool DROP, bool BF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR, BF, false>::wpe, Occ<NR, BF, false>::wpe)))
+template <int H, int NR, bool DROP, bool BF, bool XF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Occ<NR, BF, false, XF>::wpe,
+                                                                    Occ<NR, BF, false, XF>::wpe)))
 void lg3_bwd_dst_kernel(Params p) {
   if constexpr (DROP) resolve_drop(p.drop);
   constexpr int C = D / H;
@@ -714,35 +793,42 @@ void lg3_bwd_dst_kernel(Params p) {
         inv_den[h] = 1.0f / readlane_f(p.den_in[d * H + (lane % H)], h);
       }
     }
+    W1Regs W;
+    if constexpr (XF) load_w1(p.W1, p.b1, j0, W);
     __syncthreads();  // one wave: orders the LDS stores before the loop's reads
     const int32_t last = end - 1;  // unconditional loads, clamped indices (see lg3_fwd_kernel)
     using R = typename RingT<BF>::type;
     R ra[G];
-    load_group<BF>(ra, p, beg, last, j0);
-    auto grp = [&](const R (&r)[G], int32_t t) {
+    XRow xa;
+    load_group<BF, XF>(ra, xa, p, beg, last, j0);
+    auto grp = [&](const R (&r)[G], const XRow& xr, int32_t t) {
       Edge e[G];
-      to_f32<BF>(r, e);
+      to_f32<BF, XF>(r, e);
+      if constexpr (XF) angle_rows<BF>(xr, W, e);
       bwd_group<H, NR, DROP>(p, e, uv, t, end, lane, hl, j0, scale, q, go, mk, c, mst, inv_den, sgz_row, sz, dqa);
     };
     if constexpr (NR == 1) {
       for (int32_t tb = beg;; tb += G) {
-        grp(ra, tb);
+        grp(ra, xa, tb);
         if (tb + G >= end) break;
-        load_group<BF>(ra, p, tb + G, last, j0);
+        load_group<BF, XF>(ra, xa, p, tb + G, last, j0);
       }
     } else if constexpr (NR == 4) {
-      auto ld = [&](R (&r)[G], int32_t t) { load_group<BF>(r, p, t, last, j0); };
-      ALIGNN_LG3_RING4_BODY(ld, grp);
+      static_assert(!XF, "the four-group ring streams the edge-feature rows");
+      auto ld = [&](R (&r)[G], int32_t t) { load_group<BF>(r, xa, p, t, last, j0); };
+      auto g4 = [&](const R (&r)[G], int32_t t) { grp(r, xa, t); };
+      ALIGNN_LG3_RING4_BODY(ld, g4);
     } else {
       R rb[G];
-      load_group<BF>(rb, p, beg + G, last, j0);
+      XRow xb;
+      load_group<BF, XF>(rb, xb, p, beg + G, last, j0);
       const int32_t pairs = (end - beg + 2 * G - 1) / (2 * G);
       int32_t tb = beg;
       for (int32_t it = 0; it < pairs; ++it, tb += 2 * G) {
-        grp(ra, tb);
-        load_group<BF>(ra, p, tb + 2 * G, last, j0);
-        grp(rb, tb + G);
-        load_group<BF>(rb, p, tb + 3 * G, last, j0);
+        grp(ra, xa, tb);
+        load_group<BF, XF>(ra, xa, p, tb + 2 * G, last, j0);
+        grp(rb, xb, tb + G);
+        load_group<BF, XF>(rb, xb, p, tb + 3 * G, last, j0);
       }
     }
   }
@@ -770,15 +856,34 @@ void lg3_bwd_dst_kernel(Params p) {
 #ifndef ALIGNN_LG3_NR_BF
 #define ALIGNN_LG3_NR_BF 1
 #endif
+// XF: groups in flight (fp32 keeps the streamed-row kernels' 2; bf16 K|V: 1 or 2)
+#ifndef ALIGNN_LG3_NR_BF_XF
+#define ALIGNN_LG3_NR_BF_XF 1
+#endif
 template <int H, bool DROP, bool BF>
 static void launch_fwd_h(const Params& p, hipStream_t s) {
   constexpr int NR = BF ? ALIGNN_LG3_NR_BF : ALIGNN_LG3_NR_FWD;
-  launch((lg3_fwd_kernel<H, NR, DROP, BF>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+  launch((lg3_fwd_kernel<H, NR, DROP, BF, false>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
 }
 template <int H, bool DROP, bool BF>
 static void launch_bwd_h(const Params& p, hipStream_t s) {
   constexpr int NR = BF ? ALIGNN_LG3_NR_BF : ALIGNN_LG3_NR_BWD;
-  launch((lg3_bwd_dst_kernel<H, NR, DROP, BF>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+  launch((lg3_bwd_dst_kernel<H, NR, DROP, BF, false>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+}
+// XF (H = 4 only: the configuration of train.py's model, D = 256 / H = 4)
+template <bool DROP, bool BF>
+static void launch_fwd_x(const Params& p, hipStream_t s) {
+  constexpr int NR = BF ? ALIGNN_LG3_NR_BF_XF : ALIGNN_LG3_NR_FWD;
+  launch((lg3_fwd_kernel<4, NR, DROP, BF, true>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
+}
+// fp32 target-side backward with W1 in registers: two groups in flight spill (255 VGPRs), one fits
+#ifndef ALIGNN_LG3_NR_BWD_XF
+#define ALIGNN_LG3_NR_BWD_XF 1
+#endif
+template <bool DROP, bool BF>
+static void launch_bwd_x(const Params& p, hipStream_t s) {
+  constexpr int NR = BF ? ALIGNN_LG3_NR_BF_XF : ALIGNN_LG3_NR_BWD_XF;
+  launch((lg3_bwd_dst_kernel<4, NR, DROP, BF, true>), dim3((unsigned)p.n_items), dim3(64), 0, s, p);
 }
 
 #define ALIGNN_LG3_DISPATCH_H(FN, H_, DROP_, BF_, ...)   \
@@ -904,6 +1009,82 @@ extern "C" int alignn_lg_bwd_dst_bf16(int64_t n, int64_t m, int32_t D, int32_t H
   return lg3_bwd_dst(n, m, H, off_dst, src_at, sched, Q, ldq, U, Vd, wbar, nullptr, ldf, dout, outp, mstat, den, dq,
                      lddq, Sz, sigz, dz_e, alpha_e, make_drop(drop_p, seed), reinterpret_cast<hipStream_t>(stream),
                      KV16, ldkv, F16);
+}
+
+// Shape checks of the recompute (XF) entry points (host side, before any launch)
+static int lgx_check(int64_t n, int32_t D, int32_t H, const AlignnSchedule* sched, const float* Q, int64_t ldq,
+                     const uint16_t* KV16, int64_t ldkv, const float* X, int64_t ldx, int32_t kin, const float* W1,
+                     const float* b1) {
+  if (D != lg3::D || H != 4 || kin != lg3::KX) {
+    set_error("lg x: needs hidden 256, 4 heads and %d raw angle inputs (got %d, %d, %d)", lg3::KX, (int)D, (int)H,
+              (int)kin);
+    return ALIGNN_E_UNSUPPORTED;
+  }
+  if (!sched || !(sched->flags & ALIGNN_SCHED_WAVE_ITEMS) || sched->n_heavy != 0 || (n > 0 && !sched->light)) {
+    set_error("lg x: needs an ALIGNN_SCHED_WAVE_ITEMS schedule listing every target (no heavy list)");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (n > 0 && (!Q || ldq < 3 * D || (KV16 && (ldkv < 2 * D || ldkv % 4 || !aligned8(KV16))))) {
+    set_error("lg x: Q|K|V rows (ldq >= 3D) and, for bf16 storage, K|V bf16 rows (ldkv >= 2D, 8-byte aligned)");
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  if (n > 0 && (!X || ldx != lg3::KXP || (reinterpret_cast<uintptr_t>(X) & 15u) || !W1 || !b1)) {
+    set_error("lg x: raw angle inputs as 16-byte aligned rows of %d floats (ldx = %lld), W1 [256, %d] and b1 required",
+              lg3::KXP, (long long)ldx, lg3::KX);
+    return ALIGNN_E_BAD_SHAPE;
+  }
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_lg_fwd_x(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                               const int32_t* src_at, const AlignnSchedule* sched, const float* QKV, int64_t ldq,
+                               const uint16_t* KV16, int64_t ldkv, const float* U, const float* wbar, const float* X,
+                               int64_t ldx, int32_t kin, const float* W1, const float* b1, float* aggV, float* S,
+                               float* sumA, float* mstat, float* den, float drop_p, uint64_t seed, void* stream) {
+  int rc = lgx_check(n, D, H, sched, QKV, ldq, KV16, ldkv, X, ldx, kin, W1, b1);
+  if (rc || n == 0) return rc;
+  lg3::Params p{};
+  p.n = n; p.m = m; p.off = off_dst; p.src_at = src_at; p.items = sched->light; p.n_items = sched->n_light;
+  p.QKV = QKV; p.ldq = ldq; p.U = U; p.wbar = wbar; p.KV16 = KV16; p.ldkv = ldkv;
+  p.X = X; p.ldx = ldx; p.W1 = W1; p.b1 = b1;
+  p.aggV = aggV; p.S = S; p.sumA = sumA; p.mstat = mstat; p.den = den;
+  p.drop = make_drop(drop_p, seed);
+  if (p.n_items <= 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool drop = p.drop.active != 0, bf = KV16 != nullptr;
+  if (drop && bf) lg3::launch_fwd_x<true, true>(p, s);
+  else if (drop) lg3::launch_fwd_x<true, false>(p, s);
+  else if (bf) lg3::launch_fwd_x<false, true>(p, s);
+  else lg3::launch_fwd_x<false, false>(p, s);
+  ALIGNN_LAUNCH_CHECK("lg3_fwd_kernel (x)");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_lg_bwd_dst_x(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst,
+                                   const int32_t* src_at, const AlignnSchedule* sched, const float* QKV, int64_t ldq,
+                                   const uint16_t* KV16, int64_t ldkv, const float* U, const float* Vd,
+                                   const float* wbar, const float* X, int64_t ldx, int32_t kin, const float* W1,
+                                   const float* b1, const float* dout, const float* outp, const float* mstat,
+                                   const float* den, float* dq, int64_t lddq, float* Sz, float* sigz, float* dz_e,
+                                   float* alpha_e, float drop_p, uint64_t seed, void* stream) {
+  int rc = lgx_check(n, D, H, sched, QKV, ldq, KV16, ldkv, X, ldx, kin, W1, b1);
+  if (rc || n == 0) return rc;
+  lg3::Params p{};
+  p.n = n; p.m = m; p.off = off_dst; p.src_at = src_at; p.items = sched->light; p.n_items = sched->n_light;
+  p.QKV = QKV; p.ldq = ldq; p.U = U; p.Vd = Vd; p.wbar = wbar; p.KV16 = KV16; p.ldkv = ldkv;
+  p.X = X; p.ldx = ldx; p.W1 = W1; p.b1 = b1;
+  p.dout = dout; p.outp = outp; p.mstat_in = mstat; p.den_in = den;
+  p.dq = dq; p.lddq = lddq; p.Sz = Sz; p.sigz = sigz; p.dz_e = dz_e; p.alpha_e = alpha_e;
+  p.drop = make_drop(drop_p, seed);
+  if (p.n_items <= 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool drop = p.drop.active != 0, bf = KV16 != nullptr;
+  if (drop && bf) lg3::launch_bwd_x<true, true>(p, s);
+  else if (drop) lg3::launch_bwd_x<true, false>(p, s);
+  else if (bf) lg3::launch_bwd_x<false, true>(p, s);
+  else lg3::launch_bwd_x<false, false>(p, s);
+  ALIGNN_LAUNCH_CHECK("lg3_bwd_dst_kernel (x)");
+  return ALIGNN_OK;
 }
 
 extern "C" int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, uint16_t* dst,

@@ -173,7 +173,9 @@ int alignn_enc_bwd_f32(const AlignnEncBwdArgs* args, void* stream);
  * per target and chunk of 32 edges G = [dz | alpha'] . [U ; Vd], dpre = G * [f > 0] with f the
  * forward's bf16 hidden layer F16 [T, ldf] itself (ReLU's backward reads its output), and
  * [dW1^T | db1] (+)= dpre^T . [x | 1].  Needs D = 256 (else ALIGNN_E_UNSUPPORTED); same workspace and
- * determinism as alignn_enc_bwd_f32. */
+ * determinism as alignn_enc_bwd_f32.  F16 == NULL (the line convs recompute the hidden layer,
+ * alignn_lg_fwd_x): the mask comes from bf16(relu(W1 x + b1)) recomputed with the forward's arithmetic
+ * (a k-ordered fused multiply-add chain, bitwise the stored layer's mask); kin <= 12. */
 int alignn_enc_bwd_bf16(const AlignnEncBwdArgs* args, const uint16_t* F16, int64_t ldf, void* stream);
 
 /* Column sums: out[n] (+)= sum_m X[m*ldx + n], m < M, n < N.  Bias gradients of every Linear.
@@ -325,6 +327,27 @@ int alignn_lg_bwd_dst_bf16(int64_t n, int64_t m, int32_t D, int32_t H, const int
                            const uint16_t* F16, int64_t ldf, const float* dout, const float* outp,
                            const float* mstat, const float* den, float* dq, int64_t lddq, float* Sz, float* sigz,
                            float* dz_e, float* alpha_e, float drop_p, uint64_t seed, void* stream);
+/* The line-graph attention with the edge features RECOMPUTED instead of read (replaces the
+ * [T, 256] angle hidden layer that train.py:553-554 materialises and every line conv reads,
+ * train.py:315): f_t = relu(W1 x_t + b1) of the 11 raw inputs x_t (lg_edge_attr in target-sorted
+ * order, rows of ldx = 12 floats, 16-byte aligned; W1 [256, 11], b1 [256] contiguous fp32), computed
+ * per edge group on the matrix cores as the same k-ordered fused multiply-add chain as
+ * alignn_linear_smallk_f32 (bitwise the stored layer).  KV16 == NULL: fp32 (K|V read from QKV, f in
+ * fp32 — config C2); KV16 given: bf16 storage (K|V from KV16, f rounded to bf16 as
+ * alignn_linear_smallk_bf16out stores it — config C3).  Same outputs as alignn_lg_fwd_bf16 /
+ * alignn_lg_bwd_dst_bf16 on the materialised layer.  Needs D = 256, H = 4, kin = 11 (else
+ * ALIGNN_E_UNSUPPORTED) and an ALIGNN_SCHED_WAVE_ITEMS schedule listing every target. */
+int alignn_lg_fwd_x(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
+                    const AlignnSchedule* sched, const float* QKV, int64_t ldq, const uint16_t* KV16, int64_t ldkv,
+                    const float* U, const float* wbar, const float* X, int64_t ldx, int32_t kin, const float* W1,
+                    const float* b1, float* aggV, float* S, float* sumA, float* mstat, float* den, float drop_p,
+                    uint64_t seed, void* stream);
+int alignn_lg_bwd_dst_x(int64_t n, int64_t m, int32_t D, int32_t H, const int32_t* off_dst, const int32_t* src_at,
+                        const AlignnSchedule* sched, const float* QKV, int64_t ldq, const uint16_t* KV16,
+                        int64_t ldkv, const float* U, const float* Vd, const float* wbar, const float* X, int64_t ldx,
+                        int32_t kin, const float* W1, const float* b1, const float* dout, const float* outp,
+                        const float* mstat, const float* den, float* dq, int64_t lddq, float* Sz, float* sigz,
+                        float* dz_e, float* alpha_e, float drop_p, uint64_t seed, void* stream);
 /* dst (bf16, RNE) = src (fp32) for a [rows, cols] block; cols and both leading dimensions multiples
  * of 4, src rows 16-byte aligned. */
 int alignn_cast_bf16_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, uint16_t* dst, int64_t ldd,

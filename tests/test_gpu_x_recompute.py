@@ -1,0 +1,174 @@
+"""The line convs' edge features recomputed inside the attention kernels (csrc/lgconv.hip XF path,
+alignn_lg_fwd_x / alignn_lg_bwd_dst_x, and alignn_enc_bwd_bf16 without F16): the angle encoder's
+hidden layer f = relu(x W1^T + b1) (train.py:358-364, :553-556) is recomputed from the 11 raw inputs
+per edge group on the matrix cores instead of being materialised by linear_smallk and re-read.
+
+* Against the streamed-row kernels on the materialised layer (linear_smallk / linear_smallk_bf16
+  output): bitwise where both run the same number of edge groups in flight (fp32 forward, bf16
+  forward and backward); the fp32 target-side backward runs one group in flight against the
+  streamed kernel's two, and the compiler contracts the per-edge softmax terms differently
+  (1-ulp differences): 1e-6 of each output's largest magnitude.
+* The bf16 deferred encoder backward with its mask recomputed against the mask read from the
+  stored bf16 layer: bitwise.
+* The whole step: recompute_angle on vs off — loss and gradients (C2 fp32, B = 4; C3 bf16, B = 16).
+"""
+import pytest
+import torch
+
+from test_gpu_x_lg3 import DEGREES, _case
+from test_gpu_x_pending import _rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+D, H = 256, 4
+
+
+def _ops():
+    from alignn_mi355x import ops
+    return ops
+
+
+def _xcase(degs, seed, with_wbar):
+    ops = _ops()
+    csr, m, t = _case(H, degs, seed, with_wbar)
+    csr._sched = None
+    csr.policy = ops.SchedulePolicy(wave_items=True, xcd_items=True)
+    g = torch.Generator().manual_seed(seed + 1000)
+    xbuf = torch.empty(max(m, 1), 12, device=DEV)
+    x = xbuf[:, :11]
+    x.copy_(torch.randn(max(m, 1), 11, generator=g).to(DEV))
+    W1 = (torch.randn(D, 11, generator=g) * 0.4).to(DEV)
+    b1 = (torch.randn(D, generator=g) * 0.1).to(DEV)
+    return csr, m, t, x, W1, b1
+
+
+def _outs(n, m):
+    o = dict(outp=torch.empty(n, D, device=DEV), S=torch.empty(n, H, D, device=DEV))
+    for k in ("sumA", "mstat", "den", "sigz"):
+        o[k] = torch.empty(n, H, device=DEV)
+    o["dq"] = torch.full((n, D), float("nan"), device=DEV)
+    o["Sz"] = torch.empty(n, H, D, device=DEV)
+    o["dz"], o["al"] = torch.empty(max(m, 1), H, device=DEV), torch.empty(max(m, 1), H, device=DEV)
+    return o
+
+
+def _streamed(csr, m, t, x, W1, b1, drop, bf16):
+    ops = _ops()
+    n = csr.n
+    o = _outs(n, m)
+    QKV = t["QKVR"]
+    if bf16:
+        F16 = torch.empty(max(m, 1), D, device=DEV, dtype=torch.bfloat16)
+        ops.linear_smallk_bf16(x, W1, b1, F16, relu=True)
+        KV16 = ops.cast_bf16(QKV[:, :3 * D].contiguous())[:, D:3 * D]
+        ops.lg_fwd_bf16(csr, D, H, QKV, KV16, t["U"], t["wbar"], F16, o["outp"], o["S"], o["sumA"], o["mstat"],
+                        o["den"], drop, 77)
+        ops.lg_bwd_dst_bf16(csr, D, H, QKV, KV16, t["U"], t["Vd"], t["wbar"], F16, t["dout"], o["outp"], o["mstat"],
+                            o["den"], o["dq"], o["Sz"], o["sigz"], o["dz"], o["al"], drop, 77)
+    else:
+        F = torch.empty(max(m, 1), D, device=DEV)
+        ops.linear_smallk(x, W1, b1, F, relu=True)
+        assert csr.family(D, H, F) == 3
+        ops.tconv_fwd(csr, D, H, QKV, t["U"], t["wbar"], F, None, o["outp"], o["S"], o["sumA"], o["mstat"], o["den"],
+                      drop, 77)
+        ops.tconv_bwd_dst(csr, D, H, QKV, t["U"], t["Vd"], t["wbar"], F, None, t["dout"], o["outp"], o["mstat"],
+                          o["den"], o["dq"], o["Sz"], o["sigz"], o["dz"], o["al"], None, 0, drop, 77)
+    torch.cuda.synchronize()
+    return o
+
+
+def _recomputed(csr, m, t, x, W1, b1, drop, bf16):
+    ops = _ops()
+    n = csr.n
+    o = _outs(n, m)
+    QKV = t["QKVR"]
+    KV16 = ops.cast_bf16(QKV[:, :3 * D].contiguous())[:, D:3 * D] if bf16 else None
+    ops.lg_fwd_x(csr, D, H, QKV, KV16, t["U"], t["wbar"], x, W1, b1, o["outp"], o["S"], o["sumA"], o["mstat"],
+                 o["den"], drop, 77)
+    ops.lg_bwd_dst_x(csr, D, H, QKV, KV16, t["U"], t["Vd"], t["wbar"], x, W1, b1, t["dout"], o["outp"], o["mstat"],
+                     o["den"], o["dq"], o["Sz"], o["sigz"], o["dz"], o["al"], drop, 77)
+    torch.cuda.synchronize()
+    return o
+
+
+FWD = ("outp", "S", "sumA", "mstat", "den")
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("drop", [0.0, 0.15])
+@pytest.mark.parametrize("degs", list(DEGREES))
+def test_recomputed_edge_features_match_streamed_rows(bf16, drop, degs):
+    for seed, with_wbar in enumerate((True, False)):
+        csr, m, t, x, W1, b1 = _xcase(DEGREES[degs], 60 + seed, with_wbar)
+        a = _streamed(csr, m, t, x, W1, b1, drop, bf16)
+        b = _recomputed(csr, m, t, x, W1, b1, drop, bf16)
+        for k in a:
+            if k in ("dz", "al"):
+                if m == 0:
+                    continue
+                a[k], b[k] = a[k][:m], b[k][:m]
+            if bf16 or k in FWD:
+                assert torch.equal(a[k], b[k]), (k, bf16, drop, degs, seed, _rel(b[k], a[k]))
+            else:
+                assert _rel(b[k], a[k]) < 1e-6, (k, drop, degs, seed)
+
+
+def test_recompute_rejects_unsupported_shapes():
+    ops = _ops()
+    csr, m, t, x, W1, b1 = _xcase(DEGREES["mp_mix"], 3, True)
+    o = _outs(csr.n, m)
+    bad_x = torch.empty(m, 11, device=DEV)   # rows of 11 floats (not the padded 12)
+    with pytest.raises(ValueError):
+        ops.lg_fwd_x(csr, D, H, t["QKVR"], None, t["U"], None, bad_x, W1, b1, o["outp"], o["S"], o["sumA"],
+                     o["mstat"], o["den"], 0.0, 1)
+    with pytest.raises(ValueError):
+        ops.lg_fwd_x(csr, D, H, t["QKVR"], None, t["U"], None, x, W1[:, :10].contiguous(), b1, o["outp"], o["S"],
+                     o["sumA"], o["mstat"], o["den"], 0.0, 1)
+
+
+@pytest.mark.parametrize("n,L", [(40, 4), (9, 2)])
+def test_enc_bwd_bf16_mask_recomputed_bitwise(n, L):
+    from test_gpu_x_encbwd import _case as eb_case
+    ops = _ops()
+    csr, x, W1, b1, U, Vd, dz, al = eb_case(n, 256, 4, L, 11, seed=n + L)
+    T = x.size(0)
+    F16 = torch.empty(T, 256, device=DEV, dtype=torch.bfloat16)
+    ops.linear_smallk_bf16(x, W1, b1, F16, relu=True)
+    dW1a, db1a = torch.empty(256, 11, device=DEV), torch.empty(256, device=DEV)
+    dW1b, db1b = torch.empty(256, 11, device=DEV), torch.empty(256, device=DEV)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1a, db1a, F=F16)
+    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1b, db1b, bf16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dW1a, dW1b) and torch.equal(db1a, db1b)
+
+
+@pytest.mark.parametrize("precision,B", [("fp32", 4), ("bf16", 16)])
+def test_step_with_recomputed_angle_layer(precision, B):
+    """The training step's loss and gradients with recompute_angle on (the default) and off: the
+    forward is bitwise (same attention arithmetic on bitwise the same edge features); gradients to
+    fp32 summation order of the target-side backward (fp32: one group in flight vs two) — bitwise
+    at bf16, where both run one."""
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_batch
+    res = {}
+    batch = mp_like_batch(B).to(DEV)
+    for on in (True, False):
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(DEV)
+        tr = A.FusedTrainer(model, precision=precision)
+        model._engine.recompute_angle = on
+        model._engine.recompute_angle_bf16 = on
+        assert model._engine._angle_xf(A.engine.batch_cache(batch), 256) == on
+        loss = tr.forward_backward(batch, 5).clone()
+        torch.cuda.synchronize()
+        res[on] = (loss, {k: v.clone() for k, v in tr.st.G.named.items()})
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert torch.equal(l1, l0)
+    gmax = max(float(v.abs().max()) for v in g0.values())
+    for k in g0:
+        if precision == "bf16" and "angle_encoder.0" not in k:
+            assert torch.equal(g1[k], g0[k]), k
+        else:
+            # (bf16: the deferred encoder backward's recompute form runs 512 workgroups instead of 768,
+            # so its per-workgroup partial sums of dW1 / db1 group the targets differently)
+            assert float((g1[k] - g0[k]).abs().max()) <= 1e-5 * gmax, k

@@ -184,3 +184,27 @@ def test_module_api_autocast_outputs_and_embed_dtype():
     with pytest.raises(NotImplementedError):
         with torch.autocast("cuda", dtype=torch.float16):
             m(batch)
+
+
+def test_device_schedule_with_an_undersized_degree_bound_stays_a_permutation():
+    """A host in-degree bound that is wrong (a target above the schedule's threshold): the device-built
+    work list still lists every target exactly once (the over-threshold one after the zero-degree
+    targets), so no attention kernel reads an unwritten entry as a node id; the error flag reports it
+    at the next check (alignn_schedule_build)."""
+    from alignn_mi355x import ops
+    degs = torch.tensor([3, 0, 100, 7, 0, 5] * 5)
+    n = degs.numel()
+    dst = torch.repeat_interleave(torch.arange(n), degs)
+    src = torch.randint(0, n, (dst.numel(),), generator=torch.Generator().manual_seed(1))
+    g = ops.GraphCSR(torch.stack([src, dst]).to(DEV), n,
+                     policy=ops.SchedulePolicy(wave_items=True, xcd_items=True, heavy_threshold=64))
+    g.deg_bound = 10                       # wrong: one in-degree is 100
+    assert g.device_schedule_ok()
+    sc = g.schedule()
+    light = g._sched[1].cpu().tolist()
+    assert sc.n_light == n and sorted(light) == list(range(n))
+    lit = [i for i in range(n) if 0 < int(degs[i]) <= 64]
+    assert sorted(light[:len(lit)]) == lit                       # listed targets first
+    assert all(int(degs[i]) in (0, 100) for i in light[len(lit):])
+    with pytest.raises(RuntimeError, match="host bound"):
+        g.check_indices("lg_edge_index")

@@ -14,6 +14,13 @@ for step in "$@"; do
     bench) run bench 420 python bench.py --steps 20 --warmup 5 ;;
     c2) run c2 300 python bench.py --steps 20 --warmup 5 --no-secondary ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    xf) run xf 300 "${PT[@]}" tests/test_gpu_x_recompute.py tests/test_gpu_x_round5.py tests/test_gpu_x_round4.py ;;
+    lgx) run lgx 300 python tools/lgx_bench.py ;;
+    c3) run c3 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline ;;
+    abx) for i in 1 2; do
+           run c2_xf_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
+           run c2_rows_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set engine.recompute_angle=0
+         done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
