@@ -39,6 +39,7 @@ class GemmArgs(ctypes.Structure):
         ("workspace", c_vp), ("workspace_elems", c_i64),
         ("reduce_batch", c_i32), ("tile", c_i32),
         ("c_rows", c_vp),
+        ("rowsum", c_vp),
     ]
 
 

@@ -643,15 +643,12 @@ def _weight_grads(cv, gv, c, side, Qh, Oh, Sz, sigz, dout_a, dQKV, dR, dQKVR, dM
                 ops.gemm(Qh, Sz.transpose(0, 1), gv.We.view(H, C, D))           # dW_edge directly
                 ops.gemm(Oh, c.S.transpose(0, 1), gv.We.view(H, C, D), beta=1.0)
             if rows is not None:
-                ops.gemm(dR.t(), c.X if c.X16 is None else c.X16, gv.Wqkvr[3 * D:])
-                ops.colsum(dR, gv.bqkvr[3 * D:])
+                ops.gemm(dR.t(), c.X if c.X16 is None else c.X16, gv.Wqkvr[3 * D:], rowsum=gv.bqkvr[3 * D:])
         if "b" in part:
             if rows is None:
-                ops.gemm(dQKVR.t(), c.X, gv.Wqkvr)
-                ops.colsum(dQKVR, gv.bqkvr)
+                ops.gemm(dQKVR.t(), c.X, gv.Wqkvr, rowsum=gv.bqkvr)
             else:
-                ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D])
-                ops.colsum(dQKV, gv.bqkvr[:3 * D])
+                ops.gemm(dQKV.t(), c.Xa, gv.Wqkvr[:3 * D], rowsum=gv.bqkvr[:3 * D])
 
 
 class _side_work:
@@ -832,15 +829,13 @@ class AlignnEngine:
         return h1, out
 
     def _mlp_bwd(self, dout, x, h1, W2, gW1, gb1, gW2, gb2, beside_side: bool = False):
-        ops.gemm(dout.t(), h1, gW2)
-        ops.colsum(dout, gb2)
+        ops.gemm(dout.t(), h1, gW2, rowsum=gb2)   # the bias gradient from the same launch
         dh1 = torch.empty_like(h1)
         # beside the deferred angle-encoder backward (side stream) the masked dX product takes the
         # tiled kernels: the bf16 streaming GEMM needs a whole CU's LDS, so it waited for enc_bwd to
         # drain (C3: 1,212 us for a 150 us product)
         ops.gemm(dout, W2, dh1, mask=h1, tile=ops.GEMM_NOSTREAM if beside_side else 0)
-        ops.gemm(dh1.t(), x, gW1)
-        ops.colsum(dh1, gb1)
+        ops.gemm(dh1.t(), x, gW1, rowsum=gb1)
 
     def forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
                 x: Optional[torch.Tensor] = None, global_x: Optional[torch.Tensor] = None, mode: str = "hetero"):
@@ -1004,24 +999,20 @@ class AlignnEngine:
             dshared = torch.empty(B, D, device=dev)
             if ctx.mode == "hetero":
                 with _side_work(side, (dout, ctx.shared)):
-                    ops.gemm(dout[:, :Tt].t(), ctx.shared, G.Wmean)
-                    ops.colsum(dout[:, :Tt], G.bmean)
-                    ops.gemm(dout[:, Tt:].t(), ctx.shared, G.Wlogvar)
-                    ops.colsum(dout[:, Tt:], G.blogvar)
+                    ops.gemm(dout[:, :Tt].t(), ctx.shared, G.Wmean, rowsum=G.bmean)
+                    ops.gemm(dout[:, Tt:].t(), ctx.shared, G.Wlogvar, rowsum=G.blogvar)
                 ops.gemm(dout[:, :Tt], P.Wmean, dshared)
                 ops.gemm(dout[:, Tt:], P.Wlogvar, dshared, beta=1.0)
             else:
                 with _side_work(side, (dout, ctx.shared)):
-                    ops.gemm(dout.t(), ctx.shared, G.Wout)
-                    ops.colsum(dout, G.bout)
+                    ops.gemm(dout.t(), ctx.shared, G.Wout, rowsum=G.bout)
                 ops.gemm(dout, P.Wout, dshared)
         # feat_proj + readout (train.py:562-573)
         dpre = torch.empty(B, D, device=dev)
         ops.dropout(dshared, dpre, ctx.pre, p_drop, site_seed(seed, 4 * L + 1))
         Wf = P.named[pre + "feat_proj.0.weight"]
         with _side_work(side, (dpre, ctx.feats)):
-            ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"])
-            ops.colsum(dpre, g[pre + "feat_proj.0.bias"])
+            ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"], rowsum=g[pre + "feat_proj.0.bias"])
         Wfeat = ctx.feats.size(1)
         dfeats = ops.zeros(B, Wfeat, device=dev)
         ops.gemm(dpre, Wf[:, :D], dfeats[:, :D])

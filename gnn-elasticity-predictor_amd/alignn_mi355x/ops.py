@@ -383,7 +383,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
          bias: Optional[torch.Tensor] = None, rowscale: Optional[torch.Tensor] = None,
          bias2: Optional[torch.Tensor] = None, relu: bool = False, mask: Optional[torch.Tensor] = None,
          split_k: Optional[int] = None, reduce_batch: bool = False,
-         c_rows: Optional[torch.Tensor] = None, tile: int = 0, path_only: bool = False):
+         c_rows: Optional[torch.Tensor] = None, tile: int = 0, path_only: bool = False,
+         rowsum: Optional[torch.Tensor] = None):
     """C = act(alpha * A @ B + beta * C + bias + rowscale[:,None] * bias2) [* (mask > 0)].
 
     A [.., M, K], B [.., K, N], C [.., M, N] are arbitrary strided views (batched when 3-D), fp32 or
@@ -391,7 +392,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     write-only; bf16 tensors need bf16 arithmetic, gemm_precision("bf16"));
     bias/bias2 [.., N], rowscale [.., M] (strided views too).  ``reduce_batch``: A/B batched, C is
     2-D and receives the sum over the batch (K must be a multiple of 16).  ``c_rows`` (int32 [M]):
-    logical row r of C is stored at C[c_rows[r]] (C then has any number of rows >= max index)."""
+    logical row r of C is stored at C[c_rows[r]] (C then has any number of rows >= max index).
+    ``rowsum`` (fp32 contiguous [M]): also rowsum[m] = sum_k A[m, k] from the same launch — the bias
+    gradient beside a weight gradient dW = dY^T X (A = dY^T), instead of a colsum pass over dY."""
     ba, sab, sam, sak, M, K = _as3(A)
     bb, sbb, sbk, sbn, K2, N = _as3(B)
     bc, scb, scm, scn, M2, N2 = _as3(C)
@@ -427,6 +430,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     a.reduce_batch = int(bool(reduce_batch) and batch > 1)
     if c_rows is not None:
         a.c_rows = c_rows.data_ptr()
+    if rowsum is not None:
+        if (rowsum.dtype != torch.float32 or rowsum.numel() != M or not rowsum.is_contiguous() or batch != 1
+                or reduce_batch):
+            raise ValueError("gemm: rowsum must be a contiguous fp32 [M] tensor (batch 1, no reduce_batch)")
+        a.rowsum = rowsum.data_ptr()
     a.split_k = 0 if split_k is None else int(split_k)   # 0: the library plans tile shape and split-K
     io = 0
     for t, flag in ((A, GEMM_A_BF16), (B, GEMM_B_BF16), (C, GEMM_C_BF16)):

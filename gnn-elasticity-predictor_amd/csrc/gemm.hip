@@ -9,7 +9,21 @@ namespace alignn {
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmParams p) {
   const int64_t total = (p.reduce_batch ? 1 : p.batch) * p.M * p.N;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t all = total + (p.rsum ? p.M : 0);   // then the row sums' partials (batch 1)
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < all; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i >= total) {   // rowsum[m]: the split partials in the same eight-chain order
+      const int64_t m = i - total;
+      const float* w = p.ws + (int64_t)p.split_k * total + m;
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int k = 0;
+      for (; k + 7 < p.split_k; k += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += w[(int64_t)(k + j) * p.M];
+      }
+      for (int j = 0; k < p.split_k; ++k, ++j) s[j] += w[(int64_t)k * p.M];
+      p.rsum[m] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+      continue;
+    }
     const int64_t col = i % p.N;
     const int64_t row = (i / p.N) % p.M;
     const int64_t b = i / (p.N * p.M);
@@ -363,12 +377,14 @@ static bool lds16(const AlignnGemmArgs* a, bool akc) {
     const char* e = std::getenv("ALIGNN_GEMM_LDS16");
     return e && std::atoi(e) == 0;
   }();
+  if (a->rowsum) return false;   // the row sums read the fp32 stage images
   if (a->tile & ALIGNN_GEMM_NOLDS16) return false;
   if (a->tile & ALIGNN_GEMM_LDS16) return true;
   return akc && !env_off;
 }
 
 static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
+  if (a->rowsum) return false;
   if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOSTREAM) || (a->tile & 15) != 0) return false;
   if (a->batch != 1 || a->reduce_batch || split != 1) return false;
   if (a->K != 64 && a->K != 128 && a->K != 256) return false;
@@ -421,7 +437,7 @@ extern "C" int64_t alignn_gemm_workspace(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
   if (!plan_args(a, pl, ktot, nb)) return -1;
-  return pl.split > 1 ? (int64_t)pl.split * nb * a->M * a->N : 0;
+  return pl.split > 1 ? (int64_t)pl.split * nb * a->M * a->N + (a->rowsum ? (int64_t)pl.split * a->M : 0) : 0;
 }
 
 extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
@@ -455,6 +471,11 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   p.alpha = a->alpha; p.beta = a->beta; p.relu = a->relu;
   p.reduce_batch = a->reduce_batch && a->batch > 1;
   p.c_rows = a->c_rows;
+  p.rsum = a->rowsum;
+  if (a->rowsum && (a->batch != 1 || a->reduce_batch)) {
+    set_error("gemm: rowsum needs batch == 1 without reduce_batch");
+    return ALIGNN_E_UNSUPPORTED;
+  }
   p.abf = (a->tile & ALIGNN_GEMM_A_BF16) ? 1 : 0;
   p.bbf = (a->tile & ALIGNN_GEMM_B_BF16) ? 1 : 0;
   p.cbf = (a->tile & ALIGNN_GEMM_C_BF16) ? 1 : 0;
@@ -481,9 +502,9 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   p.kchunk = pl.kchunk;
   p.split_k = pl.split;
   p.ws = a->workspace;
-  if (pl.split > 1 && (!a->workspace || a->workspace_elems < (int64_t)pl.split * nbatch_out * a->M * a->N)) {
-    set_error("gemm: split_k=%d needs %lld workspace floats", pl.split,
-              (long long)pl.split * nbatch_out * a->M * a->N);
+  const int64_t ws_need = (int64_t)pl.split * nbatch_out * a->M * a->N + (a->rowsum ? (int64_t)pl.split * a->M : 0);
+  if (pl.split > 1 && (!a->workspace || a->workspace_elems < ws_need)) {
+    set_error("gemm: split_k=%d needs %lld workspace floats", pl.split, (long long)ws_need);
     return ALIGNN_E_WORKSPACE;
   }
   if (bf16_stream_ok(a, pl.split)) {
@@ -499,7 +520,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   else gemm_tiled_launch<0>(p, pl.bm, pl.bn, akc, bkc, grid, pl.bk, np, s);
   ALIGNN_LAUNCH_CHECK("gemm_f32_kernel");
   if (pl.split > 1) {
-    int64_t total = nbatch_out * a->M * a->N;
+    int64_t total = nbatch_out * a->M * a->N + (a->rowsum ? a->M : 0);
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
     launch(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");

@@ -56,6 +56,9 @@ struct GemmParams {
   // bf16 storage (ALIGNN_GEMM_A_BF16 / _B_BF16 / _C_BF16): the pointer holds bf16 elements (strides
   // still in elements); A / B are widened to fp32 exactly as they are staged, C is rounded (RNE)
   int abf, bbf, cbf, pad3_;
+  // row sums of A (AlignnGemmArgs.rowsum): the first column tile's workgroups sum their A stages;
+  // with split-K the partials go to ws after the C partials, [split][M]
+  float* rsum;
 };
 
 // Element pointer arithmetic for an operand that holds fp32 or (bf) bf16 elements.
@@ -333,6 +336,23 @@ __device__ __forceinline__ void mma_stage(floatx16 (&acc)[BM / 64][BN / 64], con
   }
 }
 
+// Row sums of the A image of one LDS stage (fp32 images only: arithmetic 0 / 1), thread t < ROWS owns
+// row t: its BKT values added in k order (zero-filled past the operand's end).
+template <int ROWS, bool KC, int BKT>
+__device__ __forceinline__ float stage_rowsum(const float* __restrict__ lds, int t, float acc) {
+#pragma unroll
+  for (int k = 0; k < BKT; ++k) acc += KC ? lds[t * (BKT + 4) + k] : lds[k * (ROWS + 4) + t];
+  return acc;
+}
+template <int BM>
+__device__ __forceinline__ void store_rowsum(const GemmParams& p, int64_t m0, int sidx, float acc) {
+  const int t = threadIdx.x;
+  if (t < BM && m0 + t < p.M) {
+    if (p.split_k > 1) p.ws[(int64_t)p.split_k * p.batch * p.M * p.N + (int64_t)sidx * p.M + m0 + t] = acc;
+    else p.rsum[m0 + t] = acc;
+  }
+}
+
 // cbf: C holds bf16 (the caller passes a compile-time false for the fp32-arithmetic kernels, whose
 // operands and output are always fp32, so their loops carry no storage-type branches)
 __device__ __forceinline__ void store_c(const GemmParams& p, int64_t b, int64_t row, int64_t col, float v, bool cbf) {
@@ -342,6 +362,12 @@ __device__ __forceinline__ void store_c(const GemmParams& p, int64_t b, int64_t 
 }
 
 // Epilogue. C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+// Every operand the epilogue reads (the C rows' scatter targets, beta's C values, the column's bias
+// and bias2, the rows' rowscale, the mask) is loaded for four elements of a 32x32 block before their
+// stores (register rows r = 4q..4q+3 are four consecutive output rows): element by element, each
+// load waited behind the previous element's store (the compiler cannot move a load of possibly
+// aliasing memory past a store) — up to 16 dependent global round trips per block, now 4 (+1 for
+// the column's bias).  Same arithmetic as epilogue_value, in the same order: bitwise equal.
 template <int BM, int BN>
 __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (&acc)[BM / 64][BN / 64], int64_t m0,
                                            int64_t n0, int64_t b, int sidx, int wm, int wn, int h, int l32, bool cbf) {
@@ -352,14 +378,42 @@ __device__ __forceinline__ void store_tile(const GemmParams& p, const floatx16 (
     for (int j = 0; j < NI; ++j) {
       const int64_t col = n0 + wn * (BN / 2) + j * 32 + l32;
       if (col >= p.N) continue;
+      const int64_t row0 = m0 + wm * (BM / 2) + i * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
+      if (p.split_k > 1) {
+        float* w = p.ws + ((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M * p.N + col;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= p.M) continue;
-        if (p.split_k > 1) {
-          p.ws[(((int64_t)sidx * (p.reduce_batch ? 1 : p.batch) + b) * p.M + row) * p.N + col] = acc[i][j][r];
-        } else {
-          store_c(p, b, row, col, epilogue_value(p, b, row, col, acc[i][j][r]), cbf);
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
+          if (row < p.M) w[row * p.N] = acc[i][j][r];
+        }
+        continue;
+      }
+      // four rows at a time (registers: the loop's occupancy, not the epilogue's, is what matters)
+      const float bv = p.bias ? p.bias[b * p.sbias_b + col] : 0.f;
+      const float b2 = p.rowscale ? p.bias2[b * p.sb2_b + col] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float cv[4], rs[4], mk[4];
+        int64_t ci[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t row = min(row0 + 8 * q + u, p.M - 1);   // clamped: loads stay in range
+          ci[u] = b * p.scb + c_row(p, row) * p.scm + col * p.scn;
+          rs[u] = p.rowscale ? p.rowscale[b * p.srs_b + row * p.srs_m] : 0.f;
+          mk[u] = p.mask ? p.mask[row * p.smk_m + col * p.smk_n] : 1.f;
+          cv[u] = p.beta != 0.f ? (cbf ? bf_at(p.C, ci[u]) : p.C[ci[u]]) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float x = __fmul_rn(p.alpha, acc[i][j][4 * q + u]);
+          if (p.beta != 0.f) x = fmaf(p.beta, cv[u], x);
+          if (p.bias) x = __fadd_rn(x, bv);
+          if (p.rowscale) x = fmaf(rs[u], b2, x);
+          if (p.relu) x = fmaxf(x, 0.f);
+          if (p.mask) x = mk[u] > 0.f ? x : 0.f;
+          if (row0 + 8 * q + u >= p.M) continue;
+          if (cbf) reinterpret_cast<uint16_t*>(p.C)[ci[u]] = bf_rne(x);
+          else p.C[ci[u]] = x;
         }
       }
     }
@@ -448,11 +502,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   __syncthreads();
 
   int cur = 0;
+  const bool rs = !L16 && !RB && p.rsum != nullptr && n0 == 0;   // block-uniform
+  float rsacc = 0.f;
   for (int64_t k0 = kb; k0 < ke; k0 += BKT) {
     const bool more = k0 + BKT < ke;
     if (more) load_stage(k0 + BKT);
     const float* As = smem + cur * (LA + LB);
     mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, As, As + LA, wm, wn, h, l32);
+    if (rs && (int)threadIdx.x < BM) rsacc = stage_rowsum<BM, A_KC, BKT>(As, threadIdx.x, rsacc);
     if (more) {
       float* nxt = smem + (cur ^ 1) * (LA + LB);
       la.store(nxt);
@@ -462,6 +519,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     cur ^= 1;
   }
 
+  if (rs) store_rowsum<BM>(p, m0, sidx, rsacc);
   store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF >= 1 && p.cbf);
 }
 
@@ -545,17 +603,24 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmParams p) {
   load(qa, qb, 2);
   __syncthreads();
   const int npairs = (nst + 1) / 2;
+  const bool rs = !L16 && p.rsum != nullptr && n0 == 0;   // block-uniform
+  float rsacc = 0.f;
   for (int it = 0; it < npairs; ++it) {
     const int s0 = 2 * it;
     mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, L0, L0 + LA, wm, wn, h, l32);   // stage s0
+    if (rs && (int)threadIdx.x < BM) rsacc = stage_rowsum<BM, A_KC, BKT>(L0, threadIdx.x, rsacc);
     store(pa, pb, L1);                                                          // stage s0 + 1
     load(pa, pb, s0 + 3);
     __syncthreads();
-    if (s0 + 1 < nst) mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, L1, L1 + LA, wm, wn, h, l32);
+    if (s0 + 1 < nst) {
+      mma_stage<BM, BN, A_KC, B_KC, BKT, BF>(acc, L1, L1 + LA, wm, wn, h, l32);
+      if (rs && (int)threadIdx.x < BM) rsacc = stage_rowsum<BM, A_KC, BKT>(L1, threadIdx.x, rsacc);
+    }
     store(qa, qb, L0);                                                          // stage s0 + 2
     load(qa, qb, s0 + 4);
     __syncthreads();
   }
+  if (rs) store_rowsum<BM>(p, m0, sidx, rsacc);
   store_tile<BM, BN>(p, acc, m0, n0, b, sidx, wm, wn, h, l32, BF >= 1 && p.cbf);
 }
 

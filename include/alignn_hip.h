@@ -26,7 +26,7 @@ extern "C" {
 
 /* Library/version and error introspection.  ABI version 2 (round 3): alignn_tconv_fwd / _bwd_dst /
  * _family lost the edge-encoder argument, AlignnGemmArgs lost `counters`. */
-#define ALIGNN_ABI_VERSION 2
+#define ALIGNN_ABI_VERSION 3
 int alignn_version(void);
 const char* alignn_last_error(void);
 
@@ -70,6 +70,11 @@ typedef struct AlignnGemmArgs {
                              + ALIGNN_GEMM_BK32 / BK16 / BK64 (stage depth), + ALIGNN_GEMM_BF16 */
   const int32_t* c_rows;  /* optional: logical row r of C is stored at row c_rows[r] (scatter; beta
                              reads the same row).  bias/rowscale/mask stay indexed by r. */
+  float* rowsum;          /* optional (ABI 3): rowsum[m] = sum_k A[m][k] in fp32, written by the same
+                             launch — the bias gradient db = dY^T 1 of the Linear whose weight gradient
+                             is this product dW = dY^T X (train.py's Linear backwards), replacing a
+                             separate column-sum pass over dY.  batch == 1, no reduce_batch; with
+                             split-K the partial sums take split * M more workspace floats. */
 } AlignnGemmArgs;
 
 #define ALIGNN_GEMM_BK32 16

@@ -208,3 +208,33 @@ def test_device_schedule_with_an_undersized_degree_bound_stays_a_permutation():
     assert all(int(degs[i]) in (0, 100) for i in light[len(lit):])
     with pytest.raises(RuntimeError, match="host bound"):
         g.check_indices("lg_edge_index")
+
+
+@pytest.mark.parametrize("M,N,K,a_t,prec", [(768, 256, 2580, True, "fp32"), (256, 256, 23040, True, "fp32"),
+                                            (2, 256, 32, True, "fp32"), (256, 36, 1920, True, "fp32"),
+                                            (100, 64, 300, False, "fp32"), (768, 256, 16020, True, "bf16"),
+                                            (256, 256, 184320, True, "bf16")])
+def test_gemm_rowsum_is_the_bias_gradient(M, N, K, a_t, prec):
+    """alignn_gemm_f32 with rowsum: the weight gradient dW = dY^T X is bitwise the plain product and
+    rowsum = dY.sum(0) (the Linear's bias gradient) from the same launch, to fp32 summation order
+    against an fp64 sum (split-K partials included)."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    dY = torch.randn(K, M, generator=g).to(DEV)
+    X = torch.randn(K, N, generator=g).to(DEV)
+    A = dY.t() if a_t else dY.t().contiguous()
+    if prec == "bf16":
+        dY16 = dY.bfloat16()
+        A = dY16.t()
+        ref_rs = dY16.double().sum(0)
+    else:
+        ref_rs = dY.double().sum(0)
+    C0, C1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    rs = torch.full((M,), float("nan"), device=DEV)
+    with ops.gemm_precision(prec):
+        ops.gemm(A, X, C0)
+        ops.gemm(A, X, C1, rowsum=rs)
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1)
+    err = float((rs.double() - ref_rs).abs().max() / ref_rs.abs().max())
+    assert err < 2e-6 * max(1.0, (K / 1000) ** 0.5), err

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(lib, name), name
     assert set(_declared()) == set(_lib.EXPORTED)
-    assert lib.alignn_version() == 2  # ALIGNN_ABI_VERSION (include/alignn_hip.h)
+    assert lib.alignn_version() == 3  # ALIGNN_ABI_VERSION (include/alignn_hip.h)
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     for name in _declared():
         assert re.search(rf"\bT {name}\b", out), name

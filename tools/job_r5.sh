@@ -2,7 +2,7 @@
 # Round-5 GPU job steps (run through gpurun from the repo root).  Each step under its own time
 # limit; the script stops at the first failing step.
 set -eo pipefail
-O=gpurun_out/${JOB:-r5}
+O=$PWD/gpurun_out/${JOB:-r5}
 mkdir -p "$O"
 export PYTHONUNBUFFERED=1
 PT=(python -u -m pytest -x -q --timeout 300 --timeout-method thread)
@@ -15,12 +15,20 @@ for step in "$@"; do
     c2) run c2 300 python bench.py --steps 20 --warmup 5 --no-secondary ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     xf) run xf 300 "${PT[@]}" tests/test_gpu_x_recompute.py tests/test_gpu_x_round5.py tests/test_gpu_x_round4.py ;;
+    r5t) run r5t 300 "${PT[@]}" tests/test_gpu_x_round5.py ;;
     lgx) run lgx 300 python tools/lgx_bench.py ;;
     c3) run c3 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline ;;
     abx) for i in 1 2; do
            run c2_xf_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
            run c2_rows_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set engine.recompute_angle=0
          done ;;
+    gemmt) run gemmt 400 "${PT[@]}" tests/test_gpu_kernels.py tests/test_gpu_x_gemm_pipe.py tests/test_gpu_x_gemm_lds16.py tests/test_gpu_x_splitk.py tests/test_gpu_x_bf16_stream.py tests/test_gpu_parity.py ;;
+    abl) for i in 1 2; do
+           run c2_new_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
+           (cd abl/wt && run c2_base_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline)
+         done
+         run c3_new 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+         (cd abl/wt && run c3_base 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
