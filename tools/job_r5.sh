@@ -29,6 +29,17 @@ for step in "$@"; do
          done
          run c3_new 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
          (cd abl/wt && run c3_base 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline) ;;
+    gprobe) for t in 0 1 17 2 3 20 129 145; do run gprobe_$t 120 python tools/gemm_probe.py --tile $t; done ;;
+    gpmc) cd /tmp && export TMPDIR=/tmp
+          timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
+          timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
+          cd $OLDPWD; python tools/pmc_sq.py $O/gpmc_sq > $O/gpmc_sq.txt; python tools/pmc_mfma.py $O/gpmc_mf > $O/gpmc_mf.txt; cat $O/gpmc_sq.txt $O/gpmc_mf.txt ;;
+    rpc2) cd /tmp && export TMPDIR=/tmp
+          timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c2 -o run --output-format csv -- python $OLDPWD/bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c2.log 2>&1 || exit 1
+          cd $OLDPWD; python tools/timeline.py $O/rp_c2/run_kernel_trace.csv --top 25 > $O/rp_c2_timeline.txt; python tools/trace_by_grid.py $O/rp_c2/run_kernel_trace.csv > $O/rp_c2_by_grid.txt 2>&1; head -40 $O/rp_c2_timeline.txt ;;
+    rpc3) cd /tmp && export TMPDIR=/tmp
+          timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c3 -o run --output-format csv -- python $OLDPWD/bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c3.log 2>&1 || exit 1
+          cd $OLDPWD; python tools/timeline.py $O/rp_c3/run_kernel_trace.csv --top 25 > $O/rp_c3_timeline.txt; python tools/trace_by_grid.py $O/rp_c3/run_kernel_trace.csv > $O/rp_c3_by_grid.txt 2>&1; head -20 $O/rp_c3_timeline.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

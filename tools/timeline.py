@@ -1,6 +1,6 @@
 """Step timeline from a rocprofv3 kernel trace: busy union, per-queue busy time, idle gaps.
 
-Steps are delimited by the AdamW kernel (one per step).  Prints, for the last full step, the
+Steps are delimited by the AdamW kernel (one per step).  Prints, for one full step (the last by default), the
 device-busy union, each queue's busy time, and the largest gaps where no kernel runs at all, with
 the kernels either side — launch gaps on the critical path show up there.
 
@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--by-kernel", action="store_true", help="per-queue time by kernel (name, grid) in the step")
     ap.add_argument("--sequence", action="store_true", help="every kernel of the step in start order")
+    ap.add_argument("--step", type=int, default=1,
+                    help="which step, counted from the end (1: the last; bench.py's serialized roofline "
+                         "replays are its last 3 steps, so 4+ is a timed, concurrent one)")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -30,9 +33,9 @@ def main():
                          r["Kernel_Name"] + (f" grid={int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) * int(r['Grid_Size_Z'])}" if a.by_kernel else "")))
     rows.sort()
     ends = [e for s, e, q, n in rows if "adamw_kernel" in n]
-    if len(ends) < 3:
-        raise SystemExit("need at least 3 steps in the trace")
-    t0, t1 = ends[-2], ends[-1]
+    if len(ends) < a.step + 2:
+        raise SystemExit(f"need at least {a.step + 2} steps in the trace")
+    t0, t1 = ends[-a.step - 1], ends[-a.step]
     ks = [r for r in rows if r[0] >= t0 and r[1] <= t1]
     span = (t1 - t0) / 1e3
     busy, gaps, cur_s, cur_e, prev = 0, [], None, None, None
