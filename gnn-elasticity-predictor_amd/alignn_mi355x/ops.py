@@ -353,6 +353,8 @@ GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an 
 GEMM_STREAM = 8192    # ALIGNN_GEMM_STREAM: the streaming kernel's row floor 32768 -> 4096 (tests / A/B)
 GEMM_LDS16 = 16384    # ALIGNN_GEMM_LDS16: bf16 tiled products through bf16 LDS images (forced on; default: A k-contiguous)
 GEMM_NOLDS16 = 32768  # ALIGNN_GEMM_NOLDS16: ... forced off (A/B tests)
+GEMM_ROWS = 65536     # ALIGNN_GEMM_ROWS: the bf16 row-streaming kernel at any M (tests / A/B)
+GEMM_NOROWS = 131072  # ALIGNN_GEMM_NOROWS: ... never
 
 
 @contextmanager
@@ -445,7 +447,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if io and not ((_GEMM_FLAGS | int(tile)) & GEMM_BF16):
         raise ValueError("gemm: bf16 operands need bf16 arithmetic (ops.gemm_precision('bf16'))")
     a.tile = int(tile) | _GEMM_FLAGS | io
-    if path_only:   # which kernel the library takes (0 tiled, 1 bf16 streaming); nothing runs
+    if path_only:   # which kernel the library takes (0 tiled, 1 bf16 streaming, 2 bf16 row-streaming); nothing runs
         return int(_lib.lib().alignn_gemm_path(ctypes.byref(a)))
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
     if need < 0:

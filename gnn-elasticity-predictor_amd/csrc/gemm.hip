@@ -180,8 +180,18 @@ __device__ __forceinline__ void band_mma(floatx16 (&acc)[4], const gf4 (&a)[KT /
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
   const __bf16* Bl = Bs + (col0 + l32) * KP + 8 * h;
+  // W fragments one 16-deep slice ahead: slice t + 1's four LDS reads are in flight during slice t's
+  // MFMAs (one wave per SIMD: nothing else hides an LDS round trip behind a dependent MFMA)
+  bf16x8 hb[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) hb[0][j] = *reinterpret_cast<const bf16x8*>(Bl + 32 * j * KP);
 #pragma unroll
   for (int t = 0; t < KT / 16; ++t) {
+    if (t + 1 < KT / 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hb[(t + 1) & 1][j] = *reinterpret_cast<const bf16x8*>(Bl + 32 * j * KP + 16 * (t + 1));
+    }
+    __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the reads back next to their MFMAs
     bf16x8 ha;
     if constexpr (ABF) {
       ha = __builtin_bit_cast(bf16x8, a[t]);
@@ -193,10 +203,7 @@ __device__ __forceinline__ void band_mma(floatx16 (&acc)[4], const gf4 (&a)[KT /
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(Bl + 32 * j * KP + 16 * t);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb, acc[j], 0, 0, 0);
-    }
+    for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb[t & 1][j], acc[j], 0, 0, 0);
   }
 }
 
@@ -226,7 +233,8 @@ __device__ __forceinline__ void load_c(gf4 (&c)[16], const GemmParams& p, __amdg
 }
 
 template <bool BETA, bool MASK, bool CBF, bool CPRE = false>
-__device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], const float* __restrict__ bptr,
+__device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], bool has_bias,
+                                           const float* __restrict__ bptr,
                                            float* __restrict__ Ls, __amdgpu_buffer_rsrc_t cst,
                                            __amdgpu_buffer_rsrc_t cld, __amdgpu_buffer_rsrc_t cmk, int64_t row0,
                                            int l32, int h, int lane, const gf4* cpre = nullptr) {
@@ -244,7 +252,8 @@ __device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (
         const gf4 c = CPRE ? cpre[4 * j + i] : __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
         v = gf4{fmaf(p.beta, c.x, v.x), fmaf(p.beta, c.y, v.y), fmaf(p.beta, c.z, v.z), fmaf(p.beta, c.w, v.w)};
       }
-      if (bptr) {
+      if (has_bias) {   // bptr: the LDS copy of the wave's bias columns (no global load here, whose wait
+                        // would also drain the next band's A loads in flight)
         const gf4 bb = *reinterpret_cast<const gf4*>(bptr + bc + 4 * i);
         v = gf4{__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z), __fadd_rn(v.w, bb.w)};
       }
@@ -276,33 +285,50 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
   constexpr int KP = KT + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NB * KP];
   __shared__ __attribute__((aligned(16))) float Lepi[4 * 32 * EPI_LD];
+  __shared__ __attribute__((aligned(16))) float Lbias[NB];
   const int g = blockIdx.x;
   const int z = g % nslices, q = g / nslices, Q = gridDim.x / nslices;
   const int64_t n0 = (int64_t)z * NB;
-  // W slice -> LDS as bf16 [n][k], once (RNE, as the tiled BF path rounds its operands)
-  if (p.sbk == 1) {  // W^T given (k contiguous): 16-byte loads along k
-    for (int i = threadIdx.x; i < NB * (KT / 4); i += 256) {
-      const int n = i / (KT / 4), k = (i % (KT / 4)) * 4;
-      const float* src = p.B + (n0 + n) * p.sbn + k;
-      const gf4 v = p.vecB ? *reinterpret_cast<const gf4*>(src) : gf4{src[0], src[1], src[2], src[3]};
-      __bf16* d = Bs + n * KP + k;
-      d[0] = (__bf16)v[0]; d[1] = (__bf16)v[1]; d[2] = (__bf16)v[2]; d[3] = (__bf16)v[3];
-    }
-  } else {  // W row-major (n contiguous): loads along n, transposed into the [n][k] image
-    for (int i = threadIdx.x; i < NB * (KT / 4); i += 256) {
-      const int k = i / (NB / 4), n = (i % (NB / 4)) * 4;
-      const float* src = p.B + (int64_t)k * p.sbk + (n0 + n) * p.sbn;
-      const gf4 v = (p.sbn == 1 && p.vecB) ? *reinterpret_cast<const gf4*>(src)
-                                            : gf4{src[0], src[p.sbn], src[2 * p.sbn], src[3 * p.sbn]};
+  // W slice -> LDS as bf16 [n][k], once (RNE, as the tiled BF path rounds its operands).  KT / 4
+  // float4 per thread, loaded in batches of 16 before any is stored: a load-then-store loop waits one
+  // global round trip per float4 (64 of them at K = 256 — most of a band-streaming launch's time).
+  constexpr int PER = NB * (KT / 4) / 256, CH = 16;
+  static_assert(PER % CH == 0, "prologue batches");
+  const bool kc = p.sbk == 1;   // W^T given (k contiguous): 16-byte loads along k; else along n
+  for (int c0 = 0; c0 < PER; c0 += CH) {
+    gf4 v[CH];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Bs[(n + q) * KP + k] = (__bf16)v[q];
+    for (int u = 0; u < CH; ++u) {
+      const int i = threadIdx.x + 256 * (c0 + u);
+      if (kc) {
+        const float* src = p.B + (n0 + i / (KT / 4)) * p.sbn + (i % (KT / 4)) * 4;
+        v[u] = p.vecB ? *reinterpret_cast<const gf4*>(src) : gf4{src[0], src[1], src[2], src[3]};
+      } else {
+        const float* src = p.B + (int64_t)(i / (NB / 4)) * p.sbk + (n0 + (i % (NB / 4)) * 4) * p.sbn;
+        v[u] = (p.sbn == 1 && p.vecB) ? *reinterpret_cast<const gf4*>(src)
+                                       : gf4{src[0], src[p.sbn], src[2 * p.sbn], src[3 * p.sbn]};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int i = threadIdx.x + 256 * (c0 + u);
+      if (kc) {
+        __bf16* d = Bs + (i / (KT / 4)) * KP + (i % (KT / 4)) * 4;
+        d[0] = (__bf16)v[u][0]; d[1] = (__bf16)v[u][1]; d[2] = (__bf16)v[u][2]; d[3] = (__bf16)v[u][3];
+      } else {
+        const int k = i / (NB / 4), n = (i % (NB / 4)) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bs[(n + q) * KP + k] = (__bf16)v[u][q];
+      }
     }
   }
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int l32 = lane & 31, h = lane >> 5;
   const int wr = wave >> 1, wc = wave & 1;
   const int col0 = wc * 128;
-  const float* bias = p.bias ? p.bias + n0 + col0 : nullptr;   // this wave's 128 columns
+  const bool has_bias = p.bias != nullptr;
+  for (int i = threadIdx.x; i < NB; i += 256) Lbias[i] = has_bias ? p.bias[n0 + i] : 0.f;
+  const float* bias = Lbias + col0;   // this wave's 128 columns
   float* Cw = const_cast<float*>(eoff(p.C, n0 + col0, CBF));
   const int64_t cbytes = (p.M * p.scm - (n0 + col0)) * (CBF ? 2 : 4);
   const __amdgpu_buffer_rsrc_t cst = rsrc(Cw, cbytes);
@@ -336,13 +362,13 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, 
     lband(a1, arow(min(b1, nbands - 1)));
     lc(c1, b1);
     band_mma<KT, ABF>(acc, a0, Bs, col0, l32, h);
-    band_store<BETA, MASK, CBF, CPRE>(p, acc, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane, c0);
+    band_store<BETA, MASK, CBF, CPRE>(p, acc, has_bias, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane, c0);
     if (b1 >= nbands) break;
     const int64_t b2 = b1 + Q;
     lband(a0, arow(min(b2, nbands - 1)));
     lc(c0, b2);
     band_mma<KT, ABF>(acc, a1, Bs, col0, l32, h);
-    band_store<BETA, MASK, CBF, CPRE>(p, acc, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane, c1);
+    band_store<BETA, MASK, CBF, CPRE>(p, acc, has_bias, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane, c1);
     if (b2 >= nbands) break;
     band = b2;
   }
@@ -402,6 +428,37 @@ static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
   return true;
 }
 
+// The row-streaming kernel (gemm_rows.hip): bf16 arithmetic, K <= 256 (K % 4, % 8 for bf16 A), N a
+// multiple of 256, batch 1, no split / row scatter / rowscale / rowsum, A k-contiguous 16-byte rows,
+// fp32 W, row-major C / mask with 32-bit byte offsets; taken from ALIGNN_GEMM_ROWS_MIN_M rows up
+// (read once; default 4096), at any M on request (ALIGNN_GEMM_ROWS), never with ALIGNN_GEMM_NOROWS.
+// C3 step, same box (profiles/r05/v5_ab_gemm_rows.txt): 20,658 / 20,742 graphs/s without it,
+// 21,720 / 21,598 from 32768 rows, 21,722 / 21,808 from 4096 (the 16k-row Q/K/V projections too).
+void gemm_rows_launch(const GemmParams& p, int cus, hipStream_t s);
+static int64_t rows_min_m() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("ALIGNN_GEMM_ROWS_MIN_M");
+    return e ? std::max<int64_t>(32, std::atoll(e)) : int64_t(4096);
+  }();
+  return v;
+}
+static bool rows_ok(const AlignnGemmArgs* a, int split) {
+  if (a->rowsum || a->c_rows || a->rowscale) return false;
+  if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOROWS) || (a->tile & 15) != 0) return false;
+  if (a->batch != 1 || a->reduce_batch || split != 1) return false;
+  const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, cbf = (a->tile & ALIGNN_GEMM_C_BF16) != 0;
+  if (a->tile & ALIGNN_GEMM_B_BF16) return false;
+  if (a->K < 1 || a->K > 256 || a->K % (abf ? 8 : 4) != 0) return false;
+  if (a->N % 256 != 0 || a->M < ((a->tile & ALIGNN_GEMM_ROWS) ? 1 : rows_min_m())) return false;
+  if (a->sak != 1 || a->sam % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
+  if (a->scn != 1 || a->scm < a->N || a->scm % 4 || (reinterpret_cast<uintptr_t>(a->C) & (cbf ? 7 : 15))) return false;
+  if (cbf && (a->beta != 0.f || a->mask)) return false;
+  if (a->mask && (a->smk_n != 1 || a->smk_m < a->N || a->smk_m % 4 || (reinterpret_cast<uintptr_t>(a->mask) & 15)))
+    return false;
+  if ((a->M + 32) * std::max(a->scm, a->mask ? a->smk_m : 0) * 4 >= ((int64_t)1 << 31)) return false;
+  return true;
+}
+
 template <int KT>
 static void bf16_stream_launch_k(const GemmParams& p, dim3 grid, int nslices, int64_t nbands, hipStream_t s) {
   const bool beta = p.beta != 0.f, mask = p.mask != nullptr;
@@ -444,7 +501,7 @@ extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
   if (!plan_args(a, pl, ktot, nb)) return -1;
-  return bf16_stream_ok(a, pl.split) ? 1 : 0;
+  return rows_ok(a, pl.split) ? 2 : bf16_stream_ok(a, pl.split) ? 1 : 0;
 }
 
 extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
@@ -506,6 +563,11 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (pl.split > 1 && (!a->workspace || a->workspace_elems < ws_need)) {
     set_error("gemm: split_k=%d needs %lld workspace floats", pl.split, (long long)ws_need);
     return ALIGNN_E_WORKSPACE;
+  }
+  if (rows_ok(a, pl.split)) {
+    gemm_rows_launch(p, device_cus(), s);
+    ALIGNN_LAUNCH_CHECK("gemm_rows_kernel");
+    return ALIGNN_OK;
   }
   if (bf16_stream_ok(a, pl.split)) {
     bf16_stream_launch(p, device_cus(), s);

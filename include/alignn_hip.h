@@ -107,6 +107,11 @@ typedef struct AlignnGemmArgs {
  * gradients' transposing stores cost more than the images save); LDS16 forces it on, NOLDS16 off. */
 #define ALIGNN_GEMM_LDS16 16384
 #define ALIGNN_GEMM_NOLDS16 32768
+/* Row-streaming bf16 kernel (gemm_rows.hip: W columns in VGPRs, A bands streamed through LDS; K <= 256,
+ * N % 256 == 0, taken from 4096 rows up — the environment variable ALIGNN_GEMM_ROWS_MIN_M moves it):
+ * ALIGNN_GEMM_ROWS takes it at any M, ALIGNN_GEMM_NOROWS never.  For tests and A/B. */
+#define ALIGNN_GEMM_ROWS 65536
+#define ALIGNN_GEMM_NOROWS 131072
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
@@ -115,7 +120,8 @@ int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
 
 /* Which kernel alignn_gemm_f32 takes (host query, no GPU work): 0 tiled, 1 the bf16 streaming
- * kernel (ALIGNN_GEMM_NOSTREAM), -1 invalid arguments. */
+ * kernel (ALIGNN_GEMM_NOSTREAM), 2 the bf16 row-streaming kernel (ALIGNN_GEMM_NOROWS), -1 invalid
+ * arguments. */
 int alignn_gemm_path(const AlignnGemmArgs* args);
 
 /* ----------------------------------------------------------------------------------------

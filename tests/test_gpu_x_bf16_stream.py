@@ -5,7 +5,8 @@ against an fp64 product of the bf16-rounded operands the error is fp32 accumulat
 the tiled bf16 path (ALIGNN_GEMM_NOSTREAM) the two differ by accumulation order.  Shapes of the
 B = 256 step plus ragged M, both W layouts, and the epilogue terms it supports.  Below 32768 rows
 the kernel is taken only on request (ALIGNN_GEMM_STREAM: inside the C3 plan the tiled kernels win
-there), so the smaller cases ask for it."""
+there), so the smaller cases ask for it; every case turns the row-streaming kernel off
+(ALIGNN_GEMM_NOROWS: it takes these shapes first, tests in test_gpu_x_gemm_rows.py)."""
 import pytest
 import torch
 
@@ -35,7 +36,7 @@ def test_bf16_stream_vs_fp64_of_rounded_inputs(M, N, K, layout, epi):
     relu = epi == "bias_relu"
     C0 = torch.randn(M, N, generator=g).to(DEV)
     mask = torch.randn(M, N, generator=g).to(DEV) if epi == "mask" else None
-    BF = ops.GEMM_BF16 | (ops.GEMM_STREAM if M < 32768 else 0)
+    BF = ops.GEMM_BF16 | ops.GEMM_NOROWS | (ops.GEMM_STREAM if M < 32768 else 0)
     kw = dict(beta=beta, bias=bias, relu=relu, mask=mask)
     assert ops.gemm(A, Wv, C0, tile=BF, path_only=True, **kw) == 1
     assert ops.gemm(A, Wv, C0, tile=BF | ops.GEMM_NOSTREAM, path_only=True, **kw) == 0
@@ -60,13 +61,13 @@ def test_bf16_stream_vs_fp64_of_rounded_inputs(M, N, K, layout, epi):
 
 def test_bf16_stream_routing_and_untouched_rows():
     from alignn_mi355x import ops
-    BF = ops.GEMM_BF16 | ops.GEMM_STREAM
+    BF = ops.GEMM_BF16 | ops.GEMM_STREAM | ops.GEMM_NOROWS
     A = torch.randn(8000, 256, device=DEV)
     W = torch.randn(256, 256, device=DEV)
     C = torch.empty(8000, 256, device=DEV)
     assert ops.gemm(A, W, C, tile=BF, path_only=True) == 1
     assert ops.gemm(A, W, C, path_only=True) == 0                                 # fp32: tiled
-    assert ops.gemm(A, W, C, tile=ops.GEMM_BF16, path_only=True) == 0             # M < 32768 unasked
+    assert ops.gemm(A, W, C, tile=ops.GEMM_BF16 | ops.GEMM_NOROWS, path_only=True) == 0   # M < 32768 unasked
     assert ops.gemm(A[:4000], W, C[:4000], tile=BF, path_only=True) == 0          # M < 4096
     assert ops.gemm(A[:, :200], W[:200], C, tile=BF, path_only=True) == 0         # K not 64/128/256
     assert ops.gemm(A, W[:, :200], C[:, :200], tile=BF, path_only=True) == 0      # N % 256

@@ -1,0 +1,109 @@
+"""bf16 row-streaming GEMM (csrc/gemm_rows.hip: each wave's 32 columns of W as MFMA operands in VGPRs,
+32-row bands of A streamed through double-buffered LDS images, v_mfma_f32_32x32x16_bf16) — the kernel
+config C3's bond-level products take (every bond times a 256-wide weight: the skip projection, the
+dX += dR W product, the edge MLP).  Same operand rounding (bf16 RNE), k grouping (16-deep slices,
+k = 16 t + 8 h + j) and epilogue order as the tiled bf16 kernels, so it is compared with them
+bitwise (ALIGNN_GEMM_NOROWS | ALIGNN_GEMM_NOSTREAM), and with an fp64 product of the rounded
+operands to fp32 accumulation error.  Shapes of the B = 256 step (K = 36 the edge MLP's first
+layer: zero-padded to 64), ragged M, both W layouts, bf16 A / C storage and every epilogue term it
+supports; below 4096 rows the kernel runs on request (ALIGNN_GEMM_ROWS)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+CASES = [(184320, 256, 256, "nt"), (184320, 256, 256, "nn"), (184320, 256, 36, "nt"), (15360, 1024, 256, "nt"),
+         (16020, 768, 256, "nn"), (5001, 512, 64, "nt"), (4097, 256, 200, "nn"), (33, 256, 8, "nt")]
+
+
+@pytest.mark.parametrize("M,N,K,layout", CASES)
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "beta_bias", "mask"])
+def test_rows_kernel_matches_tiled_bitwise(M, N, K, layout, epi):
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = torch.randn(K, N, generator=g).to(DEV)
+    Wv = W if layout[1] == "n" else W.t().contiguous().t()
+    bias = torch.randn(N, generator=g).to(DEV) if epi != "plain" else None
+    beta = 0.75 if epi == "beta_bias" else 0.0
+    relu = epi == "bias_relu"
+    C0 = torch.randn(M, N, generator=g).to(DEV)
+    mask = torch.randn(M, N, generator=g).to(DEV) if epi == "mask" else None
+    BF = ops.GEMM_BF16 | (ops.GEMM_ROWS if M < 4096 else 0)
+    kw = dict(beta=beta, bias=bias, relu=relu, mask=mask)
+    assert ops.gemm(A, Wv, C0, tile=BF, path_only=True, **kw) == 2
+    C = C0.clone()
+    ops.gemm(A, Wv, C, tile=BF, **kw)
+    Ct = C0.clone()
+    ops.gemm(A, Wv, Ct, tile=ops.GEMM_BF16 | ops.GEMM_NOROWS | ops.GEMM_NOSTREAM, **kw)
+    C2 = C0.clone()
+    ops.gemm(A, Wv, C2, tile=BF, **kw)
+    torch.cuda.synchronize()
+    ref = A.bfloat16().double() @ W.bfloat16().double() + beta * C0.double()
+    if bias is not None:
+        ref = ref + bias.double()
+    if relu:
+        ref = torch.relu(ref)
+    if mask is not None:
+        ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
+    assert _rel(C, ref) < 5e-6
+    assert torch.equal(C, Ct)
+    assert torch.equal(C, C2)   # fixed order, no atomics
+
+
+@pytest.mark.parametrize("io", ["A16_C16", "A16_beta", "C16", "A16_mask"])
+def test_rows_kernel_bf16_storage(io):
+    """bf16 A rows (the skip projection reads X16, dX += dR W reads the bf16 dR) and bf16 C (R)."""
+    from alignn_mi355x import ops
+    M, N, K = 184320, 256, 256
+    g = torch.Generator(device="cpu").manual_seed(7)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = (torch.randn(N, K, generator=g) * 0.1).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    A16 = A.bfloat16() if "A16" in io else A
+    beta = 1.0 if "beta" in io else 0.0
+    mask = torch.randn(M, N, generator=g).to(DEV) if "mask" in io else None
+    C0 = torch.randn(M, N, generator=g).to(DEV)
+    if "C16" in io:
+        C0 = C0.bfloat16()
+    kw = dict(beta=beta, bias=None if beta else bias, mask=mask)
+    with ops.gemm_precision("bf16"):
+        assert ops.gemm(A16, W.t(), C0, path_only=True, **kw) == 2
+        C = C0.clone()
+        ops.gemm(A16, W.t(), C, **kw)
+        Ct = C0.clone()
+        ops.gemm(A16, W.t(), Ct, tile=ops.GEMM_NOROWS | ops.GEMM_NOSTREAM, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C, Ct)
+
+
+def test_rows_kernel_routing_and_untouched_rows():
+    from alignn_mi355x import ops
+    BF = ops.GEMM_BF16 | ops.GEMM_ROWS
+    A = torch.randn(8000, 256, device=DEV)
+    W = torch.randn(256, 256, device=DEV)
+    C = torch.empty(8000, 256, device=DEV)
+    assert ops.gemm(A, W, C, tile=BF, path_only=True) == 2
+    assert ops.gemm(A, W, C, path_only=True) == 0                                   # fp32 arithmetic: tiled
+    assert ops.gemm(A, W, C, tile=ops.GEMM_BF16, path_only=True) == 2               # M >= 4096
+    assert ops.gemm(A[:4000], W, C[:4000], tile=ops.GEMM_BF16, path_only=True) == 0  # M < 4096 unasked
+    assert ops.gemm(A, W, C, tile=BF | ops.GEMM_NOROWS, path_only=True) == 0
+    assert ops.gemm(A[:, :252], W[:252], C, tile=BF, path_only=True) == 2           # K <= 256, K % 4 == 0
+    A2, W2 = torch.randn(8000, 260, device=DEV), torch.randn(260, 256, device=DEV)
+    assert ops.gemm(A2, W2, C, tile=BF, path_only=True) == 0                        # K > 256
+    assert ops.gemm(A, W[:, :200], C[:, :200], tile=BF, path_only=True) == 0        # N % 256
+    rows = torch.arange(8000, dtype=torch.int32, device=DEV)
+    assert ops.gemm(A, W, C, tile=BF, c_rows=rows, path_only=True) == 0
+    assert ops.gemm(A, W, C, tile=BF, mask=C.t().contiguous().t(), path_only=True) == 0   # column-major mask
+    # rows past M of the last band are dropped by the store descriptor
+    buf = torch.full((4200, 256), 7.0, device=DEV)
+    ops.gemm(A[:4100], W, buf[:4100], tile=BF)
+    torch.cuda.synchronize()
+    assert bool((buf[4100:] == 7.0).all())

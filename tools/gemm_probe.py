@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--bf16", action="store_true", help="bf16 matrix-core arithmetic")
     ap.add_argument("--no-lib", action="store_true")
+    ap.add_argument("--io16", action="store_true", help="bf16 storage: A and (fwd) C bf16, dx with a bf16 dR")
     a = ap.parse_args()
     from alignn_mi355x import ops
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -51,7 +52,9 @@ def main():
     Wd = torch.randn(a.N, a.K, device="cuda", generator=g) * 0.05   # dX = dR W (W [N, K] as [k, n] = [N, K])
     C1 = torch.empty(a.M, a.N, device="cuda")
     C2 = torch.randn(a.M, a.K, device="cuda", generator=g)
-    res = {"M": a.M, "N": a.N, "K": a.K, "tile": a.tile, "bf16": a.bf16}
+    if a.io16:
+        X, C1, dR = X.bfloat16(), C1.bfloat16(), dR.bfloat16()
+    res = {"M": a.M, "N": a.N, "K": a.K, "tile": a.tile, "bf16": a.bf16, "io16": a.io16}
     prec = "bf16" if a.bf16 else "fp32"
     flops = 2.0 * a.M * a.N * a.K
     with ops.gemm_precision(prec):
@@ -63,8 +66,10 @@ def main():
             res["dx_us"], res["dx_tflops"] = t, round(flops / t / 1e6, 1)
     if not a.no_lib:
         if a.bf16:
-            Xb, Wb = X.bfloat16(), W.bfloat16()
+            Xb, Wb = X.bfloat16(), W.bfloat16()   # (bf16 in and out: half the bytes of fp32 storage)
             res["lib_fwd_us"] = timeit(lambda: torch.addmm(bias.bfloat16(), Xb, Wb.t()), a.iters)
+            dRb, Wdb = dR.bfloat16(), Wd.bfloat16()
+            res["lib_dx_us"] = timeit(lambda: torch.matmul(dRb, Wdb), a.iters)
         else:
             res["lib_fwd_us"] = timeit(lambda: torch.addmm(bias, X, W.t()), a.iters)
             res["lib_dx_us"] = timeit(lambda: torch.matmul(dR, Wd), a.iters)

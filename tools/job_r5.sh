@@ -30,6 +30,25 @@ for step in "$@"; do
          run c3_new 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
          (cd abl/wt && run c3_base 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline) ;;
     gprobe) for t in 0 1 17 2 3 20 129 145; do run gprobe_$t 120 python tools/gemm_probe.py --tile $t; done ;;
+    gbf) for sh in "16020 768 256" "15360 1024 256" "16020 256 768" "15360 256 1024"; do set -- $sh
+           for t in 0 128 16 129 130 131; do run gbf_$1_$2_$3_$t 120 python tools/gemm_probe.py --bf16 --M $1 --N $2 --K $3 --tile $t; done; done
+         for t in 0 512 640 528 641 642; do run gbf_184320_$t 120 python tools/gemm_probe.py --bf16 --M 184320 --tile $t; done
+         grep -h '^{' $O/gbf_*.log ;;
+    gbs) for sh in "184320 256 256" "16020 768 256" "15360 1024 256" "16020 256 768"; do set -- $sh
+           for t in 0 8192; do for io in "" --io16; do
+             run gbs_$1_$2_$3_$t$io 120 python tools/gemm_probe.py --bf16 --M $1 --N $2 --K $3 --tile $t $io; done; done; done
+         grep -h '^{' $O/gbs_*.log ;;
+    grows) run t_rows 300 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_bf16_stream.py
+           for sh in "184320 256 256" "184320 256 36" "16020 768 256" "15360 1024 256"; do set -- $sh
+             for t in 0 131072 65536; do for io in "" --io16; do
+               run grows_$1_$2_$3_$t$io 120 python tools/gemm_probe.py --bf16 --M $1 --N $2 --K $3 --tile $t $io; done; done; done
+           grep -h '^{' $O/grows_*.log ;;
+    rowsab) run t_rows 300 "${PT[@]}" tests/test_gpu_x_gemm_rows.py
+           for io in "" --io16; do run grows_184320$io 120 python tools/gemm_probe.py --bf16 --M 184320 $io; done
+           for io in "" --io16; do run grows_16020$io 120 python tools/gemm_probe.py --bf16 --M 16020 --N 768 --tile 65536 $io; done
+           grep -h '^{' $O/grows_*.log
+           for m in 32768 4096 999999999 32768 4096 999999999; do
+             ALIGNN_GEMM_ROWS_MIN_M=$m run c3_m$m 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
