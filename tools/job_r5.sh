@@ -49,6 +49,21 @@ for step in "$@"; do
            grep -h '^{' $O/grows_*.log
            for m in 32768 4096 999999999 32768 4096 999999999; do
              ALIGNN_GEMM_ROWS_MIN_M=$m run c3_m$m 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done ;;
+    rowsf) run t_rows 300 "${PT[@]}" tests/test_gpu_x_gemm_rows.py
+           for t in 0 131072; do run growsf_$t 120 python tools/gemm_probe.py --M 23040 --tile $t; done
+           run growsf_2003 120 python tools/gemm_probe.py --M 2003 --N 768 --tile 65536
+           run growsf_2003n 120 python tools/gemm_probe.py --M 2003 --N 768 --tile 131072
+           grep -h '^{' $O/growsf_*.log
+           for m in 4096 999999999 4096 999999999; do
+             ALIGNN_GEMM_ROWS_MIN_M_F32=$m run c2_m$m 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline; grep -o '"value": [0-9.]*' $O/c2_m$m.log; done ;;
+    npf) for L in in-tree abl/libnpf2.so; do tag=$(basename $L .so)
+           for sh in "2580 768 256" "1920 1024 256" "23040 256 256" "2580 256 256"; do set -- $sh
+             if [ $L = in-tree ]; then run gnpf_${tag}_$1_$2 120 python tools/gemm_probe.py --M $1 --N $2 --K $3 --no-lib
+             else ALIGNN_HIP_LIB=$PWD/$L run gnpf_${tag}_$1_$2 120 python tools/gemm_probe.py --M $1 --N $2 --K $3 --no-lib; fi; done; done
+         for f in $O/gnpf_*.log; do echo "$(basename $f) $(grep '^{' $f)"; done
+         for i in 1 2; do run c2_new$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
+           ALIGNN_HIP_LIB=$PWD/abl/libnpf2.so run c2_npf2_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline; done
+         for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
