@@ -248,7 +248,11 @@ class BatchCache:
         past the first pad['kg'] (those the ghost triplets use) join the active set until it has
         pad['active'] members — device arithmetic, no host round trip.  active_bound (a host bound
         of the active count, store batches): the same filling up to that many, so the size needs no
-        device->host copy either (a bond without line-graph edges is inert in the compacted graph)."""
+        device->host copy either (a bond without line-graph edges is inert in the compacted graph).
+        Equality with the unhinted step is bitwise only when the bound is exact (the synthetic MP-like
+        batches: every bond of the span active); a looser bound adds inert rows, which change the
+        compacted row count and with it split-K chunking and column-sum partitions, so the two agree to
+        fp32 summation order (and COMPACT_FRACTION is decided on the bound)."""
         if edge_index.dtype != torch.int64 or edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError("edge_index must be int64 [2, m]")
         m = edge_index.size(1)

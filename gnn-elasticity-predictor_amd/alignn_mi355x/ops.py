@@ -355,6 +355,7 @@ GEMM_LDS16 = 16384    # ALIGNN_GEMM_LDS16: bf16 tiled products through bf16 LDS 
 GEMM_NOLDS16 = 32768  # ALIGNN_GEMM_NOLDS16: ... forced off (A/B tests)
 GEMM_ROWS = 65536     # ALIGNN_GEMM_ROWS: the bf16 row-streaming kernel at any M (tests / A/B)
 GEMM_NOROWS = 131072  # ALIGNN_GEMM_NOROWS: ... never
+GEMM_NOWGRAD = 262144  # ALIGNN_GEMM_NOWGRAD: the bf16 weight-gradient kernel never (tests / A/B)
 
 
 @contextmanager
@@ -447,7 +448,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if io and not ((_GEMM_FLAGS | int(tile)) & GEMM_BF16):
         raise ValueError("gemm: bf16 operands need bf16 arithmetic (ops.gemm_precision('bf16'))")
     a.tile = int(tile) | _GEMM_FLAGS | io
-    if path_only:   # which kernel the library takes (0 tiled, 1 bf16 streaming, 2 bf16 row-streaming); nothing runs
+    if path_only:   # the kernel the library takes (0 tiled, 1 bf16 streaming, 2 bf16 row-streaming, 3 bf16
+        #             weight-gradient); nothing runs
         return int(_lib.lib().alignn_gemm_path(ctypes.byref(a)))
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
     if need < 0:
@@ -457,7 +459,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
         a.workspace, a.workspace_elems = ws.data_ptr(), ws.numel()
     if GEMM_TRACE is not None:   # tuning hook (tools/gemm_bench.py): record the call's operands
         GEMM_TRACE.append(dict(A=A, B=B, C=C, alpha=alpha, beta=beta, bias=bias, rowscale=rowscale, bias2=bias2,
-                               relu=relu, mask=mask, reduce_batch=reduce_batch, c_rows=c_rows))
+                               relu=relu, mask=mask, reduce_batch=reduce_batch, c_rows=c_rows, rowsum=rowsum))
     key = f"gemm_f32 M{M} N{N} K{K} b{batch}" + "".join(f" {n}16" for t, n in ((A, "A"), (B, "B"), (C, "C"))
                                                       if t.dtype == torch.bfloat16)
     if profiling.active(key) or profiling.active("*gemm"):

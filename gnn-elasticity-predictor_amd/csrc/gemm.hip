@@ -459,6 +459,27 @@ static bool rows_ok(const AlignnGemmArgs* a, int split) {
   return true;
 }
 
+// The weight-gradient kernel (gemm_wgrad.hip): bf16 arithmetic, A = dY^T and B = X both stored
+// row-major over the long K axis (sam == 1, sbn == 1; 16-byte rows), K >= 4096, batch 1, no split
+// request / row scatter / rowscale, M and N multiples of 4 (8 for bf16 storage) and >= 8; its partials
+// go through the split-K workspace and reduce.  ALIGNN_GEMM_NOWGRAD turns it off (tests, A/B).
+int64_t gemm_wgrad_split(int64_t M, int64_t N, int64_t K, int cus, int64_t* rows_per);
+void gemm_wgrad_launch(const GemmParams& p, int64_t S, int64_t rows_per, hipStream_t s);
+static bool wgrad_ok(const AlignnGemmArgs* a) {
+  static const bool env_off = [] {   // ALIGNN_GEMM_WGRAD=0 in the environment (read once): off (A/B)
+    const char* e = std::getenv("ALIGNN_GEMM_WGRAD");
+    return e && std::atoi(e) == 0;
+  }();
+  if (env_off || !(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOWGRAD) || (a->tile & 15) != 0) return false;
+  if (a->tile & (ALIGNN_GEMM_BK16 | ALIGNN_GEMM_BK32 | ALIGNN_GEMM_BK64)) return false;
+  if (a->batch != 1 || a->reduce_batch || a->split_k > 0 || a->c_rows || a->rowscale || a->mask) return false;
+  const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, bbf = (a->tile & ALIGNN_GEMM_B_BF16) != 0;
+  if (a->K < 4096 || a->M < 8 || a->N < 8 || a->M % (abf ? 8 : 4) || a->N % (bbf ? 8 : 4)) return false;
+  if (a->sam != 1 || a->sak < a->M || a->sak % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
+  if (a->sbn != 1 || a->sbk < a->N || a->sbk % (bbf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->B) & 15)) return false;
+  return true;
+}
+
 template <int KT>
 static void bf16_stream_launch_k(const GemmParams& p, dim3 grid, int nslices, int64_t nbands, hipStream_t s) {
   const bool beta = p.beta != 0.f, mask = p.mask != nullptr;
@@ -494,6 +515,11 @@ extern "C" int64_t alignn_gemm_workspace(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
   if (!plan_args(a, pl, ktot, nb)) return -1;
+  if (wgrad_ok(a)) {
+    int64_t rp;
+    const int64_t S = gemm_wgrad_split(a->M, a->N, a->K, device_cus(), &rp);
+    return S * a->M * a->N + (a->rowsum ? S * a->M : 0);
+  }
   return pl.split > 1 ? (int64_t)pl.split * nb * a->M * a->N + (a->rowsum ? (int64_t)pl.split * a->M : 0) : 0;
 }
 
@@ -501,7 +527,7 @@ extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
   if (!plan_args(a, pl, ktot, nb)) return -1;
-  return rows_ok(a, pl.split) ? 2 : bf16_stream_ok(a, pl.split) ? 1 : 0;
+  return wgrad_ok(a) ? 3 : rows_ok(a, pl.split) ? 2 : bf16_stream_ok(a, pl.split) ? 1 : 0;
 }
 
 extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
@@ -563,6 +589,22 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (pl.split > 1 && (!a->workspace || a->workspace_elems < ws_need)) {
     set_error("gemm: split_k=%d needs %lld workspace floats", pl.split, (long long)ws_need);
     return ALIGNN_E_WORKSPACE;
+  }
+  if (wgrad_ok(a)) {
+    int64_t rp;
+    const int64_t S = gemm_wgrad_split(a->M, a->N, a->K, device_cus(), &rp);
+    const int64_t need = S * a->M * a->N + (a->rowsum ? S * a->M : 0);
+    if (!a->workspace || a->workspace_elems < need) {
+      set_error("gemm: the weight-gradient kernel needs %lld workspace floats", (long long)need);
+      return ALIGNN_E_WORKSPACE;
+    }
+    p.split_k = (int)S;
+    gemm_wgrad_launch(p, S, rp, s);
+    ALIGNN_LAUNCH_CHECK("wgrad_kernel");
+    const int64_t total = a->M * a->N + (a->rowsum ? a->M : 0);
+    launch(splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0, s, p);
+    ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");
+    return ALIGNN_OK;
   }
   if (rows_ok(a, pl.split)) {
     gemm_rows_launch(p, device_cus(), s);

@@ -112,6 +112,10 @@ typedef struct AlignnGemmArgs {
  * ALIGNN_GEMM_ROWS takes it at any M, ALIGNN_GEMM_NOROWS never.  For tests and A/B. */
 #define ALIGNN_GEMM_ROWS 65536
 #define ALIGNN_GEMM_NOROWS 131072
+/* bf16 weight-gradient kernel (gemm_wgrad.hip: A = dY^T and B = X stored row-major over a long K >= 4096,
+ * whole 256 x 256 output tiles per workgroup over row chunks, transposed LDS reads, partials through
+ * the split-K reduce): taken by default where it applies; ALIGNN_GEMM_NOWGRAD never.  For tests and A/B. */
+#define ALIGNN_GEMM_NOWGRAD 262144
 
 int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 
@@ -120,8 +124,8 @@ int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
 int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
 
 /* Which kernel alignn_gemm_f32 takes (host query, no GPU work): 0 tiled, 1 the bf16 streaming
- * kernel (ALIGNN_GEMM_NOSTREAM), 2 the bf16 row-streaming kernel (ALIGNN_GEMM_NOROWS), -1 invalid
- * arguments. */
+ * kernel (ALIGNN_GEMM_NOSTREAM), 2 the bf16 row-streaming kernel (ALIGNN_GEMM_NOROWS), 3 the bf16
+ * weight-gradient kernel (ALIGNN_GEMM_NOWGRAD), -1 invalid arguments. */
 int alignn_gemm_path(const AlignnGemmArgs* args);
 
 /* ----------------------------------------------------------------------------------------

@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--precision", default="fp32")
 ap.add_argument("--min-m", type=int, default=0)
+ap.add_argument("--time", action="store_true", help="also time each call alone (HIP events, median of 7) and sort by time")
 a = ap.parse_args()
 torch.manual_seed(0)
 model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to("cuda")
@@ -28,12 +29,36 @@ tr.forward_backward(b, 2)
 torch.cuda.synchronize()
 calls, ops.GEMM_TRACE = ops.GEMM_TRACE, None
 bf = ops.GEMM_BF16 if a.precision == "bf16" else 0
+rows = []
 for i, c in enumerate(calls):
     if c["A"].size(-2) < a.min_m:
         continue
-    kw = {k: c[k] for k in ("alpha", "beta", "bias", "rowscale", "bias2", "relu", "mask", "reduce_batch", "c_rows")}
+    kw = {k: c[k] for k in ("alpha", "beta", "bias", "rowscale", "bias2", "relu", "mask", "reduce_batch", "c_rows",
+                            "rowsum")}
     path = ops.gemm(c["A"], c["B"], c["C"], tile=bf, path_only=True, **kw)
-    print(f"{i:3d} path={path} A{tuple(c['A'].shape)}{tuple(c['A'].stride())} B{tuple(c['B'].shape)}{tuple(c['B'].stride())} "
-          f"C{tuple(c['C'].shape)}{tuple(c['C'].stride())} beta={c['beta']} bias={c['bias'] is not None} relu={c['relu']} "
-          f"mask={None if c['mask'] is None else tuple(c['mask'].stride())} rows={c['c_rows'] is not None} "
-          f"rowscale={c['rowscale'] is not None} Cal16={c['C'].data_ptr() % 16 == 0} Aal16={c['A'].data_ptr() % 16 == 0}")
+    us = 0.0
+    if a.time:
+        C = c["C"].clone() if c["beta"] == 0 else c["C"]
+        rs = kw.pop("rowsum")
+        rs = rs.clone() if rs is not None else None
+        ts = []
+        for _ in range(8):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.gemm(c["A"], c["B"], C, tile=bf, rowsum=rs, **kw)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        us = sorted(ts[1:])[3]
+        kw["rowsum"] = rs
+    dt = "".join(n for t, n in ((c["A"], "A"), (c["B"], "B"), (c["C"], "C")) if t.dtype == torch.bfloat16)
+    rows.append((us, f"{i:3d} {us:8.1f}us path={path} A{tuple(c['A'].shape)}{tuple(c['A'].stride())} "
+                     f"B{tuple(c['B'].shape)}{tuple(c['B'].stride())} C{tuple(c['C'].shape)}{tuple(c['C'].stride())} "
+                     f"bf16[{dt}] beta={c['beta']} bias={c['bias'] is not None} relu={c['relu']} "
+                     f"mask={None if c['mask'] is None else tuple(c['mask'].stride())} rows={c['c_rows'] is not None} "
+                     f"rowscale={c['rowscale'] is not None} rowsum={c['rowsum'] is not None} rb={c['reduce_batch']}"))
+if a.time:
+    rows.sort(key=lambda r: -r[0])
+    print(f"total {sum(r[0] for r in rows):.1f} us over {len(rows)} calls")
+for _, line in rows:
+    print(line)

@@ -64,6 +64,19 @@ for step in "$@"; do
          for i in 1 2; do run c2_new$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
            ALIGNN_HIP_LIB=$PWD/abl/libnpf2.so run c2_npf2_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline; done
          for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    gtrace) run gtrace_c3 300 python tools/gemm_trace.py --batch 256 --precision bf16 --time
+           run gtrace_c2 300 python tools/gemm_trace.py --batch 32 --precision fp32 --time
+           head -30 $O/gtrace_c3.log; head -30 $O/gtrace_c2.log ;;
+    wgrad) run t_wgrad 300 "${PT[@]}" tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_x_round5.py -k "wgrad or rowsum"
+           run gtrace_c3 300 python tools/gemm_trace.py --batch 256 --precision bf16 --time
+           head -16 $O/gtrace_c3.log | cut -c1-200
+           for i in 1 2; do run c3_w$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+             ALIGNN_GEMM_WGRAD=0 run c3_nw$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done
+           for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    wgradab) for i in 1 2; do for w in 256 128 64 off; do
+             if [ $w = off ]; then ALIGNN_GEMM_WGRAD=0 run c3_w${w}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+             else ALIGNN_WGRAD_WGS=$w run c3_w${w}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; fi; done; done
+           for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
