@@ -77,6 +77,13 @@ for step in "$@"; do
              if [ $w = off ]; then ALIGNN_GEMM_WGRAD=0 run c3_w${w}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
              else ALIGNN_WGRAD_WGS=$w run c3_w${w}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; fi; done; done
            for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    sw) run t_sw 400 "${PT[@]}" tests/test_gpu_x_lg3.py tests/test_gpu_x_recompute.py tests/test_gpu_parity.py
+        run lgx_sw 300 python tools/lgx_bench.py --batch 32
+        ALIGNN_LG3_SW=1 run lgx_sw1 300 python tools/lgx_bench.py --batch 32
+        grep -h '^{' $O/lgx_sw.log $O/lgx_sw1.log | cut -c1-400
+        for i in 1 2; do for w in 4 2 1; do
+          ALIGNN_LG3_SW=$w run c2_sw${w}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline; done; done
+        for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
