@@ -429,7 +429,7 @@ static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
 }
 
 // The row-streaming kernel (gemm_rows.hip): bf16 arithmetic, K <= 256 (K % 4, % 8 for bf16 A), N a
-// multiple of 256, batch 1, no split / row scatter / rowscale / rowsum, A k-contiguous 16-byte rows,
+// multiple of 256, batched without batch reduction (and then no mask), no split / row scatter / rowscale / rowsum, A k-contiguous 16-byte rows,
 // fp32 W, row-major C / mask with 32-bit byte offsets; taken from ALIGNN_GEMM_ROWS_MIN_M rows up
 // (read once; default 4096), at any M on request (ALIGNN_GEMM_ROWS), never with ALIGNN_GEMM_NOROWS.
 // C3 step, same box (profiles/r05/v5_ab_gemm_rows.txt): 20,658 / 20,742 graphs/s without it,
@@ -445,9 +445,10 @@ static int64_t rows_min_m() {
 static bool rows_ok(const AlignnGemmArgs* a, int split) {
   if (a->rowsum || a->c_rows || a->rowscale) return false;
   if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOROWS) || (a->tile & 15) != 0) return false;
-  if (a->batch != 1 || a->reduce_batch || split != 1) return false;
+  if (a->reduce_batch || split != 1 || (a->batch > 1 && a->mask)) return false;
   const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, cbf = (a->tile & ALIGNN_GEMM_C_BF16) != 0;
   if (a->tile & ALIGNN_GEMM_B_BF16) return false;
+  if (a->batch > 1 && (a->sab % (abf ? 8 : 4) || a->scb % 4)) return false;   // 16-byte aligned batch entries
   if (a->K < 1 || a->K > 256 || a->K % (abf ? 8 : 4) != 0) return false;
   if (a->N % 256 != 0 || a->M < ((a->tile & ALIGNN_GEMM_ROWS) ? 1 : rows_min_m())) return false;
   if (a->sak != 1 || a->sam % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
@@ -460,10 +461,11 @@ static bool rows_ok(const AlignnGemmArgs* a, int split) {
 }
 
 // The weight-gradient kernel (gemm_wgrad.hip): bf16 arithmetic, A = dY^T and B = X both stored
-// row-major over the long K axis (sam == 1, sbn == 1; 16-byte rows), K >= 4096, batch 1, no split
+// row-major over the long K axis (sam == 1, sbn == 1; 16-byte rows), K >= 4096, batched or not (no
+// batch reduction), no split
 // request / row scatter / rowscale, M and N multiples of 4 (8 for bf16 storage) and >= 8; its partials
 // go through the split-K workspace and reduce.  ALIGNN_GEMM_NOWGRAD turns it off (tests, A/B).
-int64_t gemm_wgrad_split(int64_t M, int64_t N, int64_t K, int cus, int64_t* rows_per);
+int64_t gemm_wgrad_split(int64_t M, int64_t N, int64_t K, int64_t batch, int cus, int64_t* rows_per);
 void gemm_wgrad_launch(const GemmParams& p, int64_t S, int64_t rows_per, hipStream_t s);
 static bool wgrad_ok(const AlignnGemmArgs* a) {
   static const bool env_off = [] {   // ALIGNN_GEMM_WGRAD=0 in the environment (read once): off (A/B)
@@ -472,9 +474,12 @@ static bool wgrad_ok(const AlignnGemmArgs* a) {
   }();
   if (env_off || !(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOWGRAD) || (a->tile & 15) != 0) return false;
   if (a->tile & (ALIGNN_GEMM_BK16 | ALIGNN_GEMM_BK32 | ALIGNN_GEMM_BK64)) return false;
-  if (a->batch != 1 || a->reduce_batch || a->split_k > 0 || a->c_rows || a->rowscale || a->mask) return false;
+  if (a->reduce_batch || a->split_k > 0 || a->c_rows || a->rowscale || a->mask) return false;
   const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, bbf = (a->tile & ALIGNN_GEMM_B_BF16) != 0;
-  if (a->K < 4096 || a->M < 8 || a->N < 8 || a->M % (abf ? 8 : 4) || a->N % (bbf ? 8 : 4)) return false;
+  if (a->batch > 1 && (a->sab % (abf ? 8 : 4) || a->sbb % (bbf ? 8 : 4))) return false;   // 16-byte aligned entries
+  // M >= 128: the per-head dM products (M = 64, batch 4) ran slower here than tiled (45-50 vs 38 us,
+  // profiles/r05/v10_ab_gemm_batched.txt) — a 256-row output tile three-quarters empty
+  if (a->K < 4096 || a->M < 128 || a->N < 8 || a->M % (abf ? 8 : 4) || a->N % (bbf ? 8 : 4)) return false;
   if (a->sam != 1 || a->sak < a->M || a->sak % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
   if (a->sbn != 1 || a->sbk < a->N || a->sbk % (bbf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->B) & 15)) return false;
   return true;
@@ -517,8 +522,8 @@ extern "C" int64_t alignn_gemm_workspace(const AlignnGemmArgs* a) {
   if (!plan_args(a, pl, ktot, nb)) return -1;
   if (wgrad_ok(a)) {
     int64_t rp;
-    const int64_t S = gemm_wgrad_split(a->M, a->N, a->K, device_cus(), &rp);
-    return S * a->M * a->N + (a->rowsum ? S * a->M : 0);
+    const int64_t S = gemm_wgrad_split(a->M, a->N, a->K, a->batch, device_cus(), &rp);
+    return S * a->batch * a->M * a->N + (a->rowsum ? S * a->M : 0);
   }
   return pl.split > 1 ? (int64_t)pl.split * nb * a->M * a->N + (a->rowsum ? (int64_t)pl.split * a->M : 0) : 0;
 }
@@ -592,8 +597,8 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   }
   if (wgrad_ok(a)) {
     int64_t rp;
-    const int64_t S = gemm_wgrad_split(a->M, a->N, a->K, device_cus(), &rp);
-    const int64_t need = S * a->M * a->N + (a->rowsum ? S * a->M : 0);
+    const int64_t S = gemm_wgrad_split(a->M, a->N, a->K, a->batch, device_cus(), &rp);
+    const int64_t need = S * a->batch * a->M * a->N + (a->rowsum ? S * a->M : 0);
     if (!a->workspace || a->workspace_elems < need) {
       set_error("gemm: the weight-gradient kernel needs %lld workspace floats", (long long)need);
       return ALIGNN_E_WORKSPACE;
@@ -601,7 +606,7 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
     p.split_k = (int)S;
     gemm_wgrad_launch(p, S, rp, s);
     ALIGNN_LAUNCH_CHECK("wgrad_kernel");
-    const int64_t total = a->M * a->N + (a->rowsum ? a->M : 0);
+    const int64_t total = a->batch * a->M * a->N + (a->rowsum ? a->M : 0);
     launch(splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");
     return ALIGNN_OK;

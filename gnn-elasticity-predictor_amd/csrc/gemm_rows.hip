@@ -11,9 +11,9 @@
 // bands (double-buffered bf16 [32][KT + 8]) and the waves' 32 x 36 epilogue tiles (72 KB), and the
 // CU runs 8 waves (2 per SIMD) instead of 4.
 //
-// Work: a persistent grid of G workgroups (one per CU, a multiple of the N / 256 column slices);
-// workgroup g serves slice g % nslices and 32-row bands q, q + Q, ... (q = g / nslices, Q = G /
-// nslices).  Two register sets hold the next two bands' A rows (16-byte loads, two bands in flight
+// Work: a persistent grid of G workgroups (one per CU, a multiple of the batch x N / 256 work items:
+// batch entry, 256-column slice); workgroup g serves item g % items and 32-row bands q, q + Q, ...
+// (q = g / items, Q = G / items).  Two register sets hold the next two bands' A rows (16-byte loads, two bands in flight
 // per CU); per band the set loaded two bands earlier is rounded to bf16 (RNE) into the other LDS
 // image, and each wave runs KT/16 v_mfma_f32_32x32x16_bf16 (the A operand — band rows l32, k = 16 t
 // + 8 h + j — read one slice ahead) and writes its 32 x 32 block through its LDS tile as 16-byte row
@@ -88,15 +88,24 @@ struct Band {
 // BKC: W given k-contiguous (W^T, sbk == 1, 16-byte aligned rows, K % 8 == 0): two 16-byte loads per
 // operand; else element loads (W row-major: the wave's lanes read consecutive columns at each k).
 template <int KT, bool ABF, bool CBF, bool BETA, bool MASK, bool BKC>
-__global__ __launch_bounds__(NT, 1) void gemm_rows_kernel(GemmParams p, int nslices, int64_t nbands) {
+__global__ __launch_bounds__(NT, 1) void gemm_rows_kernel(GemmParams p, int nitems, int nsl, int64_t nbands) {
   static_assert(!(CBF && BETA), "bf16 C is write-only");
   constexpr int KP = KT + 8, T = KT / 16;
   __shared__ __attribute__((aligned(16))) __bf16 As[2][ROWS * KP];
   __shared__ __attribute__((aligned(16))) float Lepi[NT / 64][ROWS * EPI_LD];
   __shared__ __attribute__((aligned(16))) float Lbias[NB];
+  // work item (batch entry b, column slice z) = g % nitems; batched products (the per-head U / Vd
+  // products, batch = heads) offset the operands per entry
   const int g = blockIdx.x;
-  const int z = g % nslices, q = g / nslices, Q = gridDim.x / nslices;
+  const int item = g % nitems, q = g / nitems, Q = gridDim.x / nitems;
+  const int z = item % nsl, b = item / nsl;
   const int64_t n0 = (int64_t)z * NB;
+  if (b > 0) {
+    p.A = eoff(p.A, b * p.sab, ABF);
+    p.B += b * p.sbb;
+    p.C = const_cast<float*>(eoff(p.C, b * p.scb, CBF));
+    if (p.bias) p.bias += b * p.sbias_b;
+  }
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int l32 = lane & 31, h = lane >> 5;
   const bool has_bias = p.bias != nullptr;
@@ -226,44 +235,45 @@ __global__ __launch_bounds__(NT, 1) void gemm_rows_kernel(GemmParams p, int nsli
 }
 
 template <int KT, bool ABF, bool CBF, bool BKC>
-static void launch_kt(const GemmParams& p, dim3 grid, int nslices, int64_t nbands, hipStream_t s) {
+static void launch_kt(const GemmParams& p, dim3 grid, int nslices, int nsl, int64_t nbands, hipStream_t s) {
   const bool beta = p.beta != 0.f, mask = p.mask != nullptr;
   if constexpr (CBF) {
-    launch(gemm_rows_kernel<KT, ABF, true, false, false, BKC>, grid, dim3(NT), 0, s, p, nslices, nbands);
+    launch(gemm_rows_kernel<KT, ABF, true, false, false, BKC>, grid, dim3(NT), 0, s, p, nslices, nsl, nbands);
   } else {
-    if (beta && mask) launch(gemm_rows_kernel<KT, ABF, false, true, true, BKC>, grid, dim3(NT), 0, s, p, nslices, nbands);
-    else if (beta) launch(gemm_rows_kernel<KT, ABF, false, true, false, BKC>, grid, dim3(NT), 0, s, p, nslices, nbands);
-    else if (mask) launch(gemm_rows_kernel<KT, ABF, false, false, true, BKC>, grid, dim3(NT), 0, s, p, nslices, nbands);
-    else launch(gemm_rows_kernel<KT, ABF, false, false, false, BKC>, grid, dim3(NT), 0, s, p, nslices, nbands);
+    if (beta && mask) launch(gemm_rows_kernel<KT, ABF, false, true, true, BKC>, grid, dim3(NT), 0, s, p, nslices, nsl, nbands);
+    else if (beta) launch(gemm_rows_kernel<KT, ABF, false, true, false, BKC>, grid, dim3(NT), 0, s, p, nslices, nsl, nbands);
+    else if (mask) launch(gemm_rows_kernel<KT, ABF, false, false, true, BKC>, grid, dim3(NT), 0, s, p, nslices, nsl, nbands);
+    else launch(gemm_rows_kernel<KT, ABF, false, false, false, BKC>, grid, dim3(NT), 0, s, p, nslices, nsl, nbands);
   }
 }
 
 template <int KT, bool BKC>
-static void launch_k(const GemmParams& p, dim3 grid, int nslices, int64_t nbands, hipStream_t s) {
-  if (p.abf && p.cbf) launch_kt<KT, true, true, BKC>(p, grid, nslices, nbands, s);
-  else if (p.abf) launch_kt<KT, true, false, BKC>(p, grid, nslices, nbands, s);
-  else if (p.cbf) launch_kt<KT, false, true, BKC>(p, grid, nslices, nbands, s);
-  else launch_kt<KT, false, false, BKC>(p, grid, nslices, nbands, s);
+static void launch_k(const GemmParams& p, dim3 grid, int nslices, int nsl, int64_t nbands, hipStream_t s) {
+  if (p.abf && p.cbf) launch_kt<KT, true, true, BKC>(p, grid, nslices, nsl, nbands, s);
+  else if (p.abf) launch_kt<KT, true, false, BKC>(p, grid, nslices, nsl, nbands, s);
+  else if (p.cbf) launch_kt<KT, false, true, BKC>(p, grid, nslices, nsl, nbands, s);
+  else launch_kt<KT, false, false, BKC>(p, grid, nslices, nsl, nbands, s);
 }
 
 }  // namespace rsk
 
 // Shapes (host check, gemm.hip rows_ok): bf16 arithmetic, K <= 256 (K % 4 == 0, % 8 for bf16 A),
-// N % 256 == 0, batch 1, no split / row scatter / rowscale / rowsum, A k-contiguous 16-byte rows,
+// N % 256 == 0, batched without batch reduction (no mask then), no split / row scatter / rowscale / rowsum, A k-contiguous 16-byte rows,
 // fp32 B, row-major C and mask with 32-bit byte offsets.
 void gemm_rows_launch(const GemmParams& p, int cus, hipStream_t s) {
-  const int nslices = (int)(p.N / rsk::NB);
+  const int nsl = (int)(p.N / rsk::NB);
+  const int nslices = nsl * (int)p.batch;   // work items: (batch entry, column slice)
   const int64_t nbands = (p.M + rsk::ROWS - 1) / rsk::ROWS;
   const int64_t items = (int64_t)nslices * nbands;
   const int G = (int)(std::min<int64_t>((int64_t)cus, items) / nslices * nslices);
   const dim3 grid((unsigned)std::max(G, nslices));
   const bool bkc = p.sbk == 1 && p.vecB && p.K % 8 == 0;
   if (p.K <= 64) {
-    if (bkc) rsk::launch_k<64, true>(p, grid, nslices, nbands, s);
-    else rsk::launch_k<64, false>(p, grid, nslices, nbands, s);
+    if (bkc) rsk::launch_k<64, true>(p, grid, nslices, nsl, nbands, s);
+    else rsk::launch_k<64, false>(p, grid, nslices, nsl, nbands, s);
   } else {
-    if (bkc) rsk::launch_k<256, true>(p, grid, nslices, nbands, s);
-    else rsk::launch_k<256, false>(p, grid, nslices, nbands, s);
+    if (bkc) rsk::launch_k<256, true>(p, grid, nslices, nsl, nbands, s);
+    else rsk::launch_k<256, false>(p, grid, nslices, nsl, nbands, s);
   }
 }
 

@@ -109,6 +109,11 @@ __global__ __launch_bounds__(NT, 1) void wgrad_kernel(GemmParams p, int64_t rows
   const int64_t tiles_n = (p.N + TN - 1) / TN;
   const int64_t m0 = (blockIdx.x / tiles_n) * TM, n0 = (blockIdx.x % tiles_n) * TN;
   const int s = blockIdx.y;
+  const int64_t bz = blockIdx.z;   // batch entry (the per-head dM products: batch = heads)
+  if (bz > 0) {
+    p.A = eoff(p.A, bz * p.sab, ABF);
+    p.B = eoff(p.B, bz * p.sbb, BBF);
+  }
   const int64_t r0 = (int64_t)s * rows_per, rend = min(p.K, r0 + rows_per);
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad_kernel(GemmParams p, int64_t rows
   }
 
   // partial tile -> split-K workspace [s][M][N] (rows and columns past M / N dropped)
-  float* W = p.ws + (int64_t)s * p.M * p.N;
+  float* W = p.ws + ((int64_t)s * p.batch + bz) * p.M * p.N;   // the split-K workspace layout [s][b][M][N]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -199,12 +204,12 @@ __global__ __launch_bounds__(NT, 1) void wgrad_kernel(GemmParams p, int64_t rows
 // the critical path's attention and dX products, so half the CUs is the better share: C3 step, same
 // box (profiles/r05/v8_ab_gemm_wgrad.txt), 256 workgroups 21,702 / 21,907 graphs/s, 128 22,164 /
 // 22,424, 64 22,231 / 22,272, the tiled kernel instead 22,054 / 21,718.
-int64_t gemm_wgrad_split(int64_t M, int64_t N, int64_t K, int cus, int64_t* rows_per) {
+int64_t gemm_wgrad_split(int64_t M, int64_t N, int64_t K, int64_t batch, int cus, int64_t* rows_per) {
   static const int64_t target_env = [] {
     const char* e = std::getenv("ALIGNN_WGRAD_WGS");
     return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(0);
   }();
-  const int64_t tiles = ((M + wgk::TM - 1) / wgk::TM) * ((N + wgk::TN - 1) / wgk::TN);
+  const int64_t tiles = ((M + wgk::TM - 1) / wgk::TM) * ((N + wgk::TN - 1) / wgk::TN) * batch;
   const int64_t target = target_env ? target_env : std::max<int64_t>(1, cus / 2);
   int64_t S = std::max<int64_t>(1, target / tiles);
   int64_t rp = (K + S - 1) / S;
@@ -216,7 +221,7 @@ int64_t gemm_wgrad_split(int64_t M, int64_t N, int64_t K, int cus, int64_t* rows
 
 void gemm_wgrad_launch(const GemmParams& p, int64_t S, int64_t rows_per, hipStream_t s) {
   const int64_t tiles = ((p.M + wgk::TM - 1) / wgk::TM) * ((p.N + wgk::TN - 1) / wgk::TN);
-  const dim3 grid((unsigned)tiles, (unsigned)S);
+  const dim3 grid((unsigned)tiles, (unsigned)S, (unsigned)p.batch);
   if (p.abf && p.bbf) launch(wgk::wgrad_kernel<true, true>, grid, dim3(wgk::NT), 0, s, p, rows_per);
   else if (p.abf) launch(wgk::wgrad_kernel<true, false>, grid, dim3(wgk::NT), 0, s, p, rows_per);
   else if (p.bbf) launch(wgk::wgrad_kernel<false, true>, grid, dim3(wgk::NT), 0, s, p, rows_per);

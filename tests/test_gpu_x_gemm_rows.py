@@ -107,3 +107,27 @@ def test_rows_kernel_routing_and_untouched_rows():
     ops.gemm(A[:4100], W, buf[:4100], tile=BF)
     torch.cuda.synchronize()
     assert bool((buf[4100:] == 7.0).all())
+
+
+@pytest.mark.parametrize("M,lda", [(16020, 768), (15360, 256)])
+@pytest.mark.parametrize("a16", [False, True])
+def test_rows_kernel_batched_per_head_products(M, lda, a16):
+    """The per-head products U_h = Q_h M_h / Vd_h = dout_h M_h (batch = 4 heads, K = 64 columns of a
+    wider row, W = M_h row-major [64, 256], C rows of [n, H, D]): each batch entry its own operands."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(M + lda)
+    X = torch.randn(M, lda, generator=g).to(DEV)
+    if a16:
+        X = X.bfloat16()
+    A = X[:, :256].view(M, 4, 64).transpose(0, 1)            # (4, M, 64), strides (64, lda, 1)
+    Mh = (torch.randn(4, 64, 256, generator=g) * 0.1).to(DEV)
+    C = torch.full((M, 4, 256), float("nan"), device=DEV)
+    Ct = torch.full((M, 4, 256), float("nan"), device=DEV)
+    with ops.gemm_precision("bf16"):
+        assert ops.gemm(A, Mh, C.transpose(0, 1), path_only=True) == 2
+        ops.gemm(A, Mh, C.transpose(0, 1))
+        ops.gemm(A, Mh, Ct.transpose(0, 1), tile=ops.GEMM_NOROWS | ops.GEMM_NOSTREAM)
+    torch.cuda.synchronize()
+    ref = torch.einsum("bmk,bkn->mbn", A.bfloat16().double(), Mh.bfloat16().double())
+    assert _rel(C, ref) < 5e-6
+    assert torch.equal(C, Ct)

@@ -69,7 +69,32 @@ def test_wgrad_kernel_epilogue_and_routing():
         assert ops.gemm(dY.t().contiguous(), X, C, path_only=True) == 0           # A k-contiguous
         assert ops.gemm(dY.t(), X, C, mask=C0, path_only=True) == 0
         assert ops.gemm(dY.t(), X, C, split_k=8, path_only=True) == 0
+        assert ops.gemm(dY.t()[:64], X, C[:64], path_only=True) == 0                 # M < 128
     assert ops.gemm(dY.t(), X, C, path_only=True) == 0                             # fp32 arithmetic
     torch.cuda.synchronize()
     ref = 0.5 * (dY.bfloat16().double().t() @ X.bfloat16().double()) + 2.0 * C0.double() + bias.double()
     assert _rel(C, ref) < 1e-5
+
+
+@pytest.mark.parametrize("K,ldq", [(16020, 768), (15360, 1024), (16020, 512)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_wgrad_kernel_batched_per_head_dM(K, ldq, beta):
+    """Batched products (batch = 4 heads, one head's columns of a wider row, N = 256, K = the
+    targets), as the per-head edge-projection gradients dM_h = Q_h^T Sz_h (+ dout_h^T S_h, beta = 1)
+    with M = 128 (the step's M = 64 ones stay tiled: slower here)."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(K + ldq)
+    Q = torch.randn(K, ldq, generator=g).to(DEV)
+    Sz = torch.randn(K, 4, 256, generator=g).to(DEV)
+    A = Q[:, :512].view(K, 4, 128).permute(1, 2, 0)             # (4, 128, K), strides (128, 1, ldq)
+    B = Sz.transpose(0, 1)                                      # (4, K, 256), strides (256, 1024, 1)
+    C0 = torch.randn(4, 128, 256, generator=g).to(DEV)
+    C, Ct = C0.clone(), C0.clone()
+    with ops.gemm_precision("bf16"):
+        assert ops.gemm(A, B, C, beta=beta, path_only=True) == 3
+        ops.gemm(A, B, C, beta=beta)
+        ops.gemm(A, B, Ct, beta=beta, tile=ops.GEMM_NOWGRAD)
+    torch.cuda.synchronize()
+    ref = torch.einsum("bmk,bkn->bmn", A.bfloat16().double(), B.bfloat16().double()) + beta * C0.double()
+    tol = 2e-6 * max(1.0, (K / 1000) ** 0.5)
+    assert _rel(C, ref) < tol and _rel(C, Ct) < tol

@@ -84,6 +84,18 @@ for step in "$@"; do
         for i in 1 2; do for w in 4 2 1; do
           ALIGNN_LG3_SW=$w run c2_sw${w}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline; done; done
         for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    batched) run t_batched 400 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_x_bf16_stream.py tests/test_gpu_x_round5.py
+           run gtrace_c3 300 python tools/gemm_trace.py --batch 256 --precision bf16 --time
+           head -3 $O/gtrace_c3.log | cut -c1-120
+           for i in 1 2; do run c3_new$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+             ALIGNN_HIP_LIB=$PWD/abl/libprev.so run c3_prev$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done
+           for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    batched2) run t_b2 400 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_gemm_wgrad.py
+           for i in 1 2; do run c3_new$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+             ALIGNN_HIP_LIB=$PWD/abl/libprev.so run c3_prev$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done
+           for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done
+           run bench 600 python bench.py
+           tail -1 $O/bench.log ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
