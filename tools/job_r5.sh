@@ -96,6 +96,20 @@ for step in "$@"; do
            for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done
            run bench 600 python bench.py
            tail -1 $O/bench.log ;;
+    evid) cd /tmp && export TMPDIR=/tmp
+          B3="--steps 3 --warmup 2 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline"
+          B2="--steps 5 --warmup 2 --no-secondary --e2e 0 --no-cpu-baseline"
+          for c in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL 420 rocprofv3 --pmc $c --kernel-trace -d $O/pmc_c3_$c -o run --output-format csv -- python $OLDPWD/bench.py $B3 > $O/pmc_c3_$c.log 2>&1 || exit 1
+            timeout -s KILL 420 rocprofv3 --pmc $c --kernel-trace -d $O/pmc_c2_$c -o run --output-format csv -- python $OLDPWD/bench.py $B2 > $O/pmc_c2_$c.log 2>&1 || exit 1
+          done
+          timeout -s KILL 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_c3_mf -o run --output-format csv -- python $OLDPWD/bench.py $B3 > $O/pmc_c3_mf.log 2>&1 || exit 1
+          timeout -s KILL 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_c2_mf -o run --output-format csv -- python $OLDPWD/bench.py $B2 > $O/pmc_c2_mf.log 2>&1 || exit 1
+          cd $OLDPWD
+          for c in c2 c3; do
+            python tools/pmc_traffic.py $O/pmc_${c}_FETCH_SIZE $O/pmc_${c}_WRITE_SIZE --json $O/pmc_${c}_traffic.json --top 40 > $O/pmc_${c}_traffic.txt
+            python tools/pmc_mfma.py $O/pmc_${c}_mf > $O/pmc_${c}_mfma.txt; done
+          head -12 $O/pmc_c3_traffic.txt; head -12 $O/pmc_c2_traffic.txt ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1

@@ -50,8 +50,9 @@ def main():
                      "total_us": t * 1e6 * len(v)})
     rows.sort(key=lambda r: -r["total_us"])
     for r in rows[: a.top]:
-        print(f"{r['total_us']:9.0f}us n={r['launches']:4d} grid={r['grid']:9d} fetch={r['fetch_bytes']/1e6:9.1f}MB "
-              f"write={r['write_bytes']/1e6:8.1f}MB  {r['kernel'][:90]}")
+        print(f"{r['total_us']:9.0f}us n={r['launches']:4d} avg={r['avg_us_under_counters']:8.1f}us grid={r['grid']:9d} "
+              f"fetch={r['fetch_bytes']/1e6:9.1f}MB write={r['write_bytes']/1e6:8.1f}MB "
+              f"{(r['fetch_bytes'] + r['write_bytes']) / r['avg_us_under_counters'] / 1e6:6.2f}TB/s  {r['kernel'][:90]}")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rows, f, indent=1)
