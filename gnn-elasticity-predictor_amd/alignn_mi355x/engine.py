@@ -832,13 +832,10 @@ class AlignnEngine:
         ops.gemm(h1, W2.t(), out, bias=b2)
         return h1, out
 
-    def _mlp_bwd(self, dout, x, h1, W2, gW1, gb1, gW2, gb2, beside_side: bool = False):
+    def _mlp_bwd(self, dout, x, h1, W2, gW1, gb1, gW2, gb2):
         ops.gemm(dout.t(), h1, gW2, rowsum=gb2)   # the bias gradient from the same launch
         dh1 = torch.empty_like(h1)
-        # beside the deferred angle-encoder backward (side stream) the masked dX product takes the
-        # tiled kernels: the bf16 streaming GEMM needs a whole CU's LDS, so it waited for enc_bwd to
-        # drain (C3: 1,212 us for a 150 us product)
-        ops.gemm(dout, W2, dh1, mask=h1, tile=ops.GEMM_NOSTREAM if beside_side else 0)
+        ops.gemm(dout, W2, dh1, mask=h1)
         ops.gemm(dh1.t(), x, gW1, rowsum=gb1)
 
     def forward(self, P: FlatViews, batch, bc: BatchCache, training: bool, seed: int = 0,
@@ -1152,11 +1149,9 @@ class AlignnEngine:
                     ops.colsum(da, G.enc("angle", 0, "bias"))
         if ctx.h1e is not None:
             self._mlp_bwd(de, ctx.edge_attr, ctx.h1e, P.enc("edge", 2, "weight"), G.enc("edge", 0, "weight"),
-                          G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"),
-                          beside_side=side is not None)
+                          G.enc("edge", 0, "bias"), G.enc("edge", 2, "weight"), G.enc("edge", 2, "bias"))
         self._mlp_bwd(dh, ctx.x, ctx.h1n, P.enc("node", 2, "weight"), G.enc("node", 0, "weight"),
-                      G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"),
-                      beside_side=side is not None)
+                      G.enc("node", 0, "bias"), G.enc("node", 2, "weight"), G.enc("node", 2, "bias"))
         if side is not None:
             ops.stream_wait(torch.cuda.current_stream(dev), side)  # join: every gradient is written
         if aux is not None:

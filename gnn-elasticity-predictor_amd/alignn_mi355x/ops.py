@@ -348,9 +348,7 @@ GEMM_TRACE: Optional[list] = None
 _GEMM_FLAGS = 0       # ORed into AlignnGemmArgs.tile by gemm() (gemm_precision)
 GEMM_BF16 = 64        # ALIGNN_GEMM_BF16
 GEMM_NOPIPE = 256     # ALIGNN_GEMM_NOPIPE: force the one-stage-in-flight loop (A/B tests)
-GEMM_NOSTREAM = 512   # ALIGNN_GEMM_NOSTREAM: bf16 products never take the streaming kernel (A/B tests)
 GEMM_A_BF16, GEMM_B_BF16, GEMM_C_BF16 = 1024, 2048, 4096   # bf16 storage of an operand / the output
-GEMM_STREAM = 8192    # ALIGNN_GEMM_STREAM: the streaming kernel's row floor 32768 -> 4096 (tests / A/B)
 GEMM_LDS16 = 16384    # ALIGNN_GEMM_LDS16: bf16 tiled products through bf16 LDS images (forced on; default: A k-contiguous)
 GEMM_NOLDS16 = 32768  # ALIGNN_GEMM_NOLDS16: ... forced off (A/B tests)
 GEMM_ROWS = 65536     # ALIGNN_GEMM_ROWS: the bf16 row-streaming kernel at any M (tests / A/B)
@@ -448,8 +446,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, alpha: float = 1.
     if io and not ((_GEMM_FLAGS | int(tile)) & GEMM_BF16):
         raise ValueError("gemm: bf16 operands need bf16 arithmetic (ops.gemm_precision('bf16'))")
     a.tile = int(tile) | _GEMM_FLAGS | io
-    if path_only:   # the kernel the library takes (0 tiled, 1 bf16 streaming, 2 bf16 row-streaming, 3 bf16
-        #             weight-gradient); nothing runs
+    if path_only:   # the kernel the library takes (0 tiled, 2 bf16 row-streaming, 3 bf16 weight-gradient);
+        #             nothing runs
         return int(_lib.lib().alignn_gemm_path(ctypes.byref(a)))
     need = int(_lib.lib().alignn_gemm_workspace(ctypes.byref(a)))
     if need < 0:

@@ -1,5 +1,6 @@
-// gemm.hip — GEMM entry points (alignn_gemm_f32 / _workspace / _path): plan, split-K reduce, the bf16
-// streaming kernel and the column sums.  The tiled kernels live in gemm_tile.h, instantiated per
+// gemm.hip — GEMM entry points (alignn_gemm_f32 / _workspace / _path): plan, routing to the tiled, bf16
+// row-streaming (gemm_rows.hip) and bf16 weight-gradient (gemm_wgrad.hip) kernels, split-K reduce and
+// the column sums.  The tiled kernels live in gemm_tile.h, instantiated per
 // arithmetic in gemm_tile_p0/1.hip.
 #include <cstring>
 
@@ -130,267 +131,7 @@ static bool plan_args(const AlignnGemmArgs* a, GemmPlan& pl, int64_t& ktot, int6
   return true;
 }
 
-// -------------------------------------------------------------------------------------------
-// bf16 streaming GEMM (config C3's large-M products: C[M, N] = act(alpha A W + beta C + bias) with
-// K = 64/128/256, N a multiple of 256, M >= 4096 — every bond / node / line-graph row times a
-// weight).  With bf16 matrix cores these products are bound by HBM (fp32 A in, fp32 C out), which the
-// 64x64-tile kernel reaches only ~40 % of: it re-reads each A row band once per column tile and its
-// 16-deep stages leave the loads exposed.  Here one workgroup per CU keeps a 256-column slice of W
-// as bf16 in LDS ([n][K + 8]: the padding puts a ds_read_b128 lane group on distinct banks) for the
-// kernel's lifetime and streams 64-row bands of A: each wave owns 32 rows x 128 columns (four
-// accumulators), holds its rows' fp32 A values in VGPRs in MFMA operand order (two 16-byte loads per
-// 16-deep slice: k = 16 t + 8 h + j on lane half h), the next band's rows in flight during this
-// band's MFMAs (v_mfma_f32_32x32x16_bf16, inputs rounded to bf16 RNE as in the tiled BF path, fp32
-// accumulation), and writes each 32 x 32 accumulator through a wave-private LDS tile as 16-byte
-// row segments.  Loads and stores are unconditional (rows clamped / buffer descriptors), so the
-// compiler counts outstanding loads instead of draining the prefetch.
-// -------------------------------------------------------------------------------------------
-namespace bst {
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr int NB = 256;          // columns per slice
-constexpr int ROWS = 64;         // rows per band (2 wave rows x 32)
-constexpr int EPI_LD = 36;       // epilogue tile row stride (floats)
-
-template <int KT>
-__device__ __forceinline__ void load_band(gf4 (&a)[KT / 8], const float* __restrict__ Arow, int h) {
-#pragma unroll
-  for (int t = 0; t < KT / 16; ++t) {
-    a[2 * t] = *reinterpret_cast<const gf4*>(Arow + 16 * t + 8 * h);
-    a[2 * t + 1] = *reinterpret_cast<const gf4*>(Arow + 16 * t + 8 * h + 4);
-  }
-  asm volatile("" ::: "memory");  // a prefetch: issued here, not sunk to its first use
-}
-
-// bf16 A rows (ABF): one 16-byte load per 16-deep slice holds the lane half's eight k-values, already
-// the MFMA operand; kept in the first KT / 16 entries of the same register array
-template <int KT>
-__device__ __forceinline__ void load_band_bf(gf4 (&a)[KT / 8], const uint16_t* __restrict__ Arow, int h) {
-#pragma unroll
-  for (int t = 0; t < KT / 16; ++t) a[t] = *reinterpret_cast<const gf4*>(Arow + 16 * t + 8 * h);
-  asm volatile("" ::: "memory");
-}
-
-template <int KT, bool ABF>
-__device__ __forceinline__ void band_mma(floatx16 (&acc)[4], const gf4 (&a)[KT / 8], const __bf16* __restrict__ Bs,
-                                         int col0, int l32, int h) {
-  constexpr int KP = KT + 8;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  const __bf16* Bl = Bs + (col0 + l32) * KP + 8 * h;
-  // W fragments one 16-deep slice ahead: slice t + 1's four LDS reads are in flight during slice t's
-  // MFMAs (one wave per SIMD: nothing else hides an LDS round trip behind a dependent MFMA)
-  bf16x8 hb[2][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) hb[0][j] = *reinterpret_cast<const bf16x8*>(Bl + 32 * j * KP);
-#pragma unroll
-  for (int t = 0; t < KT / 16; ++t) {
-    if (t + 1 < KT / 16) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) hb[(t + 1) & 1][j] = *reinterpret_cast<const bf16x8*>(Bl + 32 * j * KP + 16 * (t + 1));
-    }
-    __builtin_amdgcn_sched_barrier(0);   // the scheduler would sink the reads back next to their MFMAs
-    bf16x8 ha;
-    if constexpr (ABF) {
-      ha = __builtin_bit_cast(bf16x8, a[t]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ha[q] = (__bf16)a[2 * t][q];
-        ha[4 + q] = (__bf16)a[2 * t + 1][q];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha, hb[t & 1][j], acc[j], 0, 0, 0);
-  }
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n, 0x00020000);
-}
-
-// alpha acc (column layout) -> LDS tile -> rows: fma(beta, C, .), + bias, ReLU, mask, 16-byte stores
-// (epilogue_value's order).  Rows past M fall outside the store descriptor and are dropped; beta == 0
-// reads an empty descriptor.
-// The C values band_store's beta term reads, loaded ahead (CPRE: issued before the band's MFMAs, so
-// the read is in flight while they run instead of exposed in the epilogue)
-__device__ __forceinline__ void load_c(gf4 (&c)[16], const GemmParams& p, __amdgpu_buffer_rsrc_t cld, int64_t row0,
-                                       int lane) {
-  const int rr = lane >> 1, cc = (lane & 1) * 16;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * 4);
-      c[4 * j + i] = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
-    }
-  asm volatile("" ::: "memory");
-}
-
-template <bool BETA, bool MASK, bool CBF, bool CPRE = false>
-__device__ __forceinline__ void band_store(const GemmParams& p, const floatx16 (&acc)[4], bool has_bias,
-                                           const float* __restrict__ bptr,
-                                           float* __restrict__ Ls, __amdgpu_buffer_rsrc_t cst,
-                                           __amdgpu_buffer_rsrc_t cld, __amdgpu_buffer_rsrc_t cmk, int64_t row0,
-                                           int l32, int h, int lane, const gf4* cpre = nullptr) {
-  const int rr = lane >> 1, cc = (lane & 1) * 16;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Ls[((r & 3) + 8 * (r >> 2) + 4 * h) * EPI_LD + l32] = __fmul_rn(p.alpha, acc[j][r]);
-    const int bc = 32 * j + cc;   // this lane's 16 output columns start here (bias from LDS-free registers below)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      gf4 v = *reinterpret_cast<const gf4*>(Ls + rr * EPI_LD + cc + 4 * i);
-      const int off = (int)(((row0 + rr) * p.scm + 32 * j + cc + 4 * i) * (CBF ? 2 : 4));
-      if constexpr (BETA) {   // the tiled epilogue's order: fma(beta, C, alpha acc), then + bias
-        const gf4 c = CPRE ? cpre[4 * j + i] : __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, off, 0, 0));
-        v = gf4{fmaf(p.beta, c.x, v.x), fmaf(p.beta, c.y, v.y), fmaf(p.beta, c.z, v.z), fmaf(p.beta, c.w, v.w)};
-      }
-      if (has_bias) {   // bptr: the LDS copy of the wave's bias columns (no global load here, whose wait
-                        // would also drain the next band's A loads in flight)
-        const gf4 bb = *reinterpret_cast<const gf4*>(bptr + bc + 4 * i);
-        v = gf4{__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z), __fadd_rn(v.w, bb.w)};
-      }
-      const gf4 z = {0.f, 0.f, 0.f, 0.f};
-      v = p.relu ? __builtin_elementwise_max(v, z) : v;
-      if constexpr (MASK) {  // ReLU-backward mask: keep v where mask > 0 (the tiled epilogue's rule)
-        const int moff = (int)(((row0 + rr) * p.smk_m + 32 * j + cc + 4 * i) * 4);
-        const gf4 mk = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cmk, moff, 0, 0));
-        v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
-        v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
-      }
-      if constexpr (CBF) {   // bf16 C rows (RNE): four values in 8 bytes
-        const uint32_t lo = (uint32_t)bf_rne(v.x) | ((uint32_t)bf_rne(v.y) << 16);
-        const uint32_t hi = (uint32_t)bf_rne(v.z) | ((uint32_t)bf_rne(v.w) << 16);
-        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, cst, off, 0, 0);
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cst, off, 0, 0);
-      }
-    }
-  }
-}
-
-// grid: G workgroups (<= one per CU), G a multiple of nslices = N / 256; workgroup g serves slice
-// g % nslices and bands q, q + Q, ... (q = g / nslices, Q = G / nslices).
-template <int KT, bool BETA, bool MASK, bool ABF = false, bool CBF = false>
-__global__ __launch_bounds__(256, 1) void gemm_bf16_stream_kernel(GemmParams p, int nslices, int64_t nbands) {
-  static_assert(!(CBF && BETA), "bf16 C is write-only");
-  constexpr int KP = KT + 8;
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[NB * KP];
-  __shared__ __attribute__((aligned(16))) float Lepi[4 * 32 * EPI_LD];
-  __shared__ __attribute__((aligned(16))) float Lbias[NB];
-  const int g = blockIdx.x;
-  const int z = g % nslices, q = g / nslices, Q = gridDim.x / nslices;
-  const int64_t n0 = (int64_t)z * NB;
-  // W slice -> LDS as bf16 [n][k], once (RNE, as the tiled BF path rounds its operands).  KT / 4
-  // float4 per thread, loaded in batches of 16 before any is stored: a load-then-store loop waits one
-  // global round trip per float4 (64 of them at K = 256 — most of a band-streaming launch's time).
-  constexpr int PER = NB * (KT / 4) / 256, CH = 16;
-  static_assert(PER % CH == 0, "prologue batches");
-  const bool kc = p.sbk == 1;   // W^T given (k contiguous): 16-byte loads along k; else along n
-  for (int c0 = 0; c0 < PER; c0 += CH) {
-    gf4 v[CH];
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const int i = threadIdx.x + 256 * (c0 + u);
-      if (kc) {
-        const float* src = p.B + (n0 + i / (KT / 4)) * p.sbn + (i % (KT / 4)) * 4;
-        v[u] = p.vecB ? *reinterpret_cast<const gf4*>(src) : gf4{src[0], src[1], src[2], src[3]};
-      } else {
-        const float* src = p.B + (int64_t)(i / (NB / 4)) * p.sbk + (n0 + (i % (NB / 4)) * 4) * p.sbn;
-        v[u] = (p.sbn == 1 && p.vecB) ? *reinterpret_cast<const gf4*>(src)
-                                       : gf4{src[0], src[p.sbn], src[2 * p.sbn], src[3 * p.sbn]};
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const int i = threadIdx.x + 256 * (c0 + u);
-      if (kc) {
-        __bf16* d = Bs + (i / (KT / 4)) * KP + (i % (KT / 4)) * 4;
-        d[0] = (__bf16)v[u][0]; d[1] = (__bf16)v[u][1]; d[2] = (__bf16)v[u][2]; d[3] = (__bf16)v[u][3];
-      } else {
-        const int k = i / (NB / 4), n = (i % (NB / 4)) * 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Bs[(n + q) * KP + k] = (__bf16)v[u][q];
-      }
-    }
-  }
-  const int lane = threadIdx.x & 63, wave = wave_id();
-  const int l32 = lane & 31, h = lane >> 5;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int col0 = wc * 128;
-  const bool has_bias = p.bias != nullptr;
-  for (int i = threadIdx.x; i < NB; i += 256) Lbias[i] = has_bias ? p.bias[n0 + i] : 0.f;
-  const float* bias = Lbias + col0;   // this wave's 128 columns
-  float* Cw = const_cast<float*>(eoff(p.C, n0 + col0, CBF));
-  const int64_t cbytes = (p.M * p.scm - (n0 + col0)) * (CBF ? 2 : 4);
-  const __amdgpu_buffer_rsrc_t cst = rsrc(Cw, cbytes);
-  const __amdgpu_buffer_rsrc_t cld = rsrc(Cw, (BETA && p.beta != 0.f) ? cbytes : 0);
-  const __amdgpu_buffer_rsrc_t cmk = rsrc(MASK ? p.mask + n0 + col0 : Cw, MASK ? (p.M * p.smk_m - (n0 + col0)) * 4 : 0);
-  float* Ls = Lepi + wave * 32 * EPI_LD;
-  __syncthreads();
-  auto arow = [&](int64_t band) {
-    const int64_t row = min(band * ROWS + wr * 32 + l32, p.M - 1);
-    return eoff(p.A, row * p.sam, ABF);
-  };
-  auto lband = [&](gf4 (&a)[KT / 8], const float* r) {
-    if constexpr (ABF) load_band_bf<KT>(a, reinterpret_cast<const uint16_t*>(r), h);
-    else load_band<KT>(a, r, h);
-  };
-  gf4 a0[KT / 8], a1[KT / 8];
-  floatx16 acc[4];
-  int64_t band = q;
-  if (band >= nbands) return;
-  // bf16 A with a beta term (dX += dR W at C3): the band's C rows are loaded with the band's A rows,
-  // one band ahead, into two more register sets (the bf16 A sets are half as wide: room for them)
-  constexpr bool CPRE = BETA && ABF && !MASK;
-  gf4 c0[CPRE ? 16 : 1], c1[CPRE ? 16 : 1];
-  auto lc = [&](gf4 (&c)[CPRE ? 16 : 1], int64_t b) {
-    if constexpr (CPRE) load_c(c, p, cld, min(b, nbands - 1) * ROWS + wr * 32, lane);
-  };
-  lband(a0, arow(band));
-  lc(c0, band);
-  while (true) {  // two bands per iteration: the register sets keep fixed names
-    const int64_t b1 = band + Q;
-    lband(a1, arow(min(b1, nbands - 1)));
-    lc(c1, b1);
-    band_mma<KT, ABF>(acc, a0, Bs, col0, l32, h);
-    band_store<BETA, MASK, CBF, CPRE>(p, acc, has_bias, bias, Ls, cst, cld, cmk, band * ROWS + wr * 32, l32, h, lane, c0);
-    if (b1 >= nbands) break;
-    const int64_t b2 = b1 + Q;
-    lband(a0, arow(min(b2, nbands - 1)));
-    lc(c0, b2);
-    band_mma<KT, ABF>(acc, a1, Bs, col0, l32, h);
-    band_store<BETA, MASK, CBF, CPRE>(p, acc, has_bias, bias, Ls, cst, cld, cmk, b1 * ROWS + wr * 32, l32, h, lane, c1);
-    if (b2 >= nbands) break;
-    band = b2;
-  }
-}
-
-}  // namespace bst
-
-// The streaming kernel's shapes (host check): bf16 arithmetic, K in {64, 128, 256}, N a multiple of
-// 256, M >= stream_min_m(), A k-contiguous 16-byte rows, no batch / split / batch reduction, epilogue alpha /
-// beta / bias / ReLU into a row-major C with 32-bit byte offsets.
-// Below this many rows the tiled kernels take the product. In isolation the streaming kernel still
-// wins near M = 16k (N = 768: 55 vs 60 us), but it holds one workgroup per CU for the whole product,
-// and inside the C3 plan, with the other streams' kernels resident, a 16k-row product took 235 us
-// where the tiled one fills in around them (profiles/r04). ALIGNN_GEMM_STREAM_MIN_M overrides it for
-// the A/B (read once).
-static int64_t stream_min_m() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("ALIGNN_GEMM_STREAM_MIN_M");
-    return e ? std::max<int64_t>(4096, std::atoll(e)) : int64_t(32768);
-  }();
-  return v;
-}
 
 // bf16 arithmetic through bf16 LDS images (gemm_tile.h arithmetic 2, bitwise equal to 1): forced on /
 // off by ALIGNN_GEMM_LDS16 / ALIGNN_GEMM_NOLDS16; otherwise taken when A is k-contiguous.  C3 sweep
@@ -407,25 +148,6 @@ static bool lds16(const AlignnGemmArgs* a, bool akc) {
   if (a->tile & ALIGNN_GEMM_NOLDS16) return false;
   if (a->tile & ALIGNN_GEMM_LDS16) return true;
   return akc && !env_off;
-}
-
-static bool bf16_stream_ok(const AlignnGemmArgs* a, int split) {
-  if (a->rowsum) return false;
-  if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOSTREAM) || (a->tile & 15) != 0) return false;
-  if (a->batch != 1 || a->reduce_batch || split != 1) return false;
-  if (a->K != 64 && a->K != 128 && a->K != 256) return false;
-  if (a->N % bst::NB != 0 || a->M < ((a->tile & ALIGNN_GEMM_STREAM) ? 4096 : stream_min_m())) return false;
-  const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0, cbf = (a->tile & ALIGNN_GEMM_C_BF16) != 0;
-  if (a->tile & ALIGNN_GEMM_B_BF16) return false;
-  // bf16 A or C: K = 256 instantiations only, no mask; bf16 C without beta (write-only)
-  if ((abf || cbf) && (a->K != 256 || a->mask || (cbf && a->beta != 0.f))) return false;
-  if (a->sak != 1 || a->sam % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
-  if (a->c_rows || a->rowscale || a->scn != 1 || a->scm < a->N) return false;
-  if (a->mask && (a->smk_n != 1 || a->smk_m < a->N || (reinterpret_cast<uintptr_t>(a->mask) & 15) || a->smk_m % 4))
-    return false;
-  if ((a->M + 64) * std::max(a->scm, a->mask ? a->smk_m : 0) * 4 >= ((int64_t)1 << 31)) return false;
-  if (a->scm % 4 || (reinterpret_cast<uintptr_t>(a->C) & (cbf ? 7 : 15))) return false;  // 16 / 8-byte row segments
-  return true;
 }
 
 // The row-streaming kernel (gemm_rows.hip): bf16 arithmetic, K <= 256 (K % 4, % 8 for bf16 A), N a
@@ -485,32 +207,6 @@ static bool wgrad_ok(const AlignnGemmArgs* a) {
   return true;
 }
 
-template <int KT>
-static void bf16_stream_launch_k(const GemmParams& p, dim3 grid, int nslices, int64_t nbands, hipStream_t s) {
-  const bool beta = p.beta != 0.f, mask = p.mask != nullptr;
-  if (beta && mask) launch(bst::gemm_bf16_stream_kernel<KT, true, true>, grid, dim3(256), 0, s, p, nslices, nbands);
-  else if (beta) launch(bst::gemm_bf16_stream_kernel<KT, true, false>, grid, dim3(256), 0, s, p, nslices, nbands);
-  else if (mask) launch(bst::gemm_bf16_stream_kernel<KT, false, true>, grid, dim3(256), 0, s, p, nslices, nbands);
-  else launch(bst::gemm_bf16_stream_kernel<KT, false, false>, grid, dim3(256), 0, s, p, nslices, nbands);
-}
-
-static void bf16_stream_launch(const GemmParams& p, int cus, hipStream_t s) {
-  const int nslices = (int)(p.N / bst::NB);
-  const int64_t nbands = (p.M + bst::ROWS - 1) / bst::ROWS;
-  const int G = (int)(std::min<int64_t>(cus, nslices * nbands) / nslices * nslices);
-  const dim3 grid((unsigned)std::max(G, nslices));
-  if (p.abf || p.cbf) {   // bf16 storage (K = 256, no mask: bf16_stream_ok)
-    const bool beta = p.beta != 0.f;
-    if (p.abf && p.cbf) launch(bst::gemm_bf16_stream_kernel<256, false, false, true, true>, grid, dim3(256), 0, s, p, nslices, nbands);
-    else if (p.cbf) launch(bst::gemm_bf16_stream_kernel<256, false, false, false, true>, grid, dim3(256), 0, s, p, nslices, nbands);
-    else if (beta) launch(bst::gemm_bf16_stream_kernel<256, true, false, true, false>, grid, dim3(256), 0, s, p, nslices, nbands);
-    else launch(bst::gemm_bf16_stream_kernel<256, false, false, true, false>, grid, dim3(256), 0, s, p, nslices, nbands);
-    return;
-  }
-  if (p.K == 256) bf16_stream_launch_k<256>(p, grid, nslices, nbands, s);
-  else if (p.K == 128) bf16_stream_launch_k<128>(p, grid, nslices, nbands, s);
-  else bf16_stream_launch_k<64>(p, grid, nslices, nbands, s);
-}
 
 }  // namespace alignn
 
@@ -532,7 +228,7 @@ extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
   if (!plan_args(a, pl, ktot, nb)) return -1;
-  return wgrad_ok(a) ? 3 : rows_ok(a, pl.split) ? 2 : bf16_stream_ok(a, pl.split) ? 1 : 0;
+  return wgrad_ok(a) ? 3 : rows_ok(a, pl.split) ? 2 : 0;
 }
 
 extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
@@ -614,11 +310,6 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
   if (rows_ok(a, pl.split)) {
     gemm_rows_launch(p, device_cus(), s);
     ALIGNN_LAUNCH_CHECK("gemm_rows_kernel");
-    return ALIGNN_OK;
-  }
-  if (bf16_stream_ok(a, pl.split)) {
-    bf16_stream_launch(p, device_cus(), s);
-    ALIGNN_LAUNCH_CHECK("gemm_bf16_stream_kernel");
     return ALIGNN_OK;
   }
   const int64_t tiles = ((a->M + pl.bm - 1) / pl.bm) * ((a->N + pl.bn - 1) / pl.bn);

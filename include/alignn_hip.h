@@ -88,9 +88,6 @@ typedef struct AlignnGemmArgs {
  * flight — is taken automatically when every stage is full and both operands are vectorisable; both
  * give bitwise the same result).  For A/B tests. */
 #define ALIGNN_GEMM_NOPIPE 256
-/* bf16 only: never the streaming kernel (the large-M products K in {64, 128, 256}, N % 256 == 0,
- * M >= 32768 otherwise stream A through a W slice held in LDS as bf16).  For A/B tests. */
-#define ALIGNN_GEMM_NOSTREAM 512
 /* bf16 storage (config C3, autocast's tensor dtypes, train.py:632-636): the A / B pointer holds bf16
  * elements (widened exactly as they are staged; strides stay in elements, vector loads need 8-byte
  * alignment), or C receives bf16 (RNE of the fp32 epilogue value; write-only: no beta, no mask).
@@ -98,9 +95,6 @@ typedef struct AlignnGemmArgs {
 #define ALIGNN_GEMM_A_BF16 1024
 #define ALIGNN_GEMM_B_BF16 2048
 #define ALIGNN_GEMM_C_BF16 4096
-/* bf16 only: the streaming kernel's row floor drops from 32768 (the C3-plan-measured crossover; the
- * environment variable ALIGNN_GEMM_STREAM_MIN_M moves it) to 4096.  For tests and A/B. */
-#define ALIGNN_GEMM_STREAM 8192
 /* bf16 only, tiled kernels: operands rounded to bf16 as they are staged and kept as bf16 LDS images
  * (half the LDS bytes, one 16-byte read per fragment, no per-fragment conversion); bitwise equal to
  * the fp32 images.  Taken by default when A is k-contiguous (the products over rows; the weight
@@ -123,9 +117,10 @@ int alignn_gemm_f32(const AlignnGemmArgs* args, void* stream);
  * the current device); 0 when no split is used, -1 for invalid shapes. */
 int64_t alignn_gemm_workspace(const AlignnGemmArgs* args);
 
-/* Which kernel alignn_gemm_f32 takes (host query, no GPU work): 0 tiled, 1 the bf16 streaming
- * kernel (ALIGNN_GEMM_NOSTREAM), 2 the bf16 row-streaming kernel (ALIGNN_GEMM_NOROWS), 3 the bf16
- * weight-gradient kernel (ALIGNN_GEMM_NOWGRAD), -1 invalid arguments. */
+/* Which kernel alignn_gemm_f32 takes (host query, no GPU work): 0 tiled, 2 the bf16 row-streaming
+ * kernel (ALIGNN_GEMM_NOROWS), 3 the bf16 weight-gradient kernel (ALIGNN_GEMM_NOWGRAD), -1 invalid
+ * arguments (1, the W-in-LDS streaming kernel of rounds 2-4, was removed in round 5: the row kernel
+ * takes every product it took, faster; its ALIGNN_GEMM_STREAM / _NOSTREAM bits are gone). */
 int alignn_gemm_path(const AlignnGemmArgs* args);
 
 /* ----------------------------------------------------------------------------------------

@@ -83,7 +83,7 @@ def test_lds16_bf16_storage_bitwise(which):
     outs = []
     for f in (ops.GEMM_NOLDS16, ops.GEMM_LDS16):
         C = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16 if "C" in which else torch.float32)
-        ops.gemm(Av, Bv, C, tile=ops.GEMM_BF16 | ops.GEMM_NOSTREAM | f)
+        ops.gemm(Av, Bv, C, tile=ops.GEMM_BF16 | ops.GEMM_NOROWS | f)
         outs.append(C)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])

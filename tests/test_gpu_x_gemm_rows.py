@@ -3,7 +3,7 @@
 config C3's bond-level products take (every bond times a 256-wide weight: the skip projection, the
 dX += dR W product, the edge MLP).  Same operand rounding (bf16 RNE), k grouping (16-deep slices,
 k = 16 t + 8 h + j) and epilogue order as the tiled bf16 kernels, so it is compared with them
-bitwise (ALIGNN_GEMM_NOROWS | ALIGNN_GEMM_NOSTREAM), and with an fp64 product of the rounded
+bitwise (ALIGNN_GEMM_NOROWS), and with an fp64 product of the rounded
 operands to fp32 accumulation error.  Shapes of the B = 256 step (K = 36 the edge MLP's first
 layer: zero-padded to 64), ragged M, both W layouts, bf16 A / C storage and every epilogue term it
 supports; below 4096 rows the kernel runs on request (ALIGNN_GEMM_ROWS)."""
@@ -42,7 +42,7 @@ def test_rows_kernel_matches_tiled_bitwise(M, N, K, layout, epi):
     C = C0.clone()
     ops.gemm(A, Wv, C, tile=BF, **kw)
     Ct = C0.clone()
-    ops.gemm(A, Wv, Ct, tile=ops.GEMM_BF16 | ops.GEMM_NOROWS | ops.GEMM_NOSTREAM, **kw)
+    ops.gemm(A, Wv, Ct, tile=ops.GEMM_BF16 | ops.GEMM_NOROWS, **kw)
     C2 = C0.clone()
     ops.gemm(A, Wv, C2, tile=BF, **kw)
     torch.cuda.synchronize()
@@ -79,7 +79,7 @@ def test_rows_kernel_bf16_storage(io):
         C = C0.clone()
         ops.gemm(A16, W.t(), C, **kw)
         Ct = C0.clone()
-        ops.gemm(A16, W.t(), Ct, tile=ops.GEMM_NOROWS | ops.GEMM_NOSTREAM, **kw)
+        ops.gemm(A16, W.t(), Ct, tile=ops.GEMM_NOROWS, **kw)
     torch.cuda.synchronize()
     assert torch.equal(C, Ct)
 
@@ -126,7 +126,7 @@ def test_rows_kernel_batched_per_head_products(M, lda, a16):
     with ops.gemm_precision("bf16"):
         assert ops.gemm(A, Mh, C.transpose(0, 1), path_only=True) == 2
         ops.gemm(A, Mh, C.transpose(0, 1))
-        ops.gemm(A, Mh, Ct.transpose(0, 1), tile=ops.GEMM_NOROWS | ops.GEMM_NOSTREAM)
+        ops.gemm(A, Mh, Ct.transpose(0, 1), tile=ops.GEMM_NOROWS)
     torch.cuda.synchronize()
     ref = torch.einsum("bmk,bkn->mbn", A.bfloat16().double(), Mh.bfloat16().double())
     assert _rel(C, ref) < 5e-6
