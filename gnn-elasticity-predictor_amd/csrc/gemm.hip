@@ -182,6 +182,24 @@ static bool rows_ok(const AlignnGemmArgs* a, int split) {
   return true;
 }
 
+// The per-head form of the row kernel (gemm_rows.hip gemm_heads_kernel): the S_h M_h^T / Sz_h M_h^T
+// products (batch = 4 heads, N = 64 each, K = 256, rowscale x bias2, beta); same row floor and
+// ALIGNN_GEMM_ROWS / _NOROWS switches as the row kernel.
+void gemm_heads_launch(const GemmParams& p, int cus, hipStream_t s);
+static bool heads_ok(const AlignnGemmArgs* a, int split, bool vecB) {
+  if (!(a->tile & ALIGNN_GEMM_BF16) || (a->tile & ALIGNN_GEMM_NOROWS) || (a->tile & 15) != 0) return false;
+  if (a->rowsum || a->c_rows || a->mask || a->reduce_batch || split != 1) return false;
+  if (a->batch != 4 || a->N != 64 || a->K < 8 || a->K > 256 || a->K % 8) return false;
+  if (a->M < ((a->tile & ALIGNN_GEMM_ROWS) ? 1 : rows_min_m())) return false;
+  const bool abf = (a->tile & ALIGNN_GEMM_A_BF16) != 0;
+  if ((a->tile & (ALIGNN_GEMM_B_BF16 | ALIGNN_GEMM_C_BF16)) || !vecB || a->sbk != 1) return false;
+  if (a->sak != 1 || a->sam % (abf ? 8 : 4) || a->sab % (abf ? 8 : 4) || (reinterpret_cast<uintptr_t>(a->A) & 15)) return false;
+  if (a->scn != 1 || a->scm % 4 || a->scb % 4 || (reinterpret_cast<uintptr_t>(a->C) & 15)) return false;
+  if (a->rowscale && !a->bias2) return false;
+  if ((a->M + 32) * a->scm * 4 >= ((int64_t)1 << 31)) return false;
+  return true;
+}
+
 // The weight-gradient kernel (gemm_wgrad.hip): bf16 arithmetic, A = dY^T and B = X both stored
 // row-major over the long K axis (sam == 1, sbn == 1; 16-byte rows), K >= 4096, batched or not (no
 // batch reduction), no split
@@ -228,7 +246,8 @@ extern "C" int alignn_gemm_path(const AlignnGemmArgs* a) {
   GemmPlan pl;
   int64_t ktot, nb;
   if (!plan_args(a, pl, ktot, nb)) return -1;
-  return wgrad_ok(a) ? 3 : rows_ok(a, pl.split) ? 2 : 0;
+  const bool vecB = a->sbk == 1 && a->sbn % 4 == 0 && a->sbb % 4 == 0 && (reinterpret_cast<uintptr_t>(a->B) & 15) == 0;
+  return wgrad_ok(a) ? 3 : (rows_ok(a, pl.split) || heads_ok(a, pl.split, vecB)) ? 2 : 0;
 }
 
 extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
@@ -305,6 +324,11 @@ extern "C" int alignn_gemm_f32(const AlignnGemmArgs* a, void* stream) {
     const int64_t total = a->batch * a->M * a->N + (a->rowsum ? a->M : 0);
     launch(splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0, s, p);
     ALIGNN_LAUNCH_CHECK("splitk_reduce_kernel");
+    return ALIGNN_OK;
+  }
+  if (heads_ok(a, pl.split, p.vecB)) {
+    gemm_heads_launch(p, device_cus(), s);
+    ALIGNN_LAUNCH_CHECK("gemm_heads_kernel");
     return ALIGNN_OK;
   }
   if (rows_ok(a, pl.split)) {

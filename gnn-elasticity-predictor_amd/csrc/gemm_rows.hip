@@ -255,6 +255,178 @@ static void launch_k(const GemmParams& p, dim3 grid, int nslices, int nsl, int64
   else launch_kt<KT, false, false, BKC>(p, grid, nslices, nsl, nbands, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Per-head products with 64 output columns per head (config C3's outp_h += S_h M_h^T (+ sumA_h wbar_h)
+// in the forward, dQ_h += Sz_h M_h^T (+ sigz_h wbar_h) in the backward: batch = H = 4 heads, K = 256,
+// N = 64, A_h = S[:, h, :]): one workgroup's 256 output columns are the four heads' 64, wave w serving
+// head w / 2, columns 32 (w % 2) ..; every head has its own A band, so the LDS holds the four heads'
+// 32-row bands ([4][32][KT + 8] bf16, one image: the next band waits in registers), and the epilogue
+// adds fma(rowscale[m, h], bias2[h, n], .) after beta (epilogue_value's order).  Same MFMA sequence
+// per output as the tiled bf16 path: bitwise equal to it.
+// ---------------------------------------------------------------------------------------------
+constexpr int HH = 4, HN = 64;   // heads per workgroup, columns per head
+
+template <int KT, bool ABF>
+struct HeadBand {
+  static constexpr int CH = ABF ? KT / 8 : KT / 4;   // 16-byte chunks per row
+  static constexpr int TOT = HH * ROWS * CH;
+  static constexpr int PER = TOT / NT;
+  static_assert(TOT % NT == 0, "head band chunks");
+  gf4 r[PER];
+  __device__ __forceinline__ void load(const GemmParams& p, int64_t band) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + NT * i;
+      const int h = idx / (ROWS * CH), rem = idx % (ROWS * CH);
+      const int64_t row = min(band * ROWS + rem / CH, p.M - 1);
+      const int k = (rem % CH) * (ABF ? 8 : 4);
+      const int kc = k < p.K ? k : 0;
+      r[i] = *reinterpret_cast<const gf4*>(eoff(p.A, h * p.sab + row * p.sam + kc, ABF));
+    }
+    asm volatile("" ::: "memory");
+  }
+  __device__ __forceinline__ void store(__bf16* __restrict__ img, int K) const {
+    constexpr int KP = KT + 8;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + NT * i;
+      const int h = idx / (ROWS * CH), rem = idx % (ROWS * CH);
+      const int rr = rem / CH, k = (rem % CH) * (ABF ? 8 : 4);
+      __bf16* d = img + (h * ROWS + rr) * KP + k;
+      const bool live = k < K;
+      if constexpr (ABF) {
+        u32x4 u = __builtin_bit_cast(u32x4, r[i]);
+        if (!live) u = u32x4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<u32x4*>(d) = u;
+      } else {
+        const gf4 v = live ? r[i] : gf4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<u32x2*>(d) = u32x2{pack2(v.x, v.y), pack2(v.z, v.w)};
+      }
+    }
+  }
+};
+
+template <int KT, bool ABF, bool BETA, bool RS, bool BKC>
+__global__ __launch_bounds__(NT, 1) void gemm_heads_kernel(GemmParams p, int64_t nbands) {
+  constexpr int KP = KT + 8, T = KT / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 As[HH * ROWS * KP];
+  __shared__ __attribute__((aligned(16))) float Lepi[NT / 64][ROWS * EPI_LD];
+  __shared__ __attribute__((aligned(16))) float Lb[HH * HN], Lb2[HH * HN];
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int l32 = lane & 31, h = lane >> 5;
+  const int hw = wave >> 1, c0 = (wave & 1) * 32;   // this wave's head and first column in it
+  const bool has_bias = p.bias != nullptr;
+  for (int i = threadIdx.x; i < HH * HN; i += NT) {
+    const int hh = i / HN, c = i % HN;
+    Lb[i] = has_bias ? p.bias[hh * p.sbias_b + c] : 0.f;
+    Lb2[i] = RS ? p.bias2[hh * p.sb2_b + c] : 0.f;
+  }
+  bf16x8 bw[T];
+  {
+    const int K = (int)p.K;
+    const float* Bc = p.B + hw * p.sbb + (c0 + l32) * p.sbn;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int k0 = 16 * t + 8 * h;
+      if constexpr (BKC) {
+        const int kc = min(k0, K - 8);
+        const gf4 x = *reinterpret_cast<const gf4*>(Bc + kc), y = *reinterpret_cast<const gf4*>(Bc + kc + 4);
+        const bool live = k0 < K;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bw[t][e] = (__bf16)(live ? x[e] : 0.f);
+          bw[t][4 + e] = (__bf16)(live ? y[e] : 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = Bc[(int64_t)min(k0 + e, K - 1) * p.sbk];
+          bw[t][e] = (__bf16)(k0 + e < K ? v : 0.f);
+        }
+      }
+      if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float* Cw = p.C + hw * p.scb + c0;
+  const int64_t cbytes = ((p.M - 1) * p.scm + HN - c0) * 4;   // this wave's columns of the M rows
+  const __amdgpu_buffer_rsrc_t cst = rsrc(Cw, cbytes);
+  const __amdgpu_buffer_rsrc_t cld = rsrc(Cw, BETA ? cbytes : 0);
+  float* Ls = Lepi[wave];
+  constexpr int PASS = 4, RPP = ROWS / PASS, LPR = 64 / RPP;   // fp32 C: 8 rows x 8 lanes x 16 bytes
+  const int er = lane / LPR, ec = (lane % LPR) * 4;
+  const float* rsp = RS ? p.rowscale + hw * p.srs_b : nullptr;
+
+  int64_t band = blockIdx.x;
+  const int64_t Q = gridDim.x;
+  if (band >= nbands) return;   // workgroup-uniform
+  HeadBand<KT, ABF> ld;
+  ld.load(p, band);
+  while (true) {
+    const int64_t row0 = band * ROWS;
+    __syncthreads();   // every wave done with the previous band's image
+    ld.store(As, (int)p.K);
+    __syncthreads();
+    // this band's epilogue operands, then the next band's rows (loads complete in order: the
+    // epilogue then waits for its own operands only)
+    gf4 cv[BETA ? PASS : 1];
+    float rsv[RS ? PASS : 1];
+#pragma unroll
+    for (int ps = 0; ps < PASS; ++ps) {
+      const int64_t row = row0 + RPP * ps + er;
+      if constexpr (BETA)
+        cv[ps] = __builtin_bit_cast(gf4, __builtin_amdgcn_raw_buffer_load_b128(cld, (int)((row * p.scm + ec) * 4), 0, 0));
+      if constexpr (RS) rsv[ps] = rsp[min(row, p.M - 1) * p.srs_m];
+    }
+    const int64_t b1 = band + Q;
+    if (b1 < nbands) ld.load(p, b1);   // workgroup-uniform
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const __bf16* Al = As + (hw * ROWS + l32) * KP + 8 * h;
+    bf16x8 a[2];
+    a[0] = *reinterpret_cast<const bf16x8*>(Al);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if (t + 1 < T) a[(t + 1) & 1] = *reinterpret_cast<const bf16x8*>(Al + 16 * (t + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t & 1], bw[t], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ls[((r & 3) + 8 * (r >> 2) + 4 * h) * EPI_LD + l32] = __fmul_rn(p.alpha, acc[r]);
+    const gf4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ps = 0; ps < PASS; ++ps) {
+      const int rr = RPP * ps + er;
+      gf4 v = *reinterpret_cast<const gf4*>(Ls + rr * EPI_LD + ec);
+      if constexpr (BETA)
+        v = gf4{fmaf(p.beta, cv[ps].x, v.x), fmaf(p.beta, cv[ps].y, v.y), fmaf(p.beta, cv[ps].z, v.z),
+                fmaf(p.beta, cv[ps].w, v.w)};
+      const int cb = hw * HN + c0 + ec;
+      if (has_bias) {
+        const gf4 bb = *reinterpret_cast<const gf4*>(Lb + cb);
+        v = gf4{__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z), __fadd_rn(v.w, bb.w)};
+      }
+      if constexpr (RS) {
+        const gf4 b2 = *reinterpret_cast<const gf4*>(Lb2 + cb);
+        v = gf4{fmaf(rsv[ps], b2.x, v.x), fmaf(rsv[ps], b2.y, v.y), fmaf(rsv[ps], b2.z, v.z), fmaf(rsv[ps], b2.w, v.w)};
+      }
+      v = p.relu ? __builtin_elementwise_max(v, zero) : v;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), cst, (int)(((row0 + rr) * p.scm + ec) * 4), 0, 0);
+    }
+    if (b1 >= nbands) break;
+    band = b1;
+  }
+}
+
+template <int KT, bool ABF, bool BKC>
+static void launch_heads_k(const GemmParams& p, dim3 grid, int64_t nbands, hipStream_t s) {
+  const bool beta = p.beta != 0.f, rs = p.rowscale != nullptr;
+  if (beta && rs) launch(gemm_heads_kernel<KT, ABF, true, true, BKC>, grid, dim3(NT), 0, s, p, nbands);
+  else if (beta) launch(gemm_heads_kernel<KT, ABF, true, false, BKC>, grid, dim3(NT), 0, s, p, nbands);
+  else if (rs) launch(gemm_heads_kernel<KT, ABF, false, true, BKC>, grid, dim3(NT), 0, s, p, nbands);
+  else launch(gemm_heads_kernel<KT, ABF, false, false, BKC>, grid, dim3(NT), 0, s, p, nbands);
+}
+
 }  // namespace rsk
 
 // Shapes (host check, gemm.hip rows_ok): bf16 arithmetic, K <= 256 (K % 4 == 0, % 8 for bf16 A),
@@ -275,6 +447,16 @@ void gemm_rows_launch(const GemmParams& p, int cus, hipStream_t s) {
     if (bkc) rsk::launch_k<256, true>(p, grid, nslices, nsl, nbands, s);
     else rsk::launch_k<256, false>(p, grid, nslices, nsl, nbands, s);
   }
+}
+
+// The per-head form (host check, gemm.hip heads_ok): bf16 arithmetic, batch = 4 heads of N = 64
+// columns, K <= 256 (K % 8), W k-contiguous (M_h^T: 16-byte loads), fp32 C with 16-byte rows per head,
+// no mask / split / row scatter / rowsum; rowscale x bias2 and beta allowed.
+void gemm_heads_launch(const GemmParams& p, int cus, hipStream_t s) {
+  const int64_t nbands = (p.M + rsk::ROWS - 1) / rsk::ROWS;
+  const dim3 grid((unsigned)std::min<int64_t>((int64_t)cus, nbands));
+  if (p.abf) rsk::launch_heads_k<256, true, true>(p, grid, nbands, s);   // W k-contiguous (host check)
+  else rsk::launch_heads_k<256, false, true>(p, grid, nbands, s);
 }
 
 }  // namespace alignn

@@ -131,3 +131,36 @@ def test_rows_kernel_batched_per_head_products(M, lda, a16):
     ref = torch.einsum("bmk,bkn->mbn", A.bfloat16().double(), Mh.bfloat16().double())
     assert _rel(C, ref) < 5e-6
     assert torch.equal(C, Ct)
+
+
+@pytest.mark.parametrize("M,ldc", [(16020, 256), (15360, 768)])
+@pytest.mark.parametrize("with_proj", [True, False])
+def test_heads_kernel_per_head_64_columns(M, ldc, with_proj):
+    """The per-head products outp_h += S_h M_h^T (+ sumA_h wbar_h) / dQ_h += Sz_h M_h^T (+ sigz_h
+    wbar_h): batch = 4 heads of 64 columns, A_h = S[:, h, :] (K = 256), W_h = M_h^T k-contiguous,
+    C rows of [n, H, 64] inside a wider row, beta = 1, the rowscale x bias2 term — bitwise equal
+    to the tiled kernels."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(M + ldc)
+    S = torch.randn(M, 4, 256, generator=g).to(DEV)
+    Mh = (torch.randn(4, 64, 256, generator=g) * 0.1).to(DEV)
+    out0 = torch.randn(M, ldc, generator=g).to(DEV)
+    sumA = torch.rand(M, 4, generator=g).to(DEV)
+    wbar = torch.randn(256, generator=g).to(DEV)
+    A, B = S.transpose(0, 1), Mh.transpose(1, 2)
+    kw = dict(beta=1.0)
+    if with_proj:
+        kw.update(rowscale=sumA.t(), bias2=wbar.view(4, 64))
+    C, Ct = out0.clone(), out0.clone()
+    with ops.gemm_precision("bf16"):
+        Cv = C[:, :256].view(M, 4, 64).transpose(0, 1)
+        assert ops.gemm(A, B, Cv, path_only=True, **kw) == 2
+        ops.gemm(A, B, Cv, **kw)
+        ops.gemm(A, B, Ct[:, :256].view(M, 4, 64).transpose(0, 1), tile=ops.GEMM_NOROWS, **kw)
+    torch.cuda.synchronize()
+    ref = torch.einsum("bmk,bkn->mbn", A.bfloat16().double(), B.bfloat16().double()).reshape(M, 256)
+    ref = ref + out0[:, :256].double()
+    if with_proj:
+        ref = ref + (sumA.double()[:, :, None] * wbar.double().view(1, 4, 64)).reshape(M, 256)
+    assert _rel(C[:, :256], ref) < 5e-6
+    assert torch.equal(C, Ct)   # columns past the heads' 256 untouched on both paths

@@ -110,6 +110,12 @@ for step in "$@"; do
             python tools/pmc_traffic.py $O/pmc_${c}_FETCH_SIZE $O/pmc_${c}_WRITE_SIZE --json $O/pmc_${c}_traffic.json --top 40 > $O/pmc_${c}_traffic.txt
             python tools/pmc_mfma.py $O/pmc_${c}_mf > $O/pmc_${c}_mfma.txt; done
           head -12 $O/pmc_c3_traffic.txt; head -12 $O/pmc_c2_traffic.txt ;;
+    heads) run t_heads 400 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_pending.py tests/test_gpu_x_round5.py
+           run gtrace_c3 300 python tools/gemm_trace.py --batch 256 --precision bf16 --time
+           head -1 $O/gtrace_c3.log; grep -E "B\(4, 256, 64\)" $O/gtrace_c3.log | head -4 | cut -c1-110
+           for i in 1 2; do run c3_new$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+             ALIGNN_HIP_LIB=$PWD/abl/libprev.so run c3_prev$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done
+           for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     gpmc) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/gpmc_sq -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_sq.log 2>&1 || exit 1
           timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/gpmc_mf -o run --output-format csv -- python $OLDPWD/tools/gemm_probe.py --iters 10 --no-lib > $O/gpmc_mf.log 2>&1 || exit 1
