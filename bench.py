@@ -451,10 +451,11 @@ def _roofline(summ, dominant, mfma_peak, probe_src):
             "bytes_per_launch": s["bytes_per_launch"], "timing": probe_src}
 
 
-def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roofline=True):
+def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roofline=True, streams_of=None):
     """Builds the model, trainer and a resident batch of B graphs, picks the dominant kernel (one
     untimed eager probe step), captures the step, runs `warmup` steps and times exactly `steps`
-    (barrier + synchronize on both sides, max over ranks).  Returns the numbers and the trainer."""
+    (barrier + synchronize on both sides, max over ranks).  Returns the numbers and the trainer.
+    ``streams_of``: an idle trainer whose side / aux streams this one uses (ExecContext.borrow_streams)."""
     import alignn_mi355x as A
     from alignn_mi355x import profiling
     from alignn_mi355x.dp import GradBuckets, max_over_ranks, rank_graphs
@@ -464,6 +465,8 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
     torch.manual_seed(1234)  # identical initial weights on every rank
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
                                                       args.dropout), 2).to(dev)
+    if streams_of is not None:
+        model._engine.ctx.borrow_streams(streams_of.model._engine.ctx)
     trainer = A.FusedTrainer(model, precision=precision, **apply_settings(args, model))
     mfma_peak = BF16_MFMA_TFLOPS if precision == "bf16" else FP32_MFMA_TFLOPS
     batch = mp_like_batch(B, first=rank_graphs(B, rank).start, lg_offset=lg_offset).to(dev)
@@ -813,7 +816,8 @@ def main():
         secondary = {}
         sec_steps, sec_warm = max(5, args.steps // 2), max(2, args.warmup // 2)
         if args.lg_offset == "num_nodes":
-            w = measure(args, dev, rank, world, B, "num_edges", args.precision, sec_steps, sec_warm, roofline=True)
+            w = measure(args, dev, rank, world, B, "num_edges", args.precision, sec_steps, sec_warm, roofline=True,
+                        streams_of=r["trainer"])
             secondary["corrected_wiring"] = {
                 "config": f"B={B}, lg_offset=num_edges (every bond active: no line-graph compaction), {args.precision}",
                 "value": round(w["value"], 2), "unit": "graphs/s", "ms_per_step": round(w["ms_per_step"], 3),
@@ -822,7 +826,8 @@ def main():
         if not args.no_cpu_baseline:
             secondary["c1_forward"] = c1_forward(args, dev)
         if (B, args.precision) != (256, "bf16"):
-            c3 = measure(args, dev, rank, world, 256, args.lg_offset, "bf16", sec_steps, sec_warm, roofline=True)
+            c3 = measure(args, dev, rank, world, 256, args.lg_offset, "bf16", sec_steps, sec_warm, roofline=True,
+                         streams_of=r["trainer"])
             secondary["c3_b256_bf16"] = {
                 "config": "BASELINE config 3: B=256 per GPU, bf16 matrix-core inputs (fp32 accumulation, fp32 "
                           f"softmax/LayerNorm), lg_offset={args.lg_offset}",

@@ -689,7 +689,7 @@ class AlignnEngine:
     'base' -> [B, T] (AlignnRegressor.forward), 'embed' -> shared [B, D] (embed)."""
 
     WGRAD_SPLIT_MAX_T = 1_000_000
-    ATOM_STREAM_MIN_T = 1_000_000
+    ATOM_STREAM_MIN_T = 100_000
 
     def _atom_mode(self, T: int, E: int) -> int:
         if E <= 0:
@@ -725,13 +725,18 @@ class AlignnEngine:
         # (+4.0 % graphs/s on MI355X once enc_bwd was column-parallel, profiles/r01/v13_sweep.log)
         self.defer_angle_bwd = True
         # gate/LayerNorm parameter-gradient reduction on the side stream (off the critical path)
-        self.gate_reduce_side = True  # +0.3 % (v34_sweep_gate_reduce_side.log)
+        # (round 1: +0.3 %, v34_sweep_gate_reduce_side.log).  Round 5 re-sweep on the main stream: C3 +1.9 %
+        # (23,292-23,363 -> 23,712-23,823 graphs/s), C2 +1.5 % beside the settings below (10,091-10,104
+        # -> 10,247-10,255; profiles/r05/v15_sweep_engine_*.txt)
+        self.gate_reduce_side = False
         # deferred angle-encoder backward on a third stream (see _backward): 1 always, 0 never, or
         # from this many line-graph edges on.  B = 32 (253,440 triplets): -0.6 %
         # (v31_sweep_enc_bwd_aux_rejected.log); B = 256 bf16 (2.03 M triplets, enc_bwd 1.06 ms, the
         # step's last branch): +1.8 % (17,697-17,740 -> 18,027-18,051 graphs/s,
-        # profiles/r02/v30_ab_enc_bwd_aux_c3.log)
-        self.enc_bwd_aux = 1_000_000
+        # profiles/r02/v30_ab_enc_bwd_aux_c3.log).  Round 5 (atom blocks on the aux stream at B = 32
+        # too): B = 32 +1.1 % (9,972-9,985 -> 10,077-10,090 graphs/s), B = 256 bf16 within noise:
+        # always (profiles/r05/v15_sweep_engine_c2.txt)
+        self.enc_bwd_aux = 1
         # forward: each line block's skip projection queued on the side stream before its active-row
         # gather and Q/K/V product (else after them), and the angle encoder's first Linear on the side
         # stream beside the node/edge encoders (bitwise neutral; with wgrad_early B = 32
@@ -750,7 +755,9 @@ class AlignnEngine:
         # block's gate kernel (ops.gate_ln_bwd dX_add); 2: as 1 with the atom blocks on the aux stream
         # (bitwise equal to 1); -1: 2 from ATOM_STREAM_MIN_T line-graph edges on, else 0.  B = 256
         # bf16: 0 -> 2 +2.6 % (18,963 -> 19,458 graphs/s); B = 32: 2 within noise of 0 (-0.5 %),
-        # 1 -0.6 % (profiles/r03/v21_ab_atom_stream.log)
+        # 1 -0.6 % (profiles/r03/v21_ab_atom_stream.log).  Round 5, with the faster line-graph and
+        # GEMM kernels, B = 32 (253,440 line-graph edges): 0 -> 2 +2.9 % (9,652-9,670 -> 9,929-9,957
+        # graphs/s; 1 -0.8 %, profiles/r05/v15_sweep_engine_c2.txt): ATOM_STREAM_MIN_T 1 M -> 100,000
         self.atom_stream = -1
         # bf16 storage: the atom-graph attention reads the bond state's bf16 copy (the gate kernel's
         # Xn16; autocast casts the bond state to bf16 for edge_proj) as its edge-feature rows

@@ -96,6 +96,7 @@ class ExecContext:
         self._owned_streams = []
         self.frozen = 0       # live plans / graphs holding this context's buffers
         self._eager = {}      # buffers of eager launches that outgrew a frozen buffer
+        self._lender = None   # borrow_streams
 
     def freeze(self) -> None:
         """A recorded plan now holds this context's buffers: none may be replaced while it lives."""
@@ -129,18 +130,29 @@ class ExecContext:
         self._owned_streams.append(((key, prio), h))
         return torch.cuda.ExternalStream(h, device=torch.device(key))
 
+    def borrow_streams(self, other: "ExecContext") -> None:
+        """Take ``other``'s side / aux streams instead of creating this context's own, for an engine
+        that never runs at the same time as ``other``'s (bench.py's secondary configurations, measured
+        beside the idle headline trainer).  The process then holds no more streams than one engine
+        needs: with GPU_MAX_HW_QUEUES = 4, each extra stream shares a hardware queue with one of the
+        step's, whose kernels then wait behind each other in queue order (C3 measured 21,640 beside
+        the headline trainer's own streams vs 23,515 graphs/s alone; profiles/r05/v16_*)."""
+        if self._side or self._aux:
+            raise RuntimeError("borrow_streams: this context already has streams of its own")
+        self._lender = other
+
     def side(self, device) -> torch.cuda.Stream:
         """A second stream per device for work off the critical path (weight gradients)."""
         key = _dkey(device)
         if key not in self._side:
-            self._side[key] = self._own_stream(device)
+            self._side[key] = self._lender.side(device) if self._lender is not None else self._own_stream(device)
         return self._side[key]
 
     def aux(self, device) -> torch.cuda.Stream:
         """A third stream per device for short branches beside the critical path."""
         key = _dkey(device)
         if key not in self._aux:
-            self._aux[key] = self._own_stream(device)
+            self._aux[key] = self._lender.aux(device) if self._lender is not None else self._own_stream(device)
         return self._aux[key]
 
     def __del__(self):

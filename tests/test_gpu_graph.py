@@ -69,14 +69,15 @@ def test_side_stream_overlap_is_bitwise_neutral():
 
 
 def test_plan_structure():
-    """The recorded forward/backward plan holds the whole step on two streams (critical path +
-    weight-gradient side stream) with its fork/join edges; the update plan is one stream."""
+    """The recorded forward/backward plan holds the whole step on three streams (critical path, the
+    weight-gradient side stream, the aux stream of the deferred angle-encoder backward) with its
+    fork/join edges; the update plan is one stream."""
     from alignn_mi355x import ops
     from alignn_mi355x.trainer import plan_info
     _, tr, b = _setup()
     tr.capture(b, mode="plan")
     fb, up = (plan_info(p) for p in tr._graph[3])
-    assert fb["launches"] > 150 and fb["streams"] == 2 and fb["edges"] >= 8, fb
+    assert fb["launches"] > 150 and fb["streams"] == 3 and fb["edges"] >= 8, fb
     assert up["launches"] >= 3 and up["streams"] == 1 and up["edges"] == 0, up
     tr.release_capture()
     assert tr._graph is None

@@ -238,3 +238,30 @@ def test_gemm_rowsum_is_the_bias_gradient(M, N, K, a_t, prec):
     assert torch.equal(C0, C1)
     err = float((rs.double() - ref_rs).abs().max() / ref_rs.abs().max())
     assert err < 2e-6 * max(1.0, (K / 1000) ** 0.5), err
+
+
+def test_borrowed_streams_are_the_lenders_and_the_step_is_unchanged():
+    """ExecContext.borrow_streams (bench.py's secondary configurations beside the idle headline
+    trainer): the borrower's side / aux streams are the lender's, a context with streams of its own
+    refuses to borrow, and a step on borrowed streams gives the same bits as on its own."""
+    import alignn_mi355x as A
+    from alignn_mi355x import ops
+    from alignn_mi355x.synthetic import mp_like_batch
+    lender, own = ops.ExecContext("lender"), ops.ExecContext("own")
+    own.side(DEV)
+    with pytest.raises(RuntimeError):
+        own.borrow_streams(lender)
+    res = []
+    for borrow in (False, True):
+        torch.manual_seed(0)
+        m = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(DEV)
+        if borrow:
+            m._engine.ctx.borrow_streams(lender)
+        tr = A.FusedTrainer(m)
+        loss = tr.forward_backward(mp_like_batch(4).to(DEV), 5).clone()
+        torch.cuda.synchronize()
+        if borrow:
+            assert m._engine.ctx.side(DEV).cuda_stream == lender.side(DEV).cuda_stream
+            assert m._engine.ctx.aux(DEV).cuda_stream == lender.aux(DEV).cuda_stream
+        res.append((loss, tr.st.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

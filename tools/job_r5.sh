@@ -126,6 +126,16 @@ for step in "$@"; do
     rpc3) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c3 -o run --output-format csv -- python $OLDPWD/bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c3.log 2>&1 || exit 1
           cd $OLDPWD; python tools/timeline.py $O/rp_c3/run_kernel_trace.csv --top 25 > $O/rp_c3_timeline.txt; python tools/trace_by_grid.py $O/rp_c3/run_kernel_trace.csv > $O/rp_c3_by_grid.txt 2>&1; head -20 $O/rp_c3_timeline.txt ;;
+    esweep) B2="--steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline $EXTRA"
+            for i in 1 2; do for v in base ${VARIANTS:-engine.enc_bwd_aux=1 engine.wgrad_early=1}; do
+              if [ $v = base ]; then run c2_${v}_$i 300 python bench.py $B2
+              else run c2_${v}_$i 300 python bench.py $B2 --set ${v//+/ --set }; fi; done; done
+            for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    esweep3) B3="--steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline"
+            for i in 1 2; do for v in base ${VARIANTS:-engine.wgrad_early=2 engine.wgrad_early=0}; do
+              if [ $v = base ]; then run c3_${v}_$i 300 python bench.py $B3
+              else run c3_${v}_$i 300 python bench.py $B3 --set ${v//+/ --set }; fi; done; done
+            for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
