@@ -136,6 +136,10 @@ for step in "$@"; do
               if [ $v = base ]; then run c3_${v}_$i 300 python bench.py $B3
               else run c3_${v}_$i 300 python bench.py $B3 --set ${v//+/ --set }; fi; done; done
             for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    libab) B2="--steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline $EXTRA"
+           for i in 1 2; do run c2_base_$i 300 python bench.py $B2
+             for L in $LIBS; do ALIGNN_HIP_LIB=$PWD/abl/lib$L.so run c2_${L}_$i 300 python bench.py $B2; done; done
+           for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
