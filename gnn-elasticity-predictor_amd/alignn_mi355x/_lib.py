@@ -165,6 +165,7 @@ _SIGNATURES = {
     "alignn_plan_replay": ([c_vp, c_vp], c_i32),
     "alignn_plan_replay_serial": ([c_vp, c_vp], c_i32),
     "alignn_plan_info": ([c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "alignn_plan_entries": ([c_vp, c_vp, c_vp, c_i64], c_i64),
     "alignn_plan_destroy": ([c_vp], c_i32),
     "alignn_plan_note_timestamp": ([c_vp], c_i32),
     "alignn_plan_elapsed_ms": ([c_vp, c_i32, c_i32, c_vp], c_i32),

@@ -207,6 +207,23 @@ extern "C" int alignn_plan_info(const void* plan, int64_t* launches, int64_t* wa
   return ALIGNN_OK;
 }
 
+// Introspection (tools/plan_dump.py): entry i as (kind, slot, src) — kind 0 kernel, 1 stream edge
+// (slot waits for src), 2 timestamp — and, for kernels, the device function's name.  Returns the
+// entry count; fills at most `cap` entries.
+extern "C" int64_t alignn_plan_entries(const void* plan, int32_t* kind_slot_src, const char** names, int64_t cap) {
+  const Plan* p = reinterpret_cast<const Plan*>(plan);
+  if (!p) return -1;
+  const int64_t n = (int64_t)p->entries.size();
+  for (int64_t i = 0; i < n && i < cap; ++i) {
+    const PlanEntry& e = p->entries[(size_t)i];
+    kind_slot_src[3 * i] = e.func ? 0 : (e.event < 0 ? 2 : 1);
+    kind_slot_src[3 * i + 1] = e.slot;
+    kind_slot_src[3 * i + 2] = e.func ? -1 : e.src;
+    if (names) names[i] = e.func ? hipKernelNameRefByPtr(e.func, p->streams[(size_t)e.slot]) : nullptr;
+  }
+  return n;
+}
+
 extern "C" int alignn_plan_replay(void* plan, void* stream) {
   Plan* p = reinterpret_cast<Plan*>(plan);
   if (!p) return ALIGNN_E_BAD_SHAPE;

@@ -664,6 +664,12 @@ int alignn_plan_replay(void* plan, void* stream);
  * device, so the plan timestamps give its isolated duration (the bench's roofline probes). */
 int alignn_plan_replay_serial(void* plan, void* stream);
 int alignn_plan_info(const void* plan, int64_t* launches, int64_t* waits, int64_t* streams, int64_t* arg_bytes);
+/* alignn_plan_entries(plan, kind_slot_src, names, cap): the recorded entries in issue order, entry i
+ * as kind_slot_src[3i..3i+2] = (kind, stream slot, source slot) — kind 0 kernel (source -1), 1 edge
+ * ("slot waits for source's work so far"), 2 timestamp — and names[i] the kernel's name (NULL for
+ * edges and timestamps; names may be NULL).  Fills at most cap entries; returns the entry count
+ * (-1 for a NULL plan).  Introspection of the step's stream structure (tools/plan_dump.py). */
+int64_t alignn_plan_entries(const void* plan, int32_t* kind_slot_src, const char** names, int64_t cap);
 int alignn_plan_destroy(void* plan);
 int alignn_plan_note_timestamp(void* stream);
 int alignn_plan_elapsed_ms(void* plan, int32_t i0, int32_t i1, float* ms);
