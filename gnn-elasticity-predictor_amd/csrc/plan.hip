@@ -179,7 +179,13 @@ extern "C" void* alignn_plan_end(void) {
     return nullptr;
   }
   bool ok = true;
-  for (auto& ev : p->events) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+  // Cross-stream edges of one device: no system-scope fence at the record.  The producing kernel's
+  // end-of-kernel release already makes its writes visible device-wide (as it does for the next
+  // kernel of its own stream); the default event adds a system-scope writeback that holds the source
+  // stream ~4 us per edge (tools/probe/marker_cost.hip: 7.2 us per kernel pair -> 11.1 with a default
+  // event between them, 8.8 without the system fence).
+  for (auto& ev : p->events)
+    ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
   for (auto& ev : p->stamps) ok = ok && hipEventCreate(&ev) == hipSuccess;
   if (!ok) {
     set_error("plan_end: event creation failed");

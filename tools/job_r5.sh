@@ -147,6 +147,10 @@ for step in "$@"; do
            if [ -n "$C3" ]; then for i in 1 2; do run c3_base_$i 300 python bench.py $B3
              for v in $ENVS; do (export $v; run c3_${v}_$i 300 python bench.py $B3); done; done; fi
            for f in $O/c[23]_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
+    libab3) B3="--steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline"
+           for i in 1 2; do run c3_base_$i 300 python bench.py $B3
+             for L in $LIBS; do ALIGNN_HIP_LIB=$PWD/abl/lib$L.so run c3_${L}_$i 300 python bench.py $B3; done; done
+           for f in $O/c3_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
