@@ -36,6 +36,8 @@ struct PlanEntry {
   int src;              // edge: slot whose work is waited for
   int event;            // edge: index into Plan::events; timestamp: -1 - index into Plan::stamps
   size_t arg0, nargs;   // kernel: first index into Plan::arg_off, count
+  bool reuse;           // edge: the source stream issued nothing since the previous edge from it
+                        // (that edge's event is recorded at the same point: wait on it, no new record)
 };
 
 struct Plan {
@@ -178,6 +180,26 @@ extern "C" void* alignn_plan_end(void) {
     set_error("plan_end: no plan is being recorded");
     return nullptr;
   }
+  // an edge from a stream that issued nothing since its previous edge (two streams waiting on one
+  // point, e.g. the aux and side streams both after a gate kernel of the main stream) reuses that
+  // edge's event: one marker on the source stream instead of two
+  {
+    std::vector<int> last_edge(p->streams.size(), -1);   // per source slot: event of its latest edge
+    for (PlanEntry& e : p->entries) {
+      if (e.func || e.event < 0) {   // the slot issued work (or a timestamp)
+        last_edge[(size_t)e.slot] = -1;
+        continue;
+      }
+      const int prev = last_edge[(size_t)e.src];
+      if (prev >= 0) {
+        e.reuse = true;
+        e.event = prev;
+      } else {
+        last_edge[(size_t)e.src] = e.event;
+      }
+      last_edge[(size_t)e.slot] = -1;   // the waiting stream's later work now also follows the source
+    }
+  }
   bool ok = true;
   // Cross-stream edges of one device: no system-scope fence at the record.  The producing kernel's
   // end-of-kernel release already makes its writes visible device-wide (as it does for the next
@@ -249,7 +271,7 @@ extern "C" int alignn_plan_replay(void* plan, void* stream) {
       hipError_t r = hipEventRecord(p->stamps[-1 - e.event], p->streams[e.slot]);
       if (r != hipSuccess) return hip_status(r, "plan_replay: timestamp");
     } else {
-      hipError_t r = hipEventRecord(p->events[e.event], p->streams[e.src]);
+      hipError_t r = e.reuse ? hipSuccess : hipEventRecord(p->events[e.event], p->streams[e.src]);
       if (r == hipSuccess) r = hipStreamWaitEvent(p->streams[e.slot], p->events[e.event], 0);
       if (r != hipSuccess) return hip_status(r, "plan_replay: stream edge");
     }
