@@ -131,6 +131,7 @@ _SIGNATURES = {
     "alignn_hetero_nll_amp": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_i64,
                                c_vp], c_i32),
     "alignn_add_noise_f32": ([c_i64, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_noisy_copy2_f32": ([c_i64, c_vp, c_vp, c_u64, c_i64, c_vp, c_vp, c_u64, c_f32, c_vp], c_i32),
     "alignn_ensemble_moments": ([c_i32, c_i64, c_i32, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_vp, c_vp], c_i32),
     "alignn_member_mean_f32": ([c_i32, c_i64, c_vp, c_i64, c_vp, c_vp], c_i32),

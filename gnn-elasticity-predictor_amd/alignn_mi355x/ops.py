@@ -1257,6 +1257,22 @@ def add_noise(x: torch.Tensor, std: float, seed: int):
                                           stream_ptr()), "alignn_add_noise_f32")
 
 
+def noisy_copies(x1: torch.Tensor, seed1: int, x2: torch.Tensor, seed2: int, std: float):
+    """(x1 + std * N(0, 1), x2 + std * N(0, 1)) as new contiguous fp32 tensors in one launch: the same
+    values as clone() + add_noise(seed_k) of each (alignn_noisy_copy2_f32)."""
+    _require(x1, "x1")
+    _require(x2, "x2")
+    x1, x2 = x1.contiguous(), x2.contiguous()
+    y1, y2 = torch.empty_like(x1), torch.empty_like(x2)
+    if std == 0.0:
+        copy_many([(y1, x1), (y2, x2)])
+        return y1, y2
+    check(_lib.lib().alignn_noisy_copy2_f32(x1.numel(), x1.data_ptr(), y1.data_ptr(), int(seed1) & (2**64 - 1),
+                                            x2.numel(), x2.data_ptr(), y2.data_ptr(), int(seed2) & (2**64 - 1),
+                                            float(std), stream_ptr()), "alignn_noisy_copy2_f32")
+    return y1, y2
+
+
 # ------------------------------------------------------------------------------------------------
 # Optimizer (clip_grad_norm_ + AdamW over the flat buffers)
 # ------------------------------------------------------------------------------------------------

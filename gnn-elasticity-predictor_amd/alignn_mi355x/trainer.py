@@ -156,10 +156,8 @@ class FusedTrainer:
         bc = batch_cache(batch)
         x, gx = batch.x, batch.global_x
         if training and self.jitter > 0.0:
-            x = ops.clone(x)
-            gx = ops.clone(gx)
-            ops.add_noise(x, self.jitter, site_seed(seed, 1 << 20))
-            ops.add_noise(gx, self.jitter, site_seed(seed, (1 << 20) + 1))
+            # jittered copies of the node and global features (train.py:641-646), one launch
+            x, gx = ops.noisy_copies(x, site_seed(seed, 1 << 20), gx, site_seed(seed, (1 << 20) + 1), self.jitter)
         out, ctx = model._engine.forward(st.P, batch, bc, training, seed, x, gx, "hetero")
         dout = torch.empty_like(out)
         # a batch padded to a capacity (store.BatchCapacity): the loss is the real graphs' mean and the

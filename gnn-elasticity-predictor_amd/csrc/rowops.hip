@@ -412,14 +412,31 @@ __global__ __launch_bounds__(256) void hetero_nll_amp_kernel(int64_t B, int T, c
   if (threadIdx.x == 0) *loss = red[0][0] / (float)total + l2 * (red[1][0] / (float)total);
 }
 
+// x + stdv * N(0, 1) of element i (Box-Muller over two counter hashes of (seed, i))
+__device__ __forceinline__ float jittered(float x, float stdv, uint64_t seed, int64_t i) {
+  const uint32_t a = hash_u32(seed, 2 * (uint64_t)i), b = hash_u32(seed, 2 * (uint64_t)i + 1);
+  const float u1 = ((float)a + 1.0f) * 2.3283064e-10f;  // (0, 1]
+  const float u2 = (float)b * 2.3283064e-10f;
+  const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
+  return x + stdv * z;
+}
+
 __global__ void add_noise_kernel(int64_t n, float* __restrict__ x, float stdv, uint64_t seed, const uint64_t* sptr) {
   seed = mix_seed(seed, sptr);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t a = hash_u32(seed, 2 * (uint64_t)i), b = hash_u32(seed, 2 * (uint64_t)i + 1);
-    const float u1 = ((float)a + 1.0f) * 2.3283064e-10f;  // (0, 1]
-    const float u2 = (float)b * 2.3283064e-10f;
-    const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
-    x[i] += stdv * z;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = jittered(x[i], stdv, seed, i);
+}
+
+// Two jittered copies in one launch (the step's node and global features, train.py:650-652):
+// dst_k[i] = src_k[i] + stdv * z_k(i), the same values as a copy followed by add_noise_kernel.
+__global__ void noisy_copy2_kernel(int64_t n1, const float* __restrict__ s1, float* __restrict__ d1, uint64_t seed1,
+                                   int64_t n2, const float* __restrict__ s2, float* __restrict__ d2, uint64_t seed2,
+                                   float stdv, const uint64_t* sptr) {
+  seed1 = mix_seed(seed1, sptr);
+  seed2 = mix_seed(seed2, sptr);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1 + n2; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n1) d1[i] = jittered(s1[i], stdv, seed1, i);
+    else d2[i - n1] = jittered(s2[i - n1], stdv, seed2, i - n1);
   }
 }
 
@@ -655,6 +672,17 @@ extern "C" int alignn_add_noise_f32(int64_t n, float* x, float stdv, uint64_t se
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   launch(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, x, stdv, seed, g_step_seed);
   ALIGNN_LAUNCH_CHECK("add_noise_kernel");
+  return ALIGNN_OK;
+}
+
+extern "C" int alignn_noisy_copy2_f32(int64_t n1, const float* src1, float* dst1, uint64_t seed1, int64_t n2,
+                                      const float* src2, float* dst2, uint64_t seed2, float stdv, void* stream) {
+  if (n1 < 0 || n2 < 0) return ALIGNN_E_BAD_SHAPE;
+  if (n1 + n2 == 0) return ALIGNN_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  launch(noisy_copy2_kernel, dim3(grid_for(n1 + n2)), dim3(256), 0, s, n1, src1, dst1, seed1, n2, src2, dst2, seed2,
+         stdv, g_step_seed);
+  ALIGNN_LAUNCH_CHECK("noisy_copy2_kernel");
   return ALIGNN_OK;
 }
 

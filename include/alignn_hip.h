@@ -500,6 +500,10 @@ int alignn_hetero_nll_amp(int64_t B, int32_t T, const float* heads, int64_t ldh,
 
 /* Feature jitter (train.py:641-646): x += std * N(0,1) from a counter-based generator. */
 int alignn_add_noise_f32(int64_t n, float* x, float std, uint64_t seed, void* stream);
+/* Both jittered feature copies of a step in one launch: dst_k[i] = src_k[i] + std * N(0,1), the same
+ * values as copying src_k to dst_k and calling alignn_add_noise_f32(n_k, dst_k, std, seed_k). */
+int alignn_noisy_copy2_f32(int64_t n1, const float* src1, float* dst1, uint64_t seed1, int64_t n2,
+                           const float* src2, float* dst2, uint64_t seed2, float std, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Deep-ensemble inference: moment-matched mixture of M heteroscedastic members,

@@ -265,3 +265,22 @@ def test_borrowed_streams_are_the_lenders_and_the_step_is_unchanged():
             assert m._engine.ctx.aux(DEV).cuda_stream == lender.aux(DEV).cuda_stream
         res.append((loss, tr.st.grad.clone()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_noisy_copies_equal_clone_then_add_noise():
+    """The trainer's one-launch jitter (alignn_noisy_copy2_f32) against the two copies + two
+    add_noise launches it replaced: bitwise; the sources untouched."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(1920, 206, generator=g).to(DEV)
+    gx = torch.randn(32, 289, generator=g).to(DEV)
+    x0, gx0 = x.clone(), gx.clone()
+    r1, r2 = x.clone(), gx.clone()
+    ops.add_noise(r1, 0.05, 123)
+    ops.add_noise(r2, 0.05, 456)
+    y1, y2 = ops.noisy_copies(x, 123, gx, 456, 0.05)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, r1) and torch.equal(y2, r2)
+    assert torch.equal(x, x0) and torch.equal(gx, gx0)
+    z1, z2 = ops.noisy_copies(x, 123, gx, 456, 0.0)
+    assert torch.equal(z1, x) and torch.equal(z2, gx)
