@@ -764,6 +764,10 @@ class AlignnEngine:
         self.atom_bf16 = True
         # bf16 storage: the line graph's source-side backward gathers Q and dout as bf16 copies
         self.bf16_src = True
+        # bf16 storage: the atom blocks' edge-feature gradient (the gradient autocast returns through
+        # its bf16 cast of the bond states) stored in bf16 between the atom attention backward that
+        # writes it and the line block's gate kernel that adds it (half the bytes of both)
+        self.bf16_atom_grad = True
         # the line convs' edge features (the angle encoder's hidden layer, [T, 256]) recomputed inside
         # the attention kernels from the 11 raw inputs instead of materialised and re-read 8 times
         # (ops.lg_fwd_x / lg_bwd_dst_x; the deferred encoder backward recomputes its ReLU mask)
@@ -1043,7 +1047,12 @@ class AlignnEngine:
         # atom_stream 1/2: each atom block's edge-feature gradient into a buffer of its own, added to
         # the bond-state gradient before the line block's backward; 2: the atom blocks on the aux
         # stream, atom block l-1 beside line block l (it reads only dh and its own forward state)
-        dF_atom = torch.empty(L, E, D, device=dev) if atom_mode else None
+        # bf16 storage: the atom blocks' edge-feature gradient as autocast returns it through the bf16
+        # cast of the bond states for edge_proj (train.py:325/:333 under :632-636) — written by the atom
+        # attention backward, read by the next line block's gate kernel
+        df_bf16 = self.bf16_atom_grad and self._bf16_io(D) and T > 0 and self.debug is None
+        dF_atom = (torch.empty(L, E, D, device=dev, dtype=torch.bfloat16 if df_bf16 else torch.float32)
+                   if atom_mode else None)
         aux = ops.aux_stream(dev) if (atom_mode == 2 and side is not None) else None
 
         def atom_bwd(l):

@@ -903,6 +903,11 @@ def tconv_bwd_dst(g: GraphCSR, D: int, H: int, QKVR, U, Vd, wbar, F, feat_row, d
         raise ValueError("tconv_bwd_dst: U, Vd, Sz must be [n, H, D] and dq [n, >= D]")
     if dF is not None and dF.size(0) < F.size(0):
         raise ValueError("tconv_bwd_dst: dF must cover the rows of F")
+    if dF is not None and dF.dtype == torch.bfloat16:
+        # bf16 storage: the edge features' gradient as autocast's bf16 cast returns it (write-only)
+        if accumulate_dF & 1:
+            raise ValueError("tconv_bwd_dst: a bf16 dF is written, not accumulated")
+        accumulate_dF = int(accumulate_dF) | 4
     fbf = F is not None and F.dtype == torch.bfloat16
     profiling.launch(f"tconv_bwd_dst n{g.n} m{g.m}" + (" F16" if fbf else ""), 0.0,
                      _tconv_bytes(g.n, g.m, D, H, "bwd_dst", 0 if dF is None else (2 if accumulate_dF & 1 else 1),
@@ -1147,10 +1152,11 @@ def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_w
     if dout.shape != outp.shape:
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
     wsize = int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D))
-    if R.dtype == torch.bfloat16 or dR.dtype == torch.bfloat16:
-        # bf16 storage: R read / dR written in bf16 (alignn_gate_ln_bwd_partials_ex + _reduce)
+    x2bf = dX_add is not None and dX_add.dtype == torch.bfloat16
+    if R.dtype == torch.bfloat16 or dR.dtype == torch.bfloat16 or x2bf:
+        # bf16 storage: R read / dR written / dX_add read in bf16 (alignn_gate_ln_bwd_partials_ex + _reduce)
         if dX_add is not None:
-            _require(dX_add, "gate_ln_bwd dX_add")
+            _require(dX_add, "gate_ln_bwd dX_add", dX_add.dtype if x2bf else torch.float32)
             if tuple(dX_add.shape) != (n, D) or not dX_add.is_contiguous():
                 raise ValueError("gate_ln_bwd: dX_add must be a contiguous [n, D] tensor")
         red = reduce_stream if reduce_stream is not None else torch.cuda.current_stream(outp.device)
@@ -1158,7 +1164,8 @@ def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_w
               else WS.get("gate_ln", wsize, outp.device))
         check(_lib.lib().alignn_gate_ln_bwd_partials_ex(n, D, dXnew.data_ptr(), dXnew.stride(0), _p(dX_add),
                                                         outp.data_ptr(), rp, R.data_ptr(), R.stride(0),
-                                                        int(R.dtype == torch.bfloat16), wbeta.data_ptr(),
+                                                        int(R.dtype == torch.bfloat16) | (2 if x2bf else 0),
+                                                        wbeta.data_ptr(),
                                                         ln_w.data_ptr(), ln_b.data_ptr(), beta.data_ptr(),
                                                         mu.data_ptr(), rstd.data_ptr(), dout.data_ptr(), dR.data_ptr(),
                                                         dR.stride(0), int(dR.dtype == torch.bfloat16), ws.data_ptr(),

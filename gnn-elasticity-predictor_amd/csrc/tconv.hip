@@ -123,7 +123,7 @@ struct BwdDstParams {
   float* dq; int64_t lddq;
   float* Sz; float* sigz;
   float* dz_e; float* alpha_e;
-  float* dF; int64_t lddf; int acc_dF, pad2_;
+  float* dF; int64_t lddf; int acc_dF, dfbf;   // dfbf: dF written as bf16 (acc_dF bit 0 clear)
   DropParams drop;
   int fbf, pad3_;   // F holds bf16 elements (ldf in elements)
 };
@@ -579,7 +579,8 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
             float df[VPL];
 #pragma unroll
             for (int i = 0; i < VPL; ++i) df[i] = (p.acc_dF & 2) ? (ring[j].f[i] > 0.f ? old[j][i] : 0.f) : old[j][i];
-            vstore(p.dF + rows_[j] * p.lddf + j0, df);
+            if (p.dfbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dF) + rows_[j] * p.lddf + j0, df);
+            else vstore(p.dF + rows_[j] * p.lddf + j0, df);
           }
         }
       }
@@ -1073,8 +1074,15 @@ extern "C" int alignn_tconv_bwd_dst_ex(int64_t n, int64_t m, int32_t D, int32_t 
   if (!f_bf16 && dF == nullptr && lg3_supported(D, H, feat_row, Ff, sched))
     return lg3_bwd_dst(n, m, H, off_dst, src_at, sched, QKVR, ldq, U, Vd, wbar, Ff, ldf, dout, outp, mstat, den, dq,
                        lddq, Sz, sigz, dz_e, alpha_e, make_drop(drop_p, seed), s);
+  // accumulate_dF bit 2: dF is written as bf16 (the gradient of autocast's bf16 cast of the edge
+  // features, train.py:325/:333 under :632-636); not with bit 0 (no bf16 read-modify-write)
+  const int dfbf = (accumulate_dF >> 2) & 1;
+  if (dfbf && (dF == nullptr || (accumulate_dF & 1) || lddf % 4 || (reinterpret_cast<uintptr_t>(dF) & 7))) {
+    set_error("tconv_bwd_dst: a bf16 dF is write-only, 8-byte aligned rows (lddf %% 4 == 0)");
+    return ALIGNN_E_BAD_SHAPE;
+  }
   BwdDstParams p{n, m, D, 0, off_dst, src_at, feat_row, QKVR, ldq, U, Vd, wbar, Ff, ldf, dout, outp, mstat, den,
-                 dq, lddq, Sz, sigz, dz_e, alpha_e, dF, lddf, accumulate_dF, 0, make_drop(drop_p, seed)};
+                 dq, lddq, Sz, sigz, dz_e, alpha_e, dF, lddf, accumulate_dF & 3, dfbf, make_drop(drop_p, seed)};
   p.fbf = f_bf16 ? 1 : 0;
   const Sched sc = make_sched(sched, n);
   ALIGNN_DISPATCH_VH(vpl_for(D), H, launch_bwd_dst, p, sc, s);

@@ -291,7 +291,9 @@ int alignn_tconv_fwd(int64_t n, int64_t m, int32_t D, int32_t H,
  *   dz_e[t,h] = dzs, alpha_e[t,h] = alpha' (for the source-side pass)
  *   dF[row(t)] (+)= sum_h dzs u[d,h] + alpha' Vd[d,h]   (row(t) = feat_row[t] or t)
  *   accumulate_dF: bit 0 = add to dF, bit 1 = multiply the result by (F[row(t)] > 0) (F is a
- *   ReLU output, e.g. the angle-encoder hidden layer: its backward mask is applied in place)
+ *   ReLU output, e.g. the angle-encoder hidden layer: its backward mask is applied in place),
+ *   bit 2 = dF holds bf16 elements, written (RNE) not accumulated (config C3: the gradient of the
+ *   bf16 edge features autocast hands edge_proj is a bf16 tensor; rows 8-byte aligned, lddf % 4 == 0)
  * given dout (gradient of the aggregated message, [n, D]), outp (the aggregated message),
  * Vd[d,h] = M_h^T dout[d,h].  dF may be NULL (the line graph defers the angle-encoder backward to
  * alignn_enc_bwd_f32, which recomputes the per-edge gradient there). */
@@ -452,7 +454,8 @@ int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t 
  * train.py:632-636): r_bf16 = R is the skip projection's bf16 output; Xnew16 (may be NULL) receives
  * a bf16 copy of the new state, the next Linear's input as autocast casts it; dr_bf16 = dR is written
  * as bf16.  LayerNorm, the gate and every accumulation stay fp32.  bf16 rows: 8-byte aligned,
- * leading dimension % 4 == 0. */
+ * leading dimension % 4 == 0.  alignn_gate_ln_bwd_partials_ex: r_bf16 bit 1 = dX_add holds bf16
+ * elements (the atom block's edge-feature gradient under autocast, alignn_tconv_bwd_dst_ex bit 2). */
 int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows, const void* R,
                           int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X, int64_t ldx,
                           const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, uint16_t* Xnew16,

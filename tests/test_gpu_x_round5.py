@@ -284,3 +284,27 @@ def test_noisy_copies_equal_clone_then_add_noise():
     assert torch.equal(x, x0) and torch.equal(gx, gx0)
     z1, z2 = ops.noisy_copies(x, 123, gx, 456, 0.0)
     assert torch.equal(z1, x) and torch.equal(z2, gx)
+
+
+def test_bf16_atom_edge_gradient_is_a_bf16_rounding():
+    """bf16 storage (config C3): the atom blocks' edge-feature gradient stored in bf16
+    (engine.bf16_atom_grad; alignn_tconv_bwd_dst_ex bit 2, alignn_gate_ln_bwd_partials_ex r_bf16 bit 1)
+    against fp32 storage: the same loss (forward untouched), every gradient within bf16 rounding of
+    that one tensor (normwise 1e-2), and the bf16 gradient deterministic."""
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_batch
+    res = []
+    for on in (False, True, True):
+        torch.manual_seed(0)
+        model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 256, 4, 4, 0.15), 2).to(DEV)
+        model._engine.bf16_atom_grad = on
+        model._engine.atom_stream = 2
+        tr = A.FusedTrainer(model, precision="bf16")
+        loss = tr.forward_backward(mp_like_batch(32).to(DEV), 3).clone()
+        torch.cuda.synchronize()
+        res.append((loss, tr.st.grad.clone()))
+    (l0, g0), (l1, g1), (l2, g2) = res
+    assert torch.equal(l0, l1) and torch.equal(l1, l2)
+    assert torch.equal(g1, g2)
+    rel = float((g1.double() - g0.double()).norm() / g0.double().norm())
+    assert 0.0 < rel < 1e-2, rel
