@@ -542,7 +542,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
                    wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None,
-                   bf16_src: bool = True) -> None:
+                   bf16_src: bool = True, dX_zero: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -557,7 +557,8 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     products; 1: once dQ is final, before the dX products; 2: those final after the target-side
     kernel (dM, dw̄, the skip projection's) right after it, the rest once dQ is final.
     dX_add: a second part of the incoming gradient (the atom block's edge-feature gradient), added
-    to dX by the gate kernel (ops.gate_ln_bwd)."""
+    to dX by the gate kernel (ops.gate_ln_bwd).  dX_zero: dX holds nothing yet (the last line
+    block, whose output only the atom block beside it reads): the incoming gradient is dX_add."""
     n, D = c.X.shape
     H = c.H
     C = D // H
@@ -574,7 +575,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
         dR = torch.empty(n, D, device=dev, dtype=c.R.dtype)   # bf16 storage: the gradient of a bf16 output
     ops.gate_ln_bwd(dX, c.outp, c.R, cv.wbeta, cv.lnw, cv.lnb, c.beta, c.mu, c.rstd, dout, dR, gv.wbeta, gv.lnw,
                     gv.lnb, c.p, c.seed_blk, outp_rows=c.outp_rows, reduce_stream=side if gate_reduce_side else None,
-                    dX_add=dX_add)
+                    dX_add=dX_add, dX_zero=dX_zero)
     Wb = cv.Wqkvr   # B operand [4D, D]
     dout_a = dout if (rows is None or c.outp_rows is not None) else ops.gather_rows(dout, rows)
     Vd = torch.empty(na, H, D, device=dev)
@@ -982,8 +983,19 @@ class AlignnEngine:
             return ctx.shared, ctx
         if mode == "hetero":
             out = torch.empty(B, 2 * Tt, device=dev)
-            ops.gemm(ctx.shared, P.Wmean.t(), out[:, :Tt], bias=P.bmean)
-            ops.gemm(ctx.shared, P.Wlogvar.t(), out[:, Tt:], bias=P.blogvar)
+            dw = P.Wlogvar.storage_offset() - P.Wmean.storage_offset()
+            db = P.blogvar.storage_offset() - P.bmean.storage_offset()
+            if (dw > 0 and db > 0 and P.Wmean.is_contiguous() and P.Wlogvar.is_contiguous()
+                    and P.Wmean.untyped_storage().data_ptr() == P.Wlogvar.untyped_storage().data_ptr()
+                    and P.bmean.untyped_storage().data_ptr() == P.blogvar.untyped_storage().data_ptr()):
+                # both heads in one batched launch (the flat parameter buffer holds them at a fixed
+                # distance): the same per-head products as two launches, bit for bit
+                Wb = torch.as_strided(P.Wmean, (2, D, Tt), (dw, 1, D))
+                bb = torch.as_strided(P.bmean, (2, Tt), (db, 1))
+                ops.gemm(ctx.shared, Wb, torch.as_strided(out, (2, B, Tt), (Tt, 2 * Tt, 1)), bias=bb)
+            else:
+                ops.gemm(ctx.shared, P.Wmean.t(), out[:, :Tt], bias=P.bmean)
+                ops.gemm(ctx.shared, P.Wlogvar.t(), out[:, Tt:], bias=P.blogvar)
             return out, ctx
         out = torch.empty(B, Tt, device=dev)
         ops.gemm(ctx.shared, P.Wout.t(), out, bias=P.bout)
@@ -1026,11 +1038,17 @@ class AlignnEngine:
         with _side_work(side, (dpre, ctx.feats)):
             ops.gemm(dpre.t(), ctx.feats, g[pre + "feat_proj.0.weight"], rowsum=g[pre + "feat_proj.0.bias"])
         Wfeat = ctx.feats.size(1)
-        dfeats = ops.zeros(B, Wfeat, device=dev)
+        dfeats = torch.empty(B, Wfeat, device=dev)   # the pooling backward reads its first D columns only
         ops.gemm(dpre, Wf[:, :D], dfeats[:, :D])
         dh = torch.empty(N, D, device=dev)
         ops.readout_pool_bwd(dfeats, bc.ptr, bc.batch_vec, dh, False, p_drop, site_seed(seed, 4 * L))
-        de = ops.zeros(E, D, device=dev)
+        atom_mode = self._atom_mode(T, E)
+        # the last line block's output feeds only the atom block beside it, whose edge-feature gradient
+        # (dF_atom, atom_mode >= 1) is that block's whole incoming gradient: its gate kernel writes de
+        # from it instead of adding it to a zero-filled de (ops.gate_ln_bwd dX_zero)
+        de_fresh = (atom_mode >= 1 and L > 0 and T > 0 and self.debug is None and ctx.edge[L - 1] is not None
+                    and ctx.node[L - 1] is not None)
+        de = torch.empty(E, D, device=dev) if de_fresh else ops.zeros(E, D, device=dev)
         defer = (self.defer_angle_bwd and ctx.has_angle and T > 0 and E > 0 and L > 0
                  and ops.enc_bwd_ok(D, cfg.heads, L, bc.xa.size(1)))
         da = torch.empty(T, D, device=dev) if (T > 0 and not defer) else None
@@ -1043,7 +1061,6 @@ class AlignnEngine:
         if line_proj:
             dMl_all = torch.empty(L, D, D, device=dev)
             dwl_all = torch.empty(L, D, device=dev)
-        atom_mode = self._atom_mode(T, E)
         # atom_stream 1/2: each atom block's edge-feature gradient into a buffer of its own, added to
         # the bond-state gradient before the line block's backward; 2: the atom blocks on the aux
         # stream, atom block l-1 beside line block l (it reads only dh and its own forward state)
@@ -1093,11 +1110,13 @@ class AlignnEngine:
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src)
+                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src,
+                                   dX_zero=de_fresh and l == L - 1)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src)
+                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src,
+                                   dX_zero=de_fresh and l == L - 1)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

@@ -1141,19 +1141,22 @@ def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, see
 
 def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_wbeta, d_ln_w, d_ln_b, drop_p, seed,
                 outp_rows=None, reduce_stream: Optional[torch.cuda.Stream] = None,
-                dX_add: Optional[torch.Tensor] = None):
+                dX_add: Optional[torch.Tensor] = None, dX_zero: bool = False):
     """outp_rows: as in gate_ln_fwd; dout then has outp's (compacted) rows and only those are written.
     reduce_stream: run the parameter-gradient reduction (d_wbeta, d_ln_w, d_ln_b) there, after the
     row kernel, off the current stream (nothing on it reads those gradients).
     dX_add: [n, D] contiguous addend of the incoming gradient; dXnew += dX_add is written back
-    (alignn_gate_ln_bwd_partials_add)."""
+    (alignn_gate_ln_bwd_partials_add).  dX_zero: dXnew holds nothing yet (read as zero, not loaded;
+    needs dX_add): the incoming gradient is dX_add, written to dXnew."""
     n, D = R.shape
     rp = _check_outp_rows(outp, outp_rows, n)
     if dout.shape != outp.shape:
         raise ValueError("gate_ln_bwd: dout must have outp's shape")
     wsize = int(_lib.lib().alignn_gate_ln_bwd_workspace(int(n), D))
     x2bf = dX_add is not None and dX_add.dtype == torch.bfloat16
-    if R.dtype == torch.bfloat16 or dR.dtype == torch.bfloat16 or x2bf:
+    if dX_zero and dX_add is None:
+        raise ValueError("gate_ln_bwd: dX_zero needs dX_add")
+    if R.dtype == torch.bfloat16 or dR.dtype == torch.bfloat16 or x2bf or dX_zero:
         # bf16 storage: R read / dR written / dX_add read in bf16 (alignn_gate_ln_bwd_partials_ex + _reduce)
         if dX_add is not None:
             _require(dX_add, "gate_ln_bwd dX_add", dX_add.dtype if x2bf else torch.float32)
@@ -1164,7 +1167,8 @@ def gate_ln_bwd(dXnew, outp, R, wbeta, ln_w, ln_b, beta, mu, rstd, dout, dR, d_w
               else WS.get("gate_ln", wsize, outp.device))
         check(_lib.lib().alignn_gate_ln_bwd_partials_ex(n, D, dXnew.data_ptr(), dXnew.stride(0), _p(dX_add),
                                                         outp.data_ptr(), rp, R.data_ptr(), R.stride(0),
-                                                        int(R.dtype == torch.bfloat16) | (2 if x2bf else 0),
+                                                        int(R.dtype == torch.bfloat16) | (2 if x2bf else 0)
+                                                        | (4 if dX_zero else 0),
                                                         wbeta.data_ptr(),
                                                         ln_w.data_ptr(), ln_b.data_ptr(), beta.data_ptr(),
                                                         mu.data_ptr(), rstd.data_ptr(), dout.data_ptr(), dR.data_ptr(),

@@ -128,7 +128,8 @@ struct GateBwdParams {
   const int32_t* orow;  // optional: o and dout rows through this map (-1: o = 0, dout not written)
   const float* dX2;     // optional [n, D] addend: the incoming gradient is dXn + dX2, written back to dXn
   int rbf, drbf;        // bf16 storage: R read as bf16, dR written as bf16 (autocast: grad of a bf16 output)
-  int x2bf, pad3_;      // dX2 holds bf16 elements (the atom block's edge-feature gradient under autocast)
+  int x2bf;            // dX2 holds bf16 elements (the atom block's edge-feature gradient under autocast)
+  int dxz;              // dXn holds no gradient yet: read as zero (with dX2: the sum is dX2, written to dXn)
 };
 
 template <int VPL, bool IO>
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
       if (orow >= 0) vload(p.outp + orow * D + j0, o);
       if (IO && p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
       else vload(p.R + row * p.ldr + j0, r);
-      vload(p.dXn + row * p.lddx + j0, gx);
+      if (!p.dxz) vload(p.dXn + row * p.lddx + j0, gx);
       if (p.dX2) {   // one add per element, the sum kept as the residual's gradient
         float x2[VPL];
         if (IO && p.x2bf) vload_bf(reinterpret_cast<const uint16_t*>(p.dX2) + row * D + j0, x2);
@@ -522,9 +523,15 @@ extern "C" int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew
     set_error("gate_ln_bwd: unsupported hidden %d", D);
     return ALIGNN_E_UNSUPPORTED;
   }
-  // r_bf16 bit 0: R is bf16; bit 1: dX_add is bf16
+  // r_bf16 bit 0: R is bf16; bit 1: dX_add is bf16; bit 2: dXnew is read as zero (needs dX_add; the
+  // incoming gradient is dX_add alone and is written to dXnew — no zero fill of dXnew beforehand)
   const int x2bf = (r_bf16 >> 1) & 1;
+  const int dxz = (r_bf16 >> 2) & 1;
   r_bf16 &= 1;
+  if (dxz && !dX_add) {
+    set_error("gate_ln_bwd: a zero dXnew needs dX_add");
+    return ALIGNN_E_BAD_SHAPE;
+  }
   if ((r_bf16 && (ldr % 4 || (reinterpret_cast<uintptr_t>(R) & 7))) ||
       (dr_bf16 && (lddr % 4 || (reinterpret_cast<uintptr_t>(dR) & 7))) ||
       (x2bf && (!dX_add || D % 4 || (reinterpret_cast<uintptr_t>(dX_add) & 7)))) {
@@ -535,7 +542,7 @@ extern "C" int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew
   const int nwaves = (int)std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n);
   GateBwdParams p{n, D, 0, dXnew, lddx, outp, reinterpret_cast<const float*>(R), ldr, wbeta, ln_w, ln_b, beta, mu, rstd,
                   dout, reinterpret_cast<float*>(dR), lddr, workspace, nwaves, 0, make_drop(drop_p, seed), outp_rows,
-                  dX_add, r_bf16 ? 1 : 0, dr_bf16 ? 1 : 0, x2bf, 0};
+                  dX_add, r_bf16 ? 1 : 0, dr_bf16 ? 1 : 0, x2bf, dxz};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((nwaves + 3) / 4));
   const bool io = r_bf16 || dr_bf16 || x2bf;

@@ -455,7 +455,9 @@ int alignn_gate_ln_bwd_partials_add(int64_t n, int32_t D, float* dXnew, int64_t 
  * a bf16 copy of the new state, the next Linear's input as autocast casts it; dr_bf16 = dR is written
  * as bf16.  LayerNorm, the gate and every accumulation stay fp32.  bf16 rows: 8-byte aligned,
  * leading dimension % 4 == 0.  alignn_gate_ln_bwd_partials_ex: r_bf16 bit 1 = dX_add holds bf16
- * elements (the atom block's edge-feature gradient under autocast, alignn_tconv_bwd_dst_ex bit 2). */
+ * elements (the atom block's edge-feature gradient under autocast, alignn_tconv_bwd_dst_ex bit 2);
+ * bit 2 = dXnew holds no gradient yet (read as zero; needs dX_add, whose values are written to dXnew):
+ * the last line block's incoming gradient, which comes from the atom block beside it alone. */
 int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows, const void* R,
                           int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X, int64_t ldx,
                           const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, uint16_t* Xnew16,

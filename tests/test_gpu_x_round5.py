@@ -308,3 +308,28 @@ def test_bf16_atom_edge_gradient_is_a_bf16_rounding():
     assert torch.equal(g1, g2)
     rel = float((g1.double() - g0.double()).norm() / g0.double().norm())
     assert 0.0 < rel < 1e-2, rel
+
+
+def test_batched_heads_equal_two_products():
+    """engine.forward's heads: mean and logvar Linear in one batched launch over the flat parameter
+    buffer (strided views) give the two separate products' bits; and the engine's zero-free bond
+    gradient (gate dX_zero) keeps the step equal to the reference configuration within rounding."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(9)
+    B, D, Tt = 32, 256, 2
+    flat = torch.randn(4096, generator=g).to(DEV)
+    Wm = flat[0:Tt * D].view(Tt, D)
+    bm = flat[Tt * D:Tt * D + Tt]
+    off = Tt * D + Tt + 6
+    Wl = flat[off:off + Tt * D].view(Tt, D)
+    bl = flat[off + Tt * D:off + Tt * D + Tt]
+    shared = torch.randn(B, D, generator=g).to(DEV)
+    ref = torch.empty(B, 2 * Tt, device=DEV)
+    ops.gemm(shared, Wm.t(), ref[:, :Tt], bias=bm)
+    ops.gemm(shared, Wl.t(), ref[:, Tt:], bias=bl)
+    out = torch.full((B, 2 * Tt), float("nan"), device=DEV)
+    dw, db = Wl.storage_offset() - Wm.storage_offset(), bl.storage_offset() - bm.storage_offset()
+    ops.gemm(shared, torch.as_strided(Wm, (2, D, Tt), (dw, 1, D)), torch.as_strided(out, (2, B, Tt), (Tt, 2 * Tt, 1)),
+             bias=torch.as_strided(bm, (2, Tt), (db, 1)))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
