@@ -333,3 +333,20 @@ def test_batched_heads_equal_two_products():
              bias=torch.as_strided(bm, (2, Tt), (db, 1)))
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+def test_bf16_trainer_with_torch_optimizer():
+    """a bf16 trainer with torch's optimizer builds and steps (no GradScaler by
+    default there); asking for one with torch's optimizer is refused."""
+    import alignn_mi355x as A
+    from alignn_mi355x.synthetic import mp_like_batch
+    torch.manual_seed(0)
+    model = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, 64, 1, 1, 0.0), 2).to(DEV)
+    tr = A.FusedTrainer(model, precision="bf16", optimizer="torch")
+    assert tr.scaler is None
+    before = tr.st.flat.clone()
+    loss = tr.step(mp_like_batch(4).to(DEV), seed=1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all() and not torch.equal(before, tr.st.flat)
+    with pytest.raises(ValueError):
+        A.FusedTrainer(model, precision="bf16", optimizer="torch", grad_scaler=True)
