@@ -769,6 +769,9 @@ class AlignnEngine:
         # its bf16 cast of the bond states) stored in bf16 between the atom attention backward that
         # writes it and the line block's gate kernel that adds it (half the bytes of both)
         self.bf16_atom_grad = True
+        # with the atom blocks on the aux stream: the node encoder and the atom projection folds there
+        # too (forward prologue)
+        self.encoders_aux = True
         # the line convs' edge features (the angle encoder's hidden layer, [T, 256]) recomputed inside
         # the attention kernels from the 11 raw inputs instead of materialised and re-read 8 times
         # (ops.lg_fwd_x / lg_bwd_dst_x; the deferred encoder backward recomputes its ReLU mask)
@@ -915,9 +918,22 @@ class AlignnEngine:
             with _side_work(side, (a,)):
                 self._angle_hidden(P, bc, D, dev, a)
         line_proj = T > 0 and E > 0 and L > 0 and ctx.has_angle
-        # encoders (train.py:547-556)
-        ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
-                                   P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
+        # atom blocks on the aux stream: atom block l waits for line block l, line block l+1 does not
+        # wait for it (it reads only the bond states); the readout joins the aux stream
+        aux = ops.aux_stream(dev) if (self._atom_mode(T, E) == 2 and side is not None) else None
+        # encoders (train.py:547-556).  With the atom blocks on the aux stream, the node encoder and the
+        # atom blocks' projection folds (what only atom block 0 reads) run there too, beside the edge
+        # encoder and the first line block
+        atom_pre = aux is not None and self.encoders_aux
+        if atom_pre:
+            with _side_work(aux, (x,)):
+                ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
+                                           P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
+                if E > 0 and L > 0:
+                    ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
+        else:
+            ctx.h1n, h = self._mlp_fwd(x, P.enc("node", 0, "weight"), P.enc("node", 0, "bias"),
+                                       P.enc("node", 2, "weight"), P.enc("node", 2, "bias"))
         if edge_attr.numel() > 0:
             ctx.h1e, e = self._mlp_fwd(edge_attr, P.enc("edge", 0, "weight"), P.enc("edge", 0, "bias"),
                                        P.enc("edge", 2, "weight"), P.enc("edge", 2, "bias"))
@@ -931,11 +947,8 @@ class AlignnEngine:
         ctx.edge, ctx.node = [], []
         if line_proj:
             self._line_proj(P, ctx, L, D)
-        if E > 0 and L > 0:
+        if E > 0 and L > 0 and not atom_pre:
             ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
-        # atom blocks on the aux stream: atom block l waits for line block l, line block l+1 does not
-        # wait for it (it reads only the bond states); the readout joins the aux stream
-        aux = ops.aux_stream(dev) if (self._atom_mode(T, E) == 2 and side is not None) else None
         bf16_io = self._bf16_io(D) and bc.lg is not None and bc.lg.rows is not None
         e16 = None   # bf16 copy of the bond state (written by the previous line block's gate kernel)
         for l in range(L):
