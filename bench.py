@@ -112,7 +112,11 @@ def apply_settings(args, model):
             if not hasattr(model._engine, attr):
                 raise ValueError(f"unknown engine option {attr}")
             cur = getattr(model._engine, attr)
-            setattr(model._engine, attr, int(v) if (isinstance(cur, int) and not isinstance(cur, bool)) else bool(int(v)))
+            if isinstance(cur, str):
+                setattr(model._engine, attr, v)
+            else:
+                setattr(model._engine, attr,
+                        int(v) if (isinstance(cur, int) and not isinstance(cur, bool)) else bool(int(v)))
         elif k == "optimizer":
             kw["optimizer"] = v
         elif k == "loader_priority":
