@@ -188,6 +188,8 @@ _SIGNATURES = {
     "alignn_colsum_bf16": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp], c_i32),
     "alignn_gate_ln_fwd_ex": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
+    "alignn_gate_ln_fwd_ex2": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                                c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_gate_ln_bwd_partials_ex": ([c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_f32, c_u64, c_vp], c_i32),
     "alignn_grad_norm_amp_f32": ([c_vp, c_i64, c_vp, c_vp, c_vp, c_vp], c_i32),

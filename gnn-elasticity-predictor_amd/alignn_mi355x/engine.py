@@ -437,7 +437,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
                   seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
                   skip_early: bool = False, bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
-                  want_X16: bool = False, angle_x=None):
+                  want_X16: bool = False, angle_x=None, Xa: Optional[torch.Tensor] = None, want_Xa: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     bf16_io (bf16 storage, config C3 — the tensor dtypes of the reference's autocast, train.py:632-636):
     on a compacted graph the skip projection's output R and, in the backward, its gradient dR are
@@ -451,6 +451,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
     compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
     (no zero-filled [n, D] copy; the backward writes the compacted dout directly).
+    Xa: the active rows of X, already gathered (by the previous line block's gate kernel); want_Xa:
+    this block's gate kernel writes the active rows of its new state to c.Xa_next (compact_gate).
 
     Compacted graphs (g.rows set: the graph's nodes are the active subset ``rows`` of X's rows, see
     BatchCache): Q/K/V, the attention and its per-node GEMMs run over the active rows only; the
@@ -477,7 +479,7 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
         if early:
             with _side_work(side, (X, Xs, c.R)):   # skip projection of all rows, beside Q/K/V and the attention
                 ops.gemm(Xs, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
-        c.Xa = ops.gather_rows(X, rows)
+        c.Xa = Xa if Xa is not None else ops.gather_rows(X, rows)
         c.QKV = torch.empty(na, 3 * D, device=dev)
         ops.gemm(c.Xa, cv.Wqkvr[:3 * D].t(), c.QKV, bias=cv.bqkvr[:3 * D])
         if not early:
@@ -531,8 +533,10 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.beta = torch.empty(n, device=dev)
     c.mu = torch.empty(n, device=dev)
     c.rstd = torch.empty(n, device=dev)
+    c.Xa_next = (torch.empty(na, D, device=dev) if (want_Xa and rows is not None and c.outp_rows is not None)
+                 else None)
     ops.gate_ln_fwd(c.outp, c.R, cv.wbeta, X, cv.lnw, cv.lnb, X_new, c.beta, c.mu, c.rstd, p_drop, seed_blk,
-                    outp_rows=c.outp_rows, Xnew16=c.Xn16)
+                    outp_rows=c.outp_rows, Xnew16=c.Xn16, Xa_out=c.Xa_next)
     c.p, c.seed_att, c.seed_blk, c.H, c.with_proj = p_drop, seed_att, seed_blk, H, with_proj
     return X_new, c
 
@@ -772,6 +776,9 @@ class AlignnEngine:
         # with the atom blocks on the aux stream: the node encoder and the atom projection folds there
         # too (forward prologue)
         self.encoders_aux = True
+        # each line block's gate kernel also writes the active rows of the new bond state, which the
+        # next line block reads instead of gathering them in a launch of its own
+        self.gate_gathers = True
         # the line convs' edge features (the angle encoder's hidden layer, [T, 256]) recomputed inside
         # the attention kernels from the 11 raw inputs instead of materialised and re-read 8 times
         # (ops.lg_fwd_x / lg_bwd_dst_x; the deferred encoder backward recomputes its ReLU mask)
@@ -951,6 +958,7 @@ class AlignnEngine:
             ctx.M_all, ctx.wbar_all = proj_weights(P.node_We, P.node_Wp, P.node_bp)
         bf16_io = self._bf16_io(D) and bc.lg is not None and bc.lg.rows is not None
         e16 = None   # bf16 copy of the bond state (written by the previous line block's gate kernel)
+        ea = None    # its active rows (likewise)
         for l in range(L):
             # EdgeUpdateBlock (train.py:312-317): line graph, angle embedding in target-sorted order
             if T > 0 and E > 0:
@@ -958,8 +966,10 @@ class AlignnEngine:
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
                                      site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
                                      skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
-                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16), angle_x=angle_x)
+                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16), angle_x=angle_x,
+                                     Xa=ea, want_Xa=self.gate_gathers and l + 1 < L)
                 e16 = c.Xn16
+                ea = c.Xa_next
             else:
                 c = None
             ctx.edge.append(c)

@@ -1115,12 +1115,30 @@ def _check_outp_rows(outp, outp_rows, n):
     return outp_rows.data_ptr()
 
 
-def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed, outp_rows=None, Xnew16=None):
+def gate_ln_fwd(outp, R, wbeta, X, ln_w, ln_b, Xnew, beta, mu, rstd, drop_p, seed, outp_rows=None, Xnew16=None,
+                Xa_out=None):
     """outp_rows (int32 [n], -1 = zero row): o of row r is outp[outp_rows[r]] (compacted conv output).
     R may be bf16 (the skip projection's bf16 output); Xnew16 (bf16 [n, D], optional) receives a bf16
-    copy of the new state (alignn_gate_ln_fwd_ex)."""
+    copy of the new state (alignn_gate_ln_fwd_ex).  Xa_out (fp32 contiguous [outp rows, D], needs
+    outp_rows): row r of the new state also goes to Xa_out[outp_rows[r]] where that is >= 0 — the
+    next line block's active-row gather (alignn_gate_ln_fwd_ex2)."""
     n, D = X.shape
     rp = _check_outp_rows(outp, outp_rows, n)
+    if Xa_out is not None:
+        _require(Xa_out, "gate_ln_fwd Xa_out")
+        if outp_rows is None or tuple(Xa_out.shape) != tuple(outp.shape) or not Xa_out.is_contiguous():
+            raise ValueError("gate_ln_fwd: Xa_out must be a contiguous tensor of outp's shape (with outp_rows)")
+        if Xnew16 is not None and (Xnew16.dtype != torch.bfloat16 or tuple(Xnew16.shape) != (n, D)
+                                   or Xnew16.stride(1) != 1):
+            raise ValueError("gate_ln_fwd: Xnew16 must be a bf16 [n, D] row-major tensor")
+        check(_lib.lib().alignn_gate_ln_fwd_ex2(n, D, outp.data_ptr(), rp, R.data_ptr(), R.stride(0),
+                                                int(R.dtype == torch.bfloat16), wbeta.data_ptr(), X.data_ptr(),
+                                                X.stride(0), ln_w.data_ptr(), ln_b.data_ptr(), Xnew.data_ptr(),
+                                                Xnew.stride(0), _p(Xnew16), 0 if Xnew16 is None else Xnew16.stride(0),
+                                                Xa_out.data_ptr(), beta.data_ptr(), mu.data_ptr(), rstd.data_ptr(),
+                                                float(drop_p), int(seed) & (2**64 - 1), stream_ptr()),
+              "alignn_gate_ln_fwd_ex2")
+        return
     if R.dtype == torch.bfloat16 or Xnew16 is not None:
         if Xnew16 is not None and (Xnew16.dtype != torch.bfloat16 or tuple(Xnew16.shape) != (n, D)
                                    or Xnew16.stride(1) != 1):

@@ -50,6 +50,8 @@ struct GateFwdParams {
   // (rbf); Xn16, if set, receives a bf16 copy of the new state (the next Linear's bf16 input)
   int rbf, pad2_;
   uint16_t* Xn16; int64_t ldxn16;
+  float* xa;            // optional [#active, D]: row orow[r] (>= 0) also receives the new state's row r —
+                        // the next line block's active-row gather, written here instead of by a launch
 };
 
 // IO: some operand is bf16 (bf16 storage); the fp32 instantiation carries no storage-type branches
@@ -106,6 +108,7 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
     }
     vstore(p.Xn + row * p.ldxn + j0, out);
     if (IO && p.Xn16) vstore_bf(p.Xn16 + row * p.ldxn16 + j0, out);
+    if (p.xa && orow >= 0) vstore(p.xa + orow * D + j0, out);
   }
   if (lane == 0) {
     p.beta[row] = b;
@@ -450,15 +453,19 @@ using namespace alignn;
 extern "C" int alignn_version(void) { return ALIGNN_ABI_VERSION; }
 extern "C" const char* alignn_last_error(void) { return g_err; }
 
-extern "C" int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
-                                     const void* R, int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X,
-                                     int64_t ldx, const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn,
-                                     uint16_t* Xnew16, int64_t ldxn16, float* beta, float* mu, float* rstd,
-                                     float drop_p, uint64_t seed, void* stream) {
+extern "C" int alignn_gate_ln_fwd_ex2(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
+                                      const void* R, int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X,
+                                      int64_t ldx, const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn,
+                                      uint16_t* Xnew16, int64_t ldxn16, float* Xa, float* beta, float* mu,
+                                      float* rstd, float drop_p, uint64_t seed, void* stream) {
   const int vpl = vpl_for(D);
   if (!vpl) {
     set_error("gate_ln_fwd: unsupported hidden %d", D);
     return ALIGNN_E_UNSUPPORTED;
+  }
+  if (Xa && !outp_rows) {
+    set_error("gate_ln_fwd: the active-row copy Xa needs outp_rows");
+    return ALIGNN_E_BAD_SHAPE;
   }
   if ((r_bf16 && (ldr % 4 || (reinterpret_cast<uintptr_t>(R) & 7))) ||
       (Xnew16 && (ldxn16 % 4 || (reinterpret_cast<uintptr_t>(Xnew16) & 7)))) {
@@ -467,7 +474,7 @@ extern "C" int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, co
   }
   if (n == 0) return ALIGNN_OK;
   GateFwdParams p{n, D, 0, outp, reinterpret_cast<const float*>(R), ldr, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, beta,
-                  mu, rstd, make_drop(drop_p, seed), outp_rows, r_bf16 ? 1 : 0, 0, Xnew16, ldxn16};
+                  mu, rstd, make_drop(drop_p, seed), outp_rows, r_bf16 ? 1 : 0, 0, Xnew16, ldxn16, Xa};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 g((unsigned)((n + 3) / 4));
   const bool io = r_bf16 || Xnew16;
@@ -483,6 +490,15 @@ extern "C" int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, co
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_fwd_kernel");
   return ALIGNN_OK;
+}
+
+extern "C" int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,
+                                     const void* R, int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X,
+                                     int64_t ldx, const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn,
+                                     uint16_t* Xnew16, int64_t ldxn16, float* beta, float* mu, float* rstd,
+                                     float drop_p, uint64_t seed, void* stream) {
+  return alignn_gate_ln_fwd_ex2(n, D, outp, outp_rows, R, ldr, r_bf16, wbeta, X, ldx, ln_w, ln_b, Xnew, ldxn, Xnew16,
+                                ldxn16, nullptr, beta, mu, rstd, drop_p, seed, stream);
 }
 
 extern "C" int alignn_gate_ln_fwd_rows(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows,

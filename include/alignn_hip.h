@@ -463,6 +463,14 @@ int alignn_gate_ln_fwd_ex(int64_t n, int32_t D, const float* outp, const int32_t
                           const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, uint16_t* Xnew16,
                           int64_t ldxn16, float* beta, float* mu, float* rstd, float drop_p, uint64_t seed,
                           void* stream);
+/* The same, and (Xa not NULL, needs outp_rows) row r of the new state also written to Xa[outp_rows[r]]
+ * wherever outp_rows[r] >= 0: the next line block's gather of the active rows (they are the same
+ * rows for every layer), done by the gate kernel that writes the state instead of a separate launch. */
+int alignn_gate_ln_fwd_ex2(int64_t n, int32_t D, const float* outp, const int32_t* outp_rows, const void* R,
+                           int64_t ldr, int32_t r_bf16, const float* wbeta, const float* X, int64_t ldx,
+                           const float* ln_w, const float* ln_b, float* Xnew, int64_t ldxn, uint16_t* Xnew16,
+                           int64_t ldxn16, float* Xa, float* beta, float* mu, float* rstd, float drop_p,
+                           uint64_t seed, void* stream);
 int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew, int64_t lddx, const float* dX_add,
                                    const float* outp, const int32_t* outp_rows, const void* R, int64_t ldr,
                                    int32_t r_bf16, const float* wbeta, const float* ln_w, const float* ln_b,

@@ -350,3 +350,36 @@ def test_bf16_trainer_with_torch_optimizer():
     assert torch.isfinite(loss).all() and not torch.equal(before, tr.st.flat)
     with pytest.raises(ValueError):
         A.FusedTrainer(model, precision="bf16", optimizer="torch", grad_scaler=True)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_gate_writes_the_next_blocks_active_rows(bf16):
+    """alignn_gate_ln_fwd_ex2: the gate kernel's copy of the new state's active rows (Xa_out at
+    outp_rows[r]) is bitwise gather_rows(Xnew, rows), and Xnew / its bf16 copy are unchanged."""
+    from alignn_mi355x import ops
+    g = torch.Generator(device="cpu").manual_seed(21)
+    n, D, na = 3000, 256, 700
+    rows = torch.randperm(n, generator=g)[:na].sort().values.to(torch.int32)
+    cmap = torch.full((n,), -1, dtype=torch.int32)
+    cmap[rows.long()] = torch.arange(na, dtype=torch.int32)
+    rows, cmap = rows.to(DEV), cmap.to(DEV)
+    outp = torch.randn(na, D, generator=g).to(DEV)
+    R = torch.randn(n, D, generator=g).to(DEV)
+    if bf16:
+        R = R.to(torch.bfloat16)
+    X = torch.randn(n, D, generator=g).to(DEV)
+    wbeta = torch.randn(3 * D, generator=g).to(DEV) * 0.1
+    lnw, lnb = torch.randn(D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+
+    def run(xa):
+        Xn, st = torch.empty(n, D, device=DEV), [torch.empty(n, device=DEV) for _ in range(3)]
+        X16 = torch.empty(n, D, device=DEV, dtype=torch.bfloat16) if bf16 else None
+        ops.gate_ln_fwd(outp, R, wbeta, X, lnw, lnb, Xn, *st, 0.15, 77, outp_rows=cmap, Xnew16=X16, Xa_out=xa)
+        return Xn, X16
+
+    Xn0, X160 = run(None)
+    xa = torch.full((na, D), float("nan"), device=DEV)
+    Xn1, X161 = run(xa)
+    torch.cuda.synchronize()
+    assert torch.equal(Xn0, Xn1) and (not bf16 or torch.equal(X160, X161))
+    assert torch.equal(xa, ops.gather_rows(Xn1, rows))
