@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-5 GPU job steps (run through gpurun from the repo root).  Each step under its own time
-# limit; the script stops at the first failing step.
+# limit; the script stops at the first failing step.  The A/B steps expect their comparison build
+# where they name it (abl/wt: a git worktree of the base commit with its library built; abl/lib*.so:
+# alternative builds of the library) — set up by hand before the call, removed after.
 set -eo pipefail
 O=$PWD/gpurun_out/${JOB:-r5}
 mkdir -p "$O"
@@ -22,7 +24,7 @@ for step in "$@"; do
            run c2_xf_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
            run c2_rows_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set engine.recompute_angle=0
          done ;;
-    gemmt) run gemmt 400 "${PT[@]}" tests/test_gpu_kernels.py tests/test_gpu_x_gemm_pipe.py tests/test_gpu_x_gemm_lds16.py tests/test_gpu_x_splitk.py tests/test_gpu_x_bf16_stream.py tests/test_gpu_parity.py ;;
+    gemmt) run gemmt 400 "${PT[@]}" tests/test_gpu_kernels.py tests/test_gpu_x_gemm_pipe.py tests/test_gpu_x_gemm_lds16.py tests/test_gpu_x_splitk.py tests/test_gpu_parity.py ;;
     abl) for i in 1 2; do
            run c2_new_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
            (cd abl/wt && run c2_base_$i 300 python bench.py --steps 30 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline)
@@ -38,7 +40,7 @@ for step in "$@"; do
            for t in 0 8192; do for io in "" --io16; do
              run gbs_$1_$2_$3_$t$io 120 python tools/gemm_probe.py --bf16 --M $1 --N $2 --K $3 --tile $t $io; done; done; done
          grep -h '^{' $O/gbs_*.log ;;
-    grows) run t_rows 300 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_bf16_stream.py
+    grows) run t_rows 300 "${PT[@]}" tests/test_gpu_x_gemm_rows.py
            for sh in "184320 256 256" "184320 256 36" "16020 768 256" "15360 1024 256"; do set -- $sh
              for t in 0 131072 65536; do for io in "" --io16; do
                run grows_$1_$2_$3_$t$io 120 python tools/gemm_probe.py --bf16 --M $1 --N $2 --K $3 --tile $t $io; done; done; done
@@ -84,7 +86,7 @@ for step in "$@"; do
         for i in 1 2; do for w in 4 2 1; do
           ALIGNN_LG3_SW=$w run c2_sw${w}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline; done; done
         for f in $O/c2_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f)"; done ;;
-    batched) run t_batched 400 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_x_bf16_stream.py tests/test_gpu_x_round5.py
+    batched) run t_batched 400 "${PT[@]}" tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_x_round5.py
            run gtrace_c3 300 python tools/gemm_trace.py --batch 256 --precision bf16 --time
            head -3 $O/gtrace_c3.log | cut -c1-120
            for i in 1 2; do run c3_new$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
