@@ -44,6 +44,7 @@ FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
 BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 PROBE_STEPS = 3            # untimed replays the dominant-kernel ranking sums over
 C1_WARM, C1_REPS = 10, 50   # config C1 forward timing (median of 50 after 10)
+CPU_BUDGET_S = 40.0        # CPU baseline: time-boxed sample (cpu_baseline)
 SERIAL_STEPS = 3           # serialised replays after the timed region (the dominant kernel's own duration)
 
 
@@ -70,7 +71,7 @@ def parse():
     p.add_argument("--dropout", type=float, default=0.15)
     p.add_argument("--lg-offset", default="num_nodes", choices=["num_nodes", "num_edges"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=5)
+    p.add_argument("--cpu-steps", type=int, default=5, help="minimum CPU-baseline steps (time-boxed beyond)")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary lines of the default one-GPU run (corrected wiring, config C3)")
@@ -168,16 +169,22 @@ def cpu_baseline(args, B):
         st = {k: v.detach().clone() for k, v in model.state_dict().items()}
         gs = [mp_like_graph(g) for g in range(B)]
         b = collate([RefData(**{k: getattr(d, k) for k in d.keys()}) for d in gs], lg_offset=args.lg_offset)
-        model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)  # warm-up
+        # SURVEY §8d asks for the median of 50 steps after 10 warm-ups; at ~4 s per step on the host that
+        # is minutes, so the sample is time-boxed: 2 warm-up steps, then steps until CPU_BUDGET_S have
+        # passed (at least args.cpu_steps), reported as p10 / p50 / p90 with the step count
+        for _ in range(2):
+            model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)
         times = []
-        for _ in range(args.cpu_steps):
+        t_start = time.perf_counter()
+        while len(times) < args.cpu_steps or (time.perf_counter() - t_start < CPU_BUDGET_S and len(times) < 50):
             t0 = time.perf_counter()
             model_ref.train_step(st, b, args.heads, TARGET_LOG_MEANS, TARGET_LOG_STDS, steps=1)
             times.append(time.perf_counter() - t0)
     finally:
         torch.set_num_threads(prev)
     times.sort()
-    med = times[len(times) // 2]
+    q = lambda f: times[min(len(times) - 1, int(f * len(times)))]  # noqa: E731
+    med = q(0.5)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -187,12 +194,15 @@ def cpu_baseline(args, B):
     except OSError:
         pass
     return {"value": round(B / med, 3), "unit": "graphs/s", "cores": threads, "kind": "port",
-            "sample": f"median of {args.cpu_steps} steps x {B} graphs (fp32 fwd+NLL+bwd+clip+AdamW, dropout 0) after "
-                      f"1 warm-up, torch.set_num_threads({threads}) (the job's CPU share; os.cpu_count() = "
-                      f"{os.cpu_count()}); {cpu_model}"}
+            "p10_p50_p90_graphs_per_s": [round(B / q(0.9), 3), round(B / med, 3), round(B / q(0.1), 3)],
+            "steps_timed": len(times),
+            "sample": f"median of {len(times)} steps x {B} graphs (fp32 fwd+NLL+bwd+clip+AdamW, dropout 0) after "
+                      f"2 warm-up steps, time-boxed to {CPU_BUDGET_S:.0f} s (p10/p50/p90 beside it), "
+                      f"torch.set_num_threads({threads}) (the job's CPU share; os.cpu_count() = {os.cpu_count()}); "
+                      f"{cpu_model}"}
 
 
-def c1_forward(args, dev):
+def c1_forward(args, dev, lender=None):
     """Config C1: one graph, forward only, fp32 — (1a) the reference's smoke shape
     (tests/smoke.py:106-145: node/edge/angle dims 6/8/7, hidden 32, 1 layer, 1 head) and (1b) one
     MP-like graph at L = 1 (D = 256, H = 4).  The reference's CPU path (the oracle, all of the job's
@@ -213,6 +223,8 @@ def c1_forward(args, dev):
     for name, (cfg, graph, heads) in shapes.items():
         torch.manual_seed(0)
         model = A.HeteroAlignnRegressor(A.AlignnRegressor(*cfg), 2).eval()
+        if lender is not None:   # no streams of its own beside the idle headline trainer's (see measure)
+            model._engine.ctx.borrow_streams(lender.model._engine.ctx)
         st = {k: v.detach().clone() for k, v in model.state_dict().items()}
         g = graph()
         ref = collate([RefData(**{k: getattr(g, k) for k in g.keys()})], lg_offset=args.lg_offset)
@@ -262,6 +274,46 @@ def _median_time(fn, warm, reps, sync):
     return ts[len(ts) // 2]
 
 
+def ensemble_predict(args, dev, members=5, B=256):
+    """predict.ensemble_predict / ensemble_collect (predict.py:582-653, train.py:849-904) at config C4's
+    shape on one GPU: `members` models at B graphs, bf16 (the reference predicts under autocast),
+    EnsemblePredictor.predict_batch — every member's forward on its own stream, the moment mix and the
+    log-normal conversion — timed per batch with the forwards as replayed plans (infer.py) and eager."""
+    import alignn_mi355x as A
+    from alignn_mi355x import infer
+    from alignn_mi355x.ensemble import EnsemblePredictor
+    from alignn_mi355x.synthetic import mp_like_batch
+    models = []
+    for i in range(members):
+        torch.manual_seed(1000 + i)
+        m = A.HeteroAlignnRegressor(A.AlignnRegressor(206, 36, 11, 289, 2, args.hidden, args.layers, args.heads,
+                                                      args.dropout), 2).to(dev).eval()
+        models.append(m.set_precision("bf16"))
+    batches = [mp_like_batch(B, first=B * i).to(dev) for i in range(2)]
+    ep = EnsemblePredictor(models)
+    out = {"members": members, "batch": B, "precision": "bf16"}
+    it = {"k": 0}
+
+    def call():
+        r = ep.predict_batch(batches[it["k"] % 2])   # alternating batches: every plan call re-binds
+        it["k"] += 1
+        return r
+
+    for name, enabled in (("plan", True), ("eager", False)):
+        infer.ENABLED = enabled
+        try:
+            t = _median_time(call, 4, 20, sync=True)
+        finally:
+            infer.ENABLED = True
+        out[f"{name}_ms_per_batch"] = round(t * 1e3, 3)
+        out[f"{name}_graphs_per_s"] = round(B / t, 1)
+    for m in models:
+        infer.release(m)
+    out["protocol"] = ("median of 20 predict_batch calls after 4 warm-up, alternating two batches of the same "
+                       "signature; synchronised per call")
+    return out
+
+
 def build_store(args, dev, rank):
     """This rank's shard of an HBM-resident dataset of args.e2e synthetic MP-like graphs
     (store.GraphStore; config C5's ~10k-graph dataset split over the data-parallel ranks), built
@@ -294,21 +346,18 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     from alignn_mi355x.engine import prepare_batch
 
     rng = np.random.default_rng(1234 + rank)
-    # The step's streams run at high priority (main()).  A fixed-signature loop prepares on a normal-
-    # priority loader stream, which then fills the step's idle time instead of slowing it (round 4,
-    # batch preparation without host syncs: B = 32 7,880 -> 8,497 graphs/s, C5 17,115 -> 18,733 = 96 % of
-    # the bare step; gpurun_out r4f e2ep_*).  Padded batches (capacity) need more preparation work than
-    # those gaps hold — starved, it serialised with the step (5.1 vs 3.6 ms, r4g rp_var) — so their
-    # loader shares the step's priority.  (Round 2, with host syncs in the preparation and the step at
-    # normal priority: a high-priority loader from B = 128 on, profiles/r02/v43_ab_loader_priority_*.log
-    # — kept for --set main_priority=0.)
+    # The loader stream: a pooled stream at the step's priority (high).  A dedicated hardware queue for
+    # it (round 4) stopped paying once the step used three streams: the process's GPU_MAX_HW_QUEUES = 4
+    # queues are then shared, and the dedicated queue pushed the other loops' streams together — with
+    # the secondaries' trainers alive the B = 32 loop fell to 71 % of the bare step (BENCH_r05); without
+    # them every placement gives 92 %, and the padded loop after a dedicated queue had been created
+    # lost a third (gpurun_out r6a: B = 32 e2e 9,930-10,040 graphs/s for dedicated / pooled / pooled at
+    # high priority / prefetch 2; e2e_variable 7,200 after the dedicated queue vs 11,400 without).
+    # (--set loader_priority=0 / loader_dedicated=1 / main_priority=0 keep the earlier placements.)
     prio = getattr(args, "loader_priority", None)
     if prio is None:
-        prio = (0 if capacity is None else -1) if args.main_priority else (-1 if B >= 128 else 0)
-    # A normal-priority loader gets a hardware queue of its own (ops.dedicated_stream): from the pool
-    # of four it could land on a step stream's queue, and which loop ran first decided that (B = 32:
-    # 5,760-5,800 first vs 8,450-8,610 second, gpurun_out r4h-r4k).
-    dedicated = prio == 0 and bool(int(getattr(args, "loader_dedicated", 1)))
+        prio = args.main_priority if args.main_priority else (-1 if B >= 128 else 0)
+    dedicated = prio == 0 and bool(int(getattr(args, "loader_dedicated", 0)))
     loader = None
     if dedicated:
         try:
@@ -828,7 +877,7 @@ def main():
                 "steps": sec_steps, "roofline": w["roofline"]}
             _release(w)
         if not args.no_cpu_baseline:
-            secondary["c1_forward"] = c1_forward(args, dev)
+            secondary["c1_forward"] = c1_forward(args, dev, lender=r["trainer"])
         if (B, args.precision) != (256, "bf16"):
             c3 = measure(args, dev, rank, world, 256, args.lg_offset, "bf16", sec_steps, sec_warm, roofline=True,
                          streams_of=r["trainer"])
@@ -860,6 +909,8 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
+    if world == 1 and not args.no_secondary and args.ensemble == 0:
+        secondary["c4_ensemble_predict_b256"] = ensemble_predict(args, dev)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

@@ -387,6 +387,25 @@ def adopt(batch, bc: Optional[BatchCache] = None) -> None:
             t.record_stream(s)
 
 
+_PRIVATE_SKIP = ("_alignn_cache", "_alignn_ready", "_alignn_adopted", "_staging")
+
+
+def clone_batch(batch):
+    """A private copy of ``batch`` (its tensors cloned on the current stream; hints kept, device caches
+    not): the buffers a recorded plan reads, so that re-binding other batches never writes the caller's."""
+    out = type(batch).__new__(type(batch))
+    for k, v in batch.__dict__.items():
+        if k in _PRIVATE_SKIP:
+            continue
+        out.__dict__[k] = v.clone() if torch.is_tensor(v) else v
+    return out
+
+
+def batch_versions(batch, fields) -> tuple:
+    """In-place modification counters of ``batch``'s fields (torch's tensor._version)."""
+    return tuple(getattr(batch, k)._version if torch.is_tensor(getattr(batch, k, None)) else None for k in fields)
+
+
 def site_seed(seed: int, site: int) -> int:
     return (seed * 0x9E3779B1 + site * 0x85EBCA77 + 0x165667B1) & (2**63 - 1)
 
@@ -783,10 +802,10 @@ class AlignnEngine:
         # the attention kernels from the 11 raw inputs instead of materialised and re-read 8 times
         # (ops.lg_fwd_x / lg_bwd_dst_x; the deferred encoder backward recomputes its ReLU mask)
         self.recompute_angle = True
-        # ... and at bf16 storage (config C3): the recompute kernels hold W1 in 44 registers, which
-        # halves the occupancy the bf16 kernels run at (4 / 3 -> 2 waves per SIMD; C3 20,416 ->
-        # 18,394 graphs/s, gpurun_out r5b): off until the bf16 form is restructured
-        self.recompute_angle_bf16 = False
+        # ... and at bf16 storage (config C3): the matrix-core attention kernels (lgmx.hip) recompute it
+        # as autocast does (bf16 x, W1, b1; fp32 accumulation) and take every per-edge product on the
+        # matrix cores, and the deferred encoder backward recomputes its mask the same way
+        self.recompute_angle_bf16 = True
 
     @contextmanager
     def using_precision(self, precision: str):
@@ -817,8 +836,12 @@ class AlignnEngine:
 
     def _angle_xf(self, bc, D: int) -> bool:
         """The line convs recompute their edge features (recompute_angle): D = 256, H = 4, 11 raw
-        angle inputs, the deferred encoder backward, a single-wave-item line-graph schedule."""
+        angle inputs, the deferred encoder backward, a single-wave-item line-graph schedule.  fp32: only
+        where the materialised layer would come from linear_smallk (skinny_encoder), whose fma chain the
+        recompute reproduces bit for bit."""
         if self.precision == "bf16" and self.bf16_storage and not self.recompute_angle_bf16:
+            return False
+        if not (self.precision == "bf16" and self.bf16_storage) and not self.skinny_encoder:
             return False
         return bool(self.recompute_angle and self.defer_angle_bwd and bc.xa is not None and bc.lg is not None
                     and ops.lg_x_ok(bc.lg, D, self.cfg.heads, bc.xa)

@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, infer
 from .engine import MIN_LOGVAR_FLOOR, batch_cache
 from .ops import stream_ptr
 from .synthetic import TARGET_LOG_MEANS, TARGET_LOG_STDS
@@ -51,19 +51,19 @@ class EnsemblePredictor:
 
     def member_outputs(self, batch, mode: str = "hetero") -> torch.Tensor:
         """[M, B, 2T] heads (hetero) or [M, B, D] embeddings, members in eval mode (dropout off)."""
-        bc = batch_cache(batch)
+        batch_cache(batch)   # the batch's cache built once, on the caller's stream
         dev = batch.x.device
         main = torch.cuda.current_stream(dev)
-        x, gx = batch.x.contiguous().float(), batch.global_x.contiguous().float()
         outs = []
         for m, s in zip(self.models, self._member_streams(dev)):
-            st = m._ensure_flat()
+            # each member's forward as a replayed launch plan once the batch signature repeats
+            # (infer.forward; its output lives in the plan until the stack below copies it)
             if s is None:
-                out, _ = m._engine.forward(st.P, batch, bc, False, 0, x, gx, mode)
+                out = infer.forward(m, batch, mode)
             else:
                 s.wait_stream(main)
                 with torch.cuda.stream(s):
-                    out, _ = m._engine.forward(st.P, batch, bc, False, 0, x, gx, mode)
+                    out = infer.forward(m, batch, mode)
                 out.record_stream(main)
             outs.append(out)
         for s in self._member_streams(dev):

@@ -1,0 +1,181 @@
+"""Recorded inference forwards — the forward-only consumers of the hot path.
+
+The reference calls ``model(batch)`` / ``model.embed(batch)`` without gradients every epoch and at the
+end of training: ``eval_epoch_hetero`` (train.py:726-846, under bf16 autocast :757),
+``ensemble_collect`` (:849-904), ``ensemble_collect_embeddings`` (:907), ``compute_global_knn_weights``
+(:930-1010) and ``predict.ensemble_predict`` (predict.py:582).  Issued from Python, one forward is
+~40-120 library launches of host latency (a smoke-shape forward took 2.1 ms on the GPU against 0.9 ms on
+the host CPU, round 5).  Here the forward of one model at one batch signature is recorded once as a
+native launch plan (plan.hip, as FusedTrainer records the training step) and replayed; a batch of the
+same signature (BatchCache.signature) is copied into the captured batch's buffers first, like the
+training step's re-binding.  Eval mode, no dropout: the replay is bitwise the eager forward.
+
+``forward(model, batch, mode, precision)`` is the one entry: the module API's no-grad eval forward,
+EnsemblePredictor and the KNN embedding pass call it.  A signature is recorded the second time it is
+seen (a one-off batch stays eager); each model keeps at most MAX_PLANS recorded signatures.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import weakref
+
+import torch
+
+from . import _lib, ops
+from ._lib import check
+from .engine import adopt, batch_cache, batch_versions, clone_batch
+
+# a recorded forward reads these batch fields (train.py:547-573); a re-bound batch is copied into them
+FIELDS = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "batch", "ptr")
+MAX_PLANS = 4
+ENABLED = True
+
+
+class ForwardPlan:
+    """The eval forward of ``model`` in ``mode`` ('hetero' | 'base' | 'embed') at ``precision`` on the
+    signature of one captured batch."""
+
+    def __init__(self, model, batch, mode: str, precision: str):
+        from .trainer import _check_census, _check_deps, _check_ownership, _cuda_tensors, _plan_refs, _record_plan
+        self.model, self.mode, self.precision = model, mode, precision
+        eng = model._engine
+        self.ctx = eng.ctx
+        st = model._ensure_flat()
+        dev = st.flat.device
+        # the plan reads a private copy of the batch (the slot); every call copies its batch in unless
+        # the slot already holds that batch, unmodified — the caller's tensors are never written
+        adopt(batch)
+        slot = clone_batch(batch)
+        with ops.using(self.ctx):
+            bc = batch_cache(slot)
+            bc.schedules()
+        self.slot = slot
+        self._bound = weakref.ref(batch)
+        self._bound_v = batch_versions(batch, FIELDS)
+        x, gx = slot.x, slot.global_x
+        batch = slot
+
+        def fwd():
+            with torch.autocast("cuda", enabled=False), eng.using_precision(precision):
+                out, _ = eng.forward(st.P, batch, bc, False, 0, x, gx, mode)
+            return out
+
+        # warm-up: every workspace sized at this signature, on a side stream (as FusedTrainer.capture)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s), ops.using(self.ctx):
+            for _ in range(2):
+                fwd()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
+        res = {}
+        self.plan = None
+        try:
+            with ops.recording(), ops.using(self.ctx):
+                with torch.cuda.graph(self.graph):
+                    self.plan = _record_plan(lambda: res.setdefault("out", fwd()))
+            torch.cuda.synchronize(dev)
+            ranges = []
+            for t in _cuda_tensors((st.flat, self.ctx.tensors(), batch, list(model.buffers()))):
+                u = t.untyped_storage()
+                ranges.append((u.data_ptr(), u.data_ptr() + u.nbytes()))
+            pool = tuple(self.graph.pool())
+            for seg in torch.cuda.memory_snapshot():
+                if tuple(seg.get("segment_pool_id", ())) == pool:
+                    ranges.append((seg["address"], seg["address"] + seg["total_size"]))
+            _check_census(self.graph, self.plan, "forward")
+            _check_deps(self.graph, self.plan, "forward")
+            _check_ownership(self.plan, ranges, "forward")
+        except Exception:
+            if self.plan:
+                _lib.lib().alignn_plan_destroy(self.plan)
+            self.plan = None
+            raise
+        self.out = res["out"]
+        targets = [getattr(batch, k) for k in FIELDS if getattr(batch, k, None) is not None]
+        targets += [t for t in bc.device_tensors() if t is not None]
+        targets = [t for t in targets if t.numel()]
+        self.used = _plan_refs([self.plan], targets)
+        self.ctx.freeze()
+        self.replays = 0
+
+    def release(self) -> None:
+        if self.plan:
+            _lib.lib().alignn_plan_destroy(self.plan)
+            self.plan = None
+            self.ctx.thaw()
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def run(self, batch) -> torch.Tensor:
+        """Replays on ``batch`` (copied into the plan's slot unless the slot holds it already); returns
+        the plan's output tensor, valid until the next replay of this plan."""
+        v = batch_versions(batch, FIELDS)
+        if self._bound() is not batch or v != self._bound_v:
+            adopt(batch)
+            with ops.using(self.ctx):
+                pairs = [(getattr(self.slot, k), getattr(batch, k)) for k in FIELDS
+                         if getattr(batch, k, None) is not None and getattr(batch, k).numel()]
+                pairs += batch_cache(batch).copy_pairs(batch_cache(self.slot))
+                pairs = [(d, s) for d, s in pairs if d.data_ptr() in self.used]
+                ops.copy_many(pairs)
+            self._bound, self._bound_v = weakref.ref(batch), v
+        check(_lib.lib().alignn_plan_replay(self.plan, ops.stream_ptr()), "alignn_plan_replay")
+        self.replays += 1
+        return self.out
+
+
+def _key(batch, bc, mode: str, precision: str):
+    fields = tuple((k, tuple(t.shape), t.dtype) for k in FIELDS if (t := getattr(batch, k, None)) is not None)
+    return (mode, precision, fields, bc.signature())
+
+
+def _recordable(batch) -> bool:
+    """A forward the plan can hold: fp32 contiguous node / global features (the eager path would cast them
+    with a torch kernel, which a plan cannot replay) on a device."""
+    x, gx = getattr(batch, "x", None), getattr(batch, "global_x", None)
+    return (x is not None and gx is not None and x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
+            and gx.dtype == torch.float32 and gx.is_contiguous())
+
+
+def forward(model, batch, mode: str, precision: Optional[str] = None) -> torch.Tensor:
+    """The eval forward (no dropout, no gradient) of ``model`` on ``batch``: a replayed plan when this
+    signature was seen before (the output then lives in the plan: copy it before the next call of the
+    same model and signature), else the engine's eager forward."""
+    eng = model._engine
+    precision = precision or eng.precision
+    st = model._ensure_flat()
+    with ops.using(eng.ctx):
+        bc = batch_cache(batch)
+    if ENABLED and _recordable(batch) and not torch.cuda.is_current_stream_capturing():
+        plans = model.__dict__.setdefault("_fwd_plans", {})
+        seen = model.__dict__.setdefault("_fwd_seen", {})
+        key = _key(batch, bc, mode, precision)
+        p = plans.get(key)
+        if p is None and seen.get(key, 0) >= 1:
+            if len(plans) >= MAX_PLANS:   # drop the oldest recorded signature
+                old = next(iter(plans))
+                plans.pop(old).release()
+            p = plans[key] = ForwardPlan(model, batch, mode, precision)
+        if p is not None:
+            return p.run(batch)
+        if len(seen) > 1024:   # many one-off signatures (unpadded variable-size batches): forget them
+            seen.clear()
+        seen[key] = seen.get(key, 0) + 1
+    x, gx = batch.x.contiguous().float(), batch.global_x.contiguous().float()
+    with torch.autocast("cuda", enabled=False), eng.using_precision(precision):
+        out, _ = eng.forward(st.P, batch, bc, False, 0, x, gx, mode)
+    return out
+
+
+def release(model) -> None:
+    """Releases every recorded forward of ``model`` (their private memory and frozen workspaces)."""
+    for p in model.__dict__.pop("_fwd_plans", {}).values():
+        p.release()
+    model.__dict__.pop("_fwd_seen", None)

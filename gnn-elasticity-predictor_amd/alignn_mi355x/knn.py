@@ -17,20 +17,16 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
-from . import _lib, ops
+from . import _lib, infer, ops
 from .engine import batch_cache
 from .ops import stream_ptr
 
 
 def embed_collect(model, batches) -> Tuple[torch.Tensor, torch.Tensor, np.ndarray]:
     """(Z [n, D], Y [n, T] raw targets, train_idx [n]) over the batches, Z/Y on the device."""
-    st = model._ensure_flat()
     zs, ys, idx = [], [], []
     for b in batches:
-        bc = batch_cache(b)
-        z, _ = model._engine.forward(st.P, b, bc, False, 0, b.x.contiguous().float(),
-                                     b.global_x.contiguous().float(), "embed")
-        zs.append(z)
+        zs.append(infer.forward(model, b, "embed").clone())   # a replayed plan once the signature repeats
         ys.append(b.y.view(b.num_graphs, -1).float())
         if not hasattr(b, "train_idx"):
             raise ValueError("KNN weighting requires 'train_idx' on each batch.")

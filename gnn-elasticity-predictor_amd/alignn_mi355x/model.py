@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F  # noqa: F401
 from torch import nn
 
-from . import ops
+from . import infer, ops
 from .engine import (AlignnEngine, BatchCache, FlatViews, _Conv, batch_cache, block_backward, block_forward,
                      proj_grads, proj_weights, site_seed)
 from .layout import AlignnConfig, offsets
@@ -294,10 +294,17 @@ class _EngineModelMixin:
         _require_device(data.x, type(self).__name__)
         st = self._ensure_flat()
         _require_device(st.flat, type(self).__name__)
+        amp = _autocast_dtype()
+        precision = "bf16" if amp is not None else self._engine.precision
+        seed = _next_seed()
+        if not self.training and not torch.is_grad_enabled():
+            # inference (eval_epoch_hetero, ensemble_collect, predict: no_grad + eval): the forward as a
+            # replayed launch plan once its batch signature repeats (infer.py), bitwise the eager one
+            out = infer.forward(self, data, mode, precision)
+            return out.clone() if amp is None else out.to(amp)
         bc = batch_cache(data)
         params = [dict(self.named_parameters())[n] for n in st.names]
-        amp = _autocast_dtype()
-        holder = (self, data, bc, mode, _next_seed(), "bf16" if amp is not None else self._engine.precision)
+        holder = (self, data, bc, mode, seed, precision)
         out = _ModelFn.apply(holder, data.x.contiguous().float(), data.global_x.contiguous().float(), *params)
         # autocast's Linear outputs (heads / feat_proj) are bf16: the fp32-accumulated outputs rounded
         # once, their gradient handed back to the engine in fp32

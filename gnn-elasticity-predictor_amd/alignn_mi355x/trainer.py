@@ -9,6 +9,8 @@ contiguous segments (base + mean heads | logvar heads).
 from __future__ import annotations
 
 import ctypes
+import warnings
+import weakref
 from typing import Optional, Sequence
 
 import torch
@@ -16,7 +18,7 @@ from torch import nn
 
 from . import _lib, ops, profiling
 from ._lib import check
-from .engine import MIN_LOGVAR_FLOOR, adopt, batch_cache, site_seed
+from .engine import MIN_LOGVAR_FLOOR, adopt, batch_cache, batch_versions, clone_batch, site_seed
 
 # batch fields a recorded step reads (train.py:547-573, :648-650); a re-bound batch is copied into
 # the captured batch's buffers field by field
@@ -66,6 +68,12 @@ class FusedTrainer:
         # (default on for bf16 with the HIP optimizer; torch's optimizer runs without one)
         if grad_scaler is None:
             grad_scaler = model._engine.precision == "bf16" and optimizer == "hip"
+            if model._engine.precision == "bf16" and optimizer == "torch":
+                # the reference builds a GradScaler whenever it runs autocast on the GPU (train.py:1475-1476,
+                # :690-695); torch's optimizer here has none: a non-finite step is applied, not skipped
+                warnings.warn("FusedTrainer(precision='bf16', optimizer='torch') runs without a GradScaler: a step "
+                              "with non-finite gradients is applied instead of skipped (optimizer='hip' skips it)",
+                              stacklevel=2)
         if grad_scaler and optimizer != "hip":
             raise ValueError("grad_scaler needs optimizer='hip'")
         self.growth_interval = int(growth_interval)
@@ -85,6 +93,7 @@ class FusedTrainer:
         self.loss = torch.zeros(1, device=dev)
         self.step_count = 0
         self._graph = None
+        self._bound, self._bound_v = (lambda: None), ()   # the batch the captured slot holds
         self._seed_dev = None
         # the engine's execution context (workspaces, side stream, device step seed): every launch of
         # this trainer's step runs in it, and a recorded plan owns it (its buffers never move)
@@ -178,7 +187,8 @@ class FusedTrainer:
             # a weighted capture (KNN weights, train.py:660-674) reads the per-graph weights from its
             # own device buffer: the step's weights are copied there in the re-binding launch
             extra = [] if sample_weights is None else [(self._wbuf, sample_weights)]
-            if self._graph[2] is batch:
+            if self._bound() is batch and batch_versions(batch, BATCH_FIELDS) == self._bound_v:
+                # the slot holds this batch already (the captured batch, or the last one re-bound)
                 if extra:
                     with ops.using(self.ctx):
                         ops.copy_many(extra)
@@ -207,6 +217,7 @@ class FusedTrainer:
         size the recorded launches depend on matches; False (nothing copied) otherwise.  A batch
         prepared on another stream (engine.prepare_batch) was adopted by step() (engine.adopt)."""
         slot = self._graph[2]
+        v = batch_versions(batch, BATCH_FIELDS)
         for k in BATCH_FIELDS:
             a, b = getattr(batch, k, None), getattr(slot, k, None)
             if (a is None) != (b is None):
@@ -227,6 +238,7 @@ class FusedTrainer:
             if used is not None and not self.rebind_copy_all:
                 pairs = [(d, s) for d, s in pairs if d.data_ptr() in used]
             ops.copy_many(pairs + list(extra))   # one launch for the batch, its cache and the weights
+        self._bound, self._bound_v = weakref.ref(batch), v
         self.rebinds += 1
         return True
 
@@ -268,8 +280,11 @@ class FusedTrainer:
     # reference's loop over fresh batches (train.py:639-711) replays the plan every step.
     # --------------------------------------------------------------------------------------------
     def capture(self, batch, mode: str = "plan", weighted: bool = False) -> None:
-        """Capture the training step on ``batch`` (which must stay alive with unchanged shapes; its
-        tensors may be refilled in place).  Model and optimizer state are left as they were.
+        """Capture the training step on ``batch``.  The plans read a private copy of it (the slot): a
+        step on another batch of the same signature copies that batch into the slot (re-binding), and a
+        step on the batch the slot holds — unmodified since (torch's in-place version counters) —
+        replays directly; the caller's tensors are never written.  Model and optimizer state are left
+        as they were.
         weighted: the step of the reference's KNN-weighted epochs (train.py:660-674) — the loss reads
         per-graph weights from a device buffer of this trainer that step(sample_weights=w) fills."""
         if mode not in ("plan", "graph"):
@@ -278,6 +293,9 @@ class FusedTrainer:
             raise ValueError("plan capture needs optimizer='hip' (torch's AdamW launches outside the library)")
         dev = self.st.flat.device
         self.release_capture()
+        adopt(batch)
+        self._bound, self._bound_v = weakref.ref(batch), batch_versions(batch, BATCH_FIELDS)
+        batch = clone_batch(batch)
         if self._seed_dev is None:
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         self.use_step_seed(self._seed_dev)

@@ -242,16 +242,15 @@ struct EbSlot {
   static __device__ __forceinline__ int head(int hh, int j) { return hh * JPL + j % JPL; }
 };
 
-// XF: no hidden-layer rows (the line convs recompute them, lgconv.hip): the ReLU mask comes from the
-// pre-activation W1 x + b1 recomputed here with the forward's arithmetic — a k-ordered chain of
-// v_mfma_f32_4x4x1f32 (bitwise linear_smallk's fmaf chain, tools/probe/mfma441.hip) laid out as the G
-// tile: lane L's column 64 w + 32 ct + (L & 31) is the B operand, and the A operand of MFMA q from
-// lane l is x[edge (l & 3) + 8 q + 4 (l >> 5)][k] — register rr of MFMA q then holds G register
-// 4 q + rr's edge.  kin <= EB_XF_KMAX inputs.
+// XF: no hidden-layer rows (the line convs recompute them on the matrix cores, lgmx.hip): the ReLU mask
+// comes from the pre-activation recomputed here as the forward computes it — bf16(x) . bf16(W1)^T +
+// bf16(b1) (autocast's operands for train.py:554 under :636; the bias enters as a ones column of x) on
+// one v_mfma_f32_32x32x16_bf16 per 32 x 32 tile, laid out as the G tile (A: x of edge r, inputs 8 hh + j;
+// B: W1 of column 64 w + 32 ct + r), then rounded to bf16 like the forward's f.  kin <= EB_XF_KMAX.
 constexpr int EB_XF_KMAX = 12;
-constexpr int EBF_BLOCKS_XF = EBF_BLOCKS * 2 / 3;   // 197 VGPRs: two workgroups per CU resident
+constexpr int EBF_BLOCKS_XF = EBF_BLOCKS;
 template <int H, bool XF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))  // 166 VGPRs: 3 waves/SIMD
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64_t ldf) {
   constexpr int D = 256;
   __shared__ __attribute__((aligned(16))) uint16_t fs[XF ? 8 : 32 * EBF_FP];   // the chunk's f rows
@@ -259,15 +258,16 @@ void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int kin = p.kin;
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  float w1[2][EB_XF_KMAX], b1[2];   // XF: W1 / b1 of this lane's two columns
+  ebh8 W1B[2];   // XF: [W1 | b1] of this lane's two columns (bf16), inputs 8 hh .. 8 hh + 7
   if constexpr (XF) {
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       const int col = 64 * w + 32 * ct + r;
 #pragma unroll
-      for (int k = 0; k < EB_XF_KMAX; ++k) w1[ct][k] = k < kin ? p.w1[col * kin + k] : 0.f;
-      b1[ct] = p.b1[col];
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * hh + j;
+        W1B[ct][j] = (__bf16)(k < kin ? p.w1[col * kin + k] : (k == kin ? p.b1[col] : 0.f));
+      }
     }
   }
   ebx16 Z[2];
@@ -337,6 +337,15 @@ void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64
         xs[(i >> 4) * EBF_XP + (i & 15)] = xv[u];
       }
       __syncthreads();
+      ebh8 XA;   // XF: x_aug of edge r (inputs 8 hh + j; the ones column at k = kin)
+      if constexpr (XF) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * hh + j;
+          const float v = xs[r * EBF_XP + (k < 16 ? k : 0)];   // unconditional read (zero past kin)
+          XA[j] = (__bf16)(k < kin ? v : (k == kin ? 1.f : 0.f));
+        }
+      }
       ebh8 SA[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -365,22 +374,9 @@ void enc_bwd_bf16_kernel(EncBwdParams p, const uint16_t* __restrict__ F16, int64
         const int col = 64 * w + 32 * ct + r;
         ebh8 GA[2];
         if constexpr (XF) {
-          v4f pre[4];
+          const ebx16 pre = __builtin_amdgcn_mfma_f32_32x32x16_bf16(XA, W1B[ct], ebx16{}, 0, 0, 0);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) pre[q] = v4f{0.f, 0.f, 0.f, 0.f};
-          const int ea = (lane & 3) + 4 * hh;   // A operand's edge (+ 8 q)
-#pragma unroll
-          for (int k = 0; k < EB_XF_KMAX; ++k) {
-            if (k >= kin) break;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              pre[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(xs[(ea + 8 * q) * EBF_XP + k], w1[ct][k], pre[q], 0, 0, 0);
-          }
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float f = (float)(__bf16)fmaxf(pre[i >> 2][i & 3] + b1[ct], 0.f);   // the forward's bf16 f
-            GA[i >> 3][i & 7] = (__bf16)(f > 0.f ? G[i] : 0.f);
-          }
+          for (int i = 0; i < 16; ++i) GA[i >> 3][i & 7] = (__bf16)((float)(__bf16)pre[i] > 0.f ? G[i] : 0.f);
         } else {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {

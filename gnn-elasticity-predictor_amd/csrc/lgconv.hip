@@ -917,6 +917,17 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
 
 }  // namespace lg3
 
+// The bf16 recompute kernels (matrix cores, lgmx.hip)
+int lgm_fwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, const int32_t* items, int64_t n_items,
+            const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv, const float* U, const float* wbar,
+            const float* X, int64_t ldx, const float* W1, const float* b1, float* aggV, float* S, float* sumA,
+            float* mstat, float* den, const DropParams& drop, hipStream_t s);
+int lgm_bwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, const int32_t* items, int64_t n_items,
+            const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv, const float* U, const float* Vd,
+            const float* wbar, const float* X, int64_t ldx, const float* W1, const float* b1, const float* dout,
+            const float* outp, const float* mstat, const float* den, float* dq, int64_t lddq, float* Sz, float* sigz,
+            float* dz_e, float* alpha_e, const DropParams& drop, hipStream_t s);
+
 // Entry points used by tconv.hip's C ABI when the schedule asks for single-wave items
 // (ALIGNN_SCHED_WAVE_ITEMS) and the call is in this family's domain (lg3_supported).
 bool lg3_supported(int D, int H, const int32_t* feat_row, const float* F, const AlignnSchedule* sched) {
@@ -1051,10 +1062,10 @@ extern "C" int alignn_lg_fwd_x(int64_t n, int64_t m, int32_t D, int32_t H, const
   p.drop = make_drop(drop_p, seed);
   if (p.n_items <= 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool drop = p.drop.active != 0, bf = KV16 != nullptr;
-  if (drop && bf) lg3::launch_fwd_x<true, true>(p, s);
-  else if (drop) lg3::launch_fwd_x<true, false>(p, s);
-  else if (bf) lg3::launch_fwd_x<false, true>(p, s);
+  if (KV16)   // bf16 storage (config C3): the matrix-core kernels (lgmx.hip)
+    return lgm_fwd(n, m, off_dst, src_at, p.items, p.n_items, QKV, ldq, KV16, ldkv, U, wbar, X, ldx, W1, b1, aggV, S,
+                   sumA, mstat, den, p.drop, s);
+  if (p.drop.active) lg3::launch_fwd_x<true, false>(p, s);
   else lg3::launch_fwd_x<false, false>(p, s);
   ALIGNN_LAUNCH_CHECK("lg3_fwd_kernel (x)");
   return ALIGNN_OK;
@@ -1078,10 +1089,10 @@ extern "C" int alignn_lg_bwd_dst_x(int64_t n, int64_t m, int32_t D, int32_t H, c
   p.drop = make_drop(drop_p, seed);
   if (p.n_items <= 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool drop = p.drop.active != 0, bf = KV16 != nullptr;
-  if (drop && bf) lg3::launch_bwd_x<true, true>(p, s);
-  else if (drop) lg3::launch_bwd_x<true, false>(p, s);
-  else if (bf) lg3::launch_bwd_x<false, true>(p, s);
+  if (KV16)
+    return lgm_bwd(n, m, off_dst, src_at, p.items, p.n_items, QKV, ldq, KV16, ldkv, U, Vd, wbar, X, ldx, W1, b1, dout,
+                   outp, mstat, den, dq, lddq, Sz, sigz, dz_e, alpha_e, p.drop, s);
+  if (p.drop.active) lg3::launch_bwd_x<true, false>(p, s);
   else lg3::launch_bwd_x<false, false>(p, s);
   ALIGNN_LAUNCH_CHECK("lg3_bwd_dst_kernel (x)");
   return ALIGNN_OK;

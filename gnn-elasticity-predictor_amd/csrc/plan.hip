@@ -201,13 +201,26 @@ extern "C" void* alignn_plan_end(void) {
     }
   }
   bool ok = true;
-  // Cross-stream edges of one device: no system-scope fence at the record.  The producing kernel's
-  // end-of-kernel release already makes its writes visible device-wide (as it does for the next
-  // kernel of its own stream); the default event adds a system-scope writeback that holds the source
-  // stream ~4 us per edge (tools/probe/marker_cost.hip: 7.2 us per kernel pair -> 11.1 with a default
-  // event between them, 8.8 without the system fence).
-  for (auto& ev : p->events)
-    ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
+  // Cross-stream edges inside the step: no system-scope fence at the record.  The producing kernel's
+  // end-of-kernel release (agent scope: the XCD L2s written back, gfx950 memory model) already makes its
+  // writes visible to every kernel of the device, as it does for the next kernel of its own stream; the
+  // default event adds a system-scope writeback that holds the source stream ~4 us per edge
+  // (tools/probe/marker_cost.hip: 7.2 us per kernel pair -> 11.1 with a default event between them, 8.8
+  // without the system fence).  The last edge from each other slot into slot 0 — the joins after which
+  // the caller's stream, torch ops and device-to-host copies (loss.item()) read the step's results —
+  // keeps the default, system-scope event: visibility beyond the device's kernels is then not assumed.
+  std::vector<char> fenced(p->events.size(), 0);
+  {
+    std::vector<int> last_join(p->streams.size(), -1);   // per source slot: its last edge into slot 0
+    for (const PlanEntry& e : p->entries)
+      if (!e.func && e.event >= 0 && e.slot == 0) last_join[(size_t)e.src] = e.event;
+    for (int ev : last_join)
+      if (ev >= 0) fenced[(size_t)ev] = 1;
+  }
+  for (size_t i = 0; i < p->events.size(); ++i)
+    ok = ok && hipEventCreateWithFlags(&p->events[i], fenced[i] ? hipEventDisableTiming
+                                                                 : (hipEventDisableTiming | hipEventDisableSystemFence))
+                   == hipSuccess;
   for (auto& ev : p->stamps) ok = ok && hipEventCreate(&ev) == hipSuccess;
   if (!ok) {
     set_error("plan_end: event creation failed");

@@ -4,6 +4,7 @@ ranks with identical parameters equal to a single process stepping on the mean g
 step time is the max over ranks.  (The GPU run uses the same hook over RCCL.)"""
 import os
 import socket
+import weakref
 
 import pytest
 import torch
@@ -113,6 +114,10 @@ def test_member_placement_and_seeds():
 # ------------------------------------------------------------------------------------------------
 # FusedTrainer.grad_hook between the two replayed launch plans (trainer._replay), world size 2
 # ------------------------------------------------------------------------------------------------
+class _Slot:
+    """A captured batch stand-in (weak-referenceable, no tensors)."""
+
+
 class _FakeLib:
     """Stands in for libalignn_hip's plan replay: plan 1 = forward/backward (writes this rank's
     gradient), plan 2 = clip + AdamW (the reference's two-group AdamW on CPU)."""
@@ -149,6 +154,7 @@ def _step_flat(flat, grad, s0):
 def _trainer_worker(rank, world, port, out_dir):
     import alignn_mi355x as A
     from alignn_mi355x import _lib, ops, trainer as trainer_mod
+    from alignn_mi355x.engine import batch_versions
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -170,8 +176,10 @@ def _trainer_worker(rank, world, port, out_dir):
 
         tr.grad_hook = logged_hook
         tr._seed_dev = torch.zeros(1, dtype=torch.int64)
-        batch = object()
+        batch = _Slot()
         tr._graph = (None, None, batch, [1, 2])   # two captured plans, as capture(mode="plan") leaves them
+        # ... holding this batch (the captured slot's contents)
+        tr._bound, tr._bound_v = weakref.ref(batch), batch_versions(batch, trainer_mod.BATCH_FIELDS)
         tr._exchange = tr._exchange_mode()        # and the exchange they were captured for
         before = tr.st.flat.clone()
         tr.step(batch, seed=3)
@@ -228,6 +236,7 @@ class _FakeLib3(_FakeLib):
 def _bucket_worker(rank, world, port, out_dir):
     import alignn_mi355x as A
     from alignn_mi355x import _lib, ops, trainer as trainer_mod
+    from alignn_mi355x.engine import batch_versions
     from alignn_mi355x.layout import bucket_split
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -250,8 +259,9 @@ def _bucket_worker(rank, world, port, out_dir):
         tr.grad_buckets = buckets
         tr._seed_dev = torch.zeros(1, dtype=torch.int64)
         tr.ctx.side = lambda dev: None
-        batch = object()
+        batch = _Slot()
         tr._graph = (None, None, batch, [1, 2, 3])
+        tr._bound, tr._bound_v = weakref.ref(batch), batch_versions(batch, trainer_mod.BATCH_FIELDS)
         tr._exchange = tr._exchange_mode()
         before = tr.st.flat.clone()
         tr.step(batch, seed=3)

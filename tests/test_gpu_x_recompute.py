@@ -3,14 +3,15 @@ alignn_lg_fwd_x / alignn_lg_bwd_dst_x, and alignn_enc_bwd_bf16 without F16): the
 hidden layer f = relu(x W1^T + b1) (train.py:358-364, :553-556) is recomputed from the 11 raw inputs
 per edge group on the matrix cores instead of being materialised by linear_smallk and re-read.
 
-* Against the streamed-row kernels on the materialised layer (linear_smallk / linear_smallk_bf16
-  output): bitwise where both run the same number of edge groups in flight (fp32 forward, bf16
-  forward and backward); the fp32 target-side backward runs one group in flight against the
-  streamed kernel's two, and the compiler contracts the per-edge softmax terms differently
-  (1-ulp differences): 1e-6 of each output's largest magnitude.
-* The bf16 deferred encoder backward with its mask recomputed against the mask read from the
-  stored bf16 layer: bitwise.
-* The whole step: recompute_angle on vs off — loss and gradients (C2 fp32, B = 4; C3 bf16, B = 16).
+* fp32: against the streamed-row kernels on the materialised layer (linear_smallk output): bitwise
+  forward; the target-side backward runs one group in flight against the streamed kernel's two, and
+  the compiler contracts the per-edge softmax terms differently (1-ulp differences, DESIGN §9 round
+  4): 1e-6 of each output's largest magnitude.  (The bf16 form runs on the matrix cores with
+  autocast's operand rounding: tests/test_gpu_x_lgmx.py.)
+* The whole step: recompute_angle on vs off — loss and gradients (C2 fp32, B = 4: the same
+  arithmetic; C3 bf16, B = 16: the recomputed layer is autocast's bf16(x) bf16(W1)^T + bf16(b1),
+  the materialised one linear_smallk_bf16's fp32 products rounded once, so the two steps agree to
+  bf16 rounding of the hidden layer).
 """
 import pytest
 import torch
@@ -94,7 +95,7 @@ def _recomputed(csr, m, t, x, W1, b1, drop, bf16):
 FWD = ("outp", "S", "sumA", "mstat", "den")
 
 
-@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("bf16", [False])
 @pytest.mark.parametrize("drop", [0.0, 0.15])
 @pytest.mark.parametrize("degs", list(DEGREES))
 def test_recomputed_edge_features_match_streamed_rows(bf16, drop, degs):
@@ -126,28 +127,14 @@ def test_recompute_rejects_unsupported_shapes():
                      o["sumA"], o["mstat"], o["den"], 0.0, 1)
 
 
-@pytest.mark.parametrize("n,L", [(40, 4), (9, 2)])
-def test_enc_bwd_bf16_mask_recomputed_bitwise(n, L):
-    from test_gpu_x_encbwd import _case as eb_case
-    ops = _ops()
-    csr, x, W1, b1, U, Vd, dz, al = eb_case(n, 256, 4, L, 11, seed=n + L)
-    T = x.size(0)
-    F16 = torch.empty(T, 256, device=DEV, dtype=torch.bfloat16)
-    ops.linear_smallk_bf16(x, W1, b1, F16, relu=True)
-    dW1a, db1a = torch.empty(256, 11, device=DEV), torch.empty(256, device=DEV)
-    dW1b, db1b = torch.empty(256, 11, device=DEV), torch.empty(256, device=DEV)
-    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1a, db1a, F=F16)
-    ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1b, db1b, bf16=True)
-    torch.cuda.synchronize()
-    assert torch.equal(dW1a, dW1b) and torch.equal(db1a, db1b)
-
-
 @pytest.mark.parametrize("precision,B", [("fp32", 4), ("bf16", 16)])
 def test_step_with_recomputed_angle_layer(precision, B):
-    """The training step's loss and gradients with recompute_angle on (the default) and off: the
-    forward is bitwise (same attention arithmetic on bitwise the same edge features); gradients to
-    fp32 summation order of the target-side backward (fp32: one group in flight vs two) — bitwise
-    at bf16, where both run one."""
+    """The training step's loss and gradients with recompute_angle on (the default) and off.  fp32: the
+    forward is bitwise (same attention arithmetic on bitwise the same edge features), gradients to
+    fp32 summation order of the target-side backward (one group in flight vs two).  bf16: the two
+    hidden layers differ by bf16 rounding (autocast's bf16 operands vs fp32 products rounded once):
+    loss to 1e-2, every gradient within 5e-2 normwise and cosine > 0.998 (gradients that are zero up to
+    rounding: both below 1e-4 of the largest)."""
     import alignn_mi355x as A
     from alignn_mi355x.synthetic import mp_like_batch
     res = {}
@@ -163,12 +150,21 @@ def test_step_with_recomputed_angle_layer(precision, B):
         torch.cuda.synchronize()
         res[on] = (loss, {k: v.clone() for k, v in tr.st.G.named.items()})
     (l1, g1), (l0, g0) = res[True], res[False]
+    if precision == "bf16":
+        assert abs(float(l1) - float(l0)) <= 1e-2 * abs(float(l0)), (float(l1), float(l0))
+        top = max(float(v.double().norm()) for v in g0.values())
+        for k in g0:
+            a, b = g1[k].double().flatten(), g0[k].double().flatten()
+            nb = float(b.norm())
+            if nb <= 1e-4 * top:
+                # analytically zero up to rounding (the key bias: a per-target constant shift of every
+                # score, which the softmax cancels) — its rounding noise has no direction to compare
+                assert float(a.norm()) <= 1e-4 * top, k
+                continue
+            assert float((a - b).norm()) <= 5e-2 * nb, (k, float((a - b).norm()) / nb)
+            assert float(a @ b) >= 0.998 * float(a.norm()) * nb, k
+        return
     assert torch.equal(l1, l0)
     gmax = max(float(v.abs().max()) for v in g0.values())
     for k in g0:
-        if precision == "bf16" and "angle_encoder.0" not in k:
-            assert torch.equal(g1[k], g0[k]), k
-        else:
-            # (bf16: the deferred encoder backward's recompute form runs 512 workgroups instead of 768,
-            # so its per-workgroup partial sums of dW1 / db1 group the targets differently)
-            assert float((g1[k] - g0[k]).abs().max()) <= 1e-5 * gmax, k
+        assert float((g1[k] - g0[k]).abs().max()) <= 1e-5 * gmax, k

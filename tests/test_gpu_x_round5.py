@@ -312,8 +312,8 @@ def test_bf16_atom_edge_gradient_is_a_bf16_rounding():
 
 def test_batched_heads_equal_two_products():
     """engine.forward's heads: mean and logvar Linear in one batched launch over the flat parameter
-    buffer (strided views) give the two separate products' bits; and the engine's zero-free bond
-    gradient (gate dX_zero) keeps the step equal to the reference configuration within rounding."""
+    buffer (strided views) give the two separate products' bits.  (The zero-free bond gradient, gate
+    dX_zero: tests/test_gpu_x_round6.py.)"""
     from alignn_mi355x import ops
     g = torch.Generator(device="cpu").manual_seed(9)
     B, D, Tt = 32, 256, 2

@@ -1,6 +1,8 @@
 """Host-side guards added in round 4 (no GPU): the padded batch's compaction fill, the collated
 line-graph index bound behind a store batch's trusted flag, and a replay refusing a gradient exchange
 that changed after capture."""
+import weakref
+
 import numpy as np
 import pytest
 import torch
@@ -63,12 +65,17 @@ class _ReplayLib:
         return 0
 
 
+class _Slot:
+    """A captured batch stand-in (weak-referenceable, no tensors)."""
+
+
 def test_replay_refuses_exchange_changed_after_capture(monkeypatch):
     """The phases of a captured step are cut for the exchange in place at capture (grad_buckets: three
     phases, a hook or none: two); a replay after grad_buckets / grad_hook changed raises instead of
     skipping the all_reduce or crashing (trainer.py:356)."""
     import alignn_mi355x as A
     from alignn_mi355x import _lib, ops, trainer as trainer_mod
+    from alignn_mi355x.engine import batch_versions
     torch.manual_seed(0)
     model = A.HeteroAlignnRegressor(A.AlignnRegressor(6, 8, 7, 289, 2, 32, 1, 1, 0.0), 2)
     tr = A.FusedTrainer(model, optimizer="torch")
@@ -76,10 +83,11 @@ def test_replay_refuses_exchange_changed_after_capture(monkeypatch):
     monkeypatch.setattr(ops, "stream_ptr", lambda *a, **k: 0)
     monkeypatch.setattr(trainer_mod, "check", lambda rc, what: None)
     tr._seed_dev = torch.zeros(1, dtype=torch.int64)
-    batch = object()
+    batch = _Slot()
     calls = []
     tr.grad_hook = lambda g: calls.append(1)
     tr._graph = (None, None, batch, [1, 2])
+    tr._bound, tr._bound_v = weakref.ref(batch), batch_versions(batch, trainer_mod.BATCH_FIELDS)
     tr._exchange = tr._exchange_mode()
     tr.step(batch, seed=1)
     assert calls == [1]

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-6 GPU job steps (run through gpurun from the repo root).  Each step under its own time
+# limit; the script stops at the first failing step.
+set -eo pipefail
+O=$PWD/gpurun_out/${JOB:-r6}
+mkdir -p "$O"
+export PYTHONUNBUFFERED=1
+PT=(python -u -m pytest -x -q --timeout 300 --timeout-method thread)
+run() { local name=$1 t=$2; shift 2; echo "[job] $name: $*"; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1 || { echo "[job] $name FAILED rc=$?"; tail -30 "$O/$name.log"; exit 1; }; tail -3 "$O/$name.log"; }
+val() { for f in "$@"; do echo "$(basename "$f") $(grep -o '"value": [0-9.]*' "$f" | head -1) e2e=$(python -c "import json,sys;d=json.loads([l for l in open('$f') if l.startswith('{')][-1]);e=d.get('e2e') or {};print(e.get('value'),e.get('ms_per_step'),e.get('host_ms_per_step'),e.get('stream_priorities'))" 2>/dev/null)"; done; }
+E2E=(python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 3000)
+for step in "$@"; do
+  case $step in
+    gpu) run gpu 900 "${PT[@]}" tests -m gpu ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    c2) run c2 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline ;;
+    c3) run c3 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline ;;
+    e2e) for i in 1 2; do
+           run e2e_def_$i 300 "${E2E[@]}"
+           run e2e_pool0_$i 300 "${E2E[@]}" --set loader_dedicated=0
+           run e2e_poolhi_$i 300 "${E2E[@]}" --set loader_priority=-1
+           run e2e_poolhi_pf2_$i 300 "${E2E[@]}" --set loader_priority=-1 --set prefetch=2
+           run e2e_allnorm_$i 300 "${E2E[@]}" --set main_priority=0
+         done
+         val "$O"/e2e_*.log ;;
+    lgmx) run lgmx 600 "${PT[@]}" tests/test_gpu_x_lgmx.py tests/test_gpu_x_recompute.py -v ;;
+    newt) run newt 900 "${PT[@]}" tests/test_gpu_x_lgmx.py tests/test_gpu_x_recompute.py tests/test_gpu_x_infer.py tests/test_gpu_x_round6.py -v ;;
+    lgmxb) run lgmx_bench 300 python tools/lgx_bench.py --batch 256 ;;
+    bf16t) run bf16t 900 "${PT[@]}" tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round5.py tests/test_gpu_x_round4.py tests/test_gpu_x_encbwd.py -v ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
