@@ -24,6 +24,9 @@
 //     in LDS and read transposed (ds_read_b64_tr_b16); alpha' enters as bf16 hi + lo parts (two
 //     products), so the weights keep ~16 significant bits, as autocast keeps them in fp32.
 // Softmax, its statistics and every accumulator are fp32; online softmax over the pairs.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "vec.h"
 
@@ -252,10 +255,49 @@ struct FwdState {
   f4 Sacc[4], Vacc[4];
   float m, den_l, sa_l;
 };
+// outputs of one target (lane (g, c): head c & 3 statistics; accumulator register r = head r)
+__device__ __forceinline__ void fwd_out(const Params& p, const FwdState& st, int64_t d, int w, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  const float dn = rows_sum(st.den_l) + 1e-16f;
+  const float inv = 1.0f / dn;
+  const float sa = rows_sum(st.sa_l);
+  const f4 iv = {readlane_f(inv, 0), readlane_f(inv, 1), readlane_f(inv, 2), readlane_f(inv, 3)};
+  const float ig = pick4(iv, g);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) p.S[(d * H + g) * D + 64 * w + 16 * t + c] = pick4(st.Sacc[t], g) * ig;
+  f4 vv = st.Vacc[0];
+  vv = g == 1 ? st.Vacc[1] : vv;
+  vv = g == 2 ? st.Vacc[2] : vv;
+  vv = g == 3 ? st.Vacc[3] : vv;
+  p.aggV[d * D + 64 * w + 16 * g + c] = pick4(vv, w) * pick4(iv, w);
+  if (w == 0 && lane < H) {
+    p.sumA[d * H + lane] = sa * inv;
+    p.mstat[d * H + lane] = st.m;
+    p.den[d * H + lane] = dn;
+  }
+}
+__device__ __forceinline__ void fwd_init(FwdState& st) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { st.Sacc[i] = zero4(); st.Vacc[i] = zero4(); }
+  st.m = -INFINITY;
+  st.den_l = 0.f;
+  st.sa_l = 0.f;
+}
 
-template <bool DROP>
+
+// W1 fragments of this wave: in registers, or in LDS (lane-linear 16-byte slots, the persistent kernel)
+struct W1Regs {
+  bf8 f[4];
+  __device__ __forceinline__ bf8 get(int t, int) const { return f[t]; }
+};
+struct W1Lds {
+  const u4* base;   // this wave's 4 x 64 slots
+  __device__ __forceinline__ bf8 get(int t, int lane) const { return __builtin_bit_cast(bf8, base[64 * t + lane]); }
+};
+
+template <bool DROP, class W1S>
 __device__ __forceinline__ void fwd_pair(const Params& p, const PairIn& in, int32_t tp, int32_t end, int buf,
-                                         __bf16* img, float (*zb)[4][2][H][16], const bf8 (&W1f)[4],
+                                         __bf16* img, float (*zb)[4][2][H][16], const W1S& W1f,
                                          const bf8 (&Uf)[2], const bf8 (&Qf)[2], float cadd, FwdState& st, int w,
                                          int lane) {
   const int g = lane >> 4, c = lane & 15, hc = c & 3;
@@ -266,7 +308,7 @@ __device__ __forceinline__ void fwd_pair(const Params& p, const PairIn& in, int3
   for (int x = 0; x < 2; ++x) {
     f4 T[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) T[t] = relu4(mma(W1f[t], in.X[x], zero4()));
+    for (int t = 0; t < 4; ++t) T[t] = relu4(mma(W1f.get(t, lane), in.X[x], zero4()));
     f4 Zp = mma(pack8(T[0], T[1]), Uf[0], zero4());
     Zp = mma(pack8(T[2], T[3]), Uf[1], Zp);
     Zp = mma(in.G[x][0], Qf[0], Zp);
@@ -277,7 +319,10 @@ __device__ __forceinline__ void fwd_pair(const Params& p, const PairIn& in, int3
   }
   bf8 FB[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) FB[t] = pack8(relu4(mma(in.X[0], W1f[t], zero4())), relu4(mma(in.X[1], W1f[t], zero4())));
+  for (int t = 0; t < 4; ++t) {
+    const bf8 Wt = W1f.get(t, lane);
+    FB[t] = pack8(relu4(mma(in.X[0], Wt, zero4())), relu4(mma(in.X[1], Wt, zero4())));
+  }
   __syncthreads();
   f4 z[2];
 #pragma unroll
@@ -353,18 +398,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int32_t beg = uni(sld(p.off, d)), end = uni(sld(p.off, d + 1));
 
   FwdState st;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { st.Sacc[i] = zero4(); st.Vacc[i] = zero4(); }
-  st.m = -INFINITY;
-  st.den_l = 0.f;
-  st.sa_l = 0.f;
+  fwd_init(st);
 
   if (beg < end) {
     Seg sg;
     seg_load(p, sg, beg, end, lane);
-    bf8 W1f[4], Uf[2], Qf[2];
+    W1Regs W1f;
+    bf8 Uf[2], Qf[2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) W1f[t] = w1_frag(p, 64 * w + 16 * t + c, g);
+    for (int t = 0; t < 4; ++t) W1f.f[t] = w1_frag(p, 64 * w + 16 * t + c, g);
     const float* qrow = p.Q + d * p.ldq;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -385,25 +427,85 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       fwd_pair<DROP>(p, B, beg + 32 * (pr + 1), end, (pr + 1) & 1, img, zb, W1f, Uf, Qf, cadd, st, w, lane);
     }
   }
-  // ---- outputs (lane (g, c): head c & 3 statistics; accumulator register r = head r)
-  const float dn = rows_sum(st.den_l) + 1e-16f;
-  const float inv = 1.0f / dn;
-  const float sa = rows_sum(st.sa_l);
-  const f4 iv = {readlane_f(inv, 0), readlane_f(inv, 1), readlane_f(inv, 2), readlane_f(inv, 3)};
-  const float ig = pick4(iv, g);
+  fwd_out(p, st, d, w, lane);
+}
+
+// Persistent form: a grid of a few workgroups per CU walks the schedule's list (workgroup b takes items
+// b, b + G, b + 2G, ...: the same XCD for every item of a block under round-robin placement, G % 8 == 0),
+// and the loads run one unit (target, pair) ahead across target boundaries — the next target's source
+// ids and constant fragments while the current target runs, its first pair's gathers during the current
+// target's last pair — so no target waits for its own prologue.
+struct FwdTgt {
+  int64_t d;
+  int32_t beg, end;
+  Seg sg;
+  bf8 Uf[2], Qf[2];
+  float qv, wbv;   // this lane's element of Q_w and wbar_w (c_w is their wave sum)
+};
+__device__ __forceinline__ void fwd_tgt_load(const Params& p, int64_t item, FwdTgt& T, int w, int lane) {
+  const int g = lane >> 4, c = lane & 15, hc = c & 3;
+  T.d = (int64_t)uni(sld(p.items, item));
+  T.beg = uni(sld(p.off, T.d));
+  T.end = uni(sld(p.off, T.d + 1));
+  if (p.m > 0) seg_load(p, T.sg, T.beg, max(T.end, T.beg + 1), lane);   // (an empty segment reads a valid id)
+  T.sg.deg = T.end - T.beg;
+  const float* qrow = p.Q + T.d * p.ldq;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) p.S[(d * H + g) * D + 64 * w + 16 * t + c] = pick4(st.Sacc[t], g) * ig;
-  {
-    f4 vv = st.Vacc[0];
-    vv = g == 1 ? st.Vacc[1] : vv;
-    vv = g == 2 ? st.Vacc[2] : vv;
-    vv = g == 3 ? st.Vacc[3] : vv;
-    p.aggV[d * D + 64 * w + 16 * g + c] = pick4(vv, w) * pick4(iv, w);
+  for (int s = 0; s < 2; ++s) {
+    T.Uf[s] = u_frag(p.U, T.d, hc, w, s, g);
+    T.Qf[s] = q_frag(qrow, w, s, g, hc == w);
   }
-  if (w == 0 && lane < H) {
-    p.sumA[d * H + lane] = sa * inv;
-    p.mstat[d * H + lane] = st.m;
-    p.den[d * H + lane] = dn;
+  T.qv = qrow[64 * w + lane];
+  T.wbv = p.wbar ? p.wbar[64 * w + lane] : 0.f;
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void lgm_fwd_p_kernel(Params p) {
+  if constexpr (DROP) resolve_drop(p.drop);
+  __shared__ __attribute__((aligned(16))) __bf16 imgs[4 * IMG];
+  __shared__ __attribute__((aligned(16))) float zb[2][4][2][H][16];
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int g = lane >> 4, c = lane & 15, hc = c & 3;
+  __shared__ u4 w1s[4][4 * 64];   // each wave's W1 fragments (16 KB: registers are the binding resource here)
+  __bf16* img = imgs + w * IMG;
+  int64_t it = blockIdx.x;
+  if (it >= p.n_items) return;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) w1s[w][64 * t + lane] = __builtin_bit_cast(u4, w1_frag(p, 64 * w + 16 * t + c, g));
+  const W1Lds W1f{w1s[w]};   // read back by this wave only (LDS is in order within a wave)
+  FwdTgt T, N;
+  fwd_tgt_load(p, it, T, w, lane);
+  PairIn A, B;
+  if (T.beg < T.end) pair_load(p, T.sg, 0, A, 0, D, w, lane);
+  int64_t nit = it + gridDim.x;
+  bool hasN = nit < p.n_items;
+  if (hasN) fwd_tgt_load(p, nit, N, w, lane);
+  int buf = 0;
+  while (true) {
+    FwdState st;
+    fwd_init(st);
+    const float cw = p.wbar ? wave_sum(T.wbv * T.qv) : 0.f;   // c_w = <wbar_w, Q_w>
+    const float cadd = hc == w ? cw : 0.f;
+    const int np = (T.end - T.beg + 31) / 32;
+    bool ahead = false;   // B holds the next target's first pair
+    for (int pr = 0; pr < np; ++pr) {
+      if (pr + 1 < np) {
+        pair_load(p, T.sg, pr + 1, B, 0, D, w, lane);
+      } else if (hasN && N.beg < N.end) {
+        pair_load(p, N.sg, 0, B, 0, D, w, lane);
+        ahead = true;
+      }
+      fwd_pair<DROP>(p, A, T.beg + 32 * pr, T.end, buf, img, zb, W1f, T.Uf, T.Qf, cadd, st, w, lane);
+      buf ^= 1;
+      A = B;
+    }
+    fwd_out(p, st, T.d, w, lane);
+    if (!hasN) break;
+    T = N;
+    if (!ahead && T.beg < T.end) pair_load(p, T.sg, 0, A, 0, D, w, lane);   // after an empty target
+    nit += gridDim.x;
+    hasN = nit < p.n_items;
+    if (hasN) fwd_tgt_load(p, nit, N, w, lane);
   }
 }
 
@@ -581,6 +683,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 }  // namespace lgm
 
+// Persistent grid: two workgroups per CU (the kernels' register budget: 2 waves per SIMD); a multiple
+// of 8 so that every item of a workgroup lands on one XCD under round-robin placement.
+static int lgm_persist_grid() {
+  static int g = 0;
+  if (g == 0) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t pr;
+      if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0) cus = pr.multiProcessorCount;
+    }
+    g = (2 * cus + 7) / 8 * 8;
+  }
+  return g;
+}
+// ALIGNN_LGM_PERSIST=0: one workgroup per target instead (A/B measurements)
+static bool lgm_persistent() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("ALIGNN_LGM_PERSIST");
+    v = (e && *e) ? (std::atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 // Entry points for lgconv.hip's C ABI (alignn_lg_fwd_x / alignn_lg_bwd_dst_x with bf16 K|V).
 int lgm_fwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, const int32_t* items, int64_t n_items,
             const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv, const float* U, const float* wbar,
@@ -593,8 +719,15 @@ int lgm_fwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, con
   p.aggV = aggV; p.S = S; p.sumA = sumA; p.mstat = mstat; p.den = den;
   p.drop = drop;
   if (n_items <= 0) return ALIGNN_OK;
-  if (drop.active) launch(lgm::lgm_fwd_kernel<true>, dim3((unsigned)n_items), dim3(lgm::NT), 0, s, p);
-  else launch(lgm::lgm_fwd_kernel<false>, dim3((unsigned)n_items), dim3(lgm::NT), 0, s, p);
+  if (lgm_persistent()) {
+    const unsigned grid = (unsigned)std::min<int64_t>(n_items, lgm_persist_grid());
+    if (drop.active) launch(lgm::lgm_fwd_p_kernel<true>, dim3(grid), dim3(lgm::NT), 0, s, p);
+    else launch(lgm::lgm_fwd_p_kernel<false>, dim3(grid), dim3(lgm::NT), 0, s, p);
+  } else if (drop.active) {
+    launch(lgm::lgm_fwd_kernel<true>, dim3((unsigned)n_items), dim3(lgm::NT), 0, s, p);
+  } else {
+    launch(lgm::lgm_fwd_kernel<false>, dim3((unsigned)n_items), dim3(lgm::NT), 0, s, p);
+  }
   ALIGNN_LAUNCH_CHECK("lgm_fwd_kernel");
   return ALIGNN_OK;
 }

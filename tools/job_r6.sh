@@ -26,8 +26,29 @@ for step in "$@"; do
          val "$O"/e2e_*.log ;;
     lgmx) run lgmx 600 "${PT[@]}" tests/test_gpu_x_lgmx.py tests/test_gpu_x_recompute.py -v ;;
     newt) run newt 900 "${PT[@]}" tests/test_gpu_x_lgmx.py tests/test_gpu_x_recompute.py tests/test_gpu_x_infer.py tests/test_gpu_x_round6.py -v ;;
-    lgmxb) run lgmx_bench 300 python tools/lgx_bench.py --batch 256 ;;
+    lgmxb) ALIGNN_LGM_PERSIST=1 run lgmx_bench_p1 300 python tools/lgx_bench.py --batch 256
+           ALIGNN_LGM_PERSIST=0 run lgmx_bench_p0 300 python tools/lgx_bench.py --batch 256
+           for f in $O/lgmx_bench_p*.log; do echo "$(basename $f) $(grep -o '"fwd_bf16_x_us": [0-9.]*\|"bwd_bf16_x_us": [0-9.]*\|"enc_bwd_bf16_x_us": [0-9.]*' $f | tr '\n' ' ')"; done ;;
+    c3ab) for i in 1 2; do for v in 1 0; do
+            ALIGNN_LGM_PERSIST=$v run c3_p${v}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done; done
+          for f in $O/c3_p*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
     bf16t) run bf16t 900 "${PT[@]}" tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round5.py tests/test_gpu_x_round4.py tests/test_gpu_x_encbwd.py -v ;;
+    rpc2) cd /tmp && export TMPDIR=/tmp
+          timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c2 -o run --output-format csv -- python $OLDPWD/bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c2.log 2>&1 || exit 1
+          cd $OLDPWD; python tools/timeline.py $O/rp_c2/run_kernel_trace.csv --top 25 > $O/rp_c2_timeline.txt; python tools/timeline.py $O/rp_c2/run_kernel_trace.csv --by-kernel --step 5 > $O/rp_c2_timeline_bykernel.txt; python tools/trace_by_grid.py $O/rp_c2/run_kernel_trace.csv > $O/rp_c2_by_grid.txt 2>&1; head -20 $O/rp_c2_timeline.txt ;;
+    rpc3) cd /tmp && export TMPDIR=/tmp
+          timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c3 -o run --output-format csv -- python $OLDPWD/bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c3.log 2>&1 || exit 1
+          cd $OLDPWD; python tools/timeline.py $O/rp_c3/run_kernel_trace.csv --top 25 > $O/rp_c3_timeline.txt; python tools/timeline.py $O/rp_c3/run_kernel_trace.csv --by-kernel --step 5 > $O/rp_c3_timeline_bykernel.txt; python tools/trace_by_grid.py $O/rp_c3/run_kernel_trace.csv > $O/rp_c3_by_grid.txt 2>&1; head -20 $O/rp_c3_timeline.txt ;;
+    pmcx) cd /tmp && export TMPDIR=/tmp
+          for c in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace -d $O/pmcx_$c -o run --output-format csv -- python $OLDPWD/tools/lgx_bench.py --batch 256 --reps 3 > $O/pmcx_$c.log 2>&1 || exit 1
+          done
+          timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d $O/pmcx_sq -o run --output-format csv -- python $OLDPWD/tools/lgx_bench.py --batch 256 --reps 3 > $O/pmcx_sq.log 2>&1 || exit 1
+          timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmcx_mf -o run --output-format csv -- python $OLDPWD/tools/lgx_bench.py --batch 256 --reps 3 > $O/pmcx_mf.log 2>&1 || exit 1
+          cd $OLDPWD
+          python tools/pmc_traffic.py $O/pmcx_FETCH_SIZE $O/pmcx_WRITE_SIZE --top 20 > $O/pmcx_traffic.txt
+          python tools/pmc_sq.py $O/pmcx_sq > $O/pmcx_sq.txt; python tools/pmc_mfma.py $O/pmcx_mf > $O/pmcx_mfma.txt
+          cat $O/pmcx_traffic.txt $O/pmcx_sq.txt | head -40 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
