@@ -802,10 +802,13 @@ class AlignnEngine:
         # the attention kernels from the 11 raw inputs instead of materialised and re-read 8 times
         # (ops.lg_fwd_x / lg_bwd_dst_x; the deferred encoder backward recomputes its ReLU mask)
         self.recompute_angle = True
-        # ... and at bf16 storage (config C3): the matrix-core attention kernels (lgmx.hip) recompute it
-        # as autocast does (bf16 x, W1, b1; fp32 accumulation) and take every per-edge product on the
-        # matrix cores, and the deferred encoder backward recomputes its mask the same way
-        self.recompute_angle_bf16 = True
+        # ... and at bf16 storage (config C3): opt-in — the matrix-core attention kernels (lgmx.hip)
+        # recompute it as autocast does and take every per-edge product on the matrix cores.  Off by
+        # default: C3 21.8k vs 23.2k graphs/s against the streamed bf16 rows on the same box
+        # (profiles/r06/ab_c3_recompute_mx.txt; the per-target kernels are issue- and latency-bound at
+        # 0.13 of the matrix cores).  Off, the stored layer is autocast's Linear on the matrix cores
+        # (ops.linear_smallk_bf16) and the deferred encoder backward recomputes its mask from x.
+        self.recompute_angle_bf16 = False
 
     @contextmanager
     def using_precision(self, precision: str):
@@ -853,7 +856,7 @@ class AlignnEngine:
         attention (its backward is the deferred enc_bwd)."""
         W1, b1 = P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias")
         if a.dtype == torch.bfloat16:
-            if self.skinny_encoder and bc.xa.size(1) <= ops.SMALLK_MAX and D % 4 == 0:
+            if self._angle_mx(bc, W1, a):
                 ops.linear_smallk_bf16(bc.xa, W1, b1, a, relu=True)
             else:
                 a32 = torch.empty(a.shape, device=dev)
@@ -863,6 +866,12 @@ class AlignnEngine:
             ops.linear_smallk(bc.xa, W1, b1, a, relu=True)
         else:
             ops.gemm(bc.xa, W1.t(), a, bias=b1, relu=True)
+
+    def _angle_mx(self, bc: BatchCache, W1: torch.Tensor, a: Optional[torch.Tensor]) -> bool:
+        """The bf16 hidden layer is autocast's Linear on the matrix cores (ops.linear_smallk_bf16): its
+        ReLU mask is then the one the deferred encoder backward recomputes from x, bit for bit."""
+        return (a is not None and a.dtype == torch.bfloat16 and self.skinny_encoder
+                and ops.linear_smallk_bf16_ok(bc.xa, W1, a))
 
     def _line_proj(self, P: FlatViews, ctx, L: int, D: int) -> None:
         """The line convs' edge projections with the angle encoder's second Linear folded in."""
@@ -974,6 +983,7 @@ class AlignnEngine:
         elif ctx.has_angle and not xf:
             self._angle_hidden(P, bc, D, dev, a)
         ctx.h1a = ctx.a = a
+        ctx.a_mx = ctx.has_angle and self._angle_mx(bc, P.enc("angle", 0, "weight"), a)
         ctx.edge, ctx.node = [], []
         if line_proj:
             self._line_proj(P, ctx, L, D)
@@ -1199,6 +1209,10 @@ class AlignnEngine:
         enc16 = defer and ctx.angle_x is not None and ctx.angle_x[3]
         if f_rows is not None:
             kept.append(f_rows)
+            # a stored layer from the matrix-core Linear: the mask recomputed from the 11 raw inputs is the
+            # stored one's bit for bit, and cheaper than reading the [T, 256] rows back (enc_bwd_bf16_x)
+            if getattr(ctx, "a_mx", False) and bc.xa.size(1) <= ops.ENC_XF_KMAX:
+                f_rows, enc16 = None, True
         # the deferred angle-encoder backward (the longest branch of the tail) on a third stream,
         # started as soon as the last line block is done instead of behind the side stream's queue
         use_aux = self.enc_bwd_aux == 1 or (self.enc_bwd_aux > 1 and T >= self.enc_bwd_aux)

@@ -542,14 +542,24 @@ def linear_smallk(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor]
     return out
 
 
+SMALLK_BF16_MAX = 15   # alignn_linear_smallk_bf16out: K + the bias column within one 16-deep MFMA k step
+
+
+def linear_smallk_bf16_ok(X: torch.Tensor, W: torch.Tensor, out: torch.Tensor) -> bool:
+    """Shapes alignn_linear_smallk_bf16out takes: 1 <= K <= 15, N % 32 == 0, N <= 1024, unit inner
+    strides, 16-byte aligned output rows."""
+    return (out.dtype == torch.bfloat16 and X.dim() == 2 and X.stride(1) == 1 and W.dim() == 2 and W.stride(1) == 1
+            and out.stride(1) == 1 and 1 <= W.size(1) == X.size(1) <= SMALLK_BF16_MAX and out.size(1) == W.size(0)
+            and out.size(0) == X.size(0) and W.size(0) % 32 == 0 and W.size(0) <= 1024 and out.stride(0) % 8 == 0
+            and out.data_ptr() % 16 == 0)
+
+
 def linear_smallk_bf16(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor,
                        relu: bool = False) -> torch.Tensor:
-    """out (bf16) = act(X W^T + bias), the bf16-output form of linear_smallk (same fma order)."""
-    if (out.dtype != torch.bfloat16 or not (X.dim() == 2 and X.stride(1) == 1 and W.dim() == 2 and W.stride(1) == 1
-                                            and out.stride(1) == 1 and W.size(1) == X.size(1) <= SMALLK_MAX
-                                            and out.size(1) == W.size(0) and out.size(0) == X.size(0)
-                                            and W.size(0) % 4 == 0 and out.stride(0) % 4 == 0
-                                            and out.data_ptr() % 8 == 0)):
+    """out (bf16) = act(bf16(bf16(X) bf16(W)^T + bf16(bias))) — a Linear under bf16 autocast (fp32
+    accumulation on the matrix cores, ReLU on the rounded output), the arithmetic of the deferred encoder
+    backward's recomputed mask (alignn_enc_bwd_bf16 without F) bit for bit."""
+    if not linear_smallk_bf16_ok(X, W, out):
         raise ValueError(f"linear_smallk_bf16: unsupported shapes X{tuple(X.shape)} W{tuple(W.shape)} "
                          f"out{tuple(out.shape)} {out.dtype}")
     check(_lib.lib().alignn_linear_smallk_bf16out(X.data_ptr(), X.stride(0), X.size(0), X.size(1), W.data_ptr(),
@@ -575,6 +585,9 @@ def gemm_tn_smalln(A: torch.Tensor, X: torch.Tensor, C: torch.Tensor, colsum: Op
                                         C.stride(0), None if colsum is None else colsum.data_ptr(), int(accumulate),
                                         ws.data_ptr(), ws.numel(), stream_ptr()), "alignn_gemm_tn_smalln_f32")
     return C
+
+
+ENC_XF_KMAX = 12   # alignn_enc_bwd_bf16 without the stored layer: kin + the bias column <= 16 (one k step)
 
 
 def enc_bwd_ok(D: int, H: int, L: int, kin: int) -> bool:

@@ -75,8 +75,13 @@ __device__ __forceinline__ bf8 pack8(const f4& a, const f4& b) {
   v[4] = (__bf16)b[0]; v[5] = (__bf16)b[1]; v[6] = (__bf16)b[2]; v[7] = (__bf16)b[3];
   return v;
 }
-__device__ __forceinline__ f4 relu4(const f4& a) {
-  return f4{fmaxf(a[0], 0.f), fmaxf(a[1], 0.f), fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)};
+// relu(bf16(a | b)): autocast's order (the Linear's bf16 output, then ReLU), on the rounded bits — a
+// bf16 orders as its int16 bits do on either side of zero, so one v_pk_max_i16 per two elements
+__device__ __forceinline__ bf8 relu_pack8(const f4& a, const f4& b) {
+  u4 v = __builtin_bit_cast(u4, pack8(a, b));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm("v_pk_max_i16 %0, %1, 0" : "=v"(v[i]) : "v"(v[i]));
+  return __builtin_bit_cast(bf8, v);
 }
 // v = hi + lo with hi = bf16(v), lo = bf16(v - hi): the A operand of an aggregation as two fragments
 __device__ __forceinline__ void split8(const f4& a, const f4& b, bf8& hi, bf8& lo) {
@@ -113,7 +118,7 @@ __device__ __forceinline__ float rows_max(float x) {
 // A/B fragment of x_aug (lane (g, c): the edge's inputs k = 8 g .. 8 g + 7): g = 0 x[0..7]; g = 1 x[8..10]
 // and 1 (the bias column, k = 11); g >= 2 zero.  As the B operand of W1 x^T and the A operand of x W1^T.
 __device__ __forceinline__ bf8 x_frag(const Params& p, int32_t te, int g) {
-  const float* row = p.X + (int64_t)te * p.ldx;
+  const float* row = p.X + __umul24((uint32_t)te, (uint32_t)p.ldx);   // m < 2^24 (lgm_check)
   const f4 a = ld4(row + (g == 0 ? 0 : 8));   // unconditional (every row has 12 floats)
   const f4 b = ld4(row + 4);
   const bool lo_on = g < 2, g0 = g == 0;
@@ -183,34 +188,45 @@ __device__ __forceinline__ f4 drop4(const DropParams& dp, int32_t t0, int lane, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-target edge stream.  The target's source ids are loaded once (lane l: edges l, 64 + l, 128 + l,
-// 192 + l of the segment) and handed out by bpermute, so a pair's gathers wait for one memory round
-// trip, not two; the loads of pair p + 1 are issued before pair p is computed (two register sets,
-// unconditional loads with clamped indices — a load under a condition becomes a phi whose register
-// copy waits for it).  Segments longer than 256 edges (a schedule policy above the default heavy
-// threshold) load the ids past 256 directly.
+// Per-target edge stream.  The source ids of a 256-edge window of the segment are loaded once (lane l:
+// window edges l, 64 + l, 128 + l, 192 + l) and handed out by bpermute, so a pair's gathers wait for
+// one memory round trip, not two; the loads of pair p + 1 are issued before pair p is computed (two
+// register sets).  Every load of the pair stream is unconditional, its index clamped into the segment
+// (and the edge arrays): a value that comes from a load on one path of a branch and not on the other
+// makes the compiler's wait at the join a full vmcnt(0) drain — every prefetched load of the next pair
+// with it (that one branch, a direct src_at load for edges past 256, serialised the round-5 kernels'
+// six gathers per pair).  A window past the first (segments longer than 256 edges, above the default
+// heavy threshold) is loaded between pairs, and drained on its own path.
 // ---------------------------------------------------------------------------------------------
 struct Seg {
-  int32_t beg, deg;
-  int32_t sv[4];
+  int32_t beg, deg, wb;   // segment start and length; window base (a multiple of 256)
+  int32_t s0, s1, s2, s3; // window edge wb + 64 u + lane's source (separate registers: an array
+                          // indexed by a select becomes an LDS alloca)
 };
+// edge row of segment edge k, clamped into the segment and the edge arrays (m > 0)
+__device__ __forceinline__ int32_t seg_edge(const Params& p, const Seg& sg, int32_t k) {
+  return min(sg.beg + min(max(k, 0), max(sg.deg, 1) - 1), (int32_t)p.m - 1);
+}
+__device__ __forceinline__ void seg_window_load(const Params& p, Seg& sg, int32_t wb, int lane) {
+  sg.wb = wb;
+  sg.s0 = p.src_at[seg_edge(p, sg, wb + lane)];
+  sg.s1 = p.src_at[seg_edge(p, sg, wb + 64 + lane)];
+  sg.s2 = p.src_at[seg_edge(p, sg, wb + 128 + lane)];
+  sg.s3 = p.src_at[seg_edge(p, sg, wb + 192 + lane)];
+}
 __device__ __forceinline__ void seg_load(const Params& p, Seg& sg, int32_t beg, int32_t end, int lane) {
   sg.beg = beg;
   sg.deg = end - beg;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) sg.sv[u] = p.src_at[min(beg + 64 * u + lane, end - 1)];
+  seg_window_load(p, sg, 0, lane);
 }
-// source of segment edge k (lane-varying) for a group of edges starting at k0 (wave-uniform, the
-// group within one 8-aligned block of k: every lane's clamped k lies in k0's 64-block)
-__device__ __forceinline__ int32_t seg_src(const Params& p, const Seg& sg, int32_t k, int32_t k0) {
-  const int32_t kk = min(k, sg.deg - 1), kb = min(k0, sg.deg - 1);
-  if (kb >= 256) return p.src_at[sg.beg + kk];
-  const int r = kb >> 6;
-  int32_t v = sg.sv[0];
-  v = r == 1 ? sg.sv[1] : v;
-  v = r == 2 ? sg.sv[2] : v;
-  v = r == 3 ? sg.sv[3] : v;
-  return __shfl(v, kk & 63, 64);
+// before the loads of pair pr (wave-uniform): move the window when pr starts a new 256-edge block.
+// The rare path waits for its own loads (the asm uses them), so the join carries no pending load.
+__device__ __forceinline__ void seg_advance(const Params& p, Seg& sg, int pr, int lane) {
+  const int32_t wb = (32 * pr) & ~255;
+  if (wb != sg.wb) {
+    seg_window_load(p, sg, wb, lane);
+    asm volatile("" : "+v"(sg.s0), "+v"(sg.s1), "+v"(sg.s2), "+v"(sg.s3));
+  }
 }
 // One pair's loads: raw inputs (x_aug fragments), the gathered A-operand rows of both tiles (columns
 // `gcol`: fwd K, bwd V) and the 32 rows staged into the LDS image (columns `rcol`: fwd V, bwd K)
@@ -223,20 +239,30 @@ __device__ __forceinline__ void pair_load(const Params& p, const Seg& sg, int pr
                                           int w, int lane) {
   const int g = lane >> 4, c = lane & 15;
   const int32_t k0 = 32 * pr;
+  // the pair's 32 edges lie in one 64-edge block of the window (k0 is 32-aligned)
+  const int r = (k0 - sg.wb) >> 6;
+  int32_t s0 = sg.s0, s1 = sg.s1, s2 = sg.s2, s3 = sg.s3;
+  asm("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3));   // values, not a select of addresses (no alloca)
+  int32_t blk = s0;
+  blk = r == 1 ? s1 : blk;
+  blk = r == 2 ? s2 : blk;
+  blk = r == 3 ? s3 : blk;
+  const int32_t last = max(sg.deg, 1) - 1;
 #pragma unroll
   for (int x = 0; x < 2; ++x) {
     const int32_t k = k0 + 16 * x + c;
-    in.X[x] = x_frag(p, sg.beg + min(k, sg.deg - 1), g);
-    const int32_t s = seg_src(p, sg, k, k0 + 16 * x);
-    const uint16_t* row = p.KV16 + (int64_t)s * p.ldkv + gcol;
+    in.X[x] = x_frag(p, seg_edge(p, sg, k), g);
+    const int32_t s = __shfl(blk, min(k, last) & 63, 64);
+    const uint16_t* row = p.KV16 + (__umul24((uint32_t)s, (uint32_t)p.ldkv) + gcol);   // n ldkv < 2^31
     in.G[x][0] = kv_frag(row, w, 0, g);
     in.G[x][1] = kv_frag(row, w, 1, g);
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = (lane >> 3) + 8 * u;
-    const int32_t s = seg_src(p, sg, k0 + e, k0 + 8 * u);
-    in.R[u] = *reinterpret_cast<const u4*>(p.KV16 + (int64_t)s * p.ldkv + rcol + 64 * w + 8 * (lane & 7));
+    const int32_t s = __shfl(blk, min(k0 + e, last) & 63, 64);
+    in.R[u] = *reinterpret_cast<const u4*>(p.KV16 + (__umul24((uint32_t)s, (uint32_t)p.ldkv) + rcol + 64 * w +
+                                                       8 * (lane & 7)));
   }
   asm volatile("" ::: "memory");   // keep the loads here (else they sink to their use, one pair later)
 }
@@ -308,9 +334,9 @@ __device__ __forceinline__ void fwd_pair(const Params& p, const PairIn& in, int3
   for (int x = 0; x < 2; ++x) {
     f4 T[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) T[t] = relu4(mma(W1f.get(t, lane), in.X[x], zero4()));
-    f4 Zp = mma(pack8(T[0], T[1]), Uf[0], zero4());
-    Zp = mma(pack8(T[2], T[3]), Uf[1], Zp);
+    for (int t = 0; t < 4; ++t) T[t] = mma(W1f.get(t, lane), in.X[x], zero4());
+    f4 Zp = mma(relu_pack8(T[0], T[1]), Uf[0], zero4());
+    Zp = mma(relu_pack8(T[2], T[3]), Uf[1], Zp);
     Zp = mma(in.G[x][0], Qf[0], Zp);
     Zp = mma(in.G[x][1], Qf[1], Zp);
 #pragma unroll
@@ -321,7 +347,7 @@ __device__ __forceinline__ void fwd_pair(const Params& p, const PairIn& in, int3
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const bf8 Wt = W1f.get(t, lane);
-    FB[t] = pack8(relu4(mma(in.X[0], Wt, zero4())), relu4(mma(in.X[1], Wt, zero4())));
+    FB[t] = relu_pack8(mma(in.X[0], Wt, zero4()), mma(in.X[1], Wt, zero4()));
   }
   __syncthreads();
   f4 z[2];
@@ -420,10 +446,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     PairIn A, B;
     pair_load(p, sg, 0, A, 0, D, w, lane);
     for (int pr = 0; pr < np; pr += 2) {
-      pair_load(p, sg, min(pr + 1, np - 1), B, 0, D, w, lane);
+      const int n1 = min(pr + 1, np - 1), n2 = min(pr + 2, np - 1);
+      seg_advance(p, sg, n1, lane);
+      pair_load(p, sg, n1, B, 0, D, w, lane);
       fwd_pair<DROP>(p, A, beg + 32 * pr, end, pr & 1, img, zb, W1f, Uf, Qf, cadd, st, w, lane);
       if (pr + 1 >= np) break;
-      pair_load(p, sg, min(pr + 2, np - 1), A, 0, D, w, lane);
+      seg_advance(p, sg, n2, lane);
+      pair_load(p, sg, n2, A, 0, D, w, lane);
       fwd_pair<DROP>(p, B, beg + 32 * (pr + 1), end, (pr + 1) & 1, img, zb, W1f, Uf, Qf, cadd, st, w, lane);
     }
   }
@@ -447,8 +476,7 @@ __device__ __forceinline__ void fwd_tgt_load(const Params& p, int64_t item, FwdT
   T.d = (int64_t)uni(sld(p.items, item));
   T.beg = uni(sld(p.off, T.d));
   T.end = uni(sld(p.off, T.d + 1));
-  if (p.m > 0) seg_load(p, T.sg, T.beg, max(T.end, T.beg + 1), lane);   // (an empty segment reads a valid id)
-  T.sg.deg = T.end - T.beg;
+  seg_load(p, T.sg, T.beg, T.end, lane);   // (clamped: an empty segment reads a valid id)
   const float* qrow = p.Q + T.d * p.ldq;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -470,42 +498,63 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   __bf16* img = imgs + w * IMG;
   int64_t it = blockIdx.x;
   if (it >= p.n_items) return;
+  if (p.m == 0) {   // no edges: every target's outputs are the empty softmax's
+    FwdState st;
+    fwd_init(st);
+    for (; it < p.n_items; it += gridDim.x) fwd_out(p, st, (int64_t)uni(sld(p.items, it)), w, lane);
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) w1s[w][64 * t + lane] = __builtin_bit_cast(u4, w1_frag(p, 64 * w + 16 * t + c, g));
   const W1Lds W1f{w1s[w]};   // read back by this wave only (LDS is in order within a wave)
+  // The unit stream (target T, pair pr): each unit issues the next unit's loads — (T, pr + 1), or the
+  // next target N's first pair — then computes its own.  An empty target is one unit with no compute.
+  // Two register sets alternate (a copy of a loaded set would wait for its loads); every load is
+  // unconditional: N past the list end is the list's last item again, its loads unused.
   FwdTgt T, N;
   fwd_tgt_load(p, it, T, w, lane);
+  fwd_tgt_load(p, min<int64_t>(it + gridDim.x, p.n_items - 1), N, w, lane);
   PairIn A, B;
-  if (T.beg < T.end) pair_load(p, T.sg, 0, A, 0, D, w, lane);
-  int64_t nit = it + gridDim.x;
-  bool hasN = nit < p.n_items;
-  if (hasN) fwd_tgt_load(p, nit, N, w, lane);
-  int buf = 0;
-  while (true) {
-    FwdState st;
-    fwd_init(st);
-    const float cw = p.wbar ? wave_sum(T.wbv * T.qv) : 0.f;   // c_w = <wbar_w, Q_w>
-    const float cadd = hc == w ? cw : 0.f;
+  pair_load(p, T.sg, 0, A, 0, D, w, lane);
+  FwdState st;
+  fwd_init(st);
+  float cadd = wave_sum(T.wbv * T.qv);   // c_w = <wbar_w, Q_w> (wbv = 0 without wbar), head w's columns
+  cadd = hc == w ? cadd : 0.f;
+  int pr = 0, buf = 0;
+  bool done = false;
+  auto unit = [&](const PairIn& cur, PairIn& nxt) {
     const int np = (T.end - T.beg + 31) / 32;
-    bool ahead = false;   // B holds the next target's first pair
-    for (int pr = 0; pr < np; ++pr) {
-      if (pr + 1 < np) {
-        pair_load(p, T.sg, pr + 1, B, 0, D, w, lane);
-      } else if (hasN && N.beg < N.end) {
-        pair_load(p, N.sg, 0, B, 0, D, w, lane);
-        ahead = true;
-      }
-      fwd_pair<DROP>(p, A, T.beg + 32 * pr, T.end, buf, img, zb, W1f, T.Uf, T.Qf, cadd, st, w, lane);
-      buf ^= 1;
-      A = B;
+    const bool last = pr + 1 >= max(np, 1);
+    if (!last) {
+      seg_advance(p, T.sg, pr + 1, lane);
+      pair_load(p, T.sg, pr + 1, nxt, 0, D, w, lane);
+    } else {
+      pair_load(p, N.sg, 0, nxt, 0, D, w, lane);
+    }
+    if (np > 0) fwd_pair<DROP>(p, cur, T.beg + 32 * pr, T.end, buf, img, zb, W1f, T.Uf, T.Qf, cadd, st, w, lane);
+    buf ^= 1;
+    if (!last) {
+      ++pr;
+      return;
     }
     fwd_out(p, st, T.d, w, lane);
-    if (!hasN) break;
+    it += gridDim.x;
+    if (it >= p.n_items) {
+      done = true;
+      return;
+    }
     T = N;
-    if (!ahead && T.beg < T.end) pair_load(p, T.sg, 0, A, 0, D, w, lane);   // after an empty target
-    nit += gridDim.x;
-    hasN = nit < p.n_items;
-    if (hasN) fwd_tgt_load(p, nit, N, w, lane);
+    fwd_tgt_load(p, min<int64_t>(it + gridDim.x, p.n_items - 1), N, w, lane);
+    fwd_init(st);
+    const float cw = wave_sum(T.wbv * T.qv);
+    cadd = hc == w ? cw : 0.f;
+    pr = 0;
+  };
+  while (true) {
+    unit(A, B);
+    if (done) break;
+    unit(B, A);
+    if (done) break;
   }
 }
 
@@ -535,8 +584,8 @@ __device__ __forceinline__ void bwd_pair(const Params& p, const PairIn& in, int3
   for (int x = 0; x < 2; ++x) {
     f4 T[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) T[t] = relu4(mma(k.W1f[t], in.X[x], zero4()));
-    const bf8 F0 = pack8(T[0], T[1]), F1 = pack8(T[2], T[3]);
+    for (int t = 0; t < 4; ++t) T[t] = mma(k.W1f[t], in.X[x], zero4());
+    const bf8 F0 = relu_pack8(T[0], T[1]), F1 = relu_pack8(T[2], T[3]);
     const bf8 K0 = row_frag(img, x, 0, g, c), K1 = row_frag(img, x, 1, g, c);
     f4 Zp = mma(F0, k.Uf[0], zero4());
     Zp = mma(F1, k.Uf[1], Zp);
@@ -559,7 +608,7 @@ __device__ __forceinline__ void bwd_pair(const Params& p, const PairIn& in, int3
   bf8 FB[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
-    FB[t] = pack8(relu4(mma(in.X[0], k.W1f[t], zero4())), relu4(mma(in.X[1], k.W1f[t], zero4())));
+    FB[t] = relu_pack8(mma(in.X[0], k.W1f[t], zero4()), mma(in.X[1], k.W1f[t], zero4()));
   __syncthreads();
   f4 dz[2];
 #pragma unroll
@@ -661,10 +710,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __syncthreads();
     k.pdl = cst[hc];
     for (int pr = 0; pr < np; pr += 2) {
-      pair_load(p, sg, min(pr + 1, np - 1), B, D, 0, w, lane);
+      const int n1 = min(pr + 1, np - 1), n2 = min(pr + 2, np - 1);
+      seg_advance(p, sg, n1, lane);
+      pair_load(p, sg, n1, B, D, 0, w, lane);
       bwd_pair<DROP>(p, A, beg + 32 * pr, end, pr & 1, img, zb, k, st, w, lane);
       if (pr + 1 >= np) break;
-      pair_load(p, sg, min(pr + 2, np - 1), A, D, 0, w, lane);
+      seg_advance(p, sg, n2, lane);
+      pair_load(p, sg, n2, A, D, 0, w, lane);
       bwd_pair<DROP>(p, B, beg + 32 * (pr + 1), end, (pr + 1) & 1, img, zb, k, st, w, lane);
     }
   }
@@ -707,6 +759,14 @@ static bool lgm_persistent() {
   return v != 0;
 }
 
+// The kernels address rows with 24-bit products and 32-bit offsets (engine._angle_xf keeps larger
+// batches on the streamed path)
+static bool lgm_check(int64_t n, int64_t m, int64_t ldkv, int64_t ldx) {
+  const int64_t lim = int64_t(1) << 24;
+  return n < lim && m < lim && ldkv < lim && ldx < lim && n * ldkv < (int64_t(1) << 31) &&
+         m * ldx < (int64_t(1) << 31);
+}
+
 // Entry points for lgconv.hip's C ABI (alignn_lg_fwd_x / alignn_lg_bwd_dst_x with bf16 K|V).
 int lgm_fwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, const int32_t* items, int64_t n_items,
             const float* Q, int64_t ldq, const uint16_t* KV16, int64_t ldkv, const float* U, const float* wbar,
@@ -719,6 +779,7 @@ int lgm_fwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, con
   p.aggV = aggV; p.S = S; p.sumA = sumA; p.mstat = mstat; p.den = den;
   p.drop = drop;
   if (n_items <= 0) return ALIGNN_OK;
+  if (!lgm_check(n, m, ldkv, ldx)) return ALIGNN_E_UNSUPPORTED;
   if (lgm_persistent()) {
     const unsigned grid = (unsigned)std::min<int64_t>(n_items, lgm_persist_grid());
     if (drop.active) launch(lgm::lgm_fwd_p_kernel<true>, dim3(grid), dim3(lgm::NT), 0, s, p);
@@ -745,6 +806,7 @@ int lgm_bwd(int64_t n, int64_t m, const int32_t* off, const int32_t* src_at, con
   p.dq = dq; p.lddq = lddq; p.Sz = Sz; p.sigz = sigz; p.dz_e = dz_e; p.alpha_e = alpha_e;
   p.drop = drop;
   if (n_items <= 0) return ALIGNN_OK;
+  if (!lgm_check(n, m, ldkv, ldx)) return ALIGNN_E_UNSUPPORTED;
   if (drop.active) launch(lgm::lgm_bwd_kernel<true>, dim3((unsigned)n_items), dim3(lgm::NT), 0, s, p);
   else launch(lgm::lgm_bwd_kernel<false>, dim3((unsigned)n_items), dim3(lgm::NT), 0, s, p);
   ALIGNN_LAUNCH_CHECK("lgm_bwd_kernel");

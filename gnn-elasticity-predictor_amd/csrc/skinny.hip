@@ -14,6 +14,9 @@
 // four rows in flight) and N+1 accumulators per column (the +1 is the column sum); row-lanes
 // combined in LDS in lane order; one partial per (chunk, column, n).  Stage 2: per output, the
 // chunk partials summed in chunk order (four chains, fixed combine).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace alignn {
@@ -26,8 +29,6 @@ constexpr int SK_KMAX = 16;   // linear_smallk: K <= 16
 constexpr int SN_NMAX = 16;   // tn_smalln: N <= 16
 constexpr int SN_SLOTS = SN_NMAX + 1;
 
-// OutT = float, or uint16_t for bf16 output rows (RNE, v_cvt_pk_bf16_f32): the angle encoder's hidden
-// layer under config C3's autocast precision (train.py:632-636), read by the bf16 attention kernels.
 template <typename OutT>
 __global__ __launch_bounds__(256) void linear_smallk_kernel(const float* __restrict__ X, int64_t ldx, int64_t M,
                                                             int K, const float* __restrict__ W, int64_t ldw,
@@ -193,6 +194,105 @@ static void smalln_plan(int64_t K, int64_t M, int64_t& chunks, int64_t& rows_per
 
 static bool aligned16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 output: autocast's arithmetic (train.py:554 under :636) — x, W and b rounded to bf16, the
+// products accumulated in fp32 on the matrix cores, the sum rounded to bf16, then ReLU on the bf16
+// value.  One v_mfma_f32_32x32x16_bf16 per 32 output columns x 32 rows with the operands of the
+// deferred encoder backward's mask recompute (encbwd.hip, enc_bwd_bf16_kernel<H, true>): the same
+// [W | b] fragment (lane (hh, r): column r, inputs 8 hh .. 8 hh + 7, b at k = K) and the same [x | 1]
+// fragment (row r), in swapped operand roles — D^T instead of D, each element the same 16 products
+// in the same k slots — so the stored layer's ReLU mask is the recompute's bit for bit and that
+// backward may take either.  Workgroup: 4 waves; per 32-row chunk and 256-column slab each wave
+// computes two 32-column tiles (w, w + 4) into an LDS image (lane (hh, r): row r, columns
+// 8 q + 4 hh .. + 3 of the tile for register group q), then the workgroup stores the slab's rows as
+// whole 16-byte pieces (a wave instruction writes two full 512-byte rows; nontemporal: the layer is
+// written once and read back by the next kernel from HBM).  Grid-stride over chunks, the next chunk's
+// raw inputs loaded before the current one is computed.
+typedef __bf16 skh8 __attribute__((ext_vector_type(8)));
+typedef __bf16 skh4 __attribute__((ext_vector_type(4)));
+typedef float skx16 __attribute__((ext_vector_type(16)));
+typedef uint32_t sku4 __attribute__((ext_vector_type(4)));
+constexpr int SKM_KMAX = 15;        // inputs + the ones column within one 16-deep k step
+constexpr int SKM_SLABS = 4;        // 256-column slabs (N <= 1024)
+constexpr int SKM_LDT = 256 + 8;    // LDS image row (bf16), padded
+__device__ __forceinline__ float sk_keep(float v, bool keep) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & (keep ? 0xffffffffu : 0u));
+}
+template <int SLABS>
+__global__ __launch_bounds__(256) void linear_smallk_bf16_mx_kernel(const float* __restrict__ X, int64_t ldx,
+                                                                   int64_t M, int K, const float* __restrict__ W,
+                                                                   int64_t ldw, const float* __restrict__ bias,
+                                                                   int N, int relu, uint16_t* __restrict__ out,
+                                                                   int64_t ldo) {
+  __shared__ __attribute__((aligned(16))) uint16_t img[32 * SKM_LDT];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nt = N / 32, slabs = (N + 255) / 256;
+  skh8 WB[2 * SLABS];   // tile 8 s + w + 4 j -> WB[2 s + j]
+#pragma unroll
+  for (int t = 0; t < 2 * SLABS; ++t) {
+    const int tile = 8 * (t >> 1) + w + 4 * (t & 1);
+    const int col = 32 * min(tile, nt - 1) + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * hh + j;
+      const float v = W[(int64_t)col * ldw + min(k, K - 1)];
+      const float b = bias ? bias[col] : 0.f;
+      WB[t][j] = (__bf16)(k < K ? v : (k == K ? b : 0.f));
+    }
+  }
+  // this lane's 8 raw inputs of row r of a chunk (unconditional loads, row clamped into X), one chunk ahead
+  auto load_x = [&](int64_t c0, float (&v)[8]) {
+    const float* xr = X + min(c0 + r, M - 1) * ldx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = xr[min(8 * hh + j, K - 1)];
+  };
+  const int64_t step = 32 * (int64_t)gridDim.x;
+  float xv[8];
+  load_x(32 * (int64_t)blockIdx.x, xv);
+  for (int64_t r0 = 32 * (int64_t)blockIdx.x; r0 < M; r0 += step) {
+    skh8 XB;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * hh + j;
+      XB[j] = (__bf16)(k == K ? 1.f : sk_keep(xv[j], k < K));
+    }
+    load_x(r0 + step, xv);
+#pragma unroll
+    for (int s = 0; s < SLABS; ++s) {
+      if (s >= slabs) break;   // uniform
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int tl = w + 4 * j;   // tile within the slab
+        if (8 * s + tl >= nt) break;   // wave-uniform
+        const skx16 pre = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WB[2 * s + j], XB, skx16{}, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          skh4 h;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const __bf16 b = (__bf16)pre[4 * q + i];
+            h[i] = (relu && !((float)b > 0.f)) ? (__bf16)0.f : b;
+          }
+          *reinterpret_cast<skh4*>(img + r * SKM_LDT + 32 * tl + 8 * q + 4 * hh) = h;
+        }
+      }
+      __syncthreads();
+      const int ncol = min(256, N - 256 * s);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int piece = threadIdx.x + 256 * u, row = piece >> 5, c8 = 8 * (piece & 31);
+        if (r0 + row < M && c8 < ncol) {
+          sku4* dst = reinterpret_cast<sku4*>(out + (r0 + row) * ldo + 256 * s + c8);
+          const sku4 v = *reinterpret_cast<const sku4*>(img + row * SKM_LDT + c8);
+          __builtin_nontemporal_store(v, dst);   // streamed once (1 GB at B = 256): 336 -> 216 us
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace alignn
 
 using namespace alignn;
@@ -225,18 +325,23 @@ extern "C" int alignn_linear_smallk_bf16out(const float* X, int64_t ldx, int64_t
     set_error("linear_smallk_bf16out: bad arguments");
     return ALIGNN_E_BAD_SHAPE;
   }
-  if (K > SK_KMAX || N % 4 != 0 || ldo % 4 != 0 || (reinterpret_cast<uintptr_t>(out) & 7u) || ldx < K ||
-      ldw < K || ldo < N) {
-    set_error("linear_smallk_bf16out: needs K <= %d, N %% 4 == 0, 8-byte aligned output rows (K=%d N=%lld ldo=%lld)",
-              SK_KMAX, (int)K, (long long)N, (long long)ldo);
+  if (K < 1 || K > SKM_KMAX || N % 32 != 0 || N > 256 * SKM_SLABS || ldo % 8 != 0 ||
+      (reinterpret_cast<uintptr_t>(out) & 15u) || ldx < K || ldw < K || ldo < N) {
+    set_error("linear_smallk_bf16out: needs 1 <= K <= %d, N %% 32 == 0, N <= %d, 16-byte aligned output rows "
+              "(K=%d N=%lld ldo=%lld)", SKM_KMAX, 256 * SKM_SLABS, (int)K, (long long)N, (long long)ldo);
     return ALIGNN_E_UNSUPPORTED;
   }
   if (M == 0 || N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const unsigned blocks = (unsigned)((M + SK_ROWS - 1) / SK_ROWS);
-  launch(linear_smallk_kernel<uint16_t>, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, N,
-         (int)relu, out, ldo);
-  ALIGNN_LAUNCH_CHECK("linear_smallk_kernel");
+  // 8 workgroups per CU (measured 216 us at B = 256 against 234-237 with 2 or 4, profiles/r06/ab_linear_bf16.txt)
+  const unsigned blocks = (unsigned)std::min<int64_t>((M + 31) / 32, 256 * 8);
+  if (N <= 256)
+    launch(linear_smallk_bf16_mx_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias, (int)N,
+           (int)relu, out, ldo);
+  else
+    launch(linear_smallk_bf16_mx_kernel<SKM_SLABS>, dim3(blocks), dim3(256), 0, s, X, ldx, M, (int)K, W, ldw, bias,
+           (int)N, (int)relu, out, ldo);
+  ALIGNN_LAUNCH_CHECK("linear_smallk_bf16_mx_kernel");
   return ALIGNN_OK;
 }
 

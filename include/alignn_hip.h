@@ -138,8 +138,12 @@ int alignn_gemm_path(const AlignnGemmArgs* args);
  * ---------------------------------------------------------------------------------------- */
 int alignn_linear_smallk_f32(const float* X, int64_t ldx, int64_t M, int32_t K, const float* W, int64_t ldw,
                              const float* bias, int64_t N, int32_t relu, float* out, int64_t ldo, void* stream);
-/* The same with bf16 output rows (RNE; out rows 8-byte aligned): the angle encoder's hidden layer in
- * bf16 for the bf16-storage attention kernels (config C3). */
+/* bf16 output rows: the Linear as bf16 autocast computes it (train.py:554 under :636) — X, W and bias
+ * rounded to bf16, the exact products summed in fp32 on the matrix cores (one v_mfma_f32_32x32x16_bf16
+ * per 32 x 32 tile), the sum rounded to bf16 (RNE), ReLU on the rounded value: the angle encoder's
+ * hidden layer for the bf16-storage attention kernels (config C3).  Its pre-activation is bitwise the
+ * one alignn_enc_bwd_bf16 recomputes without the stored layer.  Needs 1 <= K <= 15, N % 32 == 0,
+ * N <= 1024, out rows 16-byte aligned (else ALIGNN_E_UNSUPPORTED). */
 int alignn_linear_smallk_bf16out(const float* X, int64_t ldx, int64_t M, int32_t K, const float* W, int64_t ldw,
                                  const float* bias, int64_t N, int32_t relu, uint16_t* out, int64_t ldo,
                                  void* stream);

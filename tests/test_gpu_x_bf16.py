@@ -142,8 +142,11 @@ def test_bf16_storage_attention_vs_fp32_kernels_on_rounded_inputs():
 
 
 def test_cast_and_skinny_bf16_outputs_bitwise():
-    """alignn_cast_bf16_f32 and alignn_linear_smallk_bf16out round to nearest even exactly like
-    torch's fp32 -> bf16 conversion (of the fp32 result for the skinny Linear)."""
+    """alignn_cast_bf16_f32 rounds to nearest even exactly like torch's fp32 -> bf16 conversion;
+    alignn_linear_smallk_bf16out is the Linear + ReLU as bf16 autocast computes it (train.py:554 under
+    :636): bf16 x, W, b, exact products summed in fp32, the sum rounded to bf16 — against the float64 sum
+    of the same bf16 operands rounded once, every element within one bf16 rounding step and all but a
+    few (sums within fp32 error of a rounding boundary) equal."""
     from alignn_mi355x import ops
     g = torch.Generator(device="cpu").manual_seed(12)
     x = (torch.randn(1037, 260, generator=g) * 3).to(DEV)
@@ -154,11 +157,20 @@ def test_cast_and_skinny_bf16_outputs_bitwise():
     X = torch.randn(5000, 11, generator=g).to(DEV)
     W = torch.randn(256, 11, generator=g).to(DEV)
     b = torch.randn(256, generator=g).to(DEV)
-    h32 = torch.empty(5000, 256, device=DEV)
-    ops.linear_smallk(X, W, b, h32, relu=True)
     h16 = torch.empty(5000, 256, device=DEV, dtype=torch.bfloat16)
     ops.linear_smallk_bf16(X, W, b, h16, relu=True)
-    assert torch.equal(h16, h32.bfloat16())
+    bf = lambda t: t.bfloat16().double()  # noqa: E731
+    ref = torch.relu((bf(X) @ bf(W).t() + bf(b)).float().bfloat16().float())
+    got = h16.float()
+    assert torch.equal(got > 0, ref > 0) or float(((got > 0) != (ref > 0)).float().mean()) < 1e-5
+    ulp = ref.abs().clamp_min(2.0 ** -126) * 2.0 ** -7
+    assert bool(((got - ref).abs() <= ulp).all())
+    assert float((got != ref).float().mean()) < 1e-3
+    # rows past a 32-row chunk, and a bias-free call
+    h = torch.full((37, 256), 7.0, device=DEV, dtype=torch.bfloat16)
+    ops.linear_smallk_bf16(X[:37], W, None, h, relu=False)
+    ref = (bf(X[:37]) @ bf(W).t()).float()
+    assert float(((h.float() - ref).abs() / ref.abs().clamp_min(1e-3)).max()) < 1e-2
 
 
 def test_bf16_storage_step_vs_float64_oracle():

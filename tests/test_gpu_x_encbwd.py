@@ -85,7 +85,11 @@ def test_enc_bwd_bf16_matches_fp64(n, H, L, kin):
     csr, x, W1, b1, U, Vd, dz, al = _case(n, D, H, L, kin, seed=n * 17 + H + L + kin)
     T = x.size(0)
     f16 = torch.empty(T, D, dtype=torch.bfloat16, device=DEV)
-    ops.linear_smallk_bf16(x, W1, b1, f16, relu=True)
+    if kin <= ops.SMALLK_BF16_MAX:
+        ops.linear_smallk_bf16(x, W1, b1, f16, relu=True)
+    else:   # past the matrix-core Linear's one k step: torch's autocast arithmetic
+        f16.copy_(torch.relu(x.bfloat16().double() @ W1.bfloat16().double().t() + b1.bfloat16().double())
+                  .float().bfloat16())
     dW1 = torch.full((D, kin), float("nan"), device=DEV)
     db1 = torch.full((D,), float("nan"), device=DEV)
     ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1, db1, F=f16)
@@ -98,10 +102,11 @@ def test_enc_bwd_bf16_matches_fp64(n, H, L, kin):
     rW, rb = dpre.t() @ bf(x), dpre.sum(0)
     nrel = lambda a, b: float((a.double() - b).norm() / b.norm())  # noqa: E731
     assert nrel(dW1, rW) < 2e-3 and nrel(db1, rb) < 2e-3
-    # the fp32 VALU kernel (exact fp32 products, mask from the recomputed pre-activation) at bf16 tolerance
+    # the fp32 VALU kernel (exact fp32 products, mask from the fp32 pre-activation) at bf16 tolerance:
+    # autocast's bf16 x and W move pre-activations near 0 across the ReLU, so the masks differ too
     fW, fb = torch.empty_like(dW1), torch.empty_like(db1)
     ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, fW, fb)
-    assert nrel(dW1, fW.double()) < 3e-2 and nrel(db1, fb.double()) < 3e-2
+    assert nrel(dW1, fW.double()) < 5e-2 and nrel(db1, fb.double()) < 5e-2
     # accumulate adds exactly the same partial sums; repeated launches are bitwise equal
     dW2, db2 = dW1.clone(), db1.clone()
     ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW2, db2, accumulate=True, F=f16)

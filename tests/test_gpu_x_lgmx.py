@@ -127,15 +127,22 @@ def test_mx_kernels_dropout_masks_match_streamed_rows(degs):
         assert _rel(x_, y_) < 2e-2, (k, _rel(x_, y_))
 
 
-@pytest.mark.parametrize("n,L", [(40, 4), (9, 2)])
-def test_enc_bwd_bf16_mask_recomputed_matches_stored_layer(n, L):
+@pytest.mark.parametrize("n,L,src", [(40, 4, "torch"), (9, 2, "torch"), (40, 4, "mx"), (300, 4, "mx")])
+def test_enc_bwd_bf16_mask_recomputed_matches_stored_layer(n, L, src):
     """alignn_enc_bwd_bf16 with its mask recomputed on the matrix cores (F16 NULL) against the mask read
-    from the autocast hidden layer: the same products, the same mask (a pre-activation within one
-    rounding of 0 could sit on the other side; the random case has none)."""
+    from the stored hidden layer: the same products, the same mask.  'mx': the layer from
+    ops.linear_smallk_bf16 (config C3's stored layer), whose pre-activation is the recompute's bit for
+    bit — the engine then takes the recompute (engine._backward_tail).  'torch': torch's autocast
+    arithmetic (a pre-activation within one rounding of 0 could sit on the other side; the random case
+    has none)."""
     from test_gpu_x_encbwd import _case as eb_case
     ops = _ops()
     csr, x, W1, b1, U, Vd, dz, al = eb_case(n, 256, 4, L, 11, seed=n + L)
-    F16 = autocast_hidden(x, W1, b1).contiguous()
+    if src == "mx":
+        F16 = torch.empty(x.size(0), 256, device=DEV, dtype=torch.bfloat16)
+        ops.linear_smallk_bf16(x, W1, b1, F16, relu=True)
+    else:
+        F16 = autocast_hidden(x, W1, b1).contiguous()
     dW1a, db1a = torch.empty(256, 11, device=DEV), torch.empty(256, device=DEV)
     dW1b, db1b = torch.empty(256, 11, device=DEV), torch.empty(256, device=DEV)
     ops.enc_bwd(csr, x, W1, b1, U, Vd, dz, al, dW1a, db1a, F=F16)

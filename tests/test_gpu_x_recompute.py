@@ -9,9 +9,9 @@ per edge group on the matrix cores instead of being materialised by linear_small
   4): 1e-6 of each output's largest magnitude.  (The bf16 form runs on the matrix cores with
   autocast's operand rounding: tests/test_gpu_x_lgmx.py.)
 * The whole step: recompute_angle on vs off — loss and gradients (C2 fp32, B = 4: the same
-  arithmetic; C3 bf16, B = 16: the recomputed layer is autocast's bf16(x) bf16(W1)^T + bf16(b1),
-  the materialised one linear_smallk_bf16's fp32 products rounded once, so the two steps agree to
-  bf16 rounding of the hidden layer).
+  arithmetic; C3 bf16, B = 16: both layers are autocast's bf16(x) bf16(W1)^T + bf16(b1) with fp32
+  accumulation, on different matrix-core shapes (16x16x32 in lgmx.hip, 32x32x16 in
+  linear_smallk_bf16), so the two steps agree to bf16 rounding of the hidden layer).
 """
 import pytest
 import torch
@@ -132,7 +132,8 @@ def test_step_with_recomputed_angle_layer(precision, B):
     """The training step's loss and gradients with recompute_angle on (the default) and off.  fp32: the
     forward is bitwise (same attention arithmetic on bitwise the same edge features), gradients to
     fp32 summation order of the target-side backward (one group in flight vs two).  bf16: the two
-    hidden layers differ by bf16 rounding (autocast's bf16 operands vs fp32 products rounded once):
+    hidden layers differ by bf16 rounding (fp32 sums of the same bf16 products in another order), and
+    the attention arithmetic differs (matrix-core products with bf16 Q / U operands vs fp32 VALU):
     loss to 1e-2, every gradient within 5e-2 normwise and cosine > 0.998 (gradients that are zero up to
     rounding: both below 1e-4 of the largest)."""
     import alignn_mi355x as A

@@ -32,6 +32,12 @@ for step in "$@"; do
     c3ab) for i in 1 2; do for v in 1 0; do
             ALIGNN_LGM_PERSIST=$v run c3_p${v}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline; done; done
           for f in $O/c3_p*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
+    c3rx) for i in 1 2; do for v in 1 0; do
+            run c3_rx${v}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline --set engine.recompute_angle_bf16=$v; done; done
+          for f in $O/c3_rx*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
+    lin) run lin 300 python tools/lgx_bench.py --batch 256 --only linear_smallk_bf16 enc_bwd_bf16_rows enc_bwd_bf16_x fwd_bf16_rows bwd_bf16_rows ;;
+    linab) for nt in 0 1; do for wg in 2 4 8; do ALIGNN_SK_NT=$nt ALIGNN_SK_WG=$wg run lin_nt${nt}_wg$wg 300 python tools/lgx_bench.py --batch 256 --only linear_smallk_bf16; done; done
+           for f in $O/lin_nt*.log; do echo "$(basename $f) $(grep -o '"linear_smallk_bf16_us": [0-9.]*' $f)"; done ;;
     bf16t) run bf16t 900 "${PT[@]}" tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round5.py tests/test_gpu_x_round4.py tests/test_gpu_x_encbwd.py -v ;;
     rpc2) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c2 -o run --output-format csv -- python $OLDPWD/bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c2.log 2>&1 || exit 1
@@ -49,6 +55,17 @@ for step in "$@"; do
           python tools/pmc_traffic.py $O/pmcx_FETCH_SIZE $O/pmcx_WRITE_SIZE --top 20 > $O/pmcx_traffic.txt
           python tools/pmc_sq.py $O/pmcx_sq > $O/pmcx_sq.txt; python tools/pmc_mfma.py $O/pmcx_mf > $O/pmcx_mfma.txt
           cat $O/pmcx_traffic.txt $O/pmcx_sq.txt | head -40 ;;
+    pmcl) cd /tmp && export TMPDIR=/tmp
+          LB=(python $OLDPWD/tools/lgx_bench.py --batch 256 --reps 3 --only fwd_bf16_x bwd_bf16_x fwd_bf16_rows bwd_bf16_rows)
+          i=0
+          for cs in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" \
+                    "SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD" \
+                    "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
+            i=$((i+1))
+            timeout -s KILL 120 rocprofv3 --pmc $cs --kernel-trace -d $O/pmcl_$i -o run --output-format csv -- "${LB[@]}" > $O/pmcl_$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/pmcl_$i.log; cd $OLDPWD; exit 1; }
+          done
+          cd $OLDPWD
+          for j in $(seq 1 $i); do python tools/pmc_dump.py $O/pmcl_$j --match lg; done > $O/pmcl.txt; cat $O/pmcl.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

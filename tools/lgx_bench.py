@@ -6,7 +6,7 @@ HIP events around each call (median of R reps); also the deferred encoder backwa
 from the stored layer vs recomputed).  The library is the in-tree build unless ALIGNN_HIP_LIB names
 another (A/B builds).
 
-usage: python tools/lgx_bench.py [--reps 20] [--batch 32 256]
+usage: python tools/lgx_bench.py [--reps 20] [--batch 32 256] [--only fwd_bf16_x bwd_bf16_x ...]
 """
 import argparse
 import json
@@ -33,7 +33,7 @@ def timeit(fn, reps):
     return round(ts[len(ts) // 2], 1)
 
 
-def one(B, reps, drop):
+def one(B, reps, drop, only=None):
     from alignn_mi355x import ops
     from alignn_mi355x.engine import batch_cache
     from alignn_mi355x.synthetic import mp_like_batch
@@ -75,11 +75,15 @@ def one(B, reps, drop):
     calls["enc_bwd_f32"] = lambda: ops.enc_bwd(g, x, W1, b1, Us, Vds, dzs, als, dW1, db1)
     calls["enc_bwd_bf16_rows"] = lambda: ops.enc_bwd(g, x, W1, b1, Us, Vds, dzs, als, dW1, db1, F=F16)
     calls["enc_bwd_bf16_x"] = lambda: ops.enc_bwd(g, x, W1, b1, Us, Vds, dzs, als, dW1, db1, bf16=True)
+    if only:
+        calls = {k: v for k, v in calls.items() if k in only}
     for k, fn in calls.items():
         fn()
         torch.cuda.synchronize()
     for k, fn in calls.items():
         res[k + "_us"] = timeit(fn, reps)
+    if only:
+        return res
     for kind, p in (("f32", 4), ("bf16", 2)):
         fr, fx = ops._tconv_bytes(n, m, D, H, "fwd", 0, f_elem=p), ops._lg_x_bytes(n, m, D, H, "fwd", p)
         br, bx = ops._tconv_bytes(n, m, D, H, "bwd_dst", 0, f_elem=p), ops._lg_x_bytes(n, m, D, H, "bwd_dst", p)
@@ -97,9 +101,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, nargs="+", default=[32, 256])
     ap.add_argument("--drop", type=float, default=0.15)
+    ap.add_argument("--only", nargs="+", help="time only these calls (e.g. fwd_bf16_x bwd_bf16_x)")
     a = ap.parse_args()
     for B in a.batch:
-        print(json.dumps({"lib": os.environ.get("ALIGNN_HIP_LIB", "in-tree"), **one(B, a.reps, a.drop)}), flush=True)
+        print(json.dumps({"lib": os.environ.get("ALIGNN_HIP_LIB", "in-tree"), **one(B, a.reps, a.drop, a.only)}),
+              flush=True)
 
 
 if __name__ == "__main__":
