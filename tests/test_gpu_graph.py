@@ -168,10 +168,13 @@ def test_rebind_new_batches_replay_bitwise():
     _, tp, bp = _setup(B=8)
     tp.capture(bp)
     # re-binding copies only into the buffers the plans touch: the raw line-graph index and angle
-    # features are read when the cache is built (CSR, target-sorted angle rows), never by the step
-    used = tp._graph[5]
-    assert bp.x.data_ptr() in used and bp.y.data_ptr() in used
-    assert bp.lg_edge_index.data_ptr() not in used and bp.lg_edge_attr.data_ptr() not in used
+    # features are read when the cache is built (CSR, target-sorted angle rows), never by the step.
+    # The plans read the trainer's private copy of the captured batch (the slot), never bp itself
+    used, slot = tp._graph[5], tp._graph[2]
+    assert slot is not bp and slot.x.data_ptr() != bp.x.data_ptr()
+    assert slot.x.data_ptr() in used and slot.y.data_ptr() in used
+    assert slot.lg_edge_index.data_ptr() not in used and slot.lg_edge_attr.data_ptr() not in used
+    assert bp.x.data_ptr() not in used
     keys = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "y")
     store = GraphStore.from_data_list([Data(**{k: getattr(mp_like_graph(100 + g), k) for k in keys})
                                        for g in range(24)], DEV)

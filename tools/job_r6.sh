@@ -12,6 +12,7 @@ E2E=(python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no
 for step in "$@"; do
   case $step in
     gpu) run gpu 900 "${PT[@]}" tests -m gpu ;;
+    gpuall) run gpuall 1100 python -u -m pytest -q --maxfail 20 --timeout 300 --timeout-method thread tests -m gpu ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     c2) run c2 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline ;;
