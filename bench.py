@@ -75,6 +75,13 @@ def parse():
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary lines of the default one-GPU run (corrected wiring, config C3)")
+    p.add_argument("--roofline-parts", default="probe,stamps,serial",
+                   help="diagnostics: which parts of the roofline measurement run (probe = the dominant-kernel "
+                        "probe capture, stamps = timestamps in the timed capture, serial = serialised replays)")
+    p.add_argument("--secondaries", default="cw,c1,c3,c5,c4,var",
+                   help="which secondary lines the default one-GPU run measures (diagnostics): cw = corrected "
+                        "wiring, c1 = C1 forward, c3 = C3 step, c5 = C5 loop (needs c3), c4 = C4 predict, "
+                        "var = the e2e_variable loop")
     p.add_argument("--dump-probes", default="", help="write the per-op probe summary (JSON) to this path")
     p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM arithmetic: fp32 (BASELINE config 2, the default) or bf16 matrix-core inputs with "
@@ -354,6 +361,11 @@ def end_to_end(args, store, t_build, trainer, B, dev, rank, world, capacity=None
     # lost a third (gpurun_out r6a: B = 32 e2e 9,930-10,040 graphs/s for dedicated / pooled / pooled at
     # high priority / prefetch 2; e2e_variable 7,200 after the dedicated queue vs 11,400 without).
     # (--set loader_priority=0 / loader_dedicated=1 / main_priority=0 keep the earlier placements.)
+    # Round 6: the remaining loss (the loop at 67-71 % of the bare step whenever anything had been
+    # captured before it — the roofline probe, a secondary's trainer) was a new pooled warm-up stream
+    # per capture, which moved this stream's hardware-queue assignment onto one of the step's; every
+    # capture now warms up on one process-wide stream (ops.warmup_stream): 7,400 -> 9,820 graphs/s
+    # with the probe (gpurun_out r6y, r6ad).
     prio = getattr(args, "loader_priority", None)
     if prio is None:
         prio = args.main_priority if args.main_priority else (-1 if B >= 128 else 0)
@@ -539,7 +551,10 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
     # against 279 us in a rocprofv3 trace and 202 us under the counters), so ranking on them measured
     # overlap, not kernels.
     dominant, step_work = None, None
-    if roofline:
+    parts = set(getattr(args, "roofline_parts", "probe,stamps,serial").split(","))
+    if roofline and "probe" not in parts:
+        dominant = "gemm_f32 M23040 N256 K256 b1" if B == 32 else None
+    if roofline and "probe" in parts:
         totals, summ = {}, {}
         plan_probe = args.launch == "plan"
         if plan_probe:
@@ -582,10 +597,10 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
         mode = args.launch
         # ROCm refuses external event nodes in a captured graph: graph mode probes eagerly after
         # the timed region; a plan carries the probes as timestamps
-        if dominant is not None and mode == "plan":
+        if dominant is not None and mode == "plan" and "stamps" in parts:
             profiling.enable(dominant)
         trainer.capture(batch, mode=mode)
-        probe_in_graph = dominant is not None and mode == "plan"
+        probe_in_graph = dominant is not None and mode == "plan" and "stamps" in parts
         launch_mode = "native_plan" if mode == "plan" else "hip_graph"
         profiling.disable()
 
@@ -614,7 +629,7 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
         except Exception as e:  # noqa: BLE001
             print(f"[bench] plan probe timing unavailable ({e}); probing eagerly", file=sys.stderr)
             probe_in_graph = False
-    if dominant is not None and launch_mode != "eager" and not probe_in_graph:
+    if dominant is not None and launch_mode != "eager" and not probe_in_graph and "stamps" in parts:
         # fallback: time the dominant kernel in two extra eager steps after the timed region
         saved = trainer._graph
         trainer._graph = None
@@ -632,7 +647,7 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
     value = B * world * steps / dt
     summ = profiling.summary() if dominant is not None else {}
     in_step = summ.get(dominant)
-    if probe_in_graph and launch_mode == "native_plan":
+    if probe_in_graph and launch_mode == "native_plan" and "serial" in parts:
         # the kernel's own duration: the same plan replayed serialised (after the timed region); the
         # in-step figure (last timed replay) stays beside it
         trainer.serial_replay = True
@@ -642,7 +657,7 @@ def measure(args, dev, rank, world, B, lg_offset, precision, steps, warmup, roof
         trainer.serial_replay = False
         summ = profiling.summary()
         probe_src = f"plan timestamps, plan replayed serialised on one stream (last of {SERIAL_STEPS} replays after the timed region)"
-    roof = _roofline(summ, dominant, mfma_peak, probe_src) if dominant is not None else None
+    roof = _roofline(summ, dominant, mfma_peak, probe_src) if (dominant is not None and dominant in summ) else None
     if roof is not None and in_step is not None:
         roof["avg_us_in_step"] = round(in_step["avg_ms"] * 1e3, 2)
     step_roof = None if step_work is None else {
@@ -854,6 +869,10 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
+    sec_on = set(args.secondaries.split(","))
+    store = None
+    if args.e2e > 0 and "store_first" in sec_on:   # diagnostics: the dataset resident before any step
+        store, t_build = build_store(args, dev, rank)
     r = measure(args, dev, rank, world, B, args.lg_offset, args.precision, args.steps, args.warmup,
                 roofline=not args.no_roofline)
 
@@ -864,11 +883,16 @@ def main():
     # captured trainer alive (the C3 step measured with the dataset resident and after the e2e loops
     # read 8 % low: 16,900 vs 18,400-18,500 graphs/s; the corrected wiring with two other trainers
     # alive 5,100 vs 5,580).
+    e2e = None
+    if args.e2e > 0 and "e2e_first" in sec_on:
+        if store is None:
+            store, t_build = build_store(args, dev, rank)
+        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
     secondary, c3 = None, None
     if world == 1 and not args.no_secondary:
         secondary = {}
         sec_steps, sec_warm = max(5, args.steps // 2), max(2, args.warmup // 2)
-        if args.lg_offset == "num_nodes":
+        if args.lg_offset == "num_nodes" and "cw" in sec_on:
             w = measure(args, dev, rank, world, B, "num_edges", args.precision, sec_steps, sec_warm, roofline=True,
                         streams_of=r["trainer"])
             secondary["corrected_wiring"] = {
@@ -876,9 +900,9 @@ def main():
                 "value": round(w["value"], 2), "unit": "graphs/s", "ms_per_step": round(w["ms_per_step"], 3),
                 "steps": sec_steps, "roofline": w["roofline"]}
             _release(w)
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and "c1" in sec_on:
             secondary["c1_forward"] = c1_forward(args, dev, lender=r["trainer"])
-        if (B, args.precision) != (256, "bf16"):
+        if (B, args.precision) != (256, "bf16") and "c3" in sec_on:
             c3 = measure(args, dev, rank, world, 256, args.lg_offset, "bf16", sec_steps, sec_warm, roofline=True,
                          streams_of=r["trainer"])
             secondary["c3_b256_bf16"] = {
@@ -887,16 +911,16 @@ def main():
                 "value": round(c3["value"], 2), "unit": "graphs/s", "ms_per_step": round(c3["ms_per_step"], 3),
                 "steps": sec_steps, "roofline": c3["roofline"], "step_roofline": c3["step_roofline"]}
 
-    e2e, store = None, None
-    if args.e2e > 0:
+    if args.e2e > 0 and store is None:
         store, t_build = build_store(args, dev, rank)
         # The two loops' throughput depends on how their streams share the device's hardware queues
         # (GPU_MAX_HW_QUEUES = 4 here: step main/side/aux + loader + idle streams of the other trainer):
         # whichever loop runs second measured 8-10 % higher in either order (round 4, gpurun_out
         # r4i/r4j/r4k: C5 first 16,560-16,790 vs second 18,570-18,650 graphs/s; B = 32 first 5,760-5,800
         # vs second 8,450-8,610).  C5 (a VERDICT item) runs second.
-        e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
-        if c3 is not None:
+        if e2e is None:
+            e2e = end_to_end(args, store, t_build, r["trainer"], B, dev, rank, world)
+        if c3 is not None and "c5" in sec_on:
             # config C5 at N = 1: the B = 256 bf16 step over the ~10k-graph HBM dataset
             secondary["c5_e2e_b256_bf16"] = end_to_end(args, store, t_build, c3["trainer"], 256, dev, rank, world)
     _release(r)
@@ -904,12 +928,12 @@ def main():
         _release(c3)
     store = None
     e2e_var = None
-    if args.e2e > 0:
+    if args.e2e > 0 and "var" in sec_on:
         e2e_var = end_to_end_variable(args, dev, rank, world, B)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
-    if world == 1 and not args.no_secondary and args.ensemble == 0:
+    if world == 1 and not args.no_secondary and args.ensemble == 0 and "c4" in sec_on:
         secondary["c4_ensemble_predict_b256"] = ensemble_predict(args, dev)
     if rank == 0:
         cpu = None

@@ -62,7 +62,7 @@ class ForwardPlan:
             return out
 
         # warm-up: every workspace sized at this signature, on a side stream (as FusedTrainer.capture)
-        s = torch.cuda.Stream(device=dev)
+        s = ops.warmup_stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s), ops.using(self.ctx):
             for _ in range(2):

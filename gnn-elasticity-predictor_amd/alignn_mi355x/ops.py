@@ -38,6 +38,21 @@ def _require(t: torch.Tensor, name: str, dtype=torch.float32):
 _DEDICATED: dict = {}
 
 
+_WARMUP: dict = {}
+
+
+def warmup_stream(device) -> torch.cuda.Stream:
+    """One stream per device, kept for the process, for the warm-up passes before a capture
+    (FusedTrainer.capture, infer.ForwardPlan).  A fresh pooled stream per capture made a new HIP stream
+    (and hardware-queue assignment) every time: after a second capture in the process the B = 32 e2e
+    loop's loader stream ran ~25 % slower (7,200-7,700 vs 10,000 graphs/s, gpurun_out r6z-r6ac)."""
+    key = _dkey(device)
+    s = _WARMUP.get(key)
+    if s is None:
+        s = _WARMUP[key] = torch.cuda.Stream(device=torch.device(key))
+    return s
+
+
 def dedicated_stream(device) -> torch.cuda.Stream:
     """A stream on a hardware queue of its own (alignn_stream_create_dedicated), one per device, kept
     for the process: for a batch-preparation stream beside a replayed step.  With the process's

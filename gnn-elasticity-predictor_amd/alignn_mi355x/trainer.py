@@ -309,7 +309,7 @@ class FusedTrainer:
         # warm-up (allocations, optimizer state, every workspace at this batch's sizes) on a side
         # stream, then restore the state
         snap = self._snapshot()
-        s = torch.cuda.Stream(device=dev)
+        s = ops.warmup_stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):

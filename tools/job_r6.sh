@@ -39,6 +39,49 @@ for step in "$@"; do
     lin) run lin 300 python tools/lgx_bench.py --batch 256 --only linear_smallk_bf16 enc_bwd_bf16_rows enc_bwd_bf16_x fwd_bf16_rows bwd_bf16_rows ;;
     linab) for nt in 0 1; do for wg in 2 4 8; do ALIGNN_SK_NT=$nt ALIGNN_SK_WG=$wg run lin_nt${nt}_wg$wg 300 python tools/lgx_bench.py --batch 256 --only linear_smallk_bf16; done; done
            for f in $O/lin_nt*.log; do echo "$(basename $f) $(grep -o '"linear_smallk_bf16_us": [0-9.]*' $f)"; done ;;
+    hwq) for q in 4 8 16; do GPU_MAX_HW_QUEUES=$q run hwq_$q 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline; done
+         val "$O"/hwq_*.log
+         for f in $O/hwq_*.log; do python -c "
+import json,sys
+d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); s=d.get('secondary') or {}
+print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'), 'var', (d.get('e2e_variable') or {}).get('value'), 'c3', (s.get('c3_b256_bf16') or {}).get('value'), 'c5', (s.get('c5_e2e_b256_bf16') or {}).get('value'), 'cw', (s.get('corrected_wiring') or {}).get('value'), 'c4p', (s.get('c4_ensemble_predict_b256') or {}).get('plan_graphs_per_s'))"; done ;;
+    e2es) for sc in cw c3 c3,c5; do run e2es_$sc 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000 --secondaries $sc; done
+          val "$O"/e2es_*.log ;;
+    e2ep) cd /tmp && export TMPDIR=/tmp
+          for sc in none cw; do
+            timeout -s KILL 400 rocprofv3 --kernel-trace -d $O/rp_e2e_$sc -o run --output-format csv -- python $OLDPWD/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --e2e 3000 --secondaries $sc > $O/rp_e2e_$sc.log 2>&1 || exit 1
+          done
+          cd $OLDPWD
+          for sc in none cw; do for st in 2 5; do python tools/timeline.py $O/rp_e2e_$sc/run_kernel_trace.csv --top 12 --step $st > $O/rp_e2e_${sc}_s$st.txt; python tools/timeline.py $O/rp_e2e_$sc/run_kernel_trace.csv --by-kernel --step $st > $O/rp_e2e_${sc}_s${st}_k.txt; done; head -6 $O/rp_e2e_${sc}_s2.txt; done ;;
+    e2ef) for st in "prefetch=1" "prefetch=2" "prefetch=3" "loader_priority=0"; do run "e2ef_$st" 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --e2e 3000 --secondaries cw --set $st; done
+          val "$O"/e2ef_*.log ;;
+    e2eo) for i in 1 2; do
+            run e2eo_last_$i 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000
+            run e2eo_first_$i 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000 --secondaries cw,c1,c3,c5,c4,var,e2e_first
+          done
+          for f in $O/e2eo_*.log; do python -c "
+import json,sys
+d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); s=d.get('secondary') or {}
+print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'), 'var', (d.get('e2e_variable') or {}).get('value'), 'c3', (s.get('c3_b256_bf16') or {}).get('value'), 'c5', (s.get('c5_e2e_b256_bf16') or {}).get('value'), 'cw', (s.get('corrected_wiring') or {}).get('value'))"; done ;;
+    pdump) run pdump 300 python tools/plan_dump.py --batch 32 ;;
+    e2er) for rp in ${RPARTS:-none probe stamps stamps,serial probe,stamps,serial}; do run "e2er_$rp" 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 3000 --secondaries none --roofline-parts $rp; done
+          val "$O"/e2er_*.log ;;
+    e2ev) for n in 0 500; do ALIGNN_DIAG_EVENTS=$n run "e2ev_$n" 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 3000 --secondaries none --roofline-parts none; done
+          val "$O"/e2ev_*.log ;;
+    e2eq) E=(python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 3000 --secondaries none --roofline-parts probe)
+          ALIGNN_DIAG_PROBE_STEPS=0 run e2eq_stamps_nosteps 600 "${E[@]}"
+          ALIGNN_DIAG_PROBE_STAMPS=0 ALIGNN_DIAG_PROBE_SERIAL=1 run e2eq_nostamps_serial 600 "${E[@]}"
+          ALIGNN_DIAG_PROBE_STAMPS=1 ALIGNN_DIAG_PROBE_SERIAL=0 run e2eq_stamps_concurrent 600 "${E[@]}"
+          ALIGNN_DIAG_PROBE_STAMPS=0 ALIGNN_DIAG_PROBE_SERIAL=0 run e2eq_nostamps_concurrent 600 "${E[@]}"
+          val "$O"/e2eq_*.log ;;
+    e2et) run e2et_store_first 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 3000 --secondaries store_first,e2e_first
+          run e2et_default_nosec 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 3000 --secondaries e2e_first
+          run e2et_store_first_full 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000 --secondaries store_first,e2e_first,cw,c3,c5,var
+          val "$O"/e2et_*.log ;;
+    e2ed) run e2ed_ns3k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 3000
+          run e2ed_ns10k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 10000
+          run e2ed_sec3k 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000
+          val "$O"/e2ed_*.log ;;
     bf16t) run bf16t 900 "${PT[@]}" tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round5.py tests/test_gpu_x_round4.py tests/test_gpu_x_encbwd.py -v ;;
     rpc2) cd /tmp && export TMPDIR=/tmp
           timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $O/rp_c2 -o run --output-format csv -- python $OLDPWD/bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline > $O/rp_c2.log 2>&1 || exit 1
