@@ -261,7 +261,8 @@ def c1_forward(args, dev, lender=None):
                      "gpu_ms": round(t_gpu * 1e3, 3), "speedup": round(t_cpu / t_gpu, 1)}
         del model, b
     out["protocol"] = (f"forward only, fp32, eval mode; median of {C1_REPS} calls after {C1_WARM} warm-up; the GPU "
-                       f"figure is one model(batch) call synchronised (host launch latency included, eager)")
+                       f"figure is one model(batch) call synchronised (host launch latency included; the call replays "
+                       f"the recorded forward from the second call on, alignn_mi355x/infer.py)")
     return out
 
 

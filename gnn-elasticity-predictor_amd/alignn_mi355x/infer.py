@@ -42,6 +42,7 @@ class ForwardPlan:
         eng = model._engine
         self.ctx = eng.ctx
         st = model._ensure_flat()
+        self.flat = st.flat.data_ptr()
         dev = st.flat.device
         # the plan reads a private copy of the batch (the slot); every call copies its batch in unless
         # the slot already holds that batch, unmodified — the caller's tensors are never written
@@ -100,6 +101,30 @@ class ForwardPlan:
         self.used = _plan_refs([self.plan], targets)
         self.ctx.freeze()
         self.replays = 0
+        # the same launches as a HIP graph (the capture above): one host call instead of one per launch.
+        # Where the forward is only a few dozen small kernels (config C1) the per-launch host cost of
+        # the native plan is the call's time and the graph is faster; on a large batch the plan's
+        # concurrent streams win.  Both replays are timed here (three each) and the faster one kept
+        self.use_graph = False
+        try:
+            tp = self._time(lambda: check(_lib.lib().alignn_plan_replay(self.plan, ops.stream_ptr()),
+                                          "alignn_plan_replay"))
+            tg = self._time(self.graph.replay)
+            self.use_graph = tg < tp
+        except Exception:  # noqa: BLE001 - a graph replay the runtime refuses: the plan stays
+            self.use_graph = False
+
+    @staticmethod
+    def _time(fn, reps: int = 3) -> float:
+        import time
+        ts = []
+        for _ in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts[1:])[reps // 2]
 
     def release(self) -> None:
         if self.plan:
@@ -126,7 +151,10 @@ class ForwardPlan:
                 pairs = [(d, s) for d, s in pairs if d.data_ptr() in self.used]
                 ops.copy_many(pairs)
             self._bound, self._bound_v = weakref.ref(batch), v
-        check(_lib.lib().alignn_plan_replay(self.plan, ops.stream_ptr()), "alignn_plan_replay")
+        if self.use_graph:
+            self.graph.replay()
+        else:
+            check(_lib.lib().alignn_plan_replay(self.plan, ops.stream_ptr()), "alignn_plan_replay")
         self.replays += 1
         return self.out
 
@@ -151,6 +179,18 @@ def forward(model, batch, mode: str, precision: Optional[str] = None) -> torch.T
     eng = model._engine
     precision = precision or eng.precision
     st = model._ensure_flat()
+    flat = st.flat.data_ptr()
+    last = model.__dict__.get("_fwd_last")
+    if last is not None and ENABLED:
+        # the same batch object again, unmodified (an evaluation loop over one resident batch, C1):
+        # straight to its plan, without the signature computation
+        ref, v, mp, p = last
+        if (ref() is batch and mp == (mode, precision, flat) and p.plan
+                and batch_versions(batch, FIELDS) == v):
+            return p.run(batch)
+    plans = model.__dict__.get("_fwd_plans")
+    if plans and any(p.flat != flat for p in plans.values()):
+        release(model)   # the parameters were re-laid out (model._ensure_flat): the plans read the old buffer
     with ops.using(eng.ctx):
         bc = batch_cache(batch)
     if ENABLED and _recordable(batch) and not torch.cuda.is_current_stream_capturing():
@@ -164,7 +204,9 @@ def forward(model, batch, mode: str, precision: Optional[str] = None) -> torch.T
                 plans.pop(old).release()
             p = plans[key] = ForwardPlan(model, batch, mode, precision)
         if p is not None:
-            return p.run(batch)
+            out = p.run(batch)
+            model.__dict__["_fwd_last"] = (weakref.ref(batch), p._bound_v, (mode, precision, flat), p)
+            return out
         if len(seen) > 1024:   # many one-off signatures (unpadded variable-size batches): forget them
             seen.clear()
         seen[key] = seen.get(key, 0) + 1
@@ -179,3 +221,4 @@ def release(model) -> None:
     for p in model.__dict__.pop("_fwd_plans", {}).values():
         p.release()
     model.__dict__.pop("_fwd_seen", None)
+    model.__dict__.pop("_fwd_last", None)

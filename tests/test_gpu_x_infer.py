@@ -134,3 +134,38 @@ def test_knn_embeddings_replay_bitwise():
     knn.embed_collect(model, batches)
     z1, y1, i1 = knn.embed_collect(model, batches)
     assert torch.equal(z1, z0) and torch.equal(y1, y0) and np.array_equal(i1, i0)
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_graph_and_plan_replay_equal(use_graph):
+    """A recorded forward replays as the native plan or as the HIP graph of the same capture (the
+    faster one is chosen when it is recorded): both bitwise the eager forward."""
+    from alignn_mi355x.synthetic import mp_like_batch
+    model = _model()
+    b1, b2 = mp_like_batch(6).to(DEV), mp_like_batch(6, first=30).to(DEV)
+    ref1, ref2 = _eager(model, b1), _eager(model, b2)
+    _planned(model, b1)
+    _planned(model, b1)                       # recorded here
+    p = next(iter(model.__dict__["_fwd_plans"].values()))
+    p.use_graph = use_graph
+    for b, r in ((b2, ref2), (b1, ref1), (b1, ref1), (b2, ref2)):
+        assert torch.equal(_planned(model, b), r)
+
+
+def test_replaced_parameter_invalidates_recorded_forward():
+    """A parameter replaced after the forward was recorded re-lays the flat buffer out
+    (model._ensure_flat): the recorded plans, which read the old buffer, are released and the call
+    equals the eager forward with the new weights."""
+    from alignn_mi355x.synthetic import mp_like_batch
+    model = _model()
+    b = mp_like_batch(4).to(DEV)
+    _planned(model, b)
+    _planned(model, b)
+    assert len(model.__dict__["_fwd_plans"]) == 1
+    lin = model.base.node_encoder[0]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    lin.weight = torch.nn.Parameter((torch.randn(lin.weight.shape, generator=g) * 0.05).to(DEV))
+    ref = _eager(model, b)
+    got = _planned(model, b)
+    assert torch.equal(got, ref)
+    assert len(model.__dict__.get("_fwd_plans", {})) == 0
