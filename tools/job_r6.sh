@@ -78,6 +78,12 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
           run e2et_default_nosec 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --e2e 3000 --secondaries e2e_first
           run e2et_store_first_full 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000 --secondaries store_first,e2e_first,cw,c3,c5,var
           val "$O"/e2et_*.log ;;
+    ab) # generic same-box A/B of one engine switch: AB_KEY=engine.x AB_VALS="1 0" AB_CFG="c2|c3"
+        for i in 1 2; do for v in $AB_VALS; do
+          if [ "$AB_CFG" = c3 ]; then run ab_${v}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline --set $AB_KEY=$v
+          else run ab_${v}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set $AB_KEY=$v; fi
+        done; done
+        for f in $O/ab_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
     e2ed) run e2ed_ns3k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 3000
           run e2ed_ns10k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 10000
           run e2ed_sec3k 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000
