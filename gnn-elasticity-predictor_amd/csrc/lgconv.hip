@@ -148,6 +148,10 @@ __device__ __forceinline__ void load_w1(const float* __restrict__ W1, const floa
 typedef float v4f __attribute__((ext_vector_type(4)));
 template <bool BF>
 __device__ __forceinline__ void angle_rows(const XRow& xr, const W1Regs& W, Edge (&e)[G]) {
+  // the row's 12th float (padding) is loaded with the others but unused: this use keeps its register
+  // allocated until here — else the allocator reuses it while the load is in flight, and the write
+  // after write waits with vmcnt(0) for every load issued, the next group's prefetch included
+  asm volatile("" ::"v"(xr.c.w));
   const float xs[KXP] = {xr.a.x, xr.a.y, xr.a.z, xr.a.w, xr.b.x, xr.b.y, xr.b.z, xr.b.w, xr.c.x, xr.c.y, xr.c.z, xr.c.w};
   v4f acc[VPL];
 #pragma unroll

@@ -84,6 +84,15 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
           else run ab_${v}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set $AB_KEY=$v; fi
         done; done
         for f in $O/ab_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
+    abl) # library A/B (C2 bench + lgx_bench fp32 kernels): ab/libA.so vs the in-tree build
+         for i in 1 2; do for lib in ab/libA.so -; do
+           if [ "$lib" = "-" ]; then unset ALIGNN_HIP_LIB; t=B; else export ALIGNN_HIP_LIB=$PWD/$lib; t=A; fi
+           run abl_${t}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline ${ABL_ARGS:-}
+         done; done
+         unset ALIGNN_HIP_LIB
+         ALIGNN_HIP_LIB=$PWD/ab/libA.so run abl_lgx_A 300 python tools/lgx_bench.py --batch 32 --only fwd_f32_x bwd_f32_x
+         run abl_lgx_B 300 python tools/lgx_bench.py --batch 32 --only fwd_f32_x bwd_f32_x
+         for f in $O/abl_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*\|"fwd_f32_x_us": [0-9.]*\|"bwd_f32_x_us": [0-9.]*' $f | head -2 | tr '\n' ' ')"; done ;;
     e2ed) run e2ed_ns3k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 3000
           run e2ed_ns10k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 10000
           run e2ed_sec3k 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000
