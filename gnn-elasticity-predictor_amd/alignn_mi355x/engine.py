@@ -454,8 +454,8 @@ def proj_grads_shared(We, Wp, bp, dM, dwbar, gWe, gWp, gbp) -> None:
 
 def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch.Tensor], feat_row,
                   M: torch.Tensor, wbar: Optional[torch.Tensor], H: int, p_drop: float, seed_att: int,
-                  seed_blk: int, side: Optional[torch.cuda.Stream] = None, compact_gate: bool = False,
-                  skip_early: bool = False, bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
+                  seed_blk: int, side: Optional[torch.cuda.Stream] = None,
+                  bf16_io: bool = False, X16: Optional[torch.Tensor] = None,
                   want_X16: bool = False, angle_x=None, Xa: Optional[torch.Tensor] = None, want_Xa: bool = False):
     """M: per-head edge projection [D, D] (W_edge, or W_edge W_proj); wbar: W_edge b_proj or None.
     bf16_io (bf16 storage, config C3 — the tensor dtypes of the reference's autocast, train.py:632-636):
@@ -466,12 +466,12 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     angle_x (the line graph, F None): (X, W1, b1, bf16) — the edge features are the angle encoder's
     hidden layer relu(X W1^T + b1), recomputed inside the attention kernels from the raw inputs X
     (ops.lg_fwd_x) instead of read; bf16: the bf16-storage form (K|V and f in bf16, config C3).
-    skip_early: on a compacted graph with a side stream, the skip projection is queued there before
-    the active-row gather and the Q/K/V product, so it overlaps those as well as the attention.
-    compact_gate: on a compacted graph, the gate reads the compacted conv output through the row map
-    (no zero-filled [n, D] copy; the backward writes the compacted dout directly).
+    On a compacted graph with a side stream the skip projection is queued there before the active-row
+    gather and the Q/K/V product, so it overlaps those as well as the attention (+1 % at B = 32 against
+    after them, rounds 3 and 5), and the gate reads the compacted conv output through the row map (no
+    zero-filled [n, D] copy; the backward writes the compacted dout directly; +1.2 %, round 1).
     Xa: the active rows of X, already gathered (by the previous line block's gate kernel); want_Xa:
-    this block's gate kernel writes the active rows of its new state to c.Xa_next (compact_gate).
+    this block's gate kernel writes the active rows of its new state to c.Xa_next.
 
     Compacted graphs (g.rows set: the graph's nodes are the active subset ``rows`` of X's rows, see
     BatchCache): Q/K/V, the attention and its per-node GEMMs run over the active rows only; the
@@ -492,18 +492,13 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
         c.Xa, c.QKV, c.R = X, QKVR[:, :3 * D], QKVR[:, 3 * D:]
     else:
         na = g.n
-        early = skip_early and side is not None
         c.R = torch.empty(n, D, device=dev, dtype=torch.bfloat16 if bf16_io else torch.float32)
         Xs = X16 if (bf16_io and X16 is not None) else X   # the skip projection's A operand
-        if early:
-            with _side_work(side, (X, Xs, c.R)):   # skip projection of all rows, beside Q/K/V and the attention
-                ops.gemm(Xs, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
+        with _side_work(side, (X, Xs, c.R)):   # skip projection of all rows, beside Q/K/V and the attention
+            ops.gemm(Xs, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
         c.Xa = Xa if Xa is not None else ops.gather_rows(X, rows)
         c.QKV = torch.empty(na, 3 * D, device=dev)
         ops.gemm(c.Xa, cv.Wqkvr[:3 * D].t(), c.QKV, bias=cv.bqkvr[:3 * D])
-        if not early:
-            with _side_work(side, (X, Xs, c.R)):   # skip projection of all rows, concurrent with the attention
-                ops.gemm(Xs, cv.Wqkvr[3 * D:].t(), c.R, bias=cv.bqkvr[3 * D:])
     c.X16 = X16 if (bf16_io and rows is not None) else None
     c.U = torch.empty(na, H, D, device=dev)
     ops.gemm(c.QKV[:, :D].view(na, H, C).transpose(0, 1), c.M.view(H, C, D), c.U.transpose(0, 1))
@@ -540,11 +535,8 @@ def block_forward(cv: _Conv, X: torch.Tensor, g: ops.GraphCSR, F: Optional[torch
     c.outp_rows = None
     if rows is None:
         c.outp = c.outp_a
-    elif compact_gate:
-        c.outp, c.outp_rows = c.outp_a, g.cmap
     else:
-        c.outp = ops.zeros(n, D, device=dev)
-        ops.scatter_rows(c.outp_a, rows, c.outp)
+        c.outp, c.outp_rows = c.outp_a, g.cmap
     if side is not None and rows is not None:
         ops.stream_wait(torch.cuda.current_stream(dev), side)
     X_new = torch.empty(n, D, device=dev)
@@ -565,7 +557,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
                    dwbar: Optional[torch.Tensor] = None, side: Optional[torch.cuda.Stream] = None,
                    keep_edge_scalars: bool = False, gate_reduce_side: bool = False,
                    wgrad_early: int = 0, dX_add: Optional[torch.Tensor] = None,
-                   bf16_src: bool = True, dX_zero: bool = False) -> None:
+                   dX_zero: bool = False) -> None:
     """dX: gradient w.r.t. the block output on entry, w.r.t. the block input on exit (in place).
     dF: gradient w.r.t. the edge-feature rows (written or accumulated at the rows the forward read).
     Parameter gradients go to gv (gate/LN grads with +=, the rest overwritten); with a projection
@@ -627,7 +619,7 @@ def block_backward(cv: _Conv, gv: _Conv, c, g: ops.GraphCSR, dX: torch.Tensor, d
     early = wgrad_early if side is not None else 0
     if early >= 2:
         _weight_grads(*wg, part="a")     # final once the target-side kernel is done
-    if c.QKV16 is not None and bf16_src:
+    if c.QKV16 is not None:
         # bf16 storage: the gathered target rows (Q, dout) from bf16 copies — half the traffic
         ops.tconv_bwd_src(g, D, H, c.QKV, dout_a, dz_e, al_e, dQKV[:, D:3 * D], Q16=c.QKV16[:, :D],
                           dout16=ops.cast_bf16(dout_a))
@@ -741,9 +733,6 @@ class AlignnEngine:
         # the angle encoder's first Linear (11 inputs, T rows) and its weight/bias gradients as
         # streamed HBM-rate kernels (skinny.hip) instead of MFMA tiles (+3.2 %, v7_sweep.log)
         self.skinny_encoder = True
-        # line blocks on compacted graphs: gate/LayerNorm read the compacted conv output through the
-        # row map instead of a zero-filled full copy (+1.2 %, v7_sweep.log)
-        self.compact_gate = True
         # angle encoder backward deferred to one pass after the last line block (ops.enc_bwd): the
         # line convs leave per-edge scalars instead of read-modify-writing a [T, D] gradient per layer
         # (+4.0 % graphs/s on MI355X once enc_bwd was column-parallel, profiles/r01/v13_sweep.log)
@@ -761,12 +750,6 @@ class AlignnEngine:
         # too): B = 32 +1.1 % (9,972-9,985 -> 10,077-10,090 graphs/s), B = 256 bf16 within noise:
         # always (profiles/r05/v15_sweep_engine_c2.txt)
         self.enc_bwd_aux = 1
-        # forward: each line block's skip projection queued on the side stream before its active-row
-        # gather and Q/K/V product (else after them), and the angle encoder's first Linear on the side
-        # stream beside the node/edge encoders (bitwise neutral; with wgrad_early B = 32
-        # 8,788 -> 8,986 graphs/s, profiles/r03/v19_ab_stream_order.log)
-        self.skip_early = True
-        self.angle_side = True
         # backward: where each block's weight-gradient products are queued on the side stream (see
         # block_backward: 0 after its dX products, 1 before them, 2 split at the target-side kernel);
         # -1: 2 below WGRAD_SPLIT_MAX_T line-graph edges, else 1.  B = 32: 0 -> 2 +2.3 % (8,842 ->
@@ -783,11 +766,6 @@ class AlignnEngine:
         # GEMM kernels, B = 32 (253,440 line-graph edges): 0 -> 2 +2.9 % (9,652-9,670 -> 9,929-9,957
         # graphs/s; 1 -0.8 %, profiles/r05/v15_sweep_engine_c2.txt): ATOM_STREAM_MIN_T 1 M -> 100,000
         self.atom_stream = -1
-        # bf16 storage: the atom-graph attention reads the bond state's bf16 copy (the gate kernel's
-        # Xn16; autocast casts the bond state to bf16 for edge_proj) as its edge-feature rows
-        self.atom_bf16 = True
-        # bf16 storage: the line graph's source-side backward gathers Q and dout as bf16 copies
-        self.bf16_src = True
         # bf16 storage: the atom blocks' edge-feature gradient (the gradient autocast returns through
         # its bf16 cast of the bond states) stored in bf16 between the atom attention backward that
         # writes it and the line block's gate kernel that adds it (half the bytes of both)
@@ -945,7 +923,8 @@ class AlignnEngine:
         if xf:
             angle_x = (bc.xa, P.enc("angle", 0, "weight"), P.enc("angle", 0, "bias"), self._bf16_angle(bc, D))
         ctx.angle_x = angle_x
-        angle_side = self.angle_side and side is not None and ctx.has_angle and not xf
+        # the angle encoder's first Linear on the side stream beside the node/edge encoders (round 3)
+        angle_side = side is not None and ctx.has_angle and not xf
         if xf:
             a = None
         elif ctx.has_angle:
@@ -997,9 +976,8 @@ class AlignnEngine:
             if T > 0 and E > 0:
                 Ml, wl = (ctx.Ml_all[l], ctx.wl_all[l]) if ctx.has_angle else (P.edge[l].We, None)
                 e, c = block_forward(P.edge[l], e, bc.lg, a, None, Ml, wl, H, p_drop,
-                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side, compact_gate=self.compact_gate,
-                                     skip_early=self.skip_early, bf16_io=bf16_io, X16=e16,
-                                     want_X16=bf16_io and (l + 1 < L or self.atom_bf16), angle_x=angle_x,
+                                     site_seed(seed, 4 * l), site_seed(seed, 4 * l + 1), side=side,
+                                     bf16_io=bf16_io, X16=e16, want_X16=bf16_io, angle_x=angle_x,
                                      Xa=ea, want_Xa=self.gate_gathers and l + 1 < L)
                 e16 = c.Xn16
                 ea = c.Xa_next
@@ -1008,8 +986,9 @@ class AlignnEngine:
             ctx.edge.append(c)
             # NodeUpdateBlock (train.py:330-336): atom graph, bond states gathered through the CSR perm
             if E > 0:
-                # bf16 storage: the bond-state rows as autocast hands them to edge_proj (bf16)
-                ef = e16 if (bf16_io and self.atom_bf16 and e16 is not None) else e
+                # bf16 storage: the bond-state rows as autocast hands them to edge_proj (bf16: the gate
+                # kernel's copy), and the line graph's source-side backward gathers Q / dout as bf16 copies
+                ef = e16 if (bf16_io and e16 is not None) else e
                 with _side_work(aux, (e, ef, h, ctx.M_all, ctx.wbar_all)):
                     h, c = block_forward(P.node[l], h, bc.ag, ef, bc.ag.perm_dst, ctx.M_all[l], ctx.wbar_all[l], H,
                                          p_drop, site_seed(seed, 4 * l + 2), site_seed(seed, 4 * l + 3))
@@ -1166,13 +1145,11 @@ class AlignnEngine:
                 if line_proj:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, dMl_all[l], dwl_all[l], side=side,
                                    keep_edge_scalars=defer, gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src,
-                                   dX_zero=de_fresh and l == L - 1)
+                                   wgrad_early=wgrad, dX_add=add, dX_zero=de_fresh and l == L - 1)
                 else:
                     block_backward(P.edge[l], G.edge[l], c, bc.lg, de, da, flags, side=side,
                                    gate_reduce_side=self.gate_reduce_side,
-                                   wgrad_early=wgrad, dX_add=add, bf16_src=self.bf16_src,
-                                   dX_zero=de_fresh and l == L - 1)
+                                   wgrad_early=wgrad, dX_add=add, dX_zero=de_fresh and l == L - 1)
                 da_written = True
         t = _Ctx()
         t.P, t.G, t.ctx, t.bc, t.dh, t.de, t.da, t.defer, t.side, t.line_proj = P, G, ctx, bc, dh, de, da, defer, side, line_proj

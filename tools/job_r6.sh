@@ -93,6 +93,20 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
          ALIGNN_HIP_LIB=$PWD/ab/libA.so run abl_lgx_A 300 python tools/lgx_bench.py --batch 32 --only fwd_f32_x bwd_f32_x
          run abl_lgx_B 300 python tools/lgx_bench.py --batch 32 --only fwd_f32_x bwd_f32_x
          for f in $O/abl_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*\|"fwd_f32_x_us": [0-9.]*\|"bwd_f32_x_us": [0-9.]*' $f | head -2 | tr '\n' ' ')"; done ;;
+    pmc) cd /tmp && export TMPDIR=/tmp
+         B2="--steps 5 --warmup 2 --no-secondary --e2e 0 --no-cpu-baseline"
+         B3="--steps 3 --warmup 2 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline"
+         for c in FETCH_SIZE WRITE_SIZE; do
+           timeout -s KILL 420 rocprofv3 --pmc $c --kernel-trace -d $O/pmc_c3_$c -o run --output-format csv -- python $OLDPWD/bench.py $B3 > $O/pmc_c3_$c.log 2>&1 || exit 1
+           timeout -s KILL 420 rocprofv3 --pmc $c --kernel-trace -d $O/pmc_c2_$c -o run --output-format csv -- python $OLDPWD/bench.py $B2 > $O/pmc_c2_$c.log 2>&1 || exit 1
+         done
+         timeout -s KILL 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_c3_mf -o run --output-format csv -- python $OLDPWD/bench.py $B3 > $O/pmc_c3_mf.log 2>&1 || exit 1
+         timeout -s KILL 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_c2_mf -o run --output-format csv -- python $OLDPWD/bench.py $B2 > $O/pmc_c2_mf.log 2>&1 || exit 1
+         cd $OLDPWD
+         for c in c2 c3; do
+           python tools/pmc_traffic.py $O/pmc_${c}_FETCH_SIZE $O/pmc_${c}_WRITE_SIZE --json $O/pmc_${c}_traffic.json --top 40 > $O/pmc_${c}_traffic.txt
+           python tools/pmc_mfma.py $O/pmc_${c}_mf > $O/pmc_${c}_mfma.txt; done
+         head -12 $O/pmc_c3_traffic.txt; head -12 $O/pmc_c2_traffic.txt ;;
     e2ed) run e2ed_ns3k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 3000
           run e2ed_ns10k 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --no-roofline --e2e 10000
           run e2ed_sec3k 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e 3000
