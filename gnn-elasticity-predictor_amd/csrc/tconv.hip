@@ -41,22 +41,51 @@ struct Sched {
   __host__ __device__ int64_t items() const { return n_heavy + (n_light + 3) / 4; }
 };
 
-template <int VPL>
-struct EdgeSlot {
-  float k[VPL], v[VPL], f[VPL];
+// The streamed edge rows of the _2 kernels.  FBF: the feature rows hold bf16 (config C3: the atom
+// graph's edge features are the bond state as autocast casts it for edge_proj, train.py:325/:333
+// under :632-636), widened exactly at use.  The feature row stays in its storage format (bf16
+// pairs or fp32 bits) until the group is consumed, and nothing is computed from a row at its
+// load: a value computed at the load (the bf16 widening) would put a wait for that load right
+// behind it, and a value reaching a loop head through a phi makes the wait-count pass drain every
+// load in flight (vmcnt(0)).  Lanes past D read column 0 (their q / u / Vd / dout are zero, so
+// what they read never reaches a stored value) and callers clamp the edge index to the segment
+// (rows past its end are masked out of the softmax and out of every store).
+template <int VPL, bool FBF>
+struct EdgeRow {
+  float k[VPL], v[VPL];
+  uint32_t fb[FBF ? (VPL + 1) / 2 : VPL];
+  __device__ __forceinline__ void widen(float (&f)[VPL]) const {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+      f[i] = FBF ? __builtin_bit_cast(float, (i & 1) ? (fb[i / 2] & 0xffff0000u) : (fb[i / 2] << 16))
+                 : __builtin_bit_cast(float, fb[i]);
+  }
 };
 
-// fbf: the feature rows hold bf16 (config C3: the atom graph's edge features are the bond state as
-// autocast casts it for edge_proj, train.py:325/:333 under :632-636), widened exactly at the load
-template <int VPL>
-__device__ __forceinline__ void load_edge(EdgeSlot<VPL>& e, const float* __restrict__ QKVR, int64_t ldq, int D,
-                                          const float* __restrict__ F, int64_t ldf, int fbf, int64_t src, int64_t row,
-                                          int j0, bool act, int lane) {
-  if (act) {
-    vload(QKVR + src * ldq + D + j0, e.k);
-    vload(QKVR + src * ldq + 2 * D + j0, e.v);
-    if (fbf) vload_bf(reinterpret_cast<const uint16_t*>(F) + row * ldf + j0, e.f);
-    else vload(F + row * ldf + j0, e.f);
+template <int VPL, bool FBF>
+__device__ __forceinline__ void load_row(EdgeRow<VPL, FBF>& e, const float* __restrict__ QKVR, int64_t ldq, int D,
+                                         const float* __restrict__ F, int64_t ldf, int64_t src, int64_t row, int jc) {
+  vload(QKVR + src * ldq + D + jc, e.k);
+  vload(QKVR + src * ldq + 2 * D + jc, e.v);
+  if constexpr (FBF) {
+    const uint16_t* fp = reinterpret_cast<const uint16_t*>(F) + row * ldf + jc;
+    if constexpr (VPL % 4 == 0) {
+#pragma unroll
+      for (int q = 0; q < VPL / 4; ++q) {
+        const uint2 u = *reinterpret_cast<const uint2*>(fp + 4 * q);
+        e.fb[2 * q] = u.x;
+        e.fb[2 * q + 1] = u.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < (VPL + 1) / 2; ++i)
+        e.fb[i] = (uint32_t)fp[2 * i] | (2 * i + 1 < VPL ? (uint32_t)fp[2 * i + 1] << 16 : 0u);
+    }
+  } else {
+    float t[VPL];
+    vload(F + row * ldf + jc, t);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) e.fb[i] = __builtin_bit_cast(uint32_t, t[i]);
   }
 }
 
@@ -80,6 +109,16 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 #else
 #define TCONV_ATTR __launch_bounds__(256)
 #endif
+// waves per SIMD asked of the _2 kernels of up to 16 values per lane (0: the compiler's choice).
+// Forward: 3 (168 registers, 4 spilled at bf16; C3 atom forward 354 -> 305 us, C2 59 -> 55 us:
+// profiles/r06/ab_tconv_ring.txt)
+#ifndef ALIGNN_TCONV2_WPE_FWD
+#define ALIGNN_TCONV2_WPE_FWD 3
+#endif
+#ifndef ALIGNN_TCONV2_WPE_BWD
+#define ALIGNN_TCONV2_WPE_BWD 0
+#endif
+#define TCONV2_ATTR_(W) __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((W) > 0 ? (W) : 1)))
 
 // =============================================================================================
 // Forward
@@ -215,10 +254,23 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
 
   const int32_t first = beg + wsub * PF, stride = nw * PF;
   if (first < end) {
-    float q[VPL];
+    const int jc = act ? j0 : 0;
+    // The first group's rows go out with the node's own vectors (one round trip for both); the
+    // next group is requested slot by slot as each row of the current one is consumed.
+    EdgeRow<VPL, FBF> ring[PF];
+    auto request = [&](int j, int32_t t0) {
+      const int32_t t = min(t0 + j, end - 1);
+      load_row<VPL, FBF>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)uni(sld(p.src_at, t)),
+                         p.feat_row ? (int64_t)uni(sld(p.feat_row, t)) : t, jc);
+    };
+#pragma unroll
+    for (int j = 0; j < PF; ++j) request(j, first);
+    float q[VPL], wb[VPL];
     vzero(q);
+    vzero(wb);
     if (act) {
       vload(p.QKVR + d * p.ldq + j0, q);
+      if (p.wbar) vload(p.wbar + j0, wb);
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         float t[VPL];
@@ -237,25 +289,19 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
 #pragma unroll
     for (int h = 0; h < H; ++h) c[h] = 0.f;
     if (p.wbar) {
-      float wb[VPL];
-      vzero(wb);
-      if (act) vload(p.wbar + j0, wb);
       const float part = vdot(wb, q);
 #pragma unroll
       for (int h = 0; h < H; ++h) c[h] = (h == hl) ? part : 0.f;
       reduce_bcast<H>(c, lane);
     }
-    EdgeSlot<VPL> ring[PF];
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
-      const int32_t t = first + j;
-      if (t < end)
-        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, t)),
-                          p.feat_row ? (int64_t)uni(sld(p.feat_row, t)) : t, j0, act, lane);
-    }
+    // Straight-line control flow around the ring (the next group is requested unconditionally,
+    // clamped to the segment): a conditional request would merge the ring's registers at the loop
+    // head, and the copies of that merge wait for every load in flight.
     for (int32_t tb = first; tb < end; tb += stride) {
       asm volatile("" ::: "memory");  // keep the u reads in the loop (registers are the point)
+      float f[PF][VPL];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) ring[j].widen(f[j]);
       float pr[PF * H];
       {
         float qk[PF];
@@ -266,7 +312,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
           float u[VPL];
           vload(uv + h * RS + j0, u);
 #pragma unroll
-          for (int j = 0; j < PF; ++j) pr[j * H + h] = vdot(u, ring[j].f) + ((h == hl) ? qk[j] : 0.f);
+          for (int j = 0; j < PF; ++j) pr[j * H + h] = vdot(u, f[j]) + ((h == hl) ? qk[j] : 0.f);
         }
       }
       float b[H];
@@ -303,15 +349,12 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
         for (int h = 0; h < H; ++h) {
           e[h] = readlane_f(b[h], 16 * j);
 #pragma unroll
-          for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(e[h], ring[j].f[i], accS[h][i]);
+          for (int i = 0; i < VPL; ++i) accS[h][i] = fmaf(e[h], f[j][i], accS[h][i]);
         }
         const float el = pick_r<H>(e, hl);
 #pragma unroll
         for (int i = 0; i < VPL; ++i) accV[i] = fmaf(el, ring[j].v[i], accV[i]);
-        const int32_t tn = tb + stride + j;
-        if (tn < end)
-          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, tn)),
-                            p.feat_row ? (int64_t)uni(sld(p.feat_row, tn)) : tn, j0, act, lane);
+        request(j, tb + stride);
       }
     }
   }
@@ -393,7 +436,7 @@ __device__ __forceinline__ void fwd2_node(const FwdParams& p, float* smem, int64
 
 // FBF: bf16 edge-feature rows (a compile-time switch: the fp32 instantiation is unchanged)
 template <int VPL, int H, bool FBF>
-__global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
+__global__ TCONV2_ATTR_(VPL * H <= 16 ? ALIGNN_TCONV2_WPE_FWD : 0) void tconv_fwd2_kernel(FwdParams p, Sched sc) {
   resolve_drop(p.drop);
   __shared__ float smem[fwd2_lds_floats<VPL, H>()];
   const int wave = wave_id();
@@ -411,7 +454,9 @@ __global__ TCONV_ATTR void tconv_fwd2_kernel(FwdParams p, Sched sc) {
 template <int VPL, int H>
 constexpr int bwd2_lds_floats() { return cmax(bwd_merge_floats<VPL, H>(), 4 * 2 * H * 64 * VPL); }
 
-template <int VPL, int H, bool FBF>
+// OLD: dF is accumulated into (acc_dF bit 0): its rows are prefetched with the edge rows (a
+// compile-time switch, so the plain-write instantiation carries no conditional load)
+template <int VPL, int H, bool FBF, bool OLD>
 __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, int64_t d, int wsub, int nw, bool heavy) {
   static_assert(PF == 4, "row-distributed layout assumes one edge per row");
   constexpr int NS = H + H * VPL + VPL;
@@ -438,6 +483,19 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
 
   const int32_t first = beg + wsub * PF, stride = nw * PF;
   if (first < end) {
+    const int jc = act ? j0 : 0;
+    // the first group's rows go out with the node's own vectors (see fwd2_node)
+    EdgeRow<VPL, FBF> ring[PF];
+    int64_t rw[PF];
+    float ob[OLD ? PF : 1][VPL];
+    auto request = [&](int j, int32_t t0) {
+      const int32_t t = min(t0 + j, end - 1);
+      rw[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
+      load_row<VPL, FBF>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, (int64_t)uni(sld(p.src_at, t)), rw[j], jc);
+      if constexpr (OLD) vload(p.dF + rw[j] * p.lddf + jc, ob[j]);
+    };
+#pragma unroll
+    for (int j = 0; j < PF; ++j) request(j, first);
     float q[VPL], go[VPL];
     vzero(q);
     vzero(go);
@@ -480,24 +538,11 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
       mst[h] = p.mstat[d * H + h];
       inv_den[h] = 1.0f / p.den[d * H + h];
     }
-    EdgeSlot<VPL> ring[PF];
-    float old[PF][VPL];
-    int64_t rows_[PF];
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      vzero(ring[j].k); vzero(ring[j].v); vzero(ring[j].f);
-      vzero(old[j]);
-      const int32_t t = first + j;
-      rows_[j] = 0;
-      if (t < end) {
-        rows_[j] = p.feat_row ? uni(sld(p.feat_row, t)) : t;
-        load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, t)), rows_[j], j0, act,
-                          lane);
-        if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
-      }
-    }
-    for (int32_t tb = first; tb < end; tb += stride) {
+    for (int32_t tb = first; tb < end; tb += stride) {  // (straight-line around the ring: see fwd2_node)
       asm volatile("" ::: "memory");  // keep the u / Vd reads in the loop
+      float f[PF][VPL];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) ring[j].widen(f[j]);
       float bs[H], bd[H];
       {
         float ps[PF * H], pd[PF * H];
@@ -514,8 +559,8 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
           vload(uv + (H + h) * RS + j0, vd);
 #pragma unroll
           for (int j = 0; j < PF; ++j) {
-            ps[j * H + h] = vdot(u, ring[j].f) + ((h == hl) ? qk[j] : 0.f);
-            pd[j * H + h] = vdot(vd, ring[j].f) + ((h == hl) ? gv[j] : 0.f);
+            ps[j * H + h] = vdot(u, f[j]) + ((h == hl) ? qk[j] : 0.f);
+            pd[j * H + h] = vdot(vd, f[j]) + ((h == hl) ? gv[j] : 0.f);
           }
         }
         reduce_rows<PF * H>(ps, bs);
@@ -553,48 +598,43 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
         for (int h = 0; h < H; ++h) {
           e[h] = readlane_f(bs[h], 16 * j);
 #pragma unroll
-          for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(e[h], ring[j].f[i], sz[h][i]);
+          for (int i = 0; i < VPL; ++i) sz[h][i] = fmaf(e[h], f[j][i], sz[h][i]);
         }
         const float dzl = pick_r<H>(e, hl);
 #pragma unroll
         for (int i = 0; i < VPL; ++i) dqa[i] = fmaf(dzl, ring[j].k[i], dqa[i]);
       }
       if (do_dF) {
-        // dF[row(t)] (+)= sum_h dz u_h + alpha' Vd_h, one head at a time from LDS
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-          float u[VPL], vd[VPL];
-          vload(uv + h * RS + j0, u);
-          vload(uv + (H + h) * RS + j0, vd);
-#pragma unroll
-          for (int j = 0; j < PF; ++j) {
-            const float ez = readlane_f(bs[h], 16 * j), ea = readlane_f(bd[h], 16 * j);
-#pragma unroll
-            for (int i = 0; i < VPL; ++i) old[j][i] = fmaf(ez, u[i], fmaf(ea, vd[i], old[j][i]));
-          }
-        }
+        // dF[row(t)] (+)= sum_h dz u_h + alpha' Vd_h, one edge at a time (u / Vd re-read from LDS
+        // per edge: one edge's sum live instead of PF)
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
-          if (tb + j < end && act) {
-            float df[VPL];
+          float df[VPL];
+          if constexpr (OLD) {
 #pragma unroll
-            for (int i = 0; i < VPL; ++i) df[i] = (p.acc_dF & 2) ? (ring[j].f[i] > 0.f ? old[j][i] : 0.f) : old[j][i];
-            if (p.dfbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dF) + rows_[j] * p.lddf + j0, df);
-            else vstore(p.dF + rows_[j] * p.lddf + j0, df);
+            for (int i = 0; i < VPL; ++i) df[i] = ob[j][i];
+          } else {
+            vzero(df);
+          }
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            float u[VPL], vd[VPL];
+            vload(uv + h * RS + j0, u);
+            vload(uv + (H + h) * RS + j0, vd);
+            const float ez = readlane_f(bs[h], 16 * j), ea = readlane_f(bd[h], 16 * j);
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) df[i] = fmaf(ez, u[i], fmaf(ea, vd[i], df[i]));
+          }
+          if (tb + j < end && act) {
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) df[i] = (p.acc_dF & 2) ? (f[j][i] > 0.f ? df[i] : 0.f) : df[i];
+            if (p.dfbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dF) + rw[j] * p.lddf + j0, df);
+            else vstore(p.dF + rw[j] * p.lddf + j0, df);
           }
         }
       }
 #pragma unroll
-      for (int j = 0; j < PF; ++j) {
-        const int32_t tn = tb + stride + j;
-        vzero(old[j]);
-        if (tn < end) {
-          rows_[j] = p.feat_row ? uni(sld(p.feat_row, tn)) : tn;
-          load_edge<VPL>(ring[j], p.QKVR, p.ldq, D, p.F, p.ldf, FBF, (int64_t)uni(sld(p.src_at, tn)), rows_[j], j0,
-                            act, lane);
-          if (act && do_dF && (p.acc_dF & 1)) vload(p.dF + rows_[j] * p.lddf + j0, old[j]);
-        }
-      }
+      for (int j = 0; j < PF; ++j) request(j, tb + stride);
     }
   }
   if (heavy) {
@@ -634,18 +674,18 @@ __device__ __forceinline__ void bwd2_node(const BwdDstParams& p, float* smem, in
   if (heavy) __syncthreads();
 }
 
-template <int VPL, int H, bool FBF>
-__global__ TCONV_ATTR void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
+template <int VPL, int H, bool FBF, bool OLD>
+__global__ TCONV2_ATTR_(VPL * H <= 16 ? ALIGNN_TCONV2_WPE_BWD : 0) void tconv_bwd_dst2_kernel(BwdDstParams p, Sched sc) {
   resolve_drop(p.drop);
   __shared__ float smem[bwd2_lds_floats<VPL, H>()];
   const int wave = wave_id();
   const int64_t items = sc.items();
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     if (it < sc.n_heavy) {
-      bwd2_node<VPL, H, FBF>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
+      bwd2_node<VPL, H, FBF, OLD>(p, smem, (int64_t)uni(sld(sc.heavy, it)), wave, 4, true);
     } else {
       const int64_t i = (it - sc.n_heavy) * 4 + wave;
-      if (i < sc.n_light) bwd2_node<VPL, H, FBF>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
+      if (i < sc.n_light) bwd2_node<VPL, H, FBF, OLD>(p, smem, sc.light ? (int64_t)uni(sld(sc.light, i)) : i, 0, 1, false);
     }
   }
 }
@@ -936,8 +976,14 @@ template <int VPL, int H>
 static void launch_bwd_dst(const BwdDstParams& p, const Sched& sc, hipStream_t s) {
   const int64_t items = sc.items();
   if (items <= 0) return;
-  if (p.fbf) launch((tconv_bwd_dst2_kernel<VPL, H, true>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
-  else launch((tconv_bwd_dst2_kernel<VPL, H, false>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  const bool old = p.dF != nullptr && (p.acc_dF & 1);
+  if (p.fbf) {
+    if (old) launch((tconv_bwd_dst2_kernel<VPL, H, true, true>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+    else launch((tconv_bwd_dst2_kernel<VPL, H, true, false>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  } else {
+    if (old) launch((tconv_bwd_dst2_kernel<VPL, H, false, true>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+    else launch((tconv_bwd_dst2_kernel<VPL, H, false, false>), dim3((unsigned)items), dim3(256), 0, s, p, sc);
+  }
 }
 
 template <int VPL, int H>

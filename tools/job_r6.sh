@@ -84,6 +84,26 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
           else run ab_${v}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set $AB_KEY=$v; fi
         done; done
         for f in $O/ab_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
+    tc) run tc 900 "${PT[@]}" tests/test_gpu_kernels.py tests/test_gpu_parity.py tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round4.py tests/test_gpu_x_round5.py ;;
+    ablm) # multi-library A/B: ABL_LIBS="ab/libH.so - ab/libF3.so" ("-": the in-tree build); C2 + C3
+          # bench values, then one C3 and one C2 kernel trace per library (per-kernel averages)
+          for i in $(seq 1 ${ABL_ROUNDS:-2}); do for lib in $ABL_LIBS; do
+            if [ "$lib" = "-" ]; then unset ALIGNN_HIP_LIB; t=tree; else export ALIGNN_HIP_LIB=$PWD/$lib; t=$(basename ${lib%.so}); fi
+            run ablm_c2_${t}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline
+            run ablm_c3_${t}_$i 300 python bench.py --steps 10 --warmup 3 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline
+          done; done
+          unset ALIGNN_HIP_LIB
+          for f in $O/ablm_c*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done
+          cd /tmp && export TMPDIR=/tmp
+          for lib in $ABL_LIBS; do
+            if [ "$lib" = "-" ]; then unset ALIGNN_HIP_LIB; t=tree; else export ALIGNN_HIP_LIB=$OLDPWD/$lib; t=$(basename ${lib%.so}); fi
+            timeout -s KILL 300 rocprofv3 --kernel-trace -d $O/rpab3_$t -o run --output-format csv -- python $OLDPWD/bench.py --steps 5 --warmup 2 --batch 256 --precision bf16 --no-secondary --e2e 0 --no-cpu-baseline --no-roofline > $O/rpab3_$t.log 2>&1 || exit 1
+            timeout -s KILL 300 rocprofv3 --kernel-trace -d $O/rpab2_$t -o run --output-format csv -- python $OLDPWD/bench.py --steps 10 --warmup 2 --no-secondary --e2e 0 --no-cpu-baseline --no-roofline > $O/rpab2_$t.log 2>&1 || exit 1
+          done
+          unset ALIGNN_HIP_LIB; cd $OLDPWD
+          for lib in $ABL_LIBS; do t=tree; [ "$lib" = "-" ] || t=$(basename ${lib%.so})
+            for c in 3 2; do python tools/trace_by_grid.py $O/rpab${c}_$t/run_kernel_trace.csv > $O/rpab${c}_$t.txt 2>&1
+              echo "C$c $t: $(grep -E 'tconv_(fwd2|bwd_dst2|bwd_src)' $O/rpab${c}_$t.txt | awk '{n=$0; sub(/.*alignn::/, "", n); printf "%s %s | ", $1, n}')"; done; done ;;
     abl) # library A/B (C2 bench + lgx_bench fp32 kernels): ab/libA.so vs the in-tree build
          for i in 1 2; do for lib in ab/libA.so -; do
            if [ "$lib" = "-" ]; then unset ALIGNN_HIP_LIB; t=B; else export ALIGNN_HIP_LIB=$PWD/$lib; t=A; fi
