@@ -81,6 +81,15 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
     pl.bm = 128;
     pl.bn = 64;
   }
+  // bf16 products over many rows with a deep K (C3's dX += dQKVR Wb, M 15,360 x 256 x 1,024, and the
+  // line graph's row-scattered M 16,020 x 256 x 768): 128 x 64 tiles, 32-deep stages — 44.3 vs 50.5 us
+  // and 44.8 vs 46.0 us, the best of every tile x depth x split (profiles/r06/gemm_c3_big.log)
+  const bool bf_deep = (tile & ALIGNN_GEMM_BF16) && shape == 0 && !bf_long && !(tile & (ALIGNN_GEMM_BK16 |
+                       ALIGNN_GEMM_BK32 | ALIGNN_GEMM_BK64)) && requested <= 0 && M >= 8192 && N <= 256 && Ktot >= 512;
+  if (bf_deep) {
+    pl.bm = 128;
+    pl.bn = 64;
+  }
   const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn) * nb;
   int split = requested;
   if (bf_long) {
@@ -109,7 +118,7 @@ static GemmPlan make_plan(int64_t M, int64_t N, int64_t Ktot, int64_t nb, int re
   if (split < 1) split = 1;
   pl.split = split;
   pl.kchunk = kchunk;
-  if (bf_long) pl.bk = 32;
+  if (bf_long || bf_deep) pl.bk = 32;
   else if (tile & ALIGNN_GEMM_BK64) pl.bk = 64;
   else if (tile & ALIGNN_GEMM_BK32) pl.bk = 32;
   else if (tile & ALIGNN_GEMM_BK16) pl.bk = 16;

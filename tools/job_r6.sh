@@ -84,6 +84,8 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
           else run ab_${v}_$i 300 python bench.py --steps 20 --warmup 5 --no-secondary --e2e 0 --no-cpu-baseline --set $AB_KEY=$v; fi
         done; done
         for f in $O/ab_*.log; do echo "$(basename $f) $(grep -o '"value": [0-9.]*' $f | head -1)"; done ;;
+    tg) run tg 900 "${PT[@]}" tests/test_gpu_x_gemm_pipe.py tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_splitk.py tests/test_gpu_x_gemm_lds16.py tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_kernels.py ;;
+    gb3) run gb3 600 python tools/gemm_bench.py --batch 256 --precision bf16 --min-m 15000 --quick --reps 10 ;;
     tc) run tc 900 "${PT[@]}" tests/test_gpu_kernels.py tests/test_gpu_parity.py tests/test_gpu_x_bf16.py tests/test_gpu_x_configs.py tests/test_gpu_x_round4.py tests/test_gpu_x_round5.py ;;
     ablm) # multi-library A/B: ABL_LIBS="ab/libH.so - ab/libF3.so" ("-": the in-tree build); C2 + C3
           # bench values, then one C3 and one C2 kernel trace per library (per-kernel averages)
