@@ -16,9 +16,8 @@ seen (a one-off batch stays eager); each model keeps at most MAX_PLANS recorded 
 """
 from __future__ import annotations
 
-from typing import Optional
-
 import weakref
+from typing import Optional
 
 import torch
 
