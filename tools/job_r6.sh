@@ -87,8 +87,9 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
     lgxab) for i in 1 2; do for lib in $ABL_LIBS; do
              if [ "$lib" = "-" ]; then unset ALIGNN_HIP_LIB; t=tree; else export ALIGNN_HIP_LIB=$PWD/$lib; t=$(basename ${lib%.so}); fi
              run lgxab_${t}_$i 300 python tools/lgx_bench.py --batch 32 --only fwd_f32_x bwd_f32_x
+             run lgxab3_${t}_$i 300 python tools/lgx_bench.py --batch 256 --only fwd_bf16_rows bwd_bf16_rows
            done; done; unset ALIGNN_HIP_LIB
-           for f in $O/lgxab_*.log; do echo "$(basename $f) $(grep -o '"fwd_f32_x_us": [0-9.]*\|"bwd_f32_x_us": [0-9.]*' $f | tr '\n' ' ')"; done ;;
+           for f in $O/lgxab*.log; do echo "$(basename $f) $(grep -o '"fwd_[a-z0-9_]*_us": [0-9.]*\|"bwd_[a-z0-9_]*_us": [0-9.]*' $f | tr '\n' ' ')"; done ;;
     tl) run tl 900 "${PT[@]}" tests/test_gpu_x_lg3.py tests/test_gpu_x_recompute.py tests/test_gpu_parity.py tests/test_gpu_x_configs.py ;;
     tg) run tg 900 "${PT[@]}" tests/test_gpu_x_gemm_pipe.py tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_splitk.py tests/test_gpu_x_gemm_lds16.py tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_kernels.py ;;
     gb3) run gb3 600 python tools/gemm_bench.py --batch 256 --precision bf16 --min-m 15000 --quick --reps 10 ;;
