@@ -135,13 +135,57 @@ struct GateBwdParams {
   int dxz;              // dXn holds no gradient yet: read as zero (with dX2: the sum is dX2, written to dXn)
 };
 
-template <int VPL, bool IO>
+// A row's operand as it lies in memory (bf16 pairs or fp32 bits), widened where it is used: a
+// value computed at its load puts the wait for that load right behind it.
+template <int VPL, bool BF>
+struct RawRow {
+  uint32_t u[BF ? (VPL + 1) / 2 : VPL];
+  __device__ __forceinline__ void load(const void* base, int64_t idx) {
+    if constexpr (BF) {
+      const uint16_t* q = reinterpret_cast<const uint16_t*>(base) + idx;
+      if constexpr (VPL % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < VPL / 4; ++k) {
+          const uint2 t = *reinterpret_cast<const uint2*>(q + 4 * k);
+          u[2 * k] = t.x;
+          u[2 * k + 1] = t.y;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < (VPL + 1) / 2; ++i)
+          u[i] = (uint32_t)q[2 * i] | (2 * i + 1 < VPL ? (uint32_t)q[2 * i + 1] << 16 : 0u);
+      }
+    } else {
+      float t[VPL];
+      vload(reinterpret_cast<const float*>(base) + idx, t);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) u[i] = __builtin_bit_cast(uint32_t, t[i]);
+    }
+  }
+  __device__ __forceinline__ void widen(float (&f)[VPL], bool live) const {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const float v = BF ? __builtin_bit_cast(float, (i & 1) ? (u[i / 2] & 0xffff0000u) : (u[i / 2] << 16))
+                         : __builtin_bit_cast(float, u[i]);
+      f[i] = live ? v : 0.f;
+    }
+  }
+};
+
+// IO: some operand is bf16 (the bf16 stores take runtime flags); RBF: R is bf16; X2: an addend dX2
+// (X2BF: bf16).  Rows r and r + nwaves are walked as a pair: both rows' loads are issued before
+// either is computed (every load unconditional: the second row of the last pair is clamped to the
+// first and its results dropped; a row without an output row, or a dXn read as zero, loads a valid
+// row and zeroes it at use), then the two rows are computed in row order — the accumulations in the
+// order of the one-row loop: bitwise its results.
+template <int VPL, bool IO, bool RBF, bool X2, bool X2BF>
 __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
   resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + wave_id();
   const int D = p.D, j0 = lane * VPL;
   const bool act = j0 < D;
+  const int jc = act ? j0 : 0;
   float w1[VPL], w2[VPL], w3[VPL], g[VPL], bb[VPL];
   vzero(w1); vzero(w2); vzero(w3); vzero(g); vzero(bb);
   if (act) {
@@ -153,25 +197,41 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
   }
   float a_g[VPL], a_b[VPL], a_w1[VPL], a_w2[VPL], a_w3[VPL];
   vzero(a_g); vzero(a_b); vzero(a_w1); vzero(a_w2); vzero(a_w3);
-  for (int64_t row = wid; wid < p.nwaves && row < p.n; row += p.nwaves) {
+  struct In {
+    float o[VPL], gx[VPL];
+    RawRow<VPL, RBF> r;
+    RawRow<VPL, X2BF> x2;
+    int64_t orow;
+    float b, mean, rs;
+  };
+  auto issue = [&](In& t, int64_t row) {
+    t.orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
+    // (no output row: a valid address read instead — this row of dXn — and o zeroed at use)
+    vload((t.orow >= 0 ? p.outp + t.orow * D : p.dXn + row * p.lddx) + jc, t.o);
+    t.r.load(p.R, row * p.ldr + jc);
+    vload(p.dXn + row * p.lddx + jc, t.gx);
+    if constexpr (X2) t.x2.load(p.dX2, row * D + jc);
+    t.b = p.beta[row];
+    t.mean = p.mu[row];
+    t.rs = p.rstd[row];
+  };
+  auto finish = [&](const In& t, int64_t row) {
+    const int64_t orow = t.orow;
     float o[VPL], r[VPL], gx[VPL];
-    vzero(o); vzero(r); vzero(gx);
-    const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
-    if (act) {
-      if (orow >= 0) vload(p.outp + orow * D + j0, o);
-      if (IO && p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
-      else vload(p.R + row * p.ldr + j0, r);
-      if (!p.dxz) vload(p.dXn + row * p.lddx + j0, gx);
-      if (p.dX2) {   // one add per element, the sum kept as the residual's gradient
-        float x2[VPL];
-        if (IO && p.x2bf) vload_bf(reinterpret_cast<const uint16_t*>(p.dX2) + row * D + j0, x2);
-        else vload(p.dX2 + row * D + j0, x2);
 #pragma unroll
-        for (int i = 0; i < VPL; ++i) gx[i] += x2[i];
-        vstore(const_cast<float*>(p.dXn) + row * p.lddx + j0, gx);
-      }
+    for (int i = 0; i < VPL; ++i) {
+      o[i] = (act && orow >= 0) ? t.o[i] : 0.f;
+      gx[i] = (act && !p.dxz) ? t.gx[i] : 0.f;
     }
-    const float b = p.beta[row], mean = p.mu[row], rs = p.rstd[row];
+    t.r.widen(r, act);
+    if constexpr (X2) {   // one add per element, the sum kept as the residual's gradient
+      float x2[VPL];
+      t.x2.widen(x2, act);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) gx[i] += x2[i];
+      if (act) vstore(const_cast<float*>(p.dXn) + row * p.lddx + j0, gx);
+    }
+    const float b = t.b, mean = t.mean, rs = t.rs;
     float yh[VPL], gyh[VPL];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -212,6 +272,17 @@ __global__ __launch_bounds__(256) void gate_ln_bwd_kernel(GateBwdParams p) {
       if (orow >= 0) vstore(p.dout + orow * D + j0, dov);
       if (IO && p.drbf) vstore_bf(reinterpret_cast<uint16_t*>(p.dR) + row * p.lddr + j0, drv);
       else vstore(p.dR + row * p.lddr + j0, drv);
+    }
+  };
+  if (wid < p.nwaves) {
+    In A, B;
+    for (int64_t row = wid; row < p.n; row += 2 * (int64_t)p.nwaves) {
+      const int64_t rb = row + p.nwaves;
+      const bool two = rb < p.n;   // wave-uniform
+      issue(A, row);
+      issue(B, two ? rb : row);
+      finish(A, row);
+      if (two) finish(B, rb);
     }
   }
   // one partial row per workgroup: the 4 waves' sums merged in LDS in wave order (fixed)
@@ -523,6 +594,22 @@ extern "C" int alignn_gate_ln_fwd(int64_t n, int32_t D, const float* outp, const
 #define ALIGNN_GATE_BWD_WAVES 4096  // 2048: +1.0 % (v18); 4096 once the parameter reduction left the main stream: +0.5 % (v43_ab_gate_waves_4096.log)
 #endif
 
+template <int VPL>
+static void launch_gate_bwd(const GateBwdParams& p, dim3 g, hipStream_t s, bool io, bool rbf, bool x2, bool x2bf) {
+  if (!io) {
+    if (x2) launch(gate_ln_bwd_kernel<VPL, false, false, true, false>, g, dim3(256), 0, s, p);
+    else launch(gate_ln_bwd_kernel<VPL, false, false, false, false>, g, dim3(256), 0, s, p);
+  } else if (rbf) {
+    if (x2bf) launch(gate_ln_bwd_kernel<VPL, true, true, true, true>, g, dim3(256), 0, s, p);
+    else if (x2) launch(gate_ln_bwd_kernel<VPL, true, true, true, false>, g, dim3(256), 0, s, p);
+    else launch(gate_ln_bwd_kernel<VPL, true, true, false, false>, g, dim3(256), 0, s, p);
+  } else {
+    if (x2bf) launch(gate_ln_bwd_kernel<VPL, true, false, true, true>, g, dim3(256), 0, s, p);
+    else if (x2) launch(gate_ln_bwd_kernel<VPL, true, false, true, false>, g, dim3(256), 0, s, p);
+    else launch(gate_ln_bwd_kernel<VPL, true, false, false, false>, g, dim3(256), 0, s, p);
+  }
+}
+
 extern "C" int64_t alignn_gate_ln_bwd_workspace(int64_t n, int32_t D) {
   if (n < 0 || D <= 0) return -1;
   return std::max<int64_t>(1, std::min<int64_t>(ALIGNN_GATE_BWD_WAVES, n)) * 5 * D;
@@ -563,14 +650,10 @@ extern "C" int alignn_gate_ln_bwd_partials_ex(int64_t n, int32_t D, float* dXnew
   dim3 g((unsigned)((nwaves + 3) / 4));
   const bool io = r_bf16 || dr_bf16 || x2bf;
   switch (vpl) {
-    case 1: if (io) launch(gate_ln_bwd_kernel<1, true>, g, dim3(256), 0, s, p);
-            else launch(gate_ln_bwd_kernel<1, false>, g, dim3(256), 0, s, p); break;
-    case 2: if (io) launch(gate_ln_bwd_kernel<2, true>, g, dim3(256), 0, s, p);
-            else launch(gate_ln_bwd_kernel<2, false>, g, dim3(256), 0, s, p); break;
-    case 4: if (io) launch(gate_ln_bwd_kernel<4, true>, g, dim3(256), 0, s, p);
-            else launch(gate_ln_bwd_kernel<4, false>, g, dim3(256), 0, s, p); break;
-    default: if (io) launch(gate_ln_bwd_kernel<8, true>, g, dim3(256), 0, s, p);
-             else launch(gate_ln_bwd_kernel<8, false>, g, dim3(256), 0, s, p); break;
+    case 1: launch_gate_bwd<1>(p, g, s, io, r_bf16 != 0, dX_add != nullptr, x2bf != 0); break;
+    case 2: launch_gate_bwd<2>(p, g, s, io, r_bf16 != 0, dX_add != nullptr, x2bf != 0); break;
+    case 4: launch_gate_bwd<4>(p, g, s, io, r_bf16 != 0, dX_add != nullptr, x2bf != 0); break;
+    default: launch_gate_bwd<8>(p, g, s, io, r_bf16 != 0, dX_add != nullptr, x2bf != 0); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_bwd_kernel");
   return ALIGNN_OK;

@@ -112,7 +112,7 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
           unset ALIGNN_HIP_LIB; cd $OLDPWD
           for lib in $ABL_LIBS; do t=tree; [ "$lib" = "-" ] || t=$(basename ${lib%.so})
             for c in 3 2; do python tools/trace_by_grid.py $O/rpab${c}_$t/run_kernel_trace.csv > $O/rpab${c}_$t.txt 2>&1
-              echo "C$c $t: $(grep -E 'tconv_(fwd2|bwd_dst2|bwd_src)' $O/rpab${c}_$t.txt | awk '{n=$0; sub(/.*alignn::/, "", n); printf "%s %s | ", $1, n}')"; done; done ;;
+              echo "C$c $t: $(grep -E "${ABL_PAT:-tconv_(fwd2|bwd_dst2|bwd_src)}" $O/rpab${c}_$t.txt | awk '{n=$0; sub(/.*alignn::/, "", n); printf "%s %s | ", $1, n}')"; done; done ;;
     abl) # library A/B (C2 bench + lgx_bench fp32 kernels): ab/libA.so vs the in-tree build
          for i in 1 2; do for lib in ab/libA.so -; do
            if [ "$lib" = "-" ]; then unset ALIGNN_HIP_LIB; t=B; else export ALIGNN_HIP_LIB=$PWD/$lib; t=A; fi
