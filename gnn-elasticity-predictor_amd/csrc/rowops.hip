@@ -54,8 +54,11 @@ struct GateFwdParams {
                         // the next line block's active-row gather, written here instead of by a launch
 };
 
-// IO: some operand is bf16 (bf16 storage); the fp32 instantiation carries no storage-type branches
-template <int VPL, bool IO>
+// IO: some operand is bf16 (bf16 storage); the fp32 instantiation carries no storage-type branches.
+// RBF: R is bf16 (a template flag: no branch between the row's loads).  Every load of the row is
+// issued at once and unconditionally (a row without an output row reads its residual row and zeroes
+// o): one round trip per row.
+template <int VPL, bool IO, bool RBF>
 __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   resolve_drop(p.drop);
   const int lane = threadIdx.x & 63;
@@ -63,17 +66,23 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   if (row >= p.n) return;
   const int D = p.D, j0 = lane * VPL;
   const bool act = j0 < D;
-  float o[VPL], r[VPL], w1[VPL], w2[VPL], w3[VPL];
+  float o[VPL], r[VPL], w1[VPL], w2[VPL], w3[VPL], g[VPL], bb[VPL], x[VPL];
   vzero(o); vzero(r); vzero(w1); vzero(w2); vzero(w3);
   const int64_t orow = p.orow ? (int64_t)uni(sld(p.orow, row)) : row;
   if (act) {
-    if (orow >= 0) vload(p.outp + orow * D + j0, o);
-    if (IO && p.rbf) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
+    vload((orow >= 0 ? p.outp + orow * D : p.X + row * p.ldx) + j0, o);
+    if constexpr (RBF) vload_bf(reinterpret_cast<const uint16_t*>(p.R) + row * p.ldr + j0, r);
     else vload(p.R + row * p.ldr + j0, r);
     vload(p.wbeta + j0, w1);
     vload(p.wbeta + D + j0, w2);
     vload(p.wbeta + 2 * D + j0, w3);
+    // the LayerNorm parameters and the residual row with the rest: one round trip per row, not two
+    vload(p.lnw + j0, g);
+    vload(p.lnb + j0, bb);
+    vload(p.X + row * p.ldx + j0, x);
   }
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) o[i] = orow >= 0 ? o[i] : 0.f;
   float part = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) part += o[i] * w1[i] + r[i] * w2[i] + (o[i] - r[i]) * w3[i];
@@ -96,10 +105,7 @@ __global__ __launch_bounds__(256) void gate_ln_fwd_kernel(GateFwdParams p) {
   const float var = wave_sum(sv) / (float)D;
   const float rs = 1.0f / sqrtf(var + 1e-5f);
   if (act) {
-    float g[VPL], bb[VPL], x[VPL], out[VPL];
-    vload(p.lnw + j0, g);
-    vload(p.lnb + j0, bb);
-    vload(p.X + row * p.ldx + j0, x);
+    float out[VPL];
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       float a = fmaxf((y[i] - mean) * rs * g[i] + bb[i], 0.f);
@@ -331,6 +337,13 @@ __global__ __launch_bounds__(256) void gate_ln_slice_reduce(const float* __restr
   if (ty == 0 && col < n) out[col] += (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 
+template <int VPL>
+static void launch_gate_fwd(const GateFwdParams& p, dim3 g, hipStream_t s, bool io, bool rbf) {
+  if (!io) launch(gate_ln_fwd_kernel<VPL, false, false>, g, dim3(256), 0, s, p);
+  else if (rbf) launch(gate_ln_fwd_kernel<VPL, true, true>, g, dim3(256), 0, s, p);
+  else launch(gate_ln_fwd_kernel<VPL, true, false>, g, dim3(256), 0, s, p);
+}
+
 static int vpl_for(int D) {
   if (D <= 64) return 1;
   if (D == 128) return 2;
@@ -550,14 +563,10 @@ extern "C" int alignn_gate_ln_fwd_ex2(int64_t n, int32_t D, const float* outp, c
   dim3 g((unsigned)((n + 3) / 4));
   const bool io = r_bf16 || Xnew16;
   switch (vpl) {
-    case 1: if (io) launch(gate_ln_fwd_kernel<1, true>, g, dim3(256), 0, s, p);
-            else launch(gate_ln_fwd_kernel<1, false>, g, dim3(256), 0, s, p); break;
-    case 2: if (io) launch(gate_ln_fwd_kernel<2, true>, g, dim3(256), 0, s, p);
-            else launch(gate_ln_fwd_kernel<2, false>, g, dim3(256), 0, s, p); break;
-    case 4: if (io) launch(gate_ln_fwd_kernel<4, true>, g, dim3(256), 0, s, p);
-            else launch(gate_ln_fwd_kernel<4, false>, g, dim3(256), 0, s, p); break;
-    default: if (io) launch(gate_ln_fwd_kernel<8, true>, g, dim3(256), 0, s, p);
-             else launch(gate_ln_fwd_kernel<8, false>, g, dim3(256), 0, s, p); break;
+    case 1: launch_gate_fwd<1>(p, g, s, io, r_bf16 != 0); break;
+    case 2: launch_gate_fwd<2>(p, g, s, io, r_bf16 != 0); break;
+    case 4: launch_gate_fwd<4>(p, g, s, io, r_bf16 != 0); break;
+    default: launch_gate_fwd<8>(p, g, s, io, r_bf16 != 0); break;
   }
   ALIGNN_LAUNCH_CHECK("gate_ln_fwd_kernel");
   return ALIGNN_OK;
