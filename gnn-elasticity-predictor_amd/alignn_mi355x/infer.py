@@ -29,6 +29,13 @@ from .engine import adopt, batch_cache, batch_versions, clone_batch
 FIELDS = ("x", "edge_index", "edge_attr", "lg_edge_index", "lg_edge_attr", "global_x", "sg_one_hot", "batch", "ptr")
 MAX_PLANS = 4
 ENABLED = True
+# A forward over fewer line-graph edges than this is recorded on one stream (no side / aux stream work)
+# and may then be replayed as a HIP graph: a launch-latency-bound forward (config C1: a few dozen small
+# kernels) gains nothing from the side streams, and a graph with parallel branches makes the runtime
+# create streams of its own at instantiation, which moved the hardware-queue assignment of streams
+# created later in the process (the B = 32 e2e loop after bench's C1 forward: 10,050 -> 7,200
+# graphs/s, gpurun_out r6e2).  Larger forwards keep their streams and the native plan.
+SINGLE_STREAM_MAX_T = 65536
 
 
 class ForwardPlan:
@@ -55,10 +62,16 @@ class ForwardPlan:
         self._bound_v = batch_versions(batch, FIELDS)
         x, gx = slot.x, slot.global_x
         batch = slot
+        self.single = bc.T < SINGLE_STREAM_MAX_T
 
         def fwd():
-            with torch.autocast("cuda", enabled=False), eng.using_precision(precision):
-                out, _ = eng.forward(st.P, batch, bc, False, 0, x, gx, mode)
+            prev = eng.overlap_forward
+            eng.overlap_forward = prev and not self.single
+            try:
+                with torch.autocast("cuda", enabled=False), eng.using_precision(precision):
+                    out, _ = eng.forward(st.P, batch, bc, False, 0, x, gx, mode)
+            finally:
+                eng.overlap_forward = prev
             return out
 
         # warm-up: every workspace sized at this signature, on a side stream (as FusedTrainer.capture)
@@ -103,8 +116,11 @@ class ForwardPlan:
         # the same launches as a HIP graph (the capture above): one host call instead of one per launch.
         # Where the forward is only a few dozen small kernels (config C1) the per-launch host cost of
         # the native plan is the call's time and the graph is faster; on a large batch the plan's
-        # concurrent streams win.  Both replays are timed here (three each) and the faster one kept
+        # concurrent streams win.  For a single-stream capture (SINGLE_STREAM_MAX_T) both replays are
+        # timed here (three each) and the faster one kept
         self.use_graph = False
+        if not self.single:
+            return
         try:
             tp = self._time(lambda: check(_lib.lib().alignn_plan_replay(self.plan, ops.stream_ptr()),
                                           "alignn_plan_replay"))

@@ -152,6 +152,29 @@ def test_graph_and_plan_replay_equal(use_graph):
         assert torch.equal(_planned(model, b), r)
 
 
+def test_small_forward_single_stream_large_keeps_streams():
+    """A forward over fewer line-graph edges than infer.SINGLE_STREAM_MAX_T is recorded on one stream
+    and may replay as a HIP graph; a larger one keeps the side streams and always replays the native
+    plan (a multi-branch graph's runtime-created streams moved later streams' hardware queues).  Both
+    bitwise the eager forward, which runs on the side streams either way."""
+    from alignn_mi355x import infer
+    from alignn_mi355x.synthetic import mp_like_batch
+    for nb, single in ((6, True), (12, False)):
+        model = _model()
+        b = mp_like_batch(nb).to(DEV)
+        assert (int(b.lg_edge_index.size(1)) < infer.SINGLE_STREAM_MAX_T) == single
+        ref = _eager(model, b)
+        _planned(model, b)
+        got = _planned(model, b)                  # recorded here
+        p = next(iter(model.__dict__["_fwd_plans"].values()))
+        assert p.single == single
+        if not single:
+            assert not p.use_graph
+        assert model._engine.overlap_forward   # restored after the recording
+        assert torch.equal(got, ref)
+        assert torch.equal(_planned(model, b), ref)
+
+
 def test_replaced_parameter_invalidates_recorded_forward():
     """A parameter replaced after the forward was recorded re-lays the flat buffer out
     (model._ensure_flat): the recorded plans, which read the old buffer, are released and the call

@@ -90,6 +90,11 @@ print('$f'.split('/')[-1], d['value'], 'e2e', (d.get('e2e') or {}).get('value'),
              run lgxab3_${t}_$i 300 python tools/lgx_bench.py --batch 256 --only fwd_bf16_rows bwd_bf16_rows
            done; done; unset ALIGNN_HIP_LIB
            for f in $O/lgxab*.log; do echo "$(basename $f) $(grep -o '"fwd_[a-z0-9_]*_us": [0-9.]*\|"bwd_[a-z0-9_]*_us": [0-9.]*' $f | tr '\n' ' ')"; done ;;
+    e2ec) B=(python bench.py --steps 20 --warmup 5)   # the default line, twice (e2e after the C1 forward)
+          run e2ec_default_1 600 "${B[@]}"
+          run e2ec_default_2 600 "${B[@]}"
+          val "$O"/e2ec_*.log ;;
+    ti) run ti 600 "${PT[@]}" tests/test_gpu_x_infer.py -v ;;
     tl) run tl 900 "${PT[@]}" tests/test_gpu_x_lg3.py tests/test_gpu_x_recompute.py tests/test_gpu_parity.py tests/test_gpu_x_configs.py ;;
     tg) run tg 900 "${PT[@]}" tests/test_gpu_x_gemm_pipe.py tests/test_gpu_x_gemm_rows.py tests/test_gpu_x_splitk.py tests/test_gpu_x_gemm_lds16.py tests/test_gpu_x_gemm_wgrad.py tests/test_gpu_kernels.py ;;
     gb3) run gb3 600 python tools/gemm_bench.py --batch 256 --precision bf16 --min-m 15000 --quick --reps 10 ;;
