@@ -366,8 +366,18 @@ __global__ void readout_fwd_kernel(int64_t B, int D, const float* __restrict__ h
   for (int c = threadIdx.x; c < W; c += blockDim.x) {
     float v;
     if (c < D) {
+      // eight rows' loads in flight, summed in row order (bitwise the one-row loop; the pass is a
+      // chain of dependent round trips otherwise: 18 us for B = 32 graphs of 60 atoms)
       float acc = 0.f;
-      for (int64_t i = s; i < e; ++i) acc += h[i * D + c];
+      int64_t i = s;
+      for (; i + 8 <= e; i += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = h[(i + k) * D + c];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += v[k];
+      }
+      for (; i < e; ++i) acc += h[i * D + c];
       v = acc * inv;
     } else if (c < D + gdim) {
       v = gx[b * gdim + (c - D)];
