@@ -166,6 +166,34 @@ __global__ void scatter_rows_kernel(const float* __restrict__ in, int64_t ld_in,
   }
 }
 
+// The same two row moves with one wave per row and 16-byte accesses (rows of 4-float multiples at
+// 16-byte aligned addresses): no 64-bit divide per element — the element loops above are
+// instruction-bound at C3 (a 16k x 256 gather: 27 us for 33 MB).
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void move_rows4_kernel(const float4* __restrict__ in, int64_t ld_in4,
+                                                         const int32_t* __restrict__ idx, int64_t rows, int cols4,
+                                                         float4* __restrict__ out, int64_t ld_out4, int acc) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave_id(); r < rows; r += (int64_t)gridDim.x * 4) {
+    const int64_t j = idx[r];
+    const float4* src = in + (SCATTER ? r : j) * ld_in4;
+    float4* dst = out + (SCATTER ? j : r) * ld_out4;
+    for (int c = lane; c < cols4; c += 64) {
+      float4 v = src[c];
+      if (SCATTER && acc) {
+        const float4 o = dst[c];
+        v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+      }
+      dst[c] = v;
+    }
+  }
+}
+
+static bool rows4_ok(const float* in, int64_t ld_in, const float* out, int64_t ld_out, int64_t cols) {
+  return cols % 4 == 0 && ld_in % 4 == 0 && ld_out % 4 == 0 && cols / 4 <= (1 << 30) &&
+         ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+}
+
 static int grid_for(int64_t work, int block = 256, int64_t cap = 8192) {
   int64_t g = (work + block - 1) / block;
   if (g < 1) g = 1;
@@ -382,6 +410,12 @@ extern "C" int alignn_gather_rows_f32(const float* in, int64_t ld_in, const int3
   if (rows < 0 || cols < 0) return ALIGNN_E_BAD_SHAPE;
   if (rows == 0 || cols == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows4_ok(in, ld_in, out, ld_out, cols)) {
+    launch(move_rows4_kernel<false>, dim3(grid_for(rows, 4)), dim3(256), 0, s, reinterpret_cast<const float4*>(in),
+           ld_in / 4, idx, rows, (int)(cols / 4), reinterpret_cast<float4*>(out), ld_out / 4, 0);
+    ALIGNN_LAUNCH_CHECK("move_rows4_kernel");
+    return ALIGNN_OK;
+  }
   launch(gather_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
                      out, ld_out);
   ALIGNN_LAUNCH_CHECK("gather_rows_kernel");
@@ -393,6 +427,12 @@ extern "C" int alignn_scatter_rows_f32(const float* in, int64_t ld_in, const int
   if (rows < 0 || cols < 0) return ALIGNN_E_BAD_SHAPE;
   if (rows == 0 || cols == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows4_ok(in, ld_in, out, ld_out, cols)) {
+    launch(move_rows4_kernel<true>, dim3(grid_for(rows, 4)), dim3(256), 0, s, reinterpret_cast<const float4*>(in),
+           ld_in / 4, idx, rows, (int)(cols / 4), reinterpret_cast<float4*>(out), ld_out / 4, accumulate);
+    ALIGNN_LAUNCH_CHECK("move_rows4_kernel");
+    return ALIGNN_OK;
+  }
   launch(scatter_rows_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, in, ld_in, idx, rows, cols,
                      out, ld_out, accumulate);
   ALIGNN_LAUNCH_CHECK("scatter_rows_kernel");

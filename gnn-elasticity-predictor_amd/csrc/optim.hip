@@ -136,43 +136,19 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   const float dec0 = (float)(1.0 - lr0 * wd), dec1 = (float)(1.0 - lr1 * wd);
   float c = 1.0f;
   if (norm) c = fminf(max_norm / (*norm + 1e-6f), 1.0f);
-  auto upd = [&](int64_t i, float& pr, float& gr, float& mr, float& vr) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const bool g0 = i < split;
-    const float gi = gr * c;
-    gr = gi;  // clip_grad_norm_ scales the gradients in place
-    const float pi = pr * (g0 ? dec0 : dec1);
-    const float m0 = mr;
+    const float gi = g[i] * c;
+    g[i] = gi;  // clip_grad_norm_ scales the gradients in place
+    const float pi = p[i] * (g0 ? dec0 : dec1);
+    const float m0 = m[i];
     const float mi = m0 + omb1 * (gi - m0);            // lerp_(g, 1 - b1), weight < 0.5 branch
-    const float vi = vr * fb2 + omb2 * gi * gi;         // mul_(b2).addcmul_(g, g, value=1 - b2)
+    const float vi = v[i] * fb2 + omb2 * gi * gi;       // mul_(b2).addcmul_(g, g, value=1 - b2)
     const float den = sqrtf(vi) / bc2s + eps;
-    pr = pi + (-(g0 ? ss0 : ss1)) * mi / den;          // addcdiv_(m, denom, value=-step_size)
-    mr = mi;
-    vr = vi;
-  };
-  // Four elements per lane through 16-byte accesses when the four buffers allow it: a quarter of the
-  // waves, so the per-wave fp64 scalar prologue above (two pow, divisions) is paid a quarter as often.
-  // Per-element arithmetic as in the scalar loop (bitwise).
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t head = 0;
-  if (((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
-        reinterpret_cast<uintptr_t>(v)) & 15) == 0) {
-    const int64_t n4 = n >> 2;
-    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n4; q += stride) {
-      float4 P = reinterpret_cast<float4*>(p)[q], G = reinterpret_cast<float4*>(g)[q];
-      float4 Mv = reinterpret_cast<float4*>(m)[q], V = reinterpret_cast<float4*>(v)[q];
-      upd(4 * q, P.x, G.x, Mv.x, V.x);
-      upd(4 * q + 1, P.y, G.y, Mv.y, V.y);
-      upd(4 * q + 2, P.z, G.z, Mv.z, V.z);
-      upd(4 * q + 3, P.w, G.w, Mv.w, V.w);
-      reinterpret_cast<float4*>(p)[q] = P;
-      reinterpret_cast<float4*>(g)[q] = G;
-      reinterpret_cast<float4*>(m)[q] = Mv;
-      reinterpret_cast<float4*>(v)[q] = V;
-    }
-    head = n4 << 2;
+    p[i] = pi + (-(g0 ? ss0 : ss1)) * mi / den;        // addcdiv_(m, denom, value=-step_size)
+    m[i] = mi;
+    v[i] = vi;
   }
-  for (int64_t i = head + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
-    upd(i, p[i], g[i], m[i], v[i]);
 }
 
 }  // namespace alignn
@@ -209,7 +185,7 @@ static int adamw(float* p, float* g, float* m, float* v, int64_t n, int64_t spli
     launch(step_amp_kernel, dim3(1), dim3(1), 0, s, step, scaler, growth_interval);
   else
     launch(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
-  const int64_t blocks = std::min<int64_t>((n + 1023) / 1024, 2048);   // four elements per lane (adamw_kernel)
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   if (n > 0)
     launch(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, split, lr0, lr1,
                        weight_decay, beta1, beta2, (float)eps, norm, max_norm, step, lr_dev, scaler);

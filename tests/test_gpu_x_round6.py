@@ -77,3 +77,31 @@ def test_gate_bwd_dx_zero_equals_zero_filled_plus_add(add_bf16):
         # contract the per-row partials' fmas differently (as tests/test_gpu_x_bf16_io.py): fp32 rounding
         err = float((a[i] - b[i]).abs().max() / b[i].abs().max())
         assert err < 1e-6, (i, err)
+
+
+@pytest.mark.parametrize("cols,ld", [(256, 256), (260, 264), (30, 30), (8, 12)])
+def test_row_moves_vector_and_element_paths(cols, ld):
+    """graph.hip gather / scatter rows: the wave-per-row 16-byte path (cols and leading dimensions
+    multiples of 4: 256, and 260 = more float4s per row than lanes) and the element loop (30; 8 with
+    an odd start column below) — each a plain copy, so bitwise against torch indexing, with and
+    without accumulation."""
+    from alignn_mi355x import ops
+    torch.manual_seed(11)
+    n, na = 3000, 777
+    rows = torch.randperm(n)[:na].to(torch.int32).to(DEV)
+    big = torch.randn(n, ld, device=DEV)
+    src = big[:, :cols] if (cols, ld) != (8, 12) else big[:, 1:9]
+    g = ops.gather_rows(src, rows)
+    assert torch.equal(g, src[rows.long()])
+    vals = torch.randn(na, ld, device=DEV)[:, :cols]
+    out0 = torch.randn(n, ld, device=DEV)
+    out = out0.clone()
+    ops.scatter_rows(vals, rows, out[:, :cols])
+    ref = out0.clone()
+    ref[rows.long(), :cols] = vals
+    assert torch.equal(out, ref)
+    out = out0.clone()
+    ops.scatter_rows(vals, rows, out[:, :cols], accumulate=True)
+    ref = out0.clone()
+    ref[rows.long(), :cols] += vals
+    assert torch.equal(out, ref)
