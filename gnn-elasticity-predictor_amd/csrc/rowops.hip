@@ -393,15 +393,18 @@ __global__ void pool_bwd_kernel(int64_t N, int D, const float* __restrict__ dfea
                                 const int64_t* __restrict__ ptr, const int64_t* __restrict__ batch,
                                 float* __restrict__ dh, int acc, DropParams drop) {
   resolve_drop(drop);
-  const int64_t total = N * D;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t node = i / D;
-    const int c = (int)(i % D);
+  // one wave per node row (its graph and count loaded once, no per-element 64-bit divide); each
+  // element's value as the element loop computed it
+  const int lane = threadIdx.x & 63;
+  for (int64_t node = (int64_t)blockIdx.x * 4 + wave_id(); node < N; node += (int64_t)gridDim.x * 4) {
     const int64_t b = batch[node];
     const float cnt = (float)max((int64_t)1, ptr[b + 1] - ptr[b]);
-    float v = dfeats[b * ldf + c] / cnt;
-    if (drop.active) v *= dropout_mul(drop.seed, (uint64_t)b * ldf + c, drop.thresh, drop.inv_keep);
-    dh[i] = acc ? dh[i] + v : v;
+    for (int c = lane; c < D; c += 64) {
+      float v = dfeats[b * ldf + c] / cnt;
+      if (drop.active) v *= dropout_mul(drop.seed, (uint64_t)b * ldf + c, drop.thresh, drop.inv_keep);
+      const int64_t i = node * D + c;
+      dh[i] = acc ? dh[i] + v : v;
+    }
   }
 }
 
@@ -760,7 +763,7 @@ extern "C" int alignn_readout_pool_bwd(int64_t B, int64_t N, int32_t D, const fl
   (void)B;
   if (N == 0) return ALIGNN_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  launch(pool_bwd_kernel, dim3(grid_for(N * D)), dim3(256), 0, s, N, D, dfeats, ldf, ptr, batch, dh,
+  launch(pool_bwd_kernel, dim3(grid_for(N, 4)), dim3(256), 0, s, N, D, dfeats, ldf, ptr, batch, dh,
                      accumulate, make_drop(drop_p, seed));
   ALIGNN_LAUNCH_CHECK("pool_bwd_kernel");
   return ALIGNN_OK;
